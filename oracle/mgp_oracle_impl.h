@@ -1,0 +1,243 @@
+/*
+ * mgp_oracle_impl.h — type-generic body of the CPU oracle (TEST INFRASTRUCTURE ONLY).
+ * Included twice by mgp_oracle.c with MGO_T = float / double and MGO_S = f / d.
+ * Every arithmetic expression keeps the reference's operation order; the file is compiled
+ * with -ffp-contract=off so no multiply-add is fused.
+ */
+#define MGO_CAT2(a, b) a##_##b
+#define MGO_CAT(a, b) MGO_CAT2(a, b)
+#define FN(name) MGO_CAT(name, MGO_S)
+
+typedef MGO_T FN(real);
+
+/* Sum of the 2*dim neighbours, ghost value 0 outside the array.
+ * Order ((xl + xr) + yl) + yr [+ zl + zr] as written in cpu.lua:45-49 / cpu-raw.lua:36-41. */
+static inline MGO_T FN(nbsum)(const MGO_T* u, int dim, int64_t nx, int64_t ny, int64_t nz,
+                              int64_t i, int64_t j, int64_t k)
+{
+    const int64_t pl = nx * ny;
+    const MGO_T* c = u + i + nx * j + pl * k;
+    MGO_T xl = i > 0 ? c[-1] : (MGO_T)0;
+    MGO_T xr = i < nx - 1 ? c[1] : (MGO_T)0;
+    MGO_T yl = j > 0 ? c[-nx] : (MGO_T)0;
+    MGO_T yr = j < ny - 1 ? c[nx] : (MGO_T)0;
+    MGO_T s = xl + xr;
+    s = s + yl;
+    s = s + yr;
+    if (dim == 3) {
+        MGO_T zl = k > 0 ? c[-pl] : (MGO_T)0;
+        MGO_T zr = k < nz - 1 ? c[pl] : (MGO_T)0;
+        s = s + zl;
+        s = s + zr;
+    }
+    return s;
+}
+
+/* One smoother update of one cell: (f - askew_u) / adiag with askew_u = sum / h^2,
+ * adiag = -2*dim / h^2 (cpu.lua:49-51, cpu-raw.lua:40-43). */
+static inline MGO_T FN(relax)(MGO_T sum, MGO_T fc, MGO_T hSq, MGO_T adiag)
+{
+    MGO_T askew = sum / hSq;
+    return (fc - askew) / adiag;
+}
+
+/* Number of the cell's faces on the box boundary (a 1-cell axis counts 2). */
+static inline int FN(nfaces)(int dim, int64_t nx, int64_t ny, int64_t nz, int64_t i, int64_t j,
+                             int64_t k)
+{
+    int nb = (i == 0) + (i == nx - 1) + (j == 0) + (j == ny - 1);
+    if (dim == 3) nb += (k == 0) + (k == nz - 1);
+    return nb;
+}
+
+/* Diagonal of the level operator.  cl = 0 gives the reference's adiag = -2*dim/h^2 exactly;
+ * cl > 0 (MGO_BC_CONSISTENT) folds the extrapolated ghost -cl*u into the diagonal:
+ * diag = ((T)(-2*dim) - (T)nb * cl) / h^2. */
+static inline MGO_T FN(diag)(int dim, int nb, MGO_T cl, MGO_T hSq, MGO_T adiag)
+{
+    if (cl == (MGO_T)0 || nb == 0) return adiag;
+    MGO_T dg = (MGO_T)(-2 * dim) - (MGO_T)nb * cl;
+    return dg / hSq;
+}
+
+static void FN(jacobi)(int dim, int64_t nx, int64_t ny, int64_t nz, double h, MGO_T cl, MGO_T* u,
+                       const MGO_T* f, MGO_T* last, int threads)
+{
+    const MGO_T hh = (MGO_T)h, hSq = hh * hh, adiag = (MGO_T)(-2 * dim) / hSq;
+    const int64_t pl = nx * ny;
+    memcpy(last, u, (size_t)(pl * nz) * sizeof(MGO_T)); /* lastU = matrix(u), cpu.lua:42 */
+#pragma omp parallel for num_threads(threads) schedule(static) if (threads > 1 && pl * nz > 65536)
+    for (int64_t k = 0; k < nz; ++k)
+        for (int64_t j = 0; j < ny; ++j)
+            for (int64_t i = 0; i < nx; ++i) {
+                int64_t c = i + nx * j + pl * k;
+                MGO_T dg = FN(diag)(dim, FN(nfaces)(dim, nx, ny, nz, i, j, k), cl, hSq, adiag);
+                u[c] = FN(relax)(FN(nbsum)(last, dim, nx, ny, nz, i, j, k), f[c], hSq, dg);
+            }
+}
+
+/* Red/black Gauss-Seidel (build-defined; red = (i + j + k + z0) even, red first). */
+static void FN(rbgs)(int dim, int64_t nx, int64_t ny, int64_t nz, double h, MGO_T cl, MGO_T* u,
+                     const MGO_T* f, int threads)
+{
+    const MGO_T hh = (MGO_T)h, hSq = hh * hh, adiag = (MGO_T)(-2 * dim) / hSq;
+    const int64_t pl = nx * ny;
+    for (int color = 0; color < 2; ++color) {
+#pragma omp parallel for num_threads(threads) schedule(static) if (threads > 1 && pl * nz > 65536)
+        for (int64_t k = 0; k < nz; ++k)
+            for (int64_t j = 0; j < ny; ++j) {
+                int64_t i0 = (int64_t)((color + j + k) & 1);
+                for (int64_t i = i0; i < nx; i += 2) {
+                    int64_t c = i + nx * j + pl * k;
+                    MGO_T dg = FN(diag)(dim, FN(nfaces)(dim, nx, ny, nz, i, j, k), cl, hSq, adiag);
+                    u[c] = FN(relax)(FN(nbsum)(u, dim, nx, ny, nz, i, j, k), f[c], hSq, dg);
+                }
+            }
+    }
+}
+
+/* Lexicographic GS in cpu.lua:26-27 loop order (x outer, then y, then z). */
+static void FN(gslex)(int dim, int64_t nx, int64_t ny, int64_t nz, double h, MGO_T cl, MGO_T* u,
+                      const MGO_T* f)
+{
+    const MGO_T hh = (MGO_T)h, hSq = hh * hh, adiag = (MGO_T)(-2 * dim) / hSq;
+    const int64_t pl = nx * ny;
+    for (int64_t i = 0; i < nx; ++i)
+        for (int64_t j = 0; j < ny; ++j)
+            for (int64_t k = 0; k < nz; ++k) {
+                int64_t c = i + nx * j + pl * k;
+                MGO_T dg = FN(diag)(dim, FN(nfaces)(dim, nx, ny, nz, i, j, k), cl, hSq, adiag);
+                u[c] = FN(relax)(FN(nbsum)(u, dim, nx, ny, nz, i, j, k), f[c], hSq, dg);
+            }
+}
+
+static void FN(smooth)(int dim, int64_t nx, int64_t ny, int64_t nz, int smoother, int sweeps,
+                       double h, double cl, MGO_T* u, const MGO_T* f, MGO_T* tmp, int threads)
+{
+    const MGO_T c = (MGO_T)cl;
+    for (int s = 0; s < sweeps; ++s) {
+        if (smoother == MGO_JACOBI)
+            FN(jacobi)(dim, nx, ny, nz, h, c, u, f, tmp, threads);
+        else if (smoother == MGO_RBGS)
+            FN(rbgs)(dim, nx, ny, nz, h, c, u, f, threads);
+        else
+            FN(gslex)(dim, nx, ny, nz, h, c, u, f);
+    }
+}
+
+/* r = f - A u, A u = askew_u + adiag * u (cpu.lua:112-123, cpu-raw.lua:46-57). */
+static void FN(residual)(int dim, int64_t nx, int64_t ny, int64_t nz, double h, double cl,
+                         const MGO_T* u, const MGO_T* f, MGO_T* r, int threads)
+{
+    const MGO_T hh = (MGO_T)h, hSq = hh * hh, adiag = (MGO_T)(-2 * dim) / hSq, c = (MGO_T)cl;
+    const int64_t pl = nx * ny;
+#pragma omp parallel for num_threads(threads) schedule(static) if (threads > 1 && pl * nz > 65536)
+    for (int64_t k = 0; k < nz; ++k)
+        for (int64_t j = 0; j < ny; ++j)
+            for (int64_t i = 0; i < nx; ++i) {
+                int64_t cc = i + nx * j + pl * k;
+                MGO_T askew = FN(nbsum)(u, dim, nx, ny, nz, i, j, k) / hSq;
+                MGO_T dg = FN(diag)(dim, FN(nfaces)(dim, nx, ny, nz, i, j, k), c, hSq, adiag);
+                MGO_T a_u = askew + dg * u[cc];
+                r[cc] = f[cc] - a_u;
+            }
+}
+
+/* R = 1/4 (r00 + r10 + r01 + r11), x-first (cpu-raw.lua:59-63); 3D: 1/8 of 8 children,
+ * x fastest, then y, then z, summed left to right. */
+static void FN(restrict_)(int dim, int64_t nx, int64_t ny, int64_t nz, const MGO_T* r, MGO_T* R,
+                          int threads)
+{
+    const int64_t cx = nx / 2, cy = ny / 2, cz = dim == 3 ? nz / 2 : 1;
+    const int64_t pl = nx * ny, cpl = cx * cy;
+#pragma omp parallel for num_threads(threads) schedule(static) if (threads > 1 && pl * nz > 65536)
+    for (int64_t K = 0; K < cz; ++K)
+        for (int64_t J = 0; J < cy; ++J)
+            for (int64_t I = 0; I < cx; ++I) {
+                if (dim == 2) {
+                    const MGO_T* s = r + 2 * I + nx * (2 * J);
+                    MGO_T sum = s[0] + s[1];
+                    sum = sum + s[nx];
+                    sum = sum + s[nx + 1];
+                    R[I + cx * J] = (MGO_T)0.25 * sum;
+                } else {
+                    const MGO_T* s = r + 2 * I + nx * (2 * J) + pl * (2 * K);
+                    MGO_T sum = s[0] + s[1];
+                    sum = sum + s[nx];
+                    sum = sum + s[nx + 1];
+                    sum = sum + s[pl];
+                    sum = sum + s[pl + 1];
+                    sum = sum + s[pl + nx];
+                    sum = sum + s[pl + nx + 1];
+                    R[I + cx * J + cpl * K] = (MGO_T)0.125 * sum;
+                }
+            }
+}
+
+/* Coarse value for the linear prolongation.  Outside the box the ghost is -cl times the
+ * value of the nearest cell inside (cl = 0: the reference's ghost 0).  Only one axis can be
+ * outside at a time for the separable weights used below, but the clamp is applied per axis. */
+static inline MGO_T FN(cval)(const MGO_T* V, int64_t cx, int64_t cy, int64_t cz, int64_t I,
+                             int64_t J, int64_t K, MGO_T cl)
+{
+    MGO_T s = (MGO_T)1;
+    if (I < 0) { I = 0; s = -cl * s; } else if (I >= cx) { I = cx - 1; s = -cl * s; }
+    if (J < 0) { J = 0; s = -cl * s; } else if (J >= cy) { J = cy - 1; s = -cl * s; }
+    if (K < 0) { K = 0; s = -cl * s; } else if (K >= cz) { K = cz - 1; s = -cl * s; }
+    MGO_T v = V[I + cx * J + cx * cy * K];
+    return s == (MGO_T)1 ? v : s * v;
+}
+
+/* u += P V.  PC: v = V[parent] (cpu.lua:142-158, cpu-raw.lua:65-85).
+ * LINEAR (build-defined): cell-centred, separable 3/4-1/4 weights, x then y then z. */
+static void FN(prolong_correct)(int dim, int64_t nx, int64_t ny, int64_t nz, int prolong,
+                                double clc, MGO_T* u, const MGO_T* V, int threads)
+{
+    const int64_t cx = nx / 2, cy = ny / 2, cz = dim == 3 ? nz / 2 : 1;
+    const int64_t pl = nx * ny;
+    const MGO_T w0 = (MGO_T)0.75, w1 = (MGO_T)0.25, cl = (MGO_T)clc;
+#pragma omp parallel for num_threads(threads) schedule(static) if (threads > 1 && pl * nz > 65536)
+    for (int64_t k = 0; k < nz; ++k)
+        for (int64_t j = 0; j < ny; ++j)
+            for (int64_t i = 0; i < nx; ++i) {
+                int64_t c = i + nx * j + pl * k;
+                int64_t I = i >> 1, J = j >> 1, K = dim == 3 ? (k >> 1) : 0;
+                MGO_T v;
+                if (prolong == MGO_PROLONG_PC) {
+                    v = V[I + cx * J + cx * cy * K];
+                } else {
+                    int64_t In = (i & 1) ? I + 1 : I - 1;
+                    int64_t Jn = (j & 1) ? J + 1 : J - 1;
+                    if (dim == 2) {
+                        MGO_T a0 = w0 * FN(cval)(V, cx, cy, 1, I, J, 0, cl) + w1 * FN(cval)(V, cx, cy, 1, In, J, 0, cl);
+                        MGO_T a1 = w0 * FN(cval)(V, cx, cy, 1, I, Jn, 0, cl) + w1 * FN(cval)(V, cx, cy, 1, In, Jn, 0, cl);
+                        v = w0 * a0 + w1 * a1;
+                    } else {
+                        int64_t Kn = (k & 1) ? K + 1 : K - 1;
+                        MGO_T a00 = w0 * FN(cval)(V, cx, cy, cz, I, J, K, cl) + w1 * FN(cval)(V, cx, cy, cz, In, J, K, cl);
+                        MGO_T a10 = w0 * FN(cval)(V, cx, cy, cz, I, Jn, K, cl) + w1 * FN(cval)(V, cx, cy, cz, In, Jn, K, cl);
+                        MGO_T a01 = w0 * FN(cval)(V, cx, cy, cz, I, J, Kn, cl) + w1 * FN(cval)(V, cx, cy, cz, In, J, Kn, cl);
+                        MGO_T a11 = w0 * FN(cval)(V, cx, cy, cz, I, Jn, Kn, cl) + w1 * FN(cval)(V, cx, cy, cz, In, Jn, Kn, cl);
+                        MGO_T b0 = w0 * a00 + w1 * a10;
+                        MGO_T b1 = w0 * a01 + w1 * a11;
+                        v = w0 * b0 + w1 * b1;
+                    }
+                }
+                u[c] = u[c] + v;
+            }
+}
+
+/* sum over cells of (psi - psiOld)^2 in double; per-plane partials then in-order total. */
+static double FN(sqdiff)(int64_t n, const MGO_T* a, const MGO_T* b)
+{
+    double s = 0.0;
+    for (int64_t c = 0; c < n; ++c) {
+        double d = (double)a[c] - (double)b[c];
+        s += d * d;
+    }
+    return s;
+}
+
+#undef FN
+#undef MGO_CAT
+#undef MGO_CAT2
