@@ -1,0 +1,125 @@
+/*
+ * mgpoisson.h — C ABI of libmgpoisson.so, the MI355X (gfx950) multigrid Poisson hot path.
+ *
+ * This is the drop-in boundary for the reference's solver classes.  The reference has no
+ * native FFI (it is Lua): its boundary is the Lua class protocol of cpu.lua / cpu-raw.lua /
+ * gpu.lua.  Each entry point below names the reference interface it replaces;
+ * the Lua-side binding (LuaJIT ffi.cdef of this header) is in INTEGRATION.md and
+ * lua-multigrid-poisson_amd/lua/multigrid-poisson/hip.lua, the Python mirror in
+ * lua-multigrid-poisson_amd/mgpoisson/.
+ *
+ * Conventions
+ *  - Every function returning int returns MGP_OK (0) or a negative mgp_status; the message is
+ *    in mgp_last_error(ctx) (or mgp_last_error(NULL) when mgp_create itself failed).  No C++
+ *    exception or longjmp crosses this ABI.
+ *  - A context owns one HIP stream and all device memory; it is not thread-safe.  Calls are
+ *    synchronous at return except where stated.  Host buffers are borrowed for the call.
+ *  - Layout is the reference's: x fastest, index = i + nx*(j + ny*k) (cpu-raw.lua:9, gpu.lua:72),
+ *    0-based, real = float or double (gpu.lua:32).  With world > 1 a rank owns the z-slab
+ *    [z0, z0 + nz_local) of every distributed level (mgp_level_info).
+ */
+#ifndef MGPOISSON_H
+#define MGPOISSON_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MGP_API_VERSION 1
+#define MGP_COMM_ID_BYTES 128 /* == NCCL_UNIQUE_ID_BYTES */
+
+typedef enum mgp_status {
+    MGP_OK = 0,
+    MGP_ERR_ARG = -1,   /* invalid argument / unsupported configuration */
+    MGP_ERR_HIP = -2,   /* HIP runtime error (no device, launch failure, ...) */
+    MGP_ERR_RCCL = -3,  /* RCCL error (communicator init, send/recv, collective) */
+    MGP_ERR_OOM = -4,   /* device allocation failed */
+    MGP_ERR_STATE = -5  /* call not valid in the context's current state */
+} mgp_status;
+
+enum { MGP_JACOBI = 0, MGP_RBGS = 1 };                 /* cpu.lua:56-57 inPlaceIterativeSolver */
+enum { MGP_CYCLE_V = 0, MGP_CYCLE_F = 1 };             /* twoGrid recursion (gamma 1) / F-cycle */
+enum { MGP_PROLONG_PC = 0, MGP_PROLONG_LINEAR = 1 };   /* cpu.lua:142-150 injection / (tri)linear */
+enum { MGP_COARSE_FRESH = 0, MGP_COARSE_WARM = 1 };    /* cpu.lua:138 zeros / cpu-raw.lua:221 Vs */
+enum { MGP_BC_ZERO = 0, MGP_BC_CONSISTENT = 1 };       /* coarse ghost: 0 (ref) / extrapolated */
+enum { MGP_FIELD_U = 0, MGP_FIELD_F = 1 };             /* psi (V on coarse levels) / f (R) */
+enum { MGP_MEM_HOST = 0, MGP_MEM_DEVICE = 1 };         /* where a caller buffer lives */
+
+typedef struct mgp_opts {
+    int32_t struct_size;   /* sizeof(mgp_opts), checked by mgp_create */
+    int32_t dim;           /* 2 or 3 */
+    int64_t n[3];          /* GLOBAL cells per axis, powers of two (n[2] = 1 in 2D) */
+    int32_t real_bytes;    /* 4 = float, 8 = double (gpu.lua:32 "real") */
+    int32_t nu1, nu2;      /* pre/post sweeps (cpu.lua:20 smooth = 7) */
+    int32_t smoother;      /* MGP_JACOBI | MGP_RBGS */
+    int32_t cycle;         /* MGP_CYCLE_V | MGP_CYCLE_F */
+    int32_t prolong;       /* MGP_PROLONG_PC | MGP_PROLONG_LINEAR */
+    int32_t coarse_init;   /* MGP_COARSE_FRESH | MGP_COARSE_WARM */
+    int32_t coarse_bc;     /* MGP_BC_ZERO | MGP_BC_CONSISTENT */
+    int32_t coarse_sweeps; /* sweeps on a coarsest level with more than one cell */
+    int32_t err_mode;      /* 1: psiOld snapshot + RMS update per cycle (cpu.lua:200-203); 0: off */
+    int32_t device;        /* HIP device ordinal; -1 = current device */
+    int32_t rank, world;   /* slab-z domain decomposition over `world` GPUs (3D only) */
+    int64_t gather_cells;  /* a level with <= this many cells is replicated on every rank */
+    uint8_t comm_id[MGP_COMM_ID_BYTES]; /* from mgp_comm_unique_id() on rank 0 (world > 1) */
+} mgp_opts;
+
+typedef struct mgp_ctx mgp_ctx;
+
+int         mgp_version(void);
+/* Defaults = the reference cpu.lua configuration: 2D, double, Jacobi 7+7, V, PC, fresh, zero. */
+void        mgp_opts_default(mgp_opts* o);
+/* RCCL unique id for a world > 1 context (call on rank 0, broadcast the bytes). */
+int         mgp_comm_unique_id(void* out, int64_t nbytes);
+
+/* Replaces MultigridCPU:init{size,...} (cpu.lua:173-194) / MultigridCPURaw:init(size, real)
+ * (cpu-raw.lua:142-174) / MultigridGPU:init (gpu.lua:26-245): allocates the level hierarchy. */
+int         mgp_create(mgp_ctx** out, const mgp_opts* o);
+void        mgp_destroy(mgp_ctx* c);
+const char* mgp_last_error(const mgp_ctx* c);
+
+/* Level hierarchy.  info[0..7] = {nx, ny, nz_global, nz_local, z0, distributed, 0, 0} */
+int         mgp_num_levels(const mgp_ctx* c);
+int         mgp_level_info(const mgp_ctx* c, int level, int64_t info[8]);
+/* The same plan without a device (host logic only): fills up to max_levels rows of 8 int64s. */
+int         mgp_plan(const mgp_opts* o, int64_t* rows, int max_levels);
+
+/* f = -1e6 at 0-based (n/2, n/2[, n/2]), psi = -f (cpu.lua:180-193, cpu-raw.lua:8-20, gpu.lua:41-59). */
+int         mgp_init_point_charge(mgp_ctx* c);
+/* Copy a level's field in/out (this rank's slab on distributed levels; count in elements).
+ * Replaces direct access to mg.psi / mg.f (cpu.lua) and .psi.buffer / .f.buffer (cpu-raw.lua). */
+int         mgp_set_field(mgp_ctx* c, int level, int which, const void* src, int64_t count, int mem);
+int         mgp_get_field(const mgp_ctx* c, int level, int which, void* dst, int64_t count, int mem);
+
+/* One outer iteration = MultigridCPU:step() (cpu.lua:196-206): psiOld = psi; one V/F-cycle from
+ * the finest level with h = 1/n; *err_out = sqrt(sum (psi - psiOld)^2 / N) (NaN if err_mode 0). */
+int         mgp_cycle(mgp_ctx* c, double* err_out);
+/* k outer iterations back to back with one host synchronisation at the end (the loop of
+ * MultigridCPURaw:run, cpu-raw.lua:245, without early exit); errs[k] may be NULL. */
+int         mgp_cycles(mgp_ctx* c, int32_t k, double* errs);
+
+/* MultigridCPURaw:twoGrid(h, u, f, L) (cpu-raw.lua:186; gpu.lua:296): one cycle from the level of
+ * size L with spacing h on caller buffers of L^dim reals (mem = MGP_MEM_HOST | MGP_MEM_DEVICE);
+ * u is updated in place, f is read only.  Single-GPU contexts only. */
+int         mgp_two_grid(mgp_ctx* c, double h, void* u, const void* f, int64_t L, int mem);
+
+/* Level-granular pieces of twoGrid (cpu-raw.lua:198-236), for hybrid hand-off (cpu-gpu.lua:17-52)
+ * and kernel-level tests.  h of level l is 2^l / n[0]. */
+int         mgp_smooth(mgp_ctx* c, int level, int sweeps);          /* inPlaceIterativeSolver x sweeps */
+int         mgp_residual_restrict(mgp_ctx* c, int level);           /* calcResidual + reduceResidual -> f of level+1 */
+int         mgp_prolong_correct(mgp_ctx* c, int level);             /* expandResidual + addTo from level+1 */
+int         mgp_coarse_solve(mgp_ctx* c);                           /* L == 1 branch of twoGrid */
+
+int         mgp_sync(mgp_ctx* c);
+/* Finest-level smoother kernel timing with HIP events on the context's stream.  mgp_timing(c, 1)
+ * resets and enables; mgp_timing_read returns the summed kernel milliseconds, the number of
+ * timed launches and the number of full sweeps they performed (cells * sweeps * 3 * real_bytes
+ * is the algorithmic byte count). */
+int         mgp_timing(mgp_ctx* c, int enable);
+int         mgp_timing_read(mgp_ctx* c, double* ms_total, int64_t* launches, double* sweeps);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MGPOISSON_H */

@@ -1,0 +1,718 @@
+// mgp_api.cpp — the C ABI of libmgpoisson.so (include/mgpoisson.h): level hierarchy, the
+// recursive V/F-cycle on one HIP stream, RCCL halo exchange / coarse agglomeration over xGMI,
+// and the outer iteration with its fp64 update-RMS.
+//
+// Reference behaviour reproduced here (thenumbernine/lua-multigrid-poisson):
+//   twoGrid recursion         cpu.lua:70-165, cpu-raw.lua:186-237, gpu.lua:296-346
+//   fresh / warm coarse guess cpu.lua:138 / cpu-raw.lua:221, gpu.lua:330
+//   step / err / run          cpu.lua:196-206, cpu-raw.lua:239-258, gpu.lua:348-373
+//   hybrid level hand-off     cpu-gpu.lua:17-52 -> replicated coarse levels after an all-gather
+#include "mgp_internal.h"
+
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/mgpoisson.h"
+
+using mgp::Geo;
+
+namespace {
+
+thread_local std::string g_create_error;
+
+struct LevelPlan {
+    int64_t nx, ny, gnz;  // global dims
+    int64_t nz, z0;       // local planes / global offset (nz = gnz, z0 = 0 when replicated)
+    bool dist;            // slab-decomposed
+};
+
+int ilog2(int64_t v)
+{
+    int l = 0;
+    while ((int64_t(1) << l) < v) ++l;
+    return l;
+}
+bool is_pow2(int64_t v) { return v > 0 && (v & (v - 1)) == 0; }
+
+// Host-only hierarchy planner (mgp_plan): coarsen every axis by 2 while all active axes have
+// >= 2 cells (cpu.lua recursion down to width 1).  A level stays slab-distributed while its
+// planes split evenly with >= 2 per rank, it is not the coarsest and it has more than
+// gather_cells cells; from the first replicated level down every rank holds the whole grid.
+int plan_levels(const mgp_opts& o, std::vector<LevelPlan>& out, std::string& err)
+{
+    out.clear();
+    if (o.struct_size != (int32_t)sizeof(mgp_opts)) {
+        err = "mgp_opts.struct_size mismatch (header/library version skew)";
+        return MGP_ERR_ARG;
+    }
+    if (o.dim != 2 && o.dim != 3) { err = "dim must be 2 or 3"; return MGP_ERR_ARG; }
+    int64_t nx = o.n[0], ny = o.n[1], nz = o.dim == 3 ? o.n[2] : 1;
+    if (!is_pow2(nx) || !is_pow2(ny) || !is_pow2(nz)) { err = "n[] must be powers of two"; return MGP_ERR_ARG; }
+    if (nx * ny >= (int64_t(1) << 31)) { err = "nx*ny must be < 2^31"; return MGP_ERR_ARG; }
+    if (o.real_bytes != 4 && o.real_bytes != 8) { err = "real_bytes must be 4 or 8"; return MGP_ERR_ARG; }
+    if (o.smoother != MGP_JACOBI && o.smoother != MGP_RBGS) { err = "unknown smoother"; return MGP_ERR_ARG; }
+    if (o.cycle != MGP_CYCLE_V && o.cycle != MGP_CYCLE_F) { err = "unknown cycle"; return MGP_ERR_ARG; }
+    if (o.prolong != MGP_PROLONG_PC && o.prolong != MGP_PROLONG_LINEAR) { err = "unknown prolong"; return MGP_ERR_ARG; }
+    if (o.coarse_init != MGP_COARSE_FRESH && o.coarse_init != MGP_COARSE_WARM) { err = "unknown coarse_init"; return MGP_ERR_ARG; }
+    if (o.coarse_bc != MGP_BC_ZERO && o.coarse_bc != MGP_BC_CONSISTENT) { err = "unknown coarse_bc"; return MGP_ERR_ARG; }
+    if (o.nu1 < 0 || o.nu2 < 0 || o.coarse_sweeps < 1) { err = "nu1/nu2 >= 0 and coarse_sweeps >= 1 required"; return MGP_ERR_ARG; }
+    if (o.world < 1 || o.rank < 0 || o.rank >= o.world) { err = "need 0 <= rank < world"; return MGP_ERR_ARG; }
+    if (o.world > 1) {
+        if (o.dim != 3) { err = "domain decomposition is 3D slab-z only"; return MGP_ERR_ARG; }
+        if (nz % o.world != 0 || nz / o.world < 2) { err = "n[2] must split into >= 2 planes per rank"; return MGP_ERR_ARG; }
+    }
+    bool dist = o.world > 1;
+    for (;;) {
+        LevelPlan p;
+        p.nx = nx;
+        p.ny = ny;
+        p.gnz = nz;
+        p.dist = dist;
+        p.nz = dist ? nz / o.world : nz;
+        p.z0 = dist ? p.nz * o.rank : 0;
+        out.push_back(p);
+        bool more = nx >= 2 && ny >= 2 && (o.dim == 2 || nz >= 2);
+        if (!more || out.size() >= 40) break;
+        nx /= 2;
+        ny /= 2;
+        if (o.dim == 3) nz /= 2;
+        bool next_more = nx >= 2 && ny >= 2 && (o.dim == 2 || nz >= 2);
+        dist = dist && next_more && nz % o.world == 0 && nz / o.world >= 2 && nx * ny * nz > o.gather_cells;
+    }
+    return MGP_OK;
+}
+
+double coarse_coef(int coarse_bc, int level)
+{
+    if (coarse_bc != MGP_BC_CONSISTENT || level <= 0) return 0.0;
+    double p = std::ldexp(1.0, level);
+    return (p - 1.0) / (p + 1.0);
+}
+
+}  // namespace
+
+struct Level {
+    LevelPlan p;
+    Geo g;
+    int64_t alloc;  // elements per buffer, ghosts included
+    char* u = nullptr;
+    char* f = nullptr;
+    char* t = nullptr;  // Jacobi ping-pong partner
+    bool ghost_ok = true;
+};
+
+struct mgp_ctx {
+    mgp_opts o{};
+    int rb = 8;
+    int G = 0;  // ghost planes per side (1 in 3D, 0 in 2D)
+    std::vector<Level> lev;
+    hipStream_t s = nullptr;
+    int device = 0;
+    ncclComm_t comm = nullptr;
+    char* psi_old = nullptr;
+    double* d_part = nullptr;
+    double* d_errs = nullptr;
+    int errs_cap = 0;
+    std::string err;
+    // finest-smoother timing
+    bool timing = false;
+    std::vector<hipEvent_t> ev;
+    size_t ev_used = 0;
+    double t_ms = 0.0;
+    int64_t t_launch = 0;
+    double t_sweeps = 0.0;
+
+    int fail(int code, const char* fmt, ...)
+    {
+        char buf[1024];
+        va_list ap;
+        va_start(ap, fmt);
+        vsnprintf(buf, sizeof buf, fmt, ap);
+        va_end(ap);
+        err = buf;
+        return code;
+    }
+    char* ui(const Level& L, char* base) const { return base + (size_t)(G * L.g.plane) * rb; }
+    int64_t ncells_global() const { return lev[0].p.nx * lev[0].p.ny * lev[0].p.gnz; }
+    ncclDataType_t nccl_real() const { return rb == 8 ? ncclDouble : ncclFloat; }
+};
+
+#define HIP_TRY(c, expr)                                                                         \
+    do {                                                                                        \
+        hipError_t e_ = (expr);                                                                 \
+        if (e_ != hipSuccess)                                                                   \
+            return (c)->fail(MGP_ERR_HIP, "%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_), \
+                             __FILE__, __LINE__);                                               \
+    } while (0)
+
+#define NCCL_TRY(c, expr)                                                                           \
+    do {                                                                                           \
+        ncclResult_t r_ = (expr);                                                                  \
+        if (r_ != ncclSuccess)                                                                     \
+            return (c)->fail(MGP_ERR_RCCL, "%s failed: %s (%s:%d)", #expr, ncclGetErrorString(r_), \
+                             __FILE__, __LINE__);                                                  \
+    } while (0)
+
+#define TRY(expr)                 \
+    do {                          \
+        int rc_ = (expr);         \
+        if (rc_ != MGP_OK) return rc_; \
+    } while (0)
+
+namespace {
+
+// ---- halo exchange over RCCL (grouped send/recv to the z-neighbours) ----
+
+int exchange(mgp_ctx* c, Level& L)
+{
+    if (!L.p.dist || L.ghost_ok) return MGP_OK;
+    const int64_t pl = L.g.plane;
+    const size_t rb = (size_t)c->rb;
+    char* base = L.u;  // ghost plane -1 at base, interior plane k at base + (k+1)*pl
+    NCCL_TRY(c, ncclGroupStart());
+    if (c->o.rank > 0) {
+        NCCL_TRY(c, ncclSend(base + (size_t)pl * rb, (size_t)pl, c->nccl_real(), c->o.rank - 1, c->comm, c->s));
+        NCCL_TRY(c, ncclRecv(base, (size_t)pl, c->nccl_real(), c->o.rank - 1, c->comm, c->s));
+    }
+    if (c->o.rank < c->o.world - 1) {
+        NCCL_TRY(c, ncclSend(base + (size_t)(pl * L.g.nz) * rb, (size_t)pl, c->nccl_real(), c->o.rank + 1, c->comm, c->s));
+        NCCL_TRY(c, ncclRecv(base + (size_t)(pl * (L.g.nz + 1)) * rb, (size_t)pl, c->nccl_real(), c->o.rank + 1, c->comm, c->s));
+    }
+    NCCL_TRY(c, ncclGroupEnd());
+    L.ghost_ok = true;
+    return MGP_OK;
+}
+
+// ---- finest-level smoother timing ----
+
+int timed_begin(mgp_ctx* c, int l, hipEvent_t* e1)
+{
+    *e1 = nullptr;
+    if (!c->timing || l != 0) return MGP_OK;
+    if (c->ev_used + 2 > c->ev.size()) {
+        // harvest what we have, then reuse the pool
+        HIP_TRY(c, hipStreamSynchronize(c->s));
+        for (size_t e = 0; e + 1 < c->ev_used; e += 2) {
+            float ms = 0.f;
+            HIP_TRY(c, hipEventElapsedTime(&ms, c->ev[e], c->ev[e + 1]));
+            c->t_ms += ms;
+        }
+        c->ev_used = 0;
+    }
+    *e1 = c->ev[c->ev_used];
+    HIP_TRY(c, hipEventRecord(*e1, c->s));
+    return MGP_OK;
+}
+
+int timed_end(mgp_ctx* c, hipEvent_t e1, double sweeps)
+{
+    if (!e1) return MGP_OK;
+    HIP_TRY(c, hipEventRecord(c->ev[c->ev_used + 1], c->s));
+    c->ev_used += 2;
+    c->t_launch += 1;
+    c->t_sweeps += sweeps;
+    return MGP_OK;
+}
+
+// ---- cycle pieces ----
+
+int smooth(mgp_ctx* c, int l, int sweeps, double h)
+{
+    Level& L = c->lev[l];
+    const double cl = coarse_coef(c->o.coarse_bc, l);
+    const bool fine = l == 0;
+    for (int sw = 0; sw < sweeps; ++sw) {
+        if (c->o.smoother == MGP_JACOBI) {
+            TRY(exchange(c, L));
+            hipEvent_t e;
+            TRY(timed_begin(c, l, &e));
+            HIP_TRY(c, mgp::launch_jacobi(c->rb, c->o.dim, fine, c->ui(L, L.u), c->ui(L, L.f), c->ui(L, L.t), L.g, h, cl, c->s));
+            TRY(timed_end(c, e, 1.0));
+            std::swap(L.u, L.t);
+            L.ghost_ok = !L.p.dist;
+        } else {
+            for (int color = 0; color < 2; ++color) {
+                TRY(exchange(c, L));
+                hipEvent_t e;
+                TRY(timed_begin(c, l, &e));
+                HIP_TRY(c, mgp::launch_rb_half(c->rb, c->o.dim, fine, c->ui(L, L.u), c->ui(L, L.f), L.g, color, h, cl, c->s));
+                TRY(timed_end(c, e, 0.5));
+                L.ghost_ok = !L.p.dist;
+            }
+        }
+    }
+    return MGP_OK;
+}
+
+int residual_restrict(mgp_ctx* c, int l, double h)
+{
+    Level& L = c->lev[l];
+    Level& C = c->lev[l + 1];
+    TRY(exchange(c, L));
+    // coarse plane that corresponds to this rank's fine plane 0
+    const int64_t zc = (L.p.dist && !C.p.dist) ? L.p.z0 / 2 : 0;
+    char* R = c->ui(C, C.f) + (size_t)(zc * C.g.plane) * c->rb;
+    HIP_TRY(c, mgp::launch_residual_restrict(c->rb, c->o.dim, c->ui(L, L.u), c->ui(L, L.f), R, L.g, h,
+                                             coarse_coef(c->o.coarse_bc, l), c->s));
+    if (L.p.dist && !C.p.dist) {
+        // agglomerate: every rank gets the whole coarse right-hand side (cf. cpu-gpu.lua:22-32)
+        const size_t count = (size_t)((L.g.nz / 2) * C.g.plane);
+        NCCL_TRY(c, ncclAllGather(R, c->ui(C, C.f), count, c->nccl_real(), c->comm, c->s));
+    }
+    return MGP_OK;
+}
+
+int prolong_correct(mgp_ctx* c, int l)
+{
+    Level& L = c->lev[l];
+    Level& C = c->lev[l + 1];
+    const int linear = c->o.prolong == MGP_PROLONG_LINEAR;
+    Geo gc = C.g;
+    int64_t zc = 0;
+    if (L.p.dist && !C.p.dist) {
+        zc = L.p.z0 / 2;  // read our slice of the replicated coarse grid
+        gc.z0 = zc;
+    } else if (linear && C.p.dist) {
+        TRY(exchange(c, C));
+    }
+    char* V = c->ui(C, C.u) + (size_t)(zc * C.g.plane) * c->rb;
+    HIP_TRY(c, mgp::launch_prolong_correct(c->rb, c->o.dim, linear, c->ui(L, L.u), V, L.g, gc,
+                                           coarse_coef(c->o.coarse_bc, l + 1), c->s));
+    L.ghost_ok = !L.p.dist;
+    return MGP_OK;
+}
+
+int coarse_solve_at(mgp_ctx* c, int l, double h)
+{
+    const Level& L = c->lev[l];
+    const int64_t cells = L.p.nx * L.p.ny * L.p.gnz;
+    return smooth(c, l, cells == 1 ? 1 : c->o.coarse_sweeps, h);
+}
+
+int zero_level(mgp_ctx* c, Level& L)
+{
+    HIP_TRY(c, hipMemsetAsync(L.u, 0, (size_t)L.alloc * c->rb, c->s));
+    L.ghost_ok = true;  // every rank's V is zero, so the ghost planes are current
+    return MGP_OK;
+}
+
+int cycle_rec(mgp_ctx* c, int l, double h, bool fcycle)
+{
+    const int last = (int)c->lev.size() - 1;
+    if (l == last) return coarse_solve_at(c, l, h);
+    TRY(smooth(c, l, c->o.nu1, h));
+    TRY(residual_restrict(c, l, h));
+    if (c->o.coarse_init == MGP_COARSE_FRESH) TRY(zero_level(c, c->lev[l + 1]));
+    if (fcycle) TRY(cycle_rec(c, l + 1, 2 * h, true));
+    TRY(cycle_rec(c, l + 1, 2 * h, false));
+    TRY(prolong_correct(c, l));
+    TRY(smooth(c, l, c->o.nu2, h));
+    return MGP_OK;
+}
+
+int one_cycle(mgp_ctx* c, int slot)
+{
+    Level& L = c->lev[0];
+    const size_t bytes = (size_t)(L.g.plane * L.g.nz) * c->rb;
+    if (c->o.err_mode) HIP_TRY(c, hipMemcpyAsync(c->psi_old, c->ui(L, L.u), bytes, hipMemcpyDeviceToDevice, c->s));
+    const double h = 1.0 / (double)L.p.nx;  // cpu.lua:197-198
+    TRY(cycle_rec(c, 0, h, c->o.cycle == MGP_CYCLE_F));
+    if (c->o.err_mode) {
+        Level& L0 = c->lev[0];
+        HIP_TRY(c, mgp::launch_sqdiff_sum(c->rb, c->ui(L0, L0.u), c->psi_old, L0.g.plane * L0.g.nz, c->d_part,
+                                          c->d_errs + slot, c->s));
+        if (c->o.world > 1)
+            NCCL_TRY(c, ncclAllReduce(c->d_errs + slot, c->d_errs + slot, 1, ncclDouble, ncclSum, c->comm, c->s));
+    }
+    return MGP_OK;
+}
+
+int ensure_errs(mgp_ctx* c, int k)
+{
+    if (k <= c->errs_cap) return MGP_OK;
+    if (c->d_errs) HIP_TRY(c, hipFree(c->d_errs));
+    c->d_errs = nullptr;
+    int cap = std::max(k, 64);
+    HIP_TRY(c, hipMalloc(&c->d_errs, sizeof(double) * cap));
+    c->errs_cap = cap;
+    return MGP_OK;
+}
+
+int check_level(const mgp_ctx* c, int level)
+{
+    return (level >= 0 && level < (int)c->lev.size()) ? MGP_OK : MGP_ERR_ARG;
+}
+
+int sync_and_check(mgp_ctx* c)
+{
+    HIP_TRY(c, hipStreamSynchronize(c->s));
+    if (c->comm) {
+        ncclResult_t ar = ncclSuccess;
+        NCCL_TRY(c, ncclCommGetAsyncError(c->comm, &ar));
+        if (ar != ncclSuccess) return c->fail(MGP_ERR_RCCL, "RCCL async error: %s", ncclGetErrorString(ar));
+    }
+    return MGP_OK;
+}
+
+}  // namespace
+
+// =====================================================================================
+// C ABI
+// =====================================================================================
+
+extern "C" {
+
+int mgp_version(void) { return MGP_API_VERSION; }
+
+void mgp_opts_default(mgp_opts* o)
+{
+    if (!o) return;
+    std::memset(o, 0, sizeof(*o));
+    o->struct_size = (int32_t)sizeof(mgp_opts);
+    o->dim = 2;
+    o->n[0] = o->n[1] = 8;
+    o->n[2] = 1;
+    o->real_bytes = 8;          // gpu.lua:32 picks double when the device has fp64
+    o->nu1 = o->nu2 = 7;        // cpu.lua:20
+    o->smoother = MGP_JACOBI;   // cpu.lua:57
+    o->cycle = MGP_CYCLE_V;
+    o->prolong = MGP_PROLONG_PC;
+    o->coarse_init = MGP_COARSE_FRESH;
+    o->coarse_bc = MGP_BC_ZERO;
+    o->coarse_sweeps = 48;
+    o->err_mode = 1;
+    o->device = -1;
+    o->rank = 0;
+    o->world = 1;
+    o->gather_cells = 32768;
+}
+
+int mgp_comm_unique_id(void* out, int64_t nbytes)
+{
+    if (!out || nbytes < (int64_t)sizeof(ncclUniqueId)) {
+        g_create_error = "mgp_comm_unique_id: buffer too small";
+        return MGP_ERR_ARG;
+    }
+    ncclUniqueId id;
+    ncclResult_t r = ncclGetUniqueId(&id);
+    if (r != ncclSuccess) {
+        g_create_error = std::string("ncclGetUniqueId: ") + ncclGetErrorString(r);
+        return MGP_ERR_RCCL;
+    }
+    std::memcpy(out, &id, sizeof(id));
+    return MGP_OK;
+}
+
+int mgp_plan(const mgp_opts* o, int64_t* rows, int max_levels)
+{
+    if (!o) return MGP_ERR_ARG;
+    std::vector<LevelPlan> plan;
+    int rc = plan_levels(*o, plan, g_create_error);
+    if (rc != MGP_OK) return rc;
+    for (int l = 0; l < (int)plan.size() && l < max_levels && rows; ++l) {
+        int64_t* r = rows + 8 * l;
+        r[0] = plan[l].nx;
+        r[1] = plan[l].ny;
+        r[2] = plan[l].gnz;
+        r[3] = plan[l].nz;
+        r[4] = plan[l].z0;
+        r[5] = plan[l].dist;
+        r[6] = r[7] = 0;
+    }
+    return (int)plan.size();
+}
+
+static void destroy_impl(mgp_ctx* c)
+{
+    if (!c) return;
+    if (c->s) (void)hipStreamSynchronize(c->s);
+    for (auto& L : c->lev) {
+        if (L.u) (void)hipFree(L.u);
+        if (L.f) (void)hipFree(L.f);
+        if (L.t) (void)hipFree(L.t);
+    }
+    if (c->psi_old) (void)hipFree(c->psi_old);
+    if (c->d_part) (void)hipFree(c->d_part);
+    if (c->d_errs) (void)hipFree(c->d_errs);
+    for (auto e : c->ev) (void)hipEventDestroy(e);
+    if (c->comm) (void)ncclCommDestroy(c->comm);
+    if (c->s) (void)hipStreamDestroy(c->s);
+    delete c;
+}
+
+int mgp_create(mgp_ctx** out, const mgp_opts* o)
+{
+    if (!out || !o) {
+        g_create_error = "mgp_create: null argument";
+        return MGP_ERR_ARG;
+    }
+    *out = nullptr;
+    std::vector<LevelPlan> plan;
+    int rc = plan_levels(*o, plan, g_create_error);
+    if (rc != MGP_OK) return rc;
+
+    mgp_ctx* c = new mgp_ctx();
+    c->o = *o;
+    if (c->o.dim == 2) c->o.n[2] = 1;
+    c->rb = o->real_bytes;
+    c->G = o->dim == 3 ? 1 : 0;
+    auto bail = [&](int code) {
+        g_create_error = c->err;
+        destroy_impl(c);
+        return code;
+    };
+    int ndev = 0;
+    hipError_t he = hipGetDeviceCount(&ndev);
+    if (he != hipSuccess || ndev == 0) {
+        c->err = std::string("no HIP device available: ") + hipGetErrorString(he);
+        return bail(MGP_ERR_HIP);
+    }
+    if (o->device >= 0) {
+        if (o->device >= ndev) {
+            c->err = "device ordinal out of range";
+            return bail(MGP_ERR_ARG);
+        }
+        he = hipSetDevice(o->device);
+        if (he != hipSuccess) {
+            c->err = std::string("hipSetDevice: ") + hipGetErrorString(he);
+            return bail(MGP_ERR_HIP);
+        }
+    }
+    (void)hipGetDevice(&c->device);
+    he = hipStreamCreateWithFlags(&c->s, hipStreamNonBlocking);
+    if (he != hipSuccess) {
+        c->err = std::string("hipStreamCreate: ") + hipGetErrorString(he);
+        return bail(MGP_ERR_HIP);
+    }
+    const size_t rb = (size_t)c->rb;
+    for (auto& p : plan) {
+        Level L;
+        L.p = p;
+        L.g.nx = (int)p.nx;
+        L.g.ny = (int)p.ny;
+        L.g.lx = ilog2(p.nx);
+        L.g.ly = ilog2(p.ny);
+        L.g.nz = p.nz;
+        L.g.plane = p.nx * p.ny;
+        L.g.z0 = p.z0;
+        L.g.gnz = p.gnz;
+        L.alloc = L.g.plane * (p.nz + 2 * c->G);
+        c->lev.push_back(L);
+    }
+    for (size_t l = 0; l < c->lev.size(); ++l) {
+        Level& L = c->lev[l];
+        const size_t bytes = (size_t)L.alloc * rb;
+        const bool need_t = c->o.smoother == MGP_JACOBI;
+        if (hipMalloc(&L.u, bytes) != hipSuccess || hipMalloc(&L.f, bytes) != hipSuccess ||
+            (need_t && hipMalloc(&L.t, bytes) != hipSuccess)) {
+            c->err = "hipMalloc failed for level " + std::to_string(l) + " (" + std::to_string(bytes) + " bytes)";
+            return bail(MGP_ERR_OOM);
+        }
+        // zero everything once: physical ghost planes stay 0 for the context's lifetime
+        if (hipMemsetAsync(L.u, 0, bytes, c->s) != hipSuccess || hipMemsetAsync(L.f, 0, bytes, c->s) != hipSuccess ||
+            (need_t && hipMemsetAsync(L.t, 0, bytes, c->s) != hipSuccess)) {
+            c->err = "hipMemset failed";
+            return bail(MGP_ERR_HIP);
+        }
+    }
+    const Level& L0 = c->lev[0];
+    if (c->o.err_mode) {
+        if (hipMalloc(&c->psi_old, (size_t)(L0.g.plane * L0.g.nz) * rb) != hipSuccess) {
+            c->err = "hipMalloc failed for psiOld";
+            return bail(MGP_ERR_OOM);
+        }
+    }
+    if (hipMalloc(&c->d_part, sizeof(double) * mgp::kSumBlocks) != hipSuccess) {
+        c->err = "hipMalloc failed for reduction partials";
+        return bail(MGP_ERR_OOM);
+    }
+    if (ensure_errs(c, 64) != MGP_OK) return bail(MGP_ERR_OOM);
+    if (c->o.world > 1) {
+        ncclUniqueId id;
+        std::memcpy(&id, o->comm_id, sizeof(id));
+        ncclResult_t r = ncclCommInitRank(&c->comm, c->o.world, id, c->o.rank);
+        if (r != ncclSuccess) {
+            c->err = std::string("ncclCommInitRank: ") + ncclGetErrorString(r);
+            c->comm = nullptr;
+            return bail(MGP_ERR_RCCL);
+        }
+    }
+    if (hipStreamSynchronize(c->s) != hipSuccess) {
+        c->err = "stream synchronisation after allocation failed";
+        return bail(MGP_ERR_HIP);
+    }
+    *out = c;
+    return MGP_OK;
+}
+
+void mgp_destroy(mgp_ctx* c) { destroy_impl(c); }
+
+const char* mgp_last_error(const mgp_ctx* c) { return c ? c->err.c_str() : g_create_error.c_str(); }
+
+int mgp_num_levels(const mgp_ctx* c) { return c ? (int)c->lev.size() : MGP_ERR_ARG; }
+
+int mgp_level_info(const mgp_ctx* c, int level, int64_t info[8])
+{
+    if (!c || !info || check_level(c, level) != MGP_OK) return MGP_ERR_ARG;
+    const LevelPlan& p = c->lev[level].p;
+    info[0] = p.nx;
+    info[1] = p.ny;
+    info[2] = p.gnz;
+    info[3] = p.nz;
+    info[4] = p.z0;
+    info[5] = p.dist;
+    info[6] = info[7] = 0;
+    return MGP_OK;
+}
+
+int mgp_init_point_charge(mgp_ctx* c)
+{
+    if (!c) return MGP_ERR_ARG;
+    Level& L = c->lev[0];
+    const int64_t cz = c->o.dim == 3 ? L.p.gnz / 2 : 0;
+    HIP_TRY(c, mgp::launch_init_point_charge(c->rb, c->o.dim, c->ui(L, L.u), c->ui(L, L.f), L.g, L.p.nx / 2,
+                                             L.p.ny / 2, cz, c->s));
+    L.ghost_ok = !L.p.dist;
+    return sync_and_check(c);
+}
+
+int mgp_set_field(mgp_ctx* c, int level, int which, const void* src, int64_t count, int mem)
+{
+    if (!c || !src || check_level(c, level) != MGP_OK || (which != MGP_FIELD_U && which != MGP_FIELD_F))
+        return c ? c->fail(MGP_ERR_ARG, "mgp_set_field: bad argument") : MGP_ERR_ARG;
+    Level& L = c->lev[level];
+    if (count != L.g.plane * L.g.nz) return c->fail(MGP_ERR_ARG, "mgp_set_field: count %lld != %lld", (long long)count, (long long)(L.g.plane * L.g.nz));
+    char* dst = c->ui(L, which == MGP_FIELD_U ? L.u : L.f);
+    HIP_TRY(c, hipMemcpyAsync(dst, src, (size_t)count * c->rb, mem == MGP_MEM_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, c->s));
+    if (which == MGP_FIELD_U) L.ghost_ok = !L.p.dist;
+    return sync_and_check(c);
+}
+
+int mgp_get_field(const mgp_ctx* cc, int level, int which, void* dst, int64_t count, int mem)
+{
+    mgp_ctx* c = const_cast<mgp_ctx*>(cc);
+    if (!c || !dst || check_level(c, level) != MGP_OK || (which != MGP_FIELD_U && which != MGP_FIELD_F))
+        return c ? c->fail(MGP_ERR_ARG, "mgp_get_field: bad argument") : MGP_ERR_ARG;
+    Level& L = c->lev[level];
+    if (count != L.g.plane * L.g.nz) return c->fail(MGP_ERR_ARG, "mgp_get_field: count %lld != %lld", (long long)count, (long long)(L.g.plane * L.g.nz));
+    const char* srcp = c->ui(L, which == MGP_FIELD_U ? L.u : L.f);
+    HIP_TRY(c, hipMemcpyAsync(dst, srcp, (size_t)count * c->rb, mem == MGP_MEM_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, c->s));
+    return sync_and_check(c);
+}
+
+int mgp_cycles(mgp_ctx* c, int32_t k, double* errs)
+{
+    if (!c || k < 0) return MGP_ERR_ARG;
+    TRY(ensure_errs(c, k));
+    for (int i = 0; i < k; ++i) TRY(one_cycle(c, i));
+    TRY(sync_and_check(c));
+    if (errs) {
+        if (!c->o.err_mode) {
+            for (int i = 0; i < k; ++i) errs[i] = NAN;
+        } else {
+            std::vector<double> sums((size_t)k);
+            HIP_TRY(c, hipMemcpy(sums.data(), c->d_errs, sizeof(double) * k, hipMemcpyDeviceToHost));
+            const double n = (double)c->ncells_global();
+            for (int i = 0; i < k; ++i) errs[i] = std::sqrt(sums[i] / n);  // cpu.lua:203
+        }
+    }
+    return MGP_OK;
+}
+
+int mgp_cycle(mgp_ctx* c, double* err_out)
+{
+    double e = NAN;
+    int rc = mgp_cycles(c, 1, &e);
+    if (err_out) *err_out = e;
+    return rc;
+}
+
+int mgp_two_grid(mgp_ctx* c, double h, void* u, const void* f, int64_t L, int mem)
+{
+    if (!c || !u || !f) return MGP_ERR_ARG;
+    if (c->o.world > 1) return c->fail(MGP_ERR_STATE, "mgp_two_grid: single-GPU contexts only");
+    for (int l = 0; l < (int)c->lev.size(); ++l) {
+        Level& Lv = c->lev[l];
+        if (Lv.p.nx != L) continue;
+        const int64_t n = Lv.g.plane * Lv.g.nz;
+        TRY(mgp_set_field(c, l, MGP_FIELD_U, u, n, mem));
+        TRY(mgp_set_field(c, l, MGP_FIELD_F, f, n, mem));
+        TRY(cycle_rec(c, l, h, c->o.cycle == MGP_CYCLE_F));
+        return mgp_get_field(c, l, MGP_FIELD_U, u, n, mem);
+    }
+    return c->fail(MGP_ERR_ARG, "mgp_two_grid: no level of size %lld", (long long)L);
+}
+
+static double level_h(const mgp_ctx* c, int level) { return std::ldexp(1.0 / (double)c->lev[0].p.nx, level); }
+
+int mgp_smooth(mgp_ctx* c, int level, int sweeps)
+{
+    if (!c || check_level(c, level) != MGP_OK || sweeps < 0) return MGP_ERR_ARG;
+    TRY(smooth(c, level, sweeps, level_h(c, level)));
+    return sync_and_check(c);
+}
+
+int mgp_residual_restrict(mgp_ctx* c, int level)
+{
+    if (!c || level < 0 || level + 1 >= (int)c->lev.size()) return MGP_ERR_ARG;
+    TRY(residual_restrict(c, level, level_h(c, level)));
+    return sync_and_check(c);
+}
+
+int mgp_prolong_correct(mgp_ctx* c, int level)
+{
+    if (!c || level < 0 || level + 1 >= (int)c->lev.size()) return MGP_ERR_ARG;
+    TRY(prolong_correct(c, level));
+    return sync_and_check(c);
+}
+
+int mgp_coarse_solve(mgp_ctx* c)
+{
+    if (!c) return MGP_ERR_ARG;
+    const int l = (int)c->lev.size() - 1;
+    TRY(coarse_solve_at(c, l, level_h(c, l)));
+    return sync_and_check(c);
+}
+
+int mgp_sync(mgp_ctx* c) { return c ? sync_and_check(c) : MGP_ERR_ARG; }
+
+int mgp_timing(mgp_ctx* c, int enable)
+{
+    if (!c) return MGP_ERR_ARG;
+    TRY(sync_and_check(c));
+    if (enable && c->ev.empty()) {
+        c->ev.resize(4096);
+        for (auto& e : c->ev) HIP_TRY(c, hipEventCreate(&e));
+    }
+    c->timing = enable != 0;
+    c->ev_used = 0;
+    c->t_ms = 0.0;
+    c->t_launch = 0;
+    c->t_sweeps = 0.0;
+    return MGP_OK;
+}
+
+int mgp_timing_read(mgp_ctx* c, double* ms_total, int64_t* launches, double* sweeps)
+{
+    if (!c) return MGP_ERR_ARG;
+    TRY(sync_and_check(c));
+    for (size_t e = 0; e + 1 < c->ev_used; e += 2) {
+        float ms = 0.f;
+        HIP_TRY(c, hipEventElapsedTime(&ms, c->ev[e], c->ev[e + 1]));
+        c->t_ms += ms;
+    }
+    c->ev_used = 0;
+    if (ms_total) *ms_total = c->t_ms;
+    if (launches) *launches = c->t_launch;
+    if (sweeps) *sweeps = c->t_sweeps;
+    return MGP_OK;
+}
+
+}  // extern "C"

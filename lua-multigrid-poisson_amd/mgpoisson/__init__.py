@@ -1,0 +1,10 @@
+"""mgpoisson — MI355X-native multigrid Poisson solver (host layer over libmgpoisson.so).
+
+Importing this package loads the HIP library and fails loudly if it is missing.
+"""
+from ._lib import MGPError, comm_unique_id, default_opts, plan  # noqa: F401
+from .context import Context, make_opts  # noqa: F401
+from .solver import MultigridHIP, MultigridHIPRaw  # noqa: F401
+
+__all__ = ["Context", "MGPError", "MultigridHIP", "MultigridHIPRaw", "comm_unique_id", "default_opts",
+           "make_opts", "plan"]

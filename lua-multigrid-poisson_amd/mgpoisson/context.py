@@ -1,0 +1,166 @@
+"""Thin object wrapper of one ``mgp_ctx`` (include/mgpoisson.h).
+
+Host buffers are numpy arrays (C-contiguous, x fastest: shape (nz, ny, nx) or (ny, nx));
+device buffers are passed as raw pointers (e.g. ``torch_tensor.data_ptr()``) with
+``mem=MEM_DEVICE``.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from . import _lib as L
+
+SMOOTHERS = {"jacobi": L.JACOBI, "rbgs": L.RBGS}
+CYCLES = {"V": L.CYCLE_V, "F": L.CYCLE_F}
+PROLONGS = {"pc": L.PROLONG_PC, "linear": L.PROLONG_LINEAR}
+COARSE_INITS = {"fresh": L.COARSE_FRESH, "warm": L.COARSE_WARM}
+COARSE_BCS = {"zero": L.BC_ZERO, "consistent": L.BC_CONSISTENT}
+REALS = {"double": 8, "float": 4}
+
+
+def make_opts(dim=2, n=(8, 8, 1), real="double", nu1=7, nu2=7, smoother="jacobi", cycle="V",
+              prolong="pc", coarse_init="fresh", coarse_bc="zero", coarse_sweeps=48, err_mode=1,
+              device=-1, rank=0, world=1, gather_cells=32768, comm_id: bytes | None = None) -> L.MGPOpts:
+    """Build mgp_opts from keyword names (defaults = the reference cpu.lua configuration)."""
+    o = L.default_opts()
+    o.dim = dim
+    nn = tuple(n) + (1,) * (3 - len(n))
+    o.n[0], o.n[1], o.n[2] = nn[0], nn[1], (nn[2] if dim == 3 else 1)
+    o.real_bytes = REALS[real] if isinstance(real, str) else int(real)
+    o.nu1, o.nu2 = nu1, nu2
+    o.smoother = SMOOTHERS[smoother] if isinstance(smoother, str) else smoother
+    o.cycle = CYCLES[cycle] if isinstance(cycle, str) else cycle
+    o.prolong = PROLONGS[prolong] if isinstance(prolong, str) else prolong
+    o.coarse_init = COARSE_INITS[coarse_init] if isinstance(coarse_init, str) else coarse_init
+    o.coarse_bc = COARSE_BCS[coarse_bc] if isinstance(coarse_bc, str) else coarse_bc
+    o.coarse_sweeps = coarse_sweeps
+    o.err_mode = err_mode
+    o.device = device
+    o.rank, o.world = rank, world
+    o.gather_cells = gather_cells
+    if comm_id is not None:
+        ctypes.memmove(o.comm_id, comm_id, L.COMM_ID_BYTES)
+    return o
+
+
+class Context:
+    """Owns one mgp_ctx: the level hierarchy, its device buffers and stream."""
+
+    def __init__(self, opts: L.MGPOpts):
+        self.opts = opts
+        self.dtype = np.dtype(np.float64 if opts.real_bytes == 8 else np.float32)
+        h = ctypes.c_void_p()
+        L.check(L.lib.mgp_create(ctypes.byref(h), ctypes.byref(opts)))
+        self._h = h
+        self.levels = []
+        info = (ctypes.c_int64 * 8)()
+        for l in range(L.lib.mgp_num_levels(self._h)):
+            L.check(L.lib.mgp_level_info(self._h, l, info), self._h)
+            self.levels.append(dict(nx=info[0], ny=info[1], nz_global=info[2], nz_local=info[3],
+                                    z0=info[4], distributed=bool(info[5])))
+
+    # -- lifecycle --
+    def close(self):
+        if getattr(self, "_h", None):
+            L.lib.mgp_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def _chk(self, rc):
+        return L.check(rc, self._h)
+
+    # -- shapes --
+    def shape(self, level=0):
+        lv = self.levels[level]
+        if self.opts.dim == 3:
+            return (lv["nz_local"], lv["ny"], lv["nx"])
+        return (lv["ny"], lv["nx"])
+
+    def count(self, level=0):
+        return int(np.prod(self.shape(level)))
+
+    # -- data --
+    def init_point_charge(self):
+        self._chk(L.lib.mgp_init_point_charge(self._h))
+
+    def set_field(self, which, arr, level=0):
+        a = np.ascontiguousarray(arr, dtype=self.dtype)
+        if a.size != self.count(level):
+            raise ValueError(f"expected {self.count(level)} elements, got {a.size}")
+        self._chk(L.lib.mgp_set_field(self._h, level, which, a.ctypes.data, a.size, L.MEM_HOST))
+
+    def get_field(self, which, level=0):
+        out = np.empty(self.shape(level), dtype=self.dtype)
+        self._chk(L.lib.mgp_get_field(self._h, level, which, out.ctypes.data, out.size, L.MEM_HOST))
+        return out
+
+    def set_psi(self, arr, level=0):
+        self.set_field(L.FIELD_U, arr, level)
+
+    def set_f(self, arr, level=0):
+        self.set_field(L.FIELD_F, arr, level)
+
+    def get_psi(self, level=0):
+        return self.get_field(L.FIELD_U, level)
+
+    def get_f(self, level=0):
+        return self.get_field(L.FIELD_F, level)
+
+    # -- cycles --
+    def cycle(self) -> float:
+        e = ctypes.c_double()
+        self._chk(L.lib.mgp_cycle(self._h, ctypes.byref(e)))
+        return e.value
+
+    def cycles(self, k: int) -> np.ndarray:
+        errs = np.zeros(k, dtype=np.float64)
+        self._chk(L.lib.mgp_cycles(self._h, k, errs.ctypes.data_as(ctypes.POINTER(ctypes.c_double))))
+        return errs
+
+    def two_grid(self, h: float, u: np.ndarray, f: np.ndarray, size: int):
+        """cpu-raw.lua:186 twoGrid(h, u, f, L) on host arrays; u updated in place."""
+        if not (u.flags.c_contiguous and u.dtype == self.dtype):
+            raise ValueError("u must be a C-contiguous array of the context's real type")
+        fc = np.ascontiguousarray(f, dtype=self.dtype)
+        self._chk(L.lib.mgp_two_grid(self._h, float(h), u.ctypes.data, fc.ctypes.data, int(size), L.MEM_HOST))
+
+    def two_grid_ptr(self, h: float, u_ptr: int, f_ptr: int, size: int, mem=L.MEM_DEVICE):
+        self._chk(L.lib.mgp_two_grid(self._h, float(h), u_ptr, f_ptr, int(size), mem))
+
+    # -- level-granular pieces --
+    def smooth(self, level, sweeps):
+        self._chk(L.lib.mgp_smooth(self._h, level, sweeps))
+
+    def residual_restrict(self, level):
+        self._chk(L.lib.mgp_residual_restrict(self._h, level))
+
+    def prolong_correct(self, level):
+        self._chk(L.lib.mgp_prolong_correct(self._h, level))
+
+    def coarse_solve(self):
+        self._chk(L.lib.mgp_coarse_solve(self._h))
+
+    def sync(self):
+        self._chk(L.lib.mgp_sync(self._h))
+
+    # -- timing --
+    def timing(self, enable=True):
+        self._chk(L.lib.mgp_timing(self._h, 1 if enable else 0))
+
+    def timing_read(self):
+        ms, n, sw = ctypes.c_double(), ctypes.c_int64(), ctypes.c_double()
+        self._chk(L.lib.mgp_timing_read(self._h, ctypes.byref(ms), ctypes.byref(n), ctypes.byref(sw)))
+        return ms.value, n.value, sw.value

@@ -1,0 +1,171 @@
+"""Host-side mirror of the reference's two solver-call protocols, over libmgpoisson.so.
+
+The reference's host language is Lua (no Lua runtime exists in this image), so the drop-in
+host layer is written in Python with the same names, argument meanings and error behaviour;
+the LuaJIT-FFI module a Lua user would load is lua/multigrid-poisson/hip.lua.
+
+* :class:`MultigridHIP` — the ``cpu.lua`` table protocol:
+  ``MultigridCPU{size=n, maxiter=?, epsilon=?, errorCallback=?, debug=?}`` then
+  ``:solve()`` / ``:step()`` / ``:twoGrid(h, u, f)`` (cpu.lua:70, 173-216).
+* :class:`MultigridHIPRaw` — the ``cpu-raw.lua`` / ``gpu.lua`` positional protocol:
+  ``MultigridCPURaw(size, real)`` then ``:run()`` (2 outer iterations) and
+  ``:twoGrid(h, uPtr, fPtr, L)`` (cpu-raw.lua:142, 186, 239-258; gpu.lua:26, 296, 348).
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+
+from . import _lib as L
+from .context import Context, make_opts
+
+
+class MultigridHIP:
+    """Drop-in for ``MultigridCPU`` (cpu.lua:15-218), solving on the GPU.
+
+    ``MultigridHIP({'size': n, 'maxiter': ..., 'epsilon': ..., 'errorCallback': fn,
+    'debug': ...})`` or the same as keyword arguments.  A missing (None) field falls back to
+    the class default exactly as the Lua ``self.maxiter = args.maxiter`` does (cpu.lua:174-177
+    with the class fields of cpu.lua:18-22).  Build options beyond the reference's (``dim``,
+    ``real``, ``smoother``, ``cycle``, ``prolong``, ``coarse_init``, ``coarse_bc``) default to
+    the reference configuration: 2D, double, Jacobi 7+7, V-cycle, injection, fresh zero guess.
+    """
+
+    debug = False
+    smooth = 7  # cpu.lua:20
+    epsilon = 1e-10  # cpu.lua:21
+    maxiter = 1000  # cpu.lua:22
+
+    def __init__(self, args=None, **kw):
+        a = dict(args or {})
+        a.update(kw)
+        if "size" not in a:
+            raise TypeError("MultigridHIP: 'size' is required (cpu.lua:178)")
+        n = int(a["size"])
+        for k in ("maxiter", "epsilon"):
+            if a.get(k) is not None:
+                setattr(self, k, a[k])
+        self.errorCallback = a.get("errorCallback")
+        if a.get("debug") is not None:
+            self.debug = a["debug"]
+        if a.get("smooth") is not None:
+            self.smooth = int(a["smooth"])
+        self.dim = int(a.get("dim", 2))
+        self.size = (n,) * self.dim  # matrix{size, size} (cpu.lua:178)
+        self._build = dict(dim=self.dim, real=a.get("real", "double"), smoother=a.get("smoother", "jacobi"),
+                           cycle=a.get("cycle", "V"), prolong=a.get("prolong", "pc"),
+                           coarse_init=a.get("coarse_init", "fresh"), coarse_bc=a.get("coarse_bc", "zero"),
+                           device=a.get("device", -1))
+        self._ctx = None
+        self._ctx_smooth = None
+        self._ensure_ctx()
+        self._ctx.init_point_charge()  # f = point charge, psi = -f (cpu.lua:180-193)
+
+    # The reference reads self.smooth inside every twoGrid call (cpu.lua:96, 161); the
+    # sweep counts are baked into the device context, so a change rebuilds it, keeping psi/f.
+    def _ensure_ctx(self):
+        if self._ctx is not None and self._ctx_smooth == self.smooth:
+            return
+        psi = f = None
+        if self._ctx is not None:
+            psi, f = self._ctx.get_psi(), self._ctx.get_f()
+            self._ctx.close()
+        n = self.size[0]
+        opts = make_opts(n=(n, n, n if self.dim == 3 else 1), nu1=self.smooth, nu2=self.smooth, **self._build)
+        self._ctx = Context(opts)
+        self._ctx_smooth = self.smooth
+        if psi is not None:
+            self._ctx.set_psi(psi)
+            self._ctx.set_f(f)
+
+    @property
+    def psi(self) -> np.ndarray:
+        """Current solution as an (n, n[, n]) host array (downloaded from HBM)."""
+        return self._ctx.get_psi()
+
+    @psi.setter
+    def psi(self, value):
+        self._ctx.set_psi(value)
+
+    @property
+    def f(self) -> np.ndarray:
+        return self._ctx.get_f()
+
+    @f.setter
+    def f(self, value):
+        self._ctx.set_f(value)
+
+    def step(self) -> float:
+        """cpu.lua:196-206: psiOld = psi; twoGrid(1/n, psi, f); return RMS(psi - psiOld)."""
+        self._ensure_ctx()
+        err = self._ctx.cycle()
+        if self.debug:
+            print("err", err)
+        return err
+
+    def solve(self):
+        """cpu.lua:208-216, including its break rules."""
+        if self.debug:
+            print("#iter", "err")
+        for it in range(1, int(self.maxiter) + 1):
+            err = self.step()
+            if self.errorCallback and self.errorCallback(it, err):
+                break
+            if err < self.epsilon or not math.isfinite(err):
+                break
+
+    def twoGrid(self, h, u, f):
+        """cpu.lua:70 twoGrid(h, u, f) on an (L, L[, L]) host array u (updated in place)."""
+        self._ensure_ctx()
+        self._ctx.two_grid(h, u, f, u.shape[-1])
+
+
+class MultigridHIPRaw:
+    """Drop-in for ``MultigridCPURaw`` / ``MultigridGPU`` (cpu-raw.lua:118-260, gpu.lua:18-375).
+
+    ``MultigridHIPRaw(size, real='double')``; ``run()`` does the reference's two hard-coded
+    outer iterations (cpu-raw.lua:245) printing ``#iter err`` lines; ``twoGrid(h, u, f, L)``
+    takes host numpy arrays or integer device pointers (``mem=MEM_DEVICE``).
+    """
+
+    debugging = False
+    smooth = 7  # cpu-raw.lua:123
+    accuracy = 1e-10  # cpu-raw.lua:124
+
+    def __init__(self, size, real="double", cpuDepth=None, **build):
+        self.real = real or "double"  # cpu-raw.lua:143
+        self.size = int(size)
+        self.cpuDepth = cpuDepth
+        dim = int(build.pop("dim", 2))
+        n = self.size
+        opts = make_opts(dim=dim, n=(n, n, n if dim == 3 else 1), real=self.real, nu1=self.smooth,
+                         nu2=self.smooth, coarse_init=build.pop("coarse_init", "warm"), **build)
+        self._ctx = Context(opts)
+        self._ctx.init_point_charge()  # call2D(initCells) (cpu-raw.lua:173)
+
+    @property
+    def psi(self):
+        return self._ctx.get_psi()
+
+    @property
+    def f(self):
+        return self._ctx.get_f()
+
+    def twoGrid(self, h, u, f, L_, mem=None):
+        if isinstance(u, np.ndarray):
+            self._ctx.two_grid(h, u, f, L_)
+        else:
+            self._ctx.two_grid_ptr(h, int(u), int(f), L_, L.MEM_DEVICE if mem is None else mem)
+
+    def run(self, iters: int = 2):
+        """cpu-raw.lua:239-258 / gpu.lua:348-373 (2 outer iterations, printed)."""
+        print("#iter", "err")
+        errs = []
+        for it in range(1, iters + 1):
+            err = self._ctx.cycle()
+            errs.append(err)
+            print(it, err)
+            if err < self.accuracy or not math.isfinite(err):
+                break
+        return errs

@@ -1,0 +1,13 @@
+"""Shared pytest setup: markers and import paths (repo root, oracle/, the package dir)."""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for p in (ROOT, os.path.join(ROOT, "oracle"), os.path.join(ROOT, "lua-multigrid-poisson_amd")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs a real MI355X (runs through libmgpoisson.so)")
+    config.addinivalue_line("markers", "slow: larger sizes")
