@@ -15,6 +15,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -104,14 +105,16 @@ struct Level {
     int64_t alloc;  // elements per buffer, ghosts included
     char* u = nullptr;
     char* f = nullptr;
-    char* t = nullptr;  // Jacobi ping-pong partner
-    bool ghost_ok = true;
+    char* t = nullptr;  // ping-pong partner of u (Jacobi, fused red/black sweeps)
+    char* w = nullptr;  // level 0 only: third buffer that keeps the cycle-start psi (fused err)
+    bool ghost_ok = true;   // u's ghost planes hold the neighbours' current planes
+    bool fghost_ok = true;  // f's ghost planes likewise
 };
 
 struct mgp_ctx {
     mgp_opts o{};
     int rb = 8;
-    int G = 0;  // ghost planes per side (1 in 3D, 0 in 2D)
+    int G = 0;  // ghost planes per side (kGhost3D in 3D, 0 in 2D)
     std::vector<Level> lev;
     hipStream_t s = nullptr;
     int device = 0;
@@ -120,6 +123,17 @@ struct mgp_ctx {
     double* d_part = nullptr;
     double* d_errs = nullptr;
     int errs_cap = 0;
+    // fused sweep kernel tuning (environment overrides MGP_KC, MGP_TY, MGP_NH)
+    int kc = 32;      // z-planes per workgroup chunk
+    int ty = 16;      // tile rows
+    int nh_max = 2;   // half-sweeps per launch (4 = two sweeps per pass)
+    // fused err (3D red/black on the finest level): the cycle-start psi stays untouched in one of
+    // three rotating buffers and the last post-sweep accumulates (psi - psiOld)^2 itself
+    bool err_fuse = false;
+    bool err_done = false;
+    char* err_old = nullptr;  // base pointer of the buffer holding psiOld during this cycle
+    int err_slot = 0;
+    int64_t part_cap = 0;
     std::string err;
     // finest-smoother timing
     bool timing = false;
@@ -170,23 +184,43 @@ namespace {
 
 // ---- halo exchange over RCCL (grouped send/recv to the z-neighbours) ----
 
-int exchange(mgp_ctx* c, Level& L)
+// Exchange `depth` boundary planes of `buf` with both z-neighbours: my first `depth` interior
+// planes go to rank-1's upper ghosts, my last `depth` to rank+1's lower ghosts.  Contiguous
+// planes, so each direction is one ncclSend/ncclRecv pair (one xGMI link per neighbour).
+int exchange_buf(mgp_ctx* c, Level& L, char* buf, int depth)
 {
-    if (!L.p.dist || L.ghost_ok) return MGP_OK;
     const int64_t pl = L.g.plane;
     const size_t rb = (size_t)c->rb;
-    char* base = L.u;  // ghost plane -1 at base, interior plane k at base + (k+1)*pl
+    const int G = c->G;
+    const size_t cnt = (size_t)(pl * depth);
+    // plane k (interior index, may be negative for ghosts) lives at buf + (k + G) * pl
+    auto at = [&](int64_t k) { return buf + (size_t)((k + G) * pl) * rb; };
     NCCL_TRY(c, ncclGroupStart());
     if (c->o.rank > 0) {
-        NCCL_TRY(c, ncclSend(base + (size_t)pl * rb, (size_t)pl, c->nccl_real(), c->o.rank - 1, c->comm, c->s));
-        NCCL_TRY(c, ncclRecv(base, (size_t)pl, c->nccl_real(), c->o.rank - 1, c->comm, c->s));
+        NCCL_TRY(c, ncclSend(at(0), cnt, c->nccl_real(), c->o.rank - 1, c->comm, c->s));
+        NCCL_TRY(c, ncclRecv(at(-depth), cnt, c->nccl_real(), c->o.rank - 1, c->comm, c->s));
     }
     if (c->o.rank < c->o.world - 1) {
-        NCCL_TRY(c, ncclSend(base + (size_t)(pl * L.g.nz) * rb, (size_t)pl, c->nccl_real(), c->o.rank + 1, c->comm, c->s));
-        NCCL_TRY(c, ncclRecv(base + (size_t)(pl * (L.g.nz + 1)) * rb, (size_t)pl, c->nccl_real(), c->o.rank + 1, c->comm, c->s));
+        NCCL_TRY(c, ncclSend(at(L.g.nz - depth), cnt, c->nccl_real(), c->o.rank + 1, c->comm, c->s));
+        NCCL_TRY(c, ncclRecv(at(L.g.nz), cnt, c->nccl_real(), c->o.rank + 1, c->comm, c->s));
     }
     NCCL_TRY(c, ncclGroupEnd());
+    return MGP_OK;
+}
+
+int exchange(mgp_ctx* c, Level& L, int depth = 1)
+{
+    if (!L.p.dist || L.ghost_ok) return MGP_OK;
+    TRY(exchange_buf(c, L, L.u, depth));
     L.ghost_ok = true;
+    return MGP_OK;
+}
+
+int exchange_f(mgp_ctx* c, Level& L, int depth)
+{
+    if (!L.p.dist || L.fghost_ok) return MGP_OK;
+    TRY(exchange_buf(c, L, L.f, depth));
+    L.fghost_ok = true;
     return MGP_OK;
 }
 
@@ -223,7 +257,27 @@ int timed_end(mgp_ctx* c, hipEvent_t e1, double sweeps)
 
 // ---- cycle pieces ----
 
-int smooth(mgp_ctx* c, int l, int sweeps, double h)
+bool fused_ok(const mgp_ctx* c, const Level& L)
+{
+    return c->o.smoother == MGP_RBGS && c->o.dim == 3 && mgp::rbgs_fused3d_supported(c->rb, 2, c->ty, L.g) &&
+           L.g.nz >= 4;
+}
+
+// After an out-of-place launch read u and wrote t: the written buffer becomes u.  On level 0
+// with fused err the buffer holding psiOld is parked in w and never written during the cycle.
+void advance(mgp_ctx* c, Level& L)
+{
+    char* prev = L.u;
+    L.u = L.t;
+    if (L.w && prev == c->err_old) {
+        L.t = L.w;
+        L.w = prev;
+    } else {
+        L.t = prev;
+    }
+}
+
+int smooth(mgp_ctx* c, int l, int sweeps, double h, bool want_err = false)
 {
     Level& L = c->lev[l];
     const double cl = coarse_coef(c->o.coarse_bc, l);
@@ -237,6 +291,33 @@ int smooth(mgp_ctx* c, int l, int sweeps, double h)
             TRY(timed_end(c, e, 1.0));
             std::swap(L.u, L.t);
             L.ghost_ok = !L.p.dist;
+        } else if (fused_ok(c, L)) {
+            // fused out-of-place sweeps: nh_max/2 per launch, a single one for an odd remainder
+            const int nh = (sweeps - sw >= 2 && c->nh_max >= 4) ? 4 : 2;
+            const bool last = sw + nh / 2 >= sweeps;
+            const bool err_here = want_err && last;
+            const char* old = err_here ? c->ui(L, c->err_old) : nullptr;
+            if (L.p.dist) {
+                // a stale ghost plane must be re-sent at full depth
+                if (!L.ghost_ok) {
+                    TRY(exchange_buf(c, L, L.u, nh));
+                    L.ghost_ok = true;
+                }
+                TRY(exchange_f(c, L, c->G));
+            }
+            hipEvent_t e;
+            TRY(timed_begin(c, l, &e));
+            HIP_TRY(c, mgp::launch_rbgs_fused3d(c->rb, fine, nh, c->ty, c->ui(L, L.u), c->ui(L, L.f), c->ui(L, L.t),
+                                                old, c->d_part, L.g, c->kc, h, cl, c->s));
+            TRY(timed_end(c, e, nh / 2));
+            if (err_here) {
+                const int nb = mgp::fused3d_blocks(L.g, c->ty, c->kc);
+                HIP_TRY(c, mgp::launch_sum_partials(c->d_part, nb, c->d_errs + c->err_slot, c->s));
+                c->err_done = true;
+            }
+            advance(c, L);
+            L.ghost_ok = !L.p.dist;
+            sw += nh / 2 - 1;
         } else {
             for (int color = 0; color < 2; ++color) {
                 TRY(exchange(c, L));
@@ -259,13 +340,18 @@ int residual_restrict(mgp_ctx* c, int l, double h)
     // coarse plane that corresponds to this rank's fine plane 0
     const int64_t zc = (L.p.dist && !C.p.dist) ? L.p.z0 / 2 : 0;
     char* R = c->ui(C, C.f) + (size_t)(zc * C.g.plane) * c->rb;
-    HIP_TRY(c, mgp::launch_residual_restrict(c->rb, c->o.dim, c->ui(L, L.u), c->ui(L, L.f), R, L.g, h,
-                                             coarse_coef(c->o.coarse_bc, l), c->s));
+    if (c->o.dim == 3 && mgp::residual_restrict3d_supported(L.g))
+        HIP_TRY(c, mgp::launch_residual_restrict3d(c->rb, c->ui(L, L.u), c->ui(L, L.f), R, L.g, h,
+                                                   coarse_coef(c->o.coarse_bc, l), c->s));
+    else
+        HIP_TRY(c, mgp::launch_residual_restrict(c->rb, c->o.dim, c->ui(L, L.u), c->ui(L, L.f), R, L.g, h,
+                                                 coarse_coef(c->o.coarse_bc, l), c->s));
     if (L.p.dist && !C.p.dist) {
         // agglomerate: every rank gets the whole coarse right-hand side (cf. cpu-gpu.lua:22-32)
         const size_t count = (size_t)((L.g.nz / 2) * C.g.plane);
         NCCL_TRY(c, ncclAllGather(R, c->ui(C, C.f), count, c->nccl_real(), c->comm, c->s));
     }
+    C.fghost_ok = !C.p.dist;
     return MGP_OK;
 }
 
@@ -283,8 +369,12 @@ int prolong_correct(mgp_ctx* c, int l)
         TRY(exchange(c, C));
     }
     char* V = c->ui(C, C.u) + (size_t)(zc * C.g.plane) * c->rb;
-    HIP_TRY(c, mgp::launch_prolong_correct(c->rb, c->o.dim, linear, c->ui(L, L.u), V, L.g, gc,
-                                           coarse_coef(c->o.coarse_bc, l + 1), c->s));
+    if (c->o.dim == 3 && mgp::prolong3d_x4_supported(L.g))
+        HIP_TRY(c, mgp::launch_prolong3d_x4(c->rb, linear, c->ui(L, L.u), V, L.g, gc, coarse_coef(c->o.coarse_bc, l + 1),
+                                            c->s));
+    else
+        HIP_TRY(c, mgp::launch_prolong_correct(c->rb, c->o.dim, linear, c->ui(L, L.u), V, L.g, gc,
+                                               coarse_coef(c->o.coarse_bc, l + 1), c->s));
     L.ghost_ok = !L.p.dist;
     return MGP_OK;
 }
@@ -313,7 +403,7 @@ int cycle_rec(mgp_ctx* c, int l, double h, bool fcycle)
     if (fcycle) TRY(cycle_rec(c, l + 1, 2 * h, true));
     TRY(cycle_rec(c, l + 1, 2 * h, false));
     TRY(prolong_correct(c, l));
-    TRY(smooth(c, l, c->o.nu2, h));
+    TRY(smooth(c, l, c->o.nu2, h, l == 0 && c->err_old != nullptr));
     return MGP_OK;
 }
 
@@ -321,10 +411,21 @@ int one_cycle(mgp_ctx* c, int slot)
 {
     Level& L = c->lev[0];
     const size_t bytes = (size_t)(L.g.plane * L.g.nz) * c->rb;
-    if (c->o.err_mode) HIP_TRY(c, hipMemcpyAsync(c->psi_old, c->ui(L, L.u), bytes, hipMemcpyDeviceToDevice, c->s));
+    const bool fuse = c->o.err_mode && c->err_fuse;
+    c->err_old = fuse ? L.u : nullptr;  // psiOld = the buffer psi is in now (no copy)
+    c->err_slot = slot;
+    c->err_done = false;
+    if (c->o.err_mode && !fuse)
+        HIP_TRY(c, hipMemcpyAsync(c->psi_old, c->ui(L, L.u), bytes, hipMemcpyDeviceToDevice, c->s));
     const double h = 1.0 / (double)L.p.nx;  // cpu.lua:197-198
     TRY(cycle_rec(c, 0, h, c->o.cycle == MGP_CYCLE_F));
-    if (c->o.err_mode) {
+    const bool fused_done = fuse && c->err_done;
+    if (fuse && !fused_done) return c->fail(MGP_ERR_STATE, "internal: fused err launch did not run");
+    c->err_old = nullptr;
+    if (fused_done) {
+        if (c->o.world > 1)
+            NCCL_TRY(c, ncclAllReduce(c->d_errs + slot, c->d_errs + slot, 1, ncclDouble, ncclSum, c->comm, c->s));
+    } else if (c->o.err_mode) {
         Level& L0 = c->lev[0];
         HIP_TRY(c, mgp::launch_sqdiff_sum(c->rb, c->ui(L0, L0.u), c->psi_old, L0.g.plane * L0.g.nz, c->d_part,
                                           c->d_errs + slot, c->s));
@@ -437,6 +538,7 @@ static void destroy_impl(mgp_ctx* c)
         if (L.u) (void)hipFree(L.u);
         if (L.f) (void)hipFree(L.f);
         if (L.t) (void)hipFree(L.t);
+        if (L.w) (void)hipFree(L.w);
     }
     if (c->psi_old) (void)hipFree(c->psi_old);
     if (c->d_part) (void)hipFree(c->d_part);
@@ -462,7 +564,10 @@ int mgp_create(mgp_ctx** out, const mgp_opts* o)
     c->o = *o;
     if (c->o.dim == 2) c->o.n[2] = 1;
     c->rb = o->real_bytes;
-    c->G = o->dim == 3 ? 1 : 0;
+    c->G = o->dim == 3 ? mgp::kGhost3D : 0;
+    if (const char* v = std::getenv("MGP_KC")) c->kc = std::max(1, std::atoi(v));
+    if (const char* v = std::getenv("MGP_TY")) c->ty = std::atoi(v) == 8 ? 8 : 16;
+    if (const char* v = std::getenv("MGP_NH")) c->nh_max = std::atoi(v) >= 4 ? 4 : 2;
     auto bail = [&](int code) {
         g_create_error = c->err;
         destroy_impl(c);
@@ -509,7 +614,7 @@ int mgp_create(mgp_ctx** out, const mgp_opts* o)
     for (size_t l = 0; l < c->lev.size(); ++l) {
         Level& L = c->lev[l];
         const size_t bytes = (size_t)L.alloc * rb;
-        const bool need_t = c->o.smoother == MGP_JACOBI;
+        const bool need_t = c->o.smoother == MGP_JACOBI || c->o.dim == 3;
         if (hipMalloc(&L.u, bytes) != hipSuccess || hipMalloc(&L.f, bytes) != hipSuccess ||
             (need_t && hipMalloc(&L.t, bytes) != hipSuccess)) {
             c->err = "hipMalloc failed for level " + std::to_string(l) + " (" + std::to_string(bytes) + " bytes)";
@@ -522,14 +627,23 @@ int mgp_create(mgp_ctx** out, const mgp_opts* o)
             return bail(MGP_ERR_HIP);
         }
     }
-    const Level& L0 = c->lev[0];
-    if (c->o.err_mode) {
+    Level& L0 = c->lev[0];
+    c->err_fuse = c->o.err_mode && fused_ok(c, L0) && c->o.nu1 >= 1 && c->o.nu2 >= 1 && c->lev.size() > 1;
+    if (c->err_fuse) {
+        const size_t bytes = (size_t)L0.alloc * rb;
+        if (hipMalloc(&L0.w, bytes) != hipSuccess || hipMemsetAsync(L0.w, 0, bytes, c->s) != hipSuccess) {
+            c->err = "hipMalloc failed for the third finest-level buffer";
+            return bail(MGP_ERR_OOM);
+        }
+    } else if (c->o.err_mode) {
         if (hipMalloc(&c->psi_old, (size_t)(L0.g.plane * L0.g.nz) * rb) != hipSuccess) {
             c->err = "hipMalloc failed for psiOld";
             return bail(MGP_ERR_OOM);
         }
     }
-    if (hipMalloc(&c->d_part, sizeof(double) * mgp::kSumBlocks) != hipSuccess) {
+    c->part_cap = mgp::kSumBlocks;
+    if (fused_ok(c, L0)) c->part_cap = std::max<int64_t>(c->part_cap, mgp::fused3d_blocks(L0.g, c->ty, c->kc));
+    if (hipMalloc(&c->d_part, sizeof(double) * c->part_cap) != hipSuccess) {
         c->err = "hipMalloc failed for reduction partials";
         return bail(MGP_ERR_OOM);
     }
@@ -580,6 +694,7 @@ int mgp_init_point_charge(mgp_ctx* c)
     HIP_TRY(c, mgp::launch_init_point_charge(c->rb, c->o.dim, c->ui(L, L.u), c->ui(L, L.f), L.g, L.p.nx / 2,
                                              L.p.ny / 2, cz, c->s));
     L.ghost_ok = !L.p.dist;
+    L.fghost_ok = !L.p.dist;
     return sync_and_check(c);
 }
 
@@ -592,6 +707,7 @@ int mgp_set_field(mgp_ctx* c, int level, int which, const void* src, int64_t cou
     char* dst = c->ui(L, which == MGP_FIELD_U ? L.u : L.f);
     HIP_TRY(c, hipMemcpyAsync(dst, src, (size_t)count * c->rb, mem == MGP_MEM_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, c->s));
     if (which == MGP_FIELD_U) L.ghost_ok = !L.p.dist;
+    else L.fghost_ok = !L.p.dist;
     return sync_and_check(c);
 }
 

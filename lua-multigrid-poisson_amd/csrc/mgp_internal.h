@@ -38,6 +38,25 @@ hipError_t launch_prolong_correct(int rb, int dim, int linear, void* u, const vo
 hipError_t launch_sqdiff_sum(int rb, const void* a, const void* b, int64_t n, double* partials,
                              double* out, hipStream_t s);
 
+// Fused out-of-place red/black sweeps of a 3D level (mgp_rbgs3d.hip): nh half-sweeps (2 or 4)
+// per launch; needs nh ghost planes of u and f (zeros at a physical boundary).
+// ty = tile height (8 or 16 rows of 64 cells).  With old != nullptr the launch also writes one fp64
+// partial of sum (uout - old)^2 per workgroup to partials[0 .. fused3d_blocks()).
+int fused3d_blocks(Geo g, int ty, int kc);
+bool rbgs_fused3d_supported(int rb, int nh, int ty, Geo g);
+hipError_t launch_rbgs_fused3d(int rb, bool fine, int nh, int ty, const void* uin, const void* f, void* uout,
+                               const void* old, double* partials, Geo g, int kc, double h, double cl, hipStream_t s);
+// LDS-tiled fused residual + 2x2x2 restriction of a 3D level (nx % 64 == 0, ny % 16 == 0, even nz).
+bool residual_restrict3d_supported(Geo g);
+hipError_t launch_residual_restrict3d(int rb, const void* u, const void* f, void* R, Geo g, double h, double cl,
+                                      hipStream_t s);
+// Vectorised 3D prolongation + correction (4 fine x-cells per thread; nx >= 4).
+bool prolong3d_x4_supported(Geo g);
+hipError_t launch_prolong3d_x4(int rb, int linear, void* u, const void* V, Geo g, Geo gc, double clc, hipStream_t s);
+// Fixed-order fp64 sum of n partials into *out (one workgroup).
+hipError_t launch_sum_partials(const double* partials, int n, double* out, hipStream_t s);
+
 constexpr int kSumBlocks = 1024;
+constexpr int kGhost3D = 4;  // ghost planes per side of every 3D level (= max nh)
 
 }  // namespace mgp

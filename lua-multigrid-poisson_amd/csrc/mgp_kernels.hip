@@ -265,6 +265,21 @@ __global__ __launch_bounds__(1024) void k_sum_partials(const double* __restrict_
     if (threadIdx.x == 0) *out = sh[0];
 }
 
+// Fixed-order sum of n fp64 partials (n arbitrary) by one workgroup.
+__global__ __launch_bounds__(1024) void k_sum_n(const double* __restrict__ partials, int n, double* __restrict__ out)
+{
+    __shared__ double sh[1024];
+    double a = 0.0;
+    for (int i = threadIdx.x; i < n; i += 1024) a += partials[i];
+    sh[threadIdx.x] = a;
+    __syncthreads();
+    for (int w = 512; w > 0; w >>= 1) {
+        if ((int)threadIdx.x < w) sh[threadIdx.x] += sh[threadIdx.x + w];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) *out = sh[0];
+}
+
 inline unsigned blocks_for(int64_t n) { return (unsigned)((n + kBlock - 1) / kBlock); }
 
 }  // namespace
@@ -336,6 +351,12 @@ hipError_t launch_sqdiff_sum(int rb, const void* a, const void* b, int64_t n, do
     else
         k_sqdiff_partial<float><<<kSumBlocks, kBlock, 0, s>>>((const float*)a, (const float*)b, n, partials);
     k_sum_partials<<<1, kSumBlocks, 0, s>>>(partials, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_sum_partials(const double* partials, int n, double* out, hipStream_t s)
+{
+    k_sum_n<<<1, 1024, 0, s>>>(partials, n, out);
     return hipGetLastError();
 }
 
