@@ -124,7 +124,7 @@ struct mgp_ctx {
     double* d_errs = nullptr;
     int errs_cap = 0;
     // fused sweep kernel tuning (environment overrides MGP_KC, MGP_TY, MGP_NH)
-    int kc = 32;      // z-planes per workgroup chunk
+    int kc = 16;      // z-planes per workgroup chunk
     int ty = 16;      // tile rows
     int nh_max = 2;   // half-sweeps per launch (4 = two sweeps per pass)
     // fused err (3D red/black on the finest level): the cycle-start psi stays untouched in one of

@@ -125,7 +125,7 @@ struct Plane {
     using C = Cfg<T, NH, TY>;
     using V = typename Vec<T>::type;
     // Global loads of local plane q into registers; zeros outside the box.
-    __device__ static void fetch(const T* __restrict__ src, int64_t q, const Geo& g, const Tile& tl, bool valid,
+    __device__ __forceinline__ static void fetch(const T* __restrict__ src, int64_t q, const Geo& g, const Tile& tl, bool valid,
                                  V (&r)[C::VPT])
     {
         const T* __restrict__ base = src + q * g.plane;
@@ -144,7 +144,7 @@ struct Plane {
             r[k] = v;
         }
     }
-    __device__ static void stash(T* __restrict__ slot, const V (&r)[C::VPT])
+    __device__ __forceinline__ static void stash(T* __restrict__ slot, const V (&r)[C::VPT])
     {
 #pragma unroll
         for (int k = 0; k < C::VPT; ++k) {
@@ -159,7 +159,7 @@ struct Plane {
     // Tile interior of a finished plane back to HBM (16 B per lane, whole rows).  With ERR the
     // squared update against `old` (the cycle-start psi) is accumulated in fp64 (cpu.lua:203).
     template <bool ERR>
-    __device__ static void writeback(T* __restrict__ dst, const T* __restrict__ slot, int64_t q, const Geo& g,
+    __device__ __forceinline__ static void writeback(T* __restrict__ dst, const T* __restrict__ slot, int64_t q, const Geo& g,
                                      const Tile& tl, const T* __restrict__ old, double& acc)
     {
         constexpr int VROW = C::TX / C::VN;
@@ -190,21 +190,59 @@ __device__ __forceinline__ int slot_of(int64_t q)
     return s < 0 ? s + N : s;
 }
 
-struct Consts {
-    double h, cl;
+// Per-thread item table of every pipeline stage, built once per workgroup: for each unrolled
+// iteration and each row-parity phase (the colour pattern flips from plane to plane) the LDS
+// offset of the cell, its x parity and its count of box faces in x/y; -1 = no cell (past the
+// region or outside the box).  The inner loop then does no index arithmetic at all.
+template <int NH, int TY>
+struct Items {
+    static constexpr int MAXIT = ((TY + 2 * (NH - 1)) * (kTX / 2 + NH - 1) + kThreads - 1) / kThreads;
+    int tab[NH][MAXIT][2];
+
+    template <typename T, int S>
+    __device__ __forceinline__ void build_stage(const Geo& g, const Tile& tl)
+    {
+        using C = Cfg<T, NH, TY>;
+        constexpr int e = NH - 1 - S;
+        constexpr int IR = kTX / 2 + e;
+        constexpr int ITEMS = (TY + 2 * e) * IR;
+#pragma unroll
+        for (int k = 0; k < MAXIT; ++k) {
+            const int it = threadIdx.x + k * kThreads;
+            const int r = it / IR;
+            const int m = it - r * IR;
+            const int y = r - e;
+#pragma unroll
+            for (int par = 0; par < 2; ++par) {
+                const int px = (par + y) & 1;
+                const int x = -e + ((px + e) & 1) + 2 * m;
+                const int gx = tl.x0 + x, gy = tl.y0 + y;
+                int v = -1;
+                if (it < ITEMS && gx >= 0 && gx < g.nx && gy >= 0 && gy < g.ny) {
+                    const int same = (y + C::E) * C::PW + px * C::HW + ((x + C::XE) >> 1);
+                    const int nb = (gx == 0) + (gx == g.nx - 1) + (gy == 0) + (gy == g.ny - 1);
+                    v = same | (px << 16) | (nb << 17);
+                }
+                tab[S][k][par] = v;
+            }
+        }
+        if constexpr (S + 1 < NH) build_stage<T, S + 1>(g, tl);
+    }
+    template <typename T>
+    __device__ __forceinline__ void build(const Geo& g, const Tile& tl)
+    {
+        build_stage<T, 0>(g, tl);
+    }
 };
 
-// One pipeline stage: colour c on plane q (neighbour planes q-1, q+1), region grown by e.
-template <typename T, int NH, int TY, int S, bool INNER>
+// One pipeline stage: colour c = S & 1 on plane q (neighbour planes q-1, q+1).
+template <typename T, int NH, int TY, int S>
 __device__ __forceinline__ void stage(T* __restrict__ lds_u, const T* __restrict__ lds_f, int64_t q, const Geo& g,
-                                      const Tile& tl, T inv_hSq, T hSq, T adiag, T yadiag, T cl)
+                                      const Tile& tl, const Items<NH, TY>& items, T hSq, T inv_hSq, T adiag, T yadiag,
+                                      T cl)
 {
     using C = Cfg<T, NH, TY>;
-    constexpr int e = NH - 1 - S;
     constexpr int c = S & 1;  // 0 = red (first), 1 = black
-    constexpr int IR = kTX / 2 + e;           // items (cells of colour c) per row
-    constexpr int ITEMS = (TY + 2 * e) * IR;
-    constexpr int ITERS = (ITEMS + kThreads - 1) / kThreads;
     const int64_t gq = g.z0 + q;
     T* __restrict__ cur = lds_u + slot_of<C::NU>(q) * C::PS;
     const T* __restrict__ lo = lds_u + slot_of<C::NU>(q - 1) * C::PS;
@@ -213,22 +251,14 @@ __device__ __forceinline__ void stage(T* __restrict__ lds_u, const T* __restrict
     const int zb = (gq == 0) + (gq == g.gnz - 1);
     const int par = (c + tl.y0 + (int)(gq & 1)) & 1;
 #pragma unroll
-    for (int k = 0; k < ITERS; ++k) {
-        const int it = threadIdx.x + k * kThreads;
-        if (ITEMS % kThreads != 0 && it >= ITEMS) break;
-        const int r = it / IR;
-        const int m = it - r * IR;
-        const int y = r - e;                        // tile-relative y
-        const int px = (par + y) & 1;               // x parity of colour-c cells in this row
-        const int x = -e + ((px + e) & 1) + 2 * m;  // tile-relative x with parity px
-        int gx = 0, gy = 0;
-        if (!INNER) {
-            gx = tl.x0 + x;
-            gy = tl.y0 + y;
-            if (gx < 0 || gx >= g.nx || gy < 0 || gy >= g.ny) continue;
-        }
-        const int same = (y + C::E) * C::PW + px * C::HW + ((x + C::XE) >> 1);
-        const int oth = same + (1 - 2 * px) * C::HW + px;  // x+1 neighbour; x-1 is oth - 1
+    for (int k = 0; k < Items<NH, TY>::MAXIT; ++k) {
+        int p0 = items.tab[S][k][0], p1 = items.tab[S][k][1];
+        asm volatile("" : "+v"(p0), "+v"(p1));  // keep the table in registers (no load-of-select)
+        const int p = par ? p1 : p0;
+        if (p < 0) continue;
+        const int same = p & 0xFFFF;
+        const int px = (p >> 16) & 1;
+        const int oth = same + (px ? 1 - C::HW : C::HW);  // x+1 neighbour; x-1 is oth - 1
         const T xl = cur[oth - 1];
         const T xr = cur[oth];
         const T yl = cur[same - C::PW];
@@ -241,18 +271,11 @@ __device__ __forceinline__ void stage(T* __restrict__ lds_u, const T* __restrict
         s = s + yr;
         s = s + zl;
         s = s + zr;
-        const T a = fc - s * inv_hSq;  // s / h^2 exactly (h^2 is a power of two)
+        const T a = fc - s * inv_hSq;  // = fc - s / h^2 exactly (h^2 is a power of two)
+        const int nb = (p >> 17) + zb;
         T res;
-        if (!INNER && cl != (T)0) {
-            const int nb = (gx == 0) + (gx == g.nx - 1) + (gy == 0) + (gy == g.ny - 1) + zb;
-            if (nb) {
-                const T dg = ((T)(-6) - (T)nb * cl) / hSq;
-                res = a / dg;
-            } else {
-                res = div_rn(a, adiag, yadiag);
-            }
-        } else if (INNER && cl != (T)0 && zb) {
-            const T dg = ((T)(-6) - (T)zb * cl) / hSq;
+        if (cl != (T)0 && nb) {
+            const T dg = ((T)(-6) - (T)nb * cl) / hSq;  // boundary cell: IEEE division as the oracle
             res = a / dg;
         } else {
             res = div_rn(a, adiag, yadiag);
@@ -261,25 +284,25 @@ __device__ __forceinline__ void stage(T* __restrict__ lds_u, const T* __restrict
     }
 }
 
-template <typename T, int NH, int TY, int S, bool INNER>
+template <typename T, int NH, int TY, int S>
 struct Stages {
-    __device__ static void run(T* lds_u, const T* lds_f, int64_t t, const Geo& g, const Tile& tl, T inv_hSq, T hSq,
-                               T adiag, T yadiag, T cl)
+    __device__ __forceinline__ static void run(T* lds_u, const T* lds_f, int64_t t, const Geo& g, const Tile& tl,
+                               const Items<NH, TY>& items, T hSq, T inv_hSq, T adiag, T yadiag, T cl)
     {
         const int64_t q = t - 1 - S;
         constexpr int e = NH - 1 - S;
         if (q >= tl.k0 - e && q <= tl.k1 - 1 + e && g.z0 + q >= 0 && g.z0 + q < g.gnz)
-            stage<T, NH, TY, S, INNER>(lds_u, lds_f, q, g, tl, inv_hSq, hSq, adiag, yadiag, cl);
+            stage<T, NH, TY, S>(lds_u, lds_f, q, g, tl, items, hSq, inv_hSq, adiag, yadiag, cl);
         __syncthreads();
-        Stages<T, NH, TY, S + 1, INNER>::run(lds_u, lds_f, t, g, tl, inv_hSq, hSq, adiag, yadiag, cl);
+        Stages<T, NH, TY, S + 1>::run(lds_u, lds_f, t, g, tl, items, hSq, inv_hSq, adiag, yadiag, cl);
     }
 };
-template <typename T, int NH, int TY, bool INNER>
-struct Stages<T, NH, TY, NH, INNER> {
-    __device__ static void run(T*, const T*, int64_t, const Geo&, const Tile&, T, T, T, T, T) {}
+template <typename T, int NH, int TY>
+struct Stages<T, NH, TY, NH> {
+    __device__ static void run(T*, const T*, int64_t, const Geo&, const Tile&, const Items<NH, TY>&, T, T, T, T, T) {}
 };
 
-template <typename T, int NH, int TY, bool INNER, bool ERR>
+template <typename T, int NH, int TY, bool ERR>
 struct Marcher {
     using C = Cfg<T, NH, TY>;
     using V = typename Vec<T>::type;
@@ -294,9 +317,10 @@ struct Marcher {
     T* lds_f;
     T hSq, inv_hSq, adiag, yadiag, cl;
     int64_t tfirst, tlast;
+    Items<NH, TY> items;
     double acc = 0.0;
 
-    __device__ bool planeok(int64_t q) const { return g.z0 + q >= 0 && g.z0 + q < g.gnz; }
+    __device__ __forceinline__ bool planeok(int64_t q) const { return g.z0 + q >= 0 && g.z0 + q < g.gnz; }
 
     // One z-step: plane t enters LDS (registers ru/rf are then refilled with plane t + 2),
     // plane t-1-NH leaves to HBM, and the NH stages advance the pipeline.
@@ -312,11 +336,12 @@ struct Marcher {
         const int64_t qo = t - 1 - NH;
         if (qo >= tl.k0 && qo < tl.k1)
             P::template writeback<ERR>(uout, lds_u + slot_of<C::NU>(qo) * C::PS, qo, g, tl, old, acc);
-        Stages<T, NH, TY, 0, INNER>::run(lds_u, lds_f, t, g, tl, inv_hSq, hSq, adiag, yadiag, cl);
+        Stages<T, NH, TY, 0>::run(lds_u, lds_f, t, g, tl, items, hSq, inv_hSq, adiag, yadiag, cl);
     }
 
-    __device__ void run()
+    __device__ __forceinline__ void run()
     {
+        items.template build<T>(g, tl);
         V ru0[C::VPT], rf0[C::VPT], ru1[C::VPT], rf1[C::VPT];
         P::fetch(uin, tfirst, g, tl, planeok(tfirst), ru0);
         P::fetch(f, tfirst, g, tl, planeok(tfirst), rf0);
@@ -332,12 +357,12 @@ struct Marcher {
     }
 };
 
-template <typename T, int NH, int TY, bool INNER, bool ERR>
+template <typename T, int NH, int TY, bool ERR>
 __device__ __forceinline__ double march(const T* __restrict__ uin, const T* __restrict__ f, T* __restrict__ uout,
                                         const T* __restrict__ old, const Geo& g, const Tile& tl, T* lds_u, T* lds_f,
                                         double h, double cld)
 {
-    Marcher<T, NH, TY, INNER, ERR> m{uin, f, uout, old, g, tl, lds_u, lds_f};
+    Marcher<T, NH, TY, ERR> m{uin, f, uout, old, g, tl, lds_u, lds_f};
     const T hh = (T)h;
     m.hSq = hh * hh;
     m.inv_hSq = (T)1 / m.hSq;  // exact: h is a power of two
@@ -375,11 +400,7 @@ __global__ __launch_bounds__(kThreads) void k_rbgs_fused3d(const T* __restrict__
     tl.k0 = (int64_t)kch * kc;
     tl.k1 = tl.k0 + kc < g.nz ? tl.k0 + kc : g.nz;
     tl.inner = tl.x0 - C::XE >= 0 && tl.x0 + kTX + C::XE <= g.nx && tl.y0 - C::E >= 0 && tl.y0 + TY + C::E <= g.ny;
-    double acc;
-    if (tl.inner)
-        acc = march<T, NH, TY, true, ERR>(uin, f, uout, old, g, tl, lds_u, lds_f, h, cld);
-    else
-        acc = march<T, NH, TY, false, ERR>(uin, f, uout, old, g, tl, lds_u, lds_f, h, cld);
+    const double acc = march<T, NH, TY, ERR>(uin, f, uout, old, g, tl, lds_u, lds_f, h, cld);
     if (ERR) {  // fixed-order block reduction -> one fp64 partial per workgroup
         __syncthreads();
         double* red = reinterpret_cast<double*>(smem);
@@ -459,7 +480,7 @@ template <typename T, int TY>
 struct RPlane {
     using C = RCfg<T, TY>;
     using V = typename Vec<T>::type;
-    __device__ static void fetch(const T* __restrict__ src, int64_t q, const Geo& g, int x0, int y0, bool inner,
+    __device__ __forceinline__ static void fetch(const T* __restrict__ src, int64_t q, const Geo& g, int x0, int y0, bool inner,
                                  bool valid, V (&r)[C::VPT])
     {
         const T* __restrict__ base = src + q * g.plane;
@@ -478,7 +499,7 @@ struct RPlane {
             r[k] = v;
         }
     }
-    __device__ static void stash(T* __restrict__ slot, const V (&r)[C::VPT])
+    __device__ __forceinline__ static void stash(T* __restrict__ slot, const V (&r)[C::VPT])
     {
 #pragma unroll
         for (int k = 0; k < C::VPT; ++k) {

@@ -184,7 +184,7 @@ def test_cycles_box_match_oracle(box):
         _check_err(e_gpu, e_ref, new, old)
 
 
-@pytest.mark.parametrize("box", [(64, 16, 2), (64, 64, 64), (128, 32, 96), (256, 256, 32)])
+@pytest.mark.parametrize("box", [(64, 16, 2), (64, 64, 64), (128, 32, 64), (256, 256, 32)])
 @pytest.mark.parametrize("real", ["double", "float"])
 @pytest.mark.parametrize("bc", ["zero", "consistent"])
 def test_residual_restrict_tiled3d(box, real, bc):
