@@ -102,11 +102,10 @@ double coarse_coef(int coarse_bc, int level)
 struct Level {
     LevelPlan p;
     Geo g;
-    int64_t alloc;  // elements per buffer, ghosts included
+    int64_t alloc;  // reals per buffer, ghost planes included
     char* u = nullptr;
     char* f = nullptr;
-    char* t = nullptr;  // ping-pong partner of u (Jacobi, fused red/black sweeps)
-    char* w = nullptr;  // level 0 only: third buffer that keeps the cycle-start psi (fused err)
+    char* t = nullptr;      // second u buffer (Jacobi ping-pong; level 0: keeps psiOld during a cycle)
     bool ghost_ok = true;   // u's ghost planes hold the neighbours' current planes
     bool fghost_ok = true;  // f's ghost planes likewise
 };
@@ -119,21 +118,20 @@ struct mgp_ctx {
     hipStream_t s = nullptr;
     int device = 0;
     ncclComm_t comm = nullptr;
-    char* psi_old = nullptr;
+    char* psi_old = nullptr;  // snapshot buffer (Jacobi path)
+    char* stage = nullptr;    // lexicographic staging buffer for set/get (level-0 size)
     double* d_part = nullptr;
+    int64_t part_cap = 0;
     double* d_errs = nullptr;
     int errs_cap = 0;
-    // fused sweep kernel tuning (environment overrides MGP_KC, MGP_TY, MGP_NH)
-    int kc = 16;      // z-planes per workgroup chunk
-    int ty = 16;      // tile rows
-    int nh_max = 2;   // half-sweeps per launch (4 = two sweeps per pass)
-    // fused err (3D red/black on the finest level): the cycle-start psi stays untouched in one of
-    // three rotating buffers and the last post-sweep accumulates (psi - psiOld)^2 itself
+    // Fused err (red/black): the cycle's first sweep on the finest level runs out of place from u
+    // into t, so t keeps psiOld untouched until the last post-sweep, whose two half-sweeps
+    // accumulate (psi - psiOld)^2 (cpu.lua:200-203 without the copy and the extra pass).
     bool err_fuse = false;
+    bool in_cycle = false;  // a one_cycle() is running (level-0 first sweep goes out of place)
+    bool first_done = false;
     bool err_done = false;
-    char* err_old = nullptr;  // base pointer of the buffer holding psiOld during this cycle
     int err_slot = 0;
-    int64_t part_cap = 0;
     std::string err;
     // finest-smoother timing
     bool timing = false;
@@ -153,7 +151,7 @@ struct mgp_ctx {
         err = buf;
         return code;
     }
-    char* ui(const Level& L, char* base) const { return base + (size_t)(G * L.g.plane) * rb; }
+    char* ui(const Level& L, char* base) const { return base + (size_t)(G * L.g.P) * rb; }
     int64_t ncells_global() const { return lev[0].p.nx * lev[0].p.ny * lev[0].p.gnz; }
     ncclDataType_t nccl_real() const { return rb == 8 ? ncclDouble : ncclFloat; }
 };
@@ -174,53 +172,59 @@ struct mgp_ctx {
                              __FILE__, __LINE__);                                                  \
     } while (0)
 
-#define TRY(expr)                 \
-    do {                          \
-        int rc_ = (expr);         \
+#define TRY(expr)                      \
+    do {                               \
+        int rc_ = (expr);              \
         if (rc_ != MGP_OK) return rc_; \
     } while (0)
 
 namespace {
 
+Geo make_geo(const LevelPlan& p, int dim)
+{
+    Geo g;
+    g.nx = (int)p.nx;
+    g.ny = (int)p.ny;
+    g.lx = ilog2(p.nx);
+    g.ly = ilog2(p.ny);
+    g.hw = p.nx >= 2 ? (int)(p.nx / 2) : 1;
+    g.lhw = ilog2(g.hw);
+    g.nz = dim == 3 ? p.nz : 1;
+    g.H = (int64_t)g.hw * g.ny;
+    g.P = 2 * g.H;
+    g.z0 = dim == 3 ? p.z0 : 0;
+    g.gnz = dim == 3 ? p.gnz : 1;
+    return g;
+}
+
 // ---- halo exchange over RCCL (grouped send/recv to the z-neighbours) ----
 
-// Exchange `depth` boundary planes of `buf` with both z-neighbours: my first `depth` interior
-// planes go to rank-1's upper ghosts, my last `depth` to rank+1's lower ghosts.  Contiguous
-// planes, so each direction is one ncclSend/ncclRecv pair (one xGMI link per neighbour).
-int exchange_buf(mgp_ctx* c, Level& L, char* buf, int depth)
+// Exchange one boundary plane of `buf` with each z-neighbour: my first interior plane goes to
+// rank-1's upper ghost, my last to rank+1's lower ghost.  A plane is contiguous in the packed
+// layout, so each direction is one ncclSend/ncclRecv pair on that neighbour's xGMI link.
+int exchange_buf(mgp_ctx* c, Level& L, char* buf)
 {
-    const int64_t pl = L.g.plane;
     const size_t rb = (size_t)c->rb;
-    const int G = c->G;
-    const size_t cnt = (size_t)(pl * depth);
-    // plane k (interior index, may be negative for ghosts) lives at buf + (k + G) * pl
-    auto at = [&](int64_t k) { return buf + (size_t)((k + G) * pl) * rb; };
+    const size_t cnt = (size_t)L.g.P;
+    auto at = [&](int64_t k) { return buf + (size_t)((k + c->G) * L.g.P) * rb; };
     NCCL_TRY(c, ncclGroupStart());
     if (c->o.rank > 0) {
         NCCL_TRY(c, ncclSend(at(0), cnt, c->nccl_real(), c->o.rank - 1, c->comm, c->s));
-        NCCL_TRY(c, ncclRecv(at(-depth), cnt, c->nccl_real(), c->o.rank - 1, c->comm, c->s));
+        NCCL_TRY(c, ncclRecv(at(-1), cnt, c->nccl_real(), c->o.rank - 1, c->comm, c->s));
     }
     if (c->o.rank < c->o.world - 1) {
-        NCCL_TRY(c, ncclSend(at(L.g.nz - depth), cnt, c->nccl_real(), c->o.rank + 1, c->comm, c->s));
+        NCCL_TRY(c, ncclSend(at(L.g.nz - 1), cnt, c->nccl_real(), c->o.rank + 1, c->comm, c->s));
         NCCL_TRY(c, ncclRecv(at(L.g.nz), cnt, c->nccl_real(), c->o.rank + 1, c->comm, c->s));
     }
     NCCL_TRY(c, ncclGroupEnd());
     return MGP_OK;
 }
 
-int exchange(mgp_ctx* c, Level& L, int depth = 1)
+int exchange(mgp_ctx* c, Level& L)
 {
     if (!L.p.dist || L.ghost_ok) return MGP_OK;
-    TRY(exchange_buf(c, L, L.u, depth));
+    TRY(exchange_buf(c, L, L.u));
     L.ghost_ok = true;
-    return MGP_OK;
-}
-
-int exchange_f(mgp_ctx* c, Level& L, int depth)
-{
-    if (!L.p.dist || L.fghost_ok) return MGP_OK;
-    TRY(exchange_buf(c, L, L.f, depth));
-    L.fghost_ok = true;
     return MGP_OK;
 }
 
@@ -231,7 +235,6 @@ int timed_begin(mgp_ctx* c, int l, hipEvent_t* e1)
     *e1 = nullptr;
     if (!c->timing || l != 0) return MGP_OK;
     if (c->ev_used + 2 > c->ev.size()) {
-        // harvest what we have, then reuse the pool
         HIP_TRY(c, hipStreamSynchronize(c->s));
         for (size_t e = 0; e + 1 < c->ev_used; e += 2) {
             float ms = 0.f;
@@ -257,79 +260,63 @@ int timed_end(mgp_ctx* c, hipEvent_t e1, double sweeps)
 
 // ---- cycle pieces ----
 
-bool fused_ok(const mgp_ctx* c, const Level& L)
+// One half-sweep (colour `color`) reading `other`, writing `dst`; level-0 launches are timed.
+int half(mgp_ctx* c, int l, int color, char* other, char* dst, const char* old, double h, double cl, int part_off)
 {
-    return c->o.smoother == MGP_RBGS && c->o.dim == 3 && mgp::rbgs_fused3d_supported(c->rb, 2, c->ty, L.g) &&
-           L.g.nz >= 4;
-}
-
-// After an out-of-place launch read u and wrote t: the written buffer becomes u.  On level 0
-// with fused err the buffer holding psiOld is parked in w and never written during the cycle.
-void advance(mgp_ctx* c, Level& L)
-{
-    char* prev = L.u;
-    L.u = L.t;
-    if (L.w && prev == c->err_old) {
-        L.t = L.w;
-        L.w = prev;
-    } else {
-        L.t = prev;
-    }
+    Level& L = c->lev[l];
+    hipEvent_t e;
+    TRY(timed_begin(c, l, &e));
+    HIP_TRY(c, mgp::launch_half_sweep(c->rb, c->o.dim, l == 0, color, c->ui(L, other), c->ui(L, L.f), c->ui(L, dst),
+                                      old ? c->ui(L, (char*)old) : nullptr, c->d_part + part_off, L.g, h, cl, c->s));
+    TRY(timed_end(c, e, 0.5));
+    return MGP_OK;
 }
 
 int smooth(mgp_ctx* c, int l, int sweeps, double h, bool want_err = false)
 {
     Level& L = c->lev[l];
     const double cl = coarse_coef(c->o.coarse_bc, l);
-    const bool fine = l == 0;
     for (int sw = 0; sw < sweeps; ++sw) {
         if (c->o.smoother == MGP_JACOBI) {
+            // both colours from the old iterate into t, then swap (no copy back, cf. gpu.lua:292)
             TRY(exchange(c, L));
-            hipEvent_t e;
-            TRY(timed_begin(c, l, &e));
-            HIP_TRY(c, mgp::launch_jacobi(c->rb, c->o.dim, fine, c->ui(L, L.u), c->ui(L, L.f), c->ui(L, L.t), L.g, h, cl, c->s));
-            TRY(timed_end(c, e, 1.0));
+            TRY(half(c, l, 0, L.u, L.t, nullptr, h, cl, 0));
+            TRY(half(c, l, 1, L.u, L.t, nullptr, h, cl, 0));
             std::swap(L.u, L.t);
             L.ghost_ok = !L.p.dist;
-        } else if (fused_ok(c, L)) {
-            // fused out-of-place sweeps: nh_max/2 per launch, a single one for an odd remainder
-            const int nh = (sweeps - sw >= 2 && c->nh_max >= 4) ? 4 : 2;
-            const bool last = sw + nh / 2 >= sweeps;
-            const bool err_here = want_err && last;
-            const char* old = err_here ? c->ui(L, c->err_old) : nullptr;
-            if (L.p.dist) {
-                // a stale ghost plane must be re-sent at full depth
-                if (!L.ghost_ok) {
-                    TRY(exchange_buf(c, L, L.u, nh));
-                    L.ghost_ok = true;
-                }
-                TRY(exchange_f(c, L, c->G));
-            }
-            hipEvent_t e;
-            TRY(timed_begin(c, l, &e));
-            HIP_TRY(c, mgp::launch_rbgs_fused3d(c->rb, fine, nh, c->ty, c->ui(L, L.u), c->ui(L, L.f), c->ui(L, L.t),
-                                                old, c->d_part, L.g, c->kc, h, cl, c->s));
-            TRY(timed_end(c, e, nh / 2));
-            if (err_here) {
-                const int nb = mgp::fused3d_blocks(L.g, c->ty, c->kc);
-                HIP_TRY(c, mgp::launch_sum_partials(c->d_part, nb, c->d_errs + c->err_slot, c->s));
-                c->err_done = true;
-            }
-            advance(c, L);
-            L.ghost_ok = !L.p.dist;
-            sw += nh / 2 - 1;
-        } else {
-            for (int color = 0; color < 2; ++color) {
-                TRY(exchange(c, L));
-                hipEvent_t e;
-                TRY(timed_begin(c, l, &e));
-                HIP_TRY(c, mgp::launch_rb_half(c->rb, c->o.dim, fine, c->ui(L, L.u), c->ui(L, L.f), L.g, color, h, cl, c->s));
-                TRY(timed_end(c, e, 0.5));
-                L.ghost_ok = !L.p.dist;
-            }
+            continue;
+        }
+        const bool oop = l == 0 && c->in_cycle && c->err_fuse && !c->first_done;  // keep psiOld in t
+        const bool last_err = want_err && sw == sweeps - 1;
+        const char* old = last_err ? L.t : nullptr;
+        const int nb = mgp::half_blocks(c->rb, L.g);
+        char* dst = oop ? L.t : L.u;
+        TRY(exchange(c, L));
+        TRY(half(c, l, 0, L.u, dst, old, h, cl, 0));  // red from black
+        if (L.p.dist) {  // black reads the new red planes of dst
+            TRY(exchange_buf(c, L, dst));
+        }
+        TRY(half(c, l, 1, dst, dst, old, h, cl, nb));  // black from red
+        if (oop) {
+            std::swap(L.u, L.t);  // u = new iterate, t = psiOld (untouched)
+            c->first_done = true;
+        }
+        L.ghost_ok = !L.p.dist;
+        if (last_err) {
+            HIP_TRY(c, mgp::launch_sum_partials(c->d_part, 2 * nb, c->d_errs + c->err_slot, c->s));
+            c->err_done = true;
         }
     }
     return MGP_OK;
+}
+
+// coarse plane (local to C's storage) and global coarse z of this rank's fine plane 0
+Geo coarse_view(const Level& L, const Level& C, int64_t* zc_local)
+{
+    Geo gc = C.g;
+    gc.z0 = L.p.z0 / 2;
+    *zc_local = (L.p.dist && !C.p.dist) ? L.p.z0 / 2 : 0;
+    return gc;
 }
 
 int residual_restrict(mgp_ctx* c, int l, double h)
@@ -337,21 +324,16 @@ int residual_restrict(mgp_ctx* c, int l, double h)
     Level& L = c->lev[l];
     Level& C = c->lev[l + 1];
     TRY(exchange(c, L));
-    // coarse plane that corresponds to this rank's fine plane 0
-    const int64_t zc = (L.p.dist && !C.p.dist) ? L.p.z0 / 2 : 0;
-    char* R = c->ui(C, C.f) + (size_t)(zc * C.g.plane) * c->rb;
-    if (c->o.dim == 3 && mgp::residual_restrict3d_supported(L.g))
-        HIP_TRY(c, mgp::launch_residual_restrict3d(c->rb, c->ui(L, L.u), c->ui(L, L.f), R, L.g, h,
-                                                   coarse_coef(c->o.coarse_bc, l), c->s));
-    else
-        HIP_TRY(c, mgp::launch_residual_restrict(c->rb, c->o.dim, c->ui(L, L.u), c->ui(L, L.f), R, L.g, h,
-                                                 coarse_coef(c->o.coarse_bc, l), c->s));
+    int64_t zc = 0;
+    const Geo gc = coarse_view(L, C, &zc);
+    char* R = c->ui(C, C.f) + (size_t)(zc * C.g.P) * c->rb;
+    HIP_TRY(c, mgp::launch_residual_restrict(c->rb, c->o.dim, c->ui(L, L.u), c->ui(L, L.f), R, L.g, gc, h,
+                                             coarse_coef(c->o.coarse_bc, l), c->s));
     if (L.p.dist && !C.p.dist) {
         // agglomerate: every rank gets the whole coarse right-hand side (cf. cpu-gpu.lua:22-32)
-        const size_t count = (size_t)((L.g.nz / 2) * C.g.plane);
+        const size_t count = (size_t)((L.g.nz / 2) * C.g.P);
         NCCL_TRY(c, ncclAllGather(R, c->ui(C, C.f), count, c->nccl_real(), c->comm, c->s));
     }
-    C.fghost_ok = !C.p.dist;
     return MGP_OK;
 }
 
@@ -360,21 +342,12 @@ int prolong_correct(mgp_ctx* c, int l)
     Level& L = c->lev[l];
     Level& C = c->lev[l + 1];
     const int linear = c->o.prolong == MGP_PROLONG_LINEAR;
-    Geo gc = C.g;
+    if (linear && C.p.dist) TRY(exchange(c, C));
     int64_t zc = 0;
-    if (L.p.dist && !C.p.dist) {
-        zc = L.p.z0 / 2;  // read our slice of the replicated coarse grid
-        gc.z0 = zc;
-    } else if (linear && C.p.dist) {
-        TRY(exchange(c, C));
-    }
-    char* V = c->ui(C, C.u) + (size_t)(zc * C.g.plane) * c->rb;
-    if (c->o.dim == 3 && mgp::prolong3d_x4_supported(L.g))
-        HIP_TRY(c, mgp::launch_prolong3d_x4(c->rb, linear, c->ui(L, L.u), V, L.g, gc, coarse_coef(c->o.coarse_bc, l + 1),
-                                            c->s));
-    else
-        HIP_TRY(c, mgp::launch_prolong_correct(c->rb, c->o.dim, linear, c->ui(L, L.u), V, L.g, gc,
-                                               coarse_coef(c->o.coarse_bc, l + 1), c->s));
+    const Geo gc = coarse_view(L, C, &zc);
+    char* V = c->ui(C, C.u) + (size_t)(zc * C.g.P) * c->rb;
+    HIP_TRY(c, mgp::launch_prolong_correct(c->rb, c->o.dim, linear, c->ui(L, L.u), V, L.g, gc,
+                                           coarse_coef(c->o.coarse_bc, l + 1), c->s));
     L.ghost_ok = !L.p.dist;
     return MGP_OK;
 }
@@ -403,35 +376,33 @@ int cycle_rec(mgp_ctx* c, int l, double h, bool fcycle)
     if (fcycle) TRY(cycle_rec(c, l + 1, 2 * h, true));
     TRY(cycle_rec(c, l + 1, 2 * h, false));
     TRY(prolong_correct(c, l));
-    TRY(smooth(c, l, c->o.nu2, h, l == 0 && c->err_old != nullptr));
+    TRY(smooth(c, l, c->o.nu2, h, l == 0 && c->in_cycle && c->err_fuse));
     return MGP_OK;
 }
 
 int one_cycle(mgp_ctx* c, int slot)
 {
     Level& L = c->lev[0];
-    const size_t bytes = (size_t)(L.g.plane * L.g.nz) * c->rb;
+    const size_t bytes = (size_t)(L.g.P * L.g.nz) * c->rb;
     const bool fuse = c->o.err_mode && c->err_fuse;
-    c->err_old = fuse ? L.u : nullptr;  // psiOld = the buffer psi is in now (no copy)
     c->err_slot = slot;
     c->err_done = false;
+    c->first_done = false;
     if (c->o.err_mode && !fuse)
         HIP_TRY(c, hipMemcpyAsync(c->psi_old, c->ui(L, L.u), bytes, hipMemcpyDeviceToDevice, c->s));
     const double h = 1.0 / (double)L.p.nx;  // cpu.lua:197-198
-    TRY(cycle_rec(c, 0, h, c->o.cycle == MGP_CYCLE_F));
-    const bool fused_done = fuse && c->err_done;
-    if (fuse && !fused_done) return c->fail(MGP_ERR_STATE, "internal: fused err launch did not run");
-    c->err_old = nullptr;
-    if (fused_done) {
-        if (c->o.world > 1)
-            NCCL_TRY(c, ncclAllReduce(c->d_errs + slot, c->d_errs + slot, 1, ncclDouble, ncclSum, c->comm, c->s));
-    } else if (c->o.err_mode) {
+    c->in_cycle = true;
+    int rc = cycle_rec(c, 0, h, c->o.cycle == MGP_CYCLE_F);
+    c->in_cycle = false;
+    TRY(rc);
+    if (fuse && !c->err_done) return c->fail(MGP_ERR_STATE, "internal: fused err launch did not run");
+    if (c->o.err_mode && !fuse) {
         Level& L0 = c->lev[0];
-        HIP_TRY(c, mgp::launch_sqdiff_sum(c->rb, c->ui(L0, L0.u), c->psi_old, L0.g.plane * L0.g.nz, c->d_part,
+        HIP_TRY(c, mgp::launch_sqdiff_sum(c->rb, c->ui(L0, L0.u), c->psi_old, L0.g.P * L0.g.nz, c->d_part,
                                           c->d_errs + slot, c->s));
-        if (c->o.world > 1)
-            NCCL_TRY(c, ncclAllReduce(c->d_errs + slot, c->d_errs + slot, 1, ncclDouble, ncclSum, c->comm, c->s));
     }
+    if (c->o.err_mode && c->o.world > 1)
+        NCCL_TRY(c, ncclAllReduce(c->d_errs + slot, c->d_errs + slot, 1, ncclDouble, ncclSum, c->comm, c->s));
     return MGP_OK;
 }
 
@@ -467,7 +438,6 @@ int sync_and_check(mgp_ctx* c)
 // =====================================================================================
 // C ABI
 // =====================================================================================
-
 extern "C" {
 
 int mgp_version(void) { return MGP_API_VERSION; }
@@ -530,6 +500,7 @@ int mgp_plan(const mgp_opts* o, int64_t* rows, int max_levels)
     return (int)plan.size();
 }
 
+
 static void destroy_impl(mgp_ctx* c)
 {
     if (!c) return;
@@ -538,9 +509,9 @@ static void destroy_impl(mgp_ctx* c)
         if (L.u) (void)hipFree(L.u);
         if (L.f) (void)hipFree(L.f);
         if (L.t) (void)hipFree(L.t);
-        if (L.w) (void)hipFree(L.w);
     }
     if (c->psi_old) (void)hipFree(c->psi_old);
+    if (c->stage) (void)hipFree(c->stage);
     if (c->d_part) (void)hipFree(c->d_part);
     if (c->d_errs) (void)hipFree(c->d_errs);
     for (auto e : c->ev) (void)hipEventDestroy(e);
@@ -565,9 +536,6 @@ int mgp_create(mgp_ctx** out, const mgp_opts* o)
     if (c->o.dim == 2) c->o.n[2] = 1;
     c->rb = o->real_bytes;
     c->G = o->dim == 3 ? mgp::kGhost3D : 0;
-    if (const char* v = std::getenv("MGP_KC")) c->kc = std::max(1, std::atoi(v));
-    if (const char* v = std::getenv("MGP_TY")) c->ty = std::atoi(v) == 8 ? 8 : 16;
-    if (const char* v = std::getenv("MGP_NH")) c->nh_max = std::atoi(v) >= 4 ? 4 : 2;
     auto bail = [&](int code) {
         g_create_error = c->err;
         destroy_impl(c);
@@ -600,21 +568,15 @@ int mgp_create(mgp_ctx** out, const mgp_opts* o)
     for (auto& p : plan) {
         Level L;
         L.p = p;
-        L.g.nx = (int)p.nx;
-        L.g.ny = (int)p.ny;
-        L.g.lx = ilog2(p.nx);
-        L.g.ly = ilog2(p.ny);
-        L.g.nz = p.nz;
-        L.g.plane = p.nx * p.ny;
-        L.g.z0 = p.z0;
-        L.g.gnz = p.gnz;
-        L.alloc = L.g.plane * (p.nz + 2 * c->G);
+        L.g = make_geo(p, c->o.dim);
+        L.alloc = L.g.P * (L.g.nz + 2 * c->G);
         c->lev.push_back(L);
     }
+    c->err_fuse = c->o.err_mode && c->o.smoother == MGP_RBGS && c->o.nu1 >= 1 && c->o.nu2 >= 1 && c->lev.size() > 1;
     for (size_t l = 0; l < c->lev.size(); ++l) {
         Level& L = c->lev[l];
         const size_t bytes = (size_t)L.alloc * rb;
-        const bool need_t = c->o.smoother == MGP_JACOBI || c->o.dim == 3;
+        const bool need_t = c->o.smoother == MGP_JACOBI || (l == 0 && c->err_fuse);
         if (hipMalloc(&L.u, bytes) != hipSuccess || hipMalloc(&L.f, bytes) != hipSuccess ||
             (need_t && hipMalloc(&L.t, bytes) != hipSuccess)) {
             c->err = "hipMalloc failed for level " + std::to_string(l) + " (" + std::to_string(bytes) + " bytes)";
@@ -627,22 +589,17 @@ int mgp_create(mgp_ctx** out, const mgp_opts* o)
             return bail(MGP_ERR_HIP);
         }
     }
-    Level& L0 = c->lev[0];
-    c->err_fuse = c->o.err_mode && fused_ok(c, L0) && c->o.nu1 >= 1 && c->o.nu2 >= 1 && c->lev.size() > 1;
-    if (c->err_fuse) {
-        const size_t bytes = (size_t)L0.alloc * rb;
-        if (hipMalloc(&L0.w, bytes) != hipSuccess || hipMemsetAsync(L0.w, 0, bytes, c->s) != hipSuccess) {
-            c->err = "hipMalloc failed for the third finest-level buffer";
-            return bail(MGP_ERR_OOM);
-        }
-    } else if (c->o.err_mode) {
-        if (hipMalloc(&c->psi_old, (size_t)(L0.g.plane * L0.g.nz) * rb) != hipSuccess) {
-            c->err = "hipMalloc failed for psiOld";
-            return bail(MGP_ERR_OOM);
-        }
+    const Level& L0 = c->lev[0];
+    const size_t interior = (size_t)(L0.g.P * L0.g.nz) * rb;
+    if (c->o.err_mode && !c->err_fuse && hipMalloc(&c->psi_old, interior) != hipSuccess) {
+        c->err = "hipMalloc failed for psiOld";
+        return bail(MGP_ERR_OOM);
     }
-    c->part_cap = mgp::kSumBlocks;
-    if (fused_ok(c, L0)) c->part_cap = std::max<int64_t>(c->part_cap, mgp::fused3d_blocks(L0.g, c->ty, c->kc));
+    if (hipMalloc(&c->stage, interior) != hipSuccess) {
+        c->err = "hipMalloc failed for the staging buffer";
+        return bail(MGP_ERR_OOM);
+    }
+    c->part_cap = std::max<int64_t>(mgp::kSumBlocks, 2 * (int64_t)mgp::half_blocks(c->rb, L0.g));
     if (hipMalloc(&c->d_part, sizeof(double) * c->part_cap) != hipSuccess) {
         c->err = "hipMalloc failed for reduction partials";
         return bail(MGP_ERR_OOM);
@@ -698,14 +655,21 @@ int mgp_init_point_charge(mgp_ctx* c)
     return sync_and_check(c);
 }
 
+static int64_t level_count(const Level& L) { return L.p.nx * L.p.ny * (L.g.nz); }
+
 int mgp_set_field(mgp_ctx* c, int level, int which, const void* src, int64_t count, int mem)
 {
     if (!c || !src || check_level(c, level) != MGP_OK || (which != MGP_FIELD_U && which != MGP_FIELD_F))
         return c ? c->fail(MGP_ERR_ARG, "mgp_set_field: bad argument") : MGP_ERR_ARG;
     Level& L = c->lev[level];
-    if (count != L.g.plane * L.g.nz) return c->fail(MGP_ERR_ARG, "mgp_set_field: count %lld != %lld", (long long)count, (long long)(L.g.plane * L.g.nz));
-    char* dst = c->ui(L, which == MGP_FIELD_U ? L.u : L.f);
-    HIP_TRY(c, hipMemcpyAsync(dst, src, (size_t)count * c->rb, mem == MGP_MEM_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, c->s));
+    if (count != level_count(L))
+        return c->fail(MGP_ERR_ARG, "mgp_set_field: count %lld != %lld", (long long)count, (long long)level_count(L));
+    const void* lex = src;
+    if (mem != MGP_MEM_DEVICE) {
+        HIP_TRY(c, hipMemcpyAsync(c->stage, src, (size_t)count * c->rb, hipMemcpyHostToDevice, c->s));
+        lex = c->stage;
+    }
+    HIP_TRY(c, mgp::launch_pack(c->rb, lex, c->ui(L, which == MGP_FIELD_U ? L.u : L.f), L.g, c->s));
     if (which == MGP_FIELD_U) L.ghost_ok = !L.p.dist;
     else L.fghost_ok = !L.p.dist;
     return sync_and_check(c);
@@ -717,9 +681,12 @@ int mgp_get_field(const mgp_ctx* cc, int level, int which, void* dst, int64_t co
     if (!c || !dst || check_level(c, level) != MGP_OK || (which != MGP_FIELD_U && which != MGP_FIELD_F))
         return c ? c->fail(MGP_ERR_ARG, "mgp_get_field: bad argument") : MGP_ERR_ARG;
     Level& L = c->lev[level];
-    if (count != L.g.plane * L.g.nz) return c->fail(MGP_ERR_ARG, "mgp_get_field: count %lld != %lld", (long long)count, (long long)(L.g.plane * L.g.nz));
-    const char* srcp = c->ui(L, which == MGP_FIELD_U ? L.u : L.f);
-    HIP_TRY(c, hipMemcpyAsync(dst, srcp, (size_t)count * c->rb, mem == MGP_MEM_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, c->s));
+    if (count != level_count(L))
+        return c->fail(MGP_ERR_ARG, "mgp_get_field: count %lld != %lld", (long long)count, (long long)level_count(L));
+    void* lex = mem == MGP_MEM_DEVICE ? dst : c->stage;
+    HIP_TRY(c, mgp::launch_unpack(c->rb, c->ui(L, which == MGP_FIELD_U ? L.u : L.f), lex, L.g, c->s));
+    if (mem != MGP_MEM_DEVICE)
+        HIP_TRY(c, hipMemcpyAsync(dst, c->stage, (size_t)count * c->rb, hipMemcpyDeviceToHost, c->s));
     return sync_and_check(c);
 }
 
@@ -757,7 +724,7 @@ int mgp_two_grid(mgp_ctx* c, double h, void* u, const void* f, int64_t L, int me
     for (int l = 0; l < (int)c->lev.size(); ++l) {
         Level& Lv = c->lev[l];
         if (Lv.p.nx != L) continue;
-        const int64_t n = Lv.g.plane * Lv.g.nz;
+        const int64_t n = level_count(Lv);
         TRY(mgp_set_field(c, l, MGP_FIELD_U, u, n, mem));
         TRY(mgp_set_field(c, l, MGP_FIELD_F, f, n, mem));
         TRY(cycle_rec(c, l, h, c->o.cycle == MGP_CYCLE_F));

@@ -6,57 +6,58 @@
 
 namespace mgp {
 
-// Geometry of one level as seen by this rank.  Arrays are x fastest; a 3D level carries one
-// ghost plane below and above its nz local planes (zeros at the physical boundary, the
-// neighbour rank's plane on a slab boundary).  Kernels receive the INTERIOR pointer (plane 0).
+// Device layout of one level ("red/black packed").  A level is a stack of planes (one plane in
+// 2D).  Each plane holds its red cells ((i + j + gk) even) in the first half and its black cells
+// in the second half; a half is ny rows of hw = max(1, nx/2) cells and cell (i, j) sits at
+// m = i >> 1 of its row.  Every stencil neighbour of a cell has the other colour, at
+// m - 1 + (i & 1) and m + (i & 1) for x-1 / x+1 and at m for y +- 1, z +- 1, so a half-sweep is a
+// plain streaming stencil over one half reading the other half.  3D levels carry one ghost plane
+// below and above (zeros at the physical boundary, the neighbour rank's plane across a slab
+// edge); kernels receive pointers to interior plane 0.
 struct Geo {
-    int nx, ny;     // in-plane cells (powers of two)
+    int nx, ny;     // cells per row / rows per plane (powers of two)
     int lx, ly;     // log2(nx), log2(ny)
+    int hw, lhw;    // cells per half row = max(1, nx / 2), log2(hw)
     int64_t nz;     // local planes (1 in 2D)
-    int64_t plane;  // nx * ny
+    int64_t H;      // cells per half plane = hw * ny
+    int64_t P;      // plane stride = 2 H
     int64_t z0;     // global index of local plane 0
-    int64_t gnz;    // global planes of this level
+    int64_t gnz;    // global planes of this level (1 in 2D)
 };
 
-// All launchers enqueue on `s` and return hipGetLastError() of the launch.
-// rb = sizeof(real) (4 or 8), dim = 2 or 3.  `fine` selects the finest-level instantiation
-// (a distinct symbol, so that rocprofv3 reports the finest smoother separately).
-hipError_t launch_init_point_charge(int rb, int dim, void* u, void* f, Geo g, int64_t cx,
-                                    int64_t cy, int64_t cz, hipStream_t s);
-hipError_t launch_jacobi(int rb, int dim, bool fine, const void* u, const void* f, void* out,
-                         Geo g, double h, double cl, hipStream_t s);
-hipError_t launch_rb_half(int rb, int dim, bool fine, void* u, const void* f, Geo g, int color,
-                          double h, double cl, hipStream_t s);
-// R points at the coarse cell that corresponds to this rank's local fine plane 0.
-hipError_t launch_residual_restrict(int rb, int dim, const void* u, const void* f, void* R, Geo g,
-                                    double h, double cl, hipStream_t s);
-// V points at the coarse interior plane that corresponds to global coarse index gc.z0; its
-// planes -1 and gc.nz must be readable (ghosts / neighbours' planes) for the linear kind.
-hipError_t launch_prolong_correct(int rb, int dim, int linear, void* u, const void* V, Geo g,
-                                  Geo gc, double clc, hipStream_t s);
-// Deterministic two-pass sum of (a - b)^2 in double into *out (overwrites).
-hipError_t launch_sqdiff_sum(int rb, const void* a, const void* b, int64_t n, double* partials,
-                             double* out, hipStream_t s);
+// Launchers enqueue on `s` and return the launch's hipGetLastError().  rb = sizeof(real),
+// dim = 2 or 3.  `fine` selects the finest-level instantiation (a distinct symbol, so rocprofv3
+// reports the finest smoother on its own line).
 
-// Fused out-of-place red/black sweeps of a 3D level (mgp_rbgs3d.hip): nh half-sweeps (2 or 4)
-// per launch; needs nh ghost planes of u and f (zeros at a physical boundary).
-// ty = tile height (8 or 16 rows of 64 cells).  With old != nullptr the launch also writes one fp64
-// partial of sum (uout - old)^2 per workgroup to partials[0 .. fused3d_blocks()).
-int fused3d_blocks(Geo g, int ty, int kc);
-bool rbgs_fused3d_supported(int rb, int nh, int ty, Geo g);
-hipError_t launch_rbgs_fused3d(int rb, bool fine, int nh, int ty, const void* uin, const void* f, void* uout,
-                               const void* old, double* partials, Geo g, int kc, double h, double cl, hipStream_t s);
-// LDS-tiled fused residual + 2x2x2 restriction of a 3D level (nx % 64 == 0, ny % 16 == 0, even nz).
-bool residual_restrict3d_supported(Geo g);
-hipError_t launch_residual_restrict3d(int rb, const void* u, const void* f, void* R, Geo g, double h, double cl,
-                                      hipStream_t s);
-// Vectorised 3D prolongation + correction (4 fine x-cells per thread; nx >= 4).
-bool prolong3d_x4_supported(Geo g);
-hipError_t launch_prolong3d_x4(int rb, int linear, void* u, const void* V, Geo g, Geo gc, double clc, hipStream_t s);
+// f = -1e6 at global (cx, cy, cz), 0 elsewhere; u = -f (cpu.lua:180-193).
+hipError_t launch_init_point_charge(int rb, int dim, void* u, void* f, Geo g, int64_t cx, int64_t cy,
+                                    int64_t cz, hipStream_t s);
+// lexicographic (x fastest, this rank's planes) <-> packed
+hipError_t launch_pack(int rb, const void* lex, void* packed, Geo g, hipStream_t s);
+hipError_t launch_unpack(int rb, const void* packed, void* lex, Geo g, hipStream_t s);
+
+// One colour of a red/black sweep: dst(colour c) = relax(other(1-c), f) (cpu.lua:40-54 update).
+// other and dst may be the same buffer (in place) or different (out of place: Jacobi, the first
+// sweep of a cycle).  With old != nullptr, sum (dst - old)^2 over colour c goes to one fp64
+// partial per workgroup in partials[0 .. half_blocks()).
+int half_blocks(int rb, Geo g);
+hipError_t launch_half_sweep(int rb, int dim, bool fine, int color, const void* other, const void* f, void* dst,
+                             const void* old, double* partials, Geo g, double h, double cl, hipStream_t s);
+// Fused residual + restriction (calcResidual + reduceResidual): R (coarse packed, pointing at the
+// coarse plane of this rank's fine plane 0; its Geo is gc) from u, f of the fine level.
+hipError_t launch_residual_restrict(int rb, int dim, const void* u, const void* f, void* R, Geo g, Geo gc, double h,
+                                    double cl, hipStream_t s);
+// u += P V (expandResidual + addTo); V points at the coarse plane gc.z0, which must correspond to
+// this rank's fine plane 0; planes -1 and gc.nz of V must be readable for the linear kind.
+hipError_t launch_prolong_correct(int rb, int dim, int linear, void* u, const void* V, Geo g, Geo gc, double clc,
+                                  hipStream_t s);
+// Deterministic two-pass fp64 sum of (a - b)^2 over n elements into *out.
+hipError_t launch_sqdiff_sum(int rb, const void* a, const void* b, int64_t n, double* partials, double* out,
+                             hipStream_t s);
 // Fixed-order fp64 sum of n partials into *out (one workgroup).
 hipError_t launch_sum_partials(const double* partials, int n, double* out, hipStream_t s);
 
 constexpr int kSumBlocks = 1024;
-constexpr int kGhost3D = 4;  // ghost planes per side of every 3D level (= max nh)
+constexpr int kGhost3D = 1;  // ghost planes per side of every 3D level
 
 }  // namespace mgp

@@ -76,15 +76,13 @@ def test_smoother_kernel(smoother, dim, n, real, level, bc):
     assert np.array_equal(ctx.get_psi(level), ref)
 
 
-@pytest.mark.parametrize("box", [(64, 64, 64), (128, 64, 32), (64, 128, 256), (256, 256, 8)])
+@pytest.mark.parametrize("box", [(64, 64, 64), (128, 64, 32), (64, 128, 256), (256, 256, 8), (8, 4, 2), (4, 8, 16)])
 @pytest.mark.parametrize("real", ["double", "float"])
 @pytest.mark.parametrize("sweeps", [1, 2, 3])
-@pytest.mark.parametrize("kc", ["32", "7"])
 @pytest.mark.parametrize("bc", ["zero", "consistent"])
-def test_fused_rbgs_sweep_shapes(box, real, sweeps, kc, bc, monkeypatch):
-    """The LDS-tiled z-marching sweep kernel (2 or 4 half-sweeps per launch, uneven z chunks)
-    equals in-place red/black sweeps of the oracle bit for bit, on cubes and boxes."""
-    monkeypatch.setenv("MGP_KC", kc)
+def test_rbgs_sweep_shapes(box, real, sweeps, bc):
+    """Red/black half-sweeps on the packed layout (vector and scalar kernels) equal in-place
+    red/black sweeps of the oracle bit for bit, on cubes and boxes."""
     ctx = _ctx(dim=3, n=box, real=real, smoother="rbgs", coarse_bc=bc)
     for level in (0, 1):
         shp = ctx.shape(level)
