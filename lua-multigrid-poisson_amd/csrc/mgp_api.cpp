@@ -599,7 +599,8 @@ int mgp_create(mgp_ctx** out, const mgp_opts* o)
         c->err = "hipMalloc failed for the staging buffer";
         return bail(MGP_ERR_OOM);
     }
-    c->part_cap = std::max<int64_t>(mgp::kSumBlocks, 2 * (int64_t)mgp::half_blocks(c->rb, L0.g));
+    const int nb2 = 2 * mgp::half_blocks(c->rb, L0.g);
+    c->part_cap = std::max<int64_t>(mgp::kSumBlocks, nb2 + mgp::sum_scratch(nb2));
     if (hipMalloc(&c->d_part, sizeof(double) * c->part_cap) != hipSuccess) {
         c->err = "hipMalloc failed for reduction partials";
         return bail(MGP_ERR_OOM);

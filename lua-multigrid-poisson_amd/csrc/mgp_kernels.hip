@@ -72,19 +72,12 @@ __device__ __forceinline__ T div_rn(T a, T d, T y)
     return fmaT(r, y, q);
 }
 
-// Level operator constants (oracle: relax(), diag(), residual()).
+// Level operator constants (oracle: relax(), diag(), residual()), computed once on the host in
+// the real type (IEEE host arithmetic gives the same values the oracle computes) and passed by
+// value to every kernel.
 template <typename T, int DIM>
 struct Op {
     T hSq, inv_hSq, adiag, yadiag, cl;
-    __device__ __forceinline__ Op(double h, double cld)
-    {
-        const T hh = (T)h;
-        hSq = hh * hh;
-        inv_hSq = (T)1 / hSq;       // exact: h is a power of two
-        adiag = (T)(-2 * DIM) / hSq;
-        yadiag = (T)1 / adiag;      // RN(1/adiag)
-        cl = (T)cld;
-    }
     // diagonal of a cell with nb faces on the box boundary (cl = 0: the reference adiag)
     __device__ __forceinline__ T diag(int nb) const
     {
@@ -106,6 +99,19 @@ struct Op {
         return fc - a_u;
     }
 };
+
+template <typename T, int DIM>
+Op<T, DIM> make_op(double h, double cl)
+{
+    Op<T, DIM> op;
+    const T hh = (T)h;
+    op.hSq = hh * hh;
+    op.inv_hSq = (T)1 / op.hSq;  // exact: h is a power of two
+    op.adiag = (T)(-2 * DIM) / op.hSq;
+    op.yadiag = (T)1 / op.adiag;  // RN(1/adiag)
+    op.cl = (T)cl;
+    return op;
+}
 
 // packed offset of cell (i, j, local plane k) (any level size, nx = 1 included)
 __device__ __forceinline__ int64_t pidx(const Geo& g, int i, int j, int64_t k)
@@ -193,8 +199,8 @@ __global__ __launch_bounds__(kBlock) void k_unpack(const T* __restrict__ in, T* 
 template <typename T, int DIM, int TAG, bool ERR>
 __global__ __launch_bounds__(kBlock) void k_half(const T* __restrict__ other, const T* __restrict__ f,
                                                  T* __restrict__ dst, const T* __restrict__ old,
-                                                 double* __restrict__ partials, Geo g, int color, double h,
-                                                 double cld)
+                                                 double* __restrict__ partials, Geo g, int color,
+                                                 Op<T, DIM> op)
 {
     constexpr int N = VN<T>::n;
     constexpr int LN = N == 4 ? 2 : 1;
@@ -206,7 +212,6 @@ __global__ __launch_bounds__(kBlock) void k_half(const T* __restrict__ other, co
     const int64_t k = it >> (lgpr + g.ly);
     double acc = 0.0;
     if (k < g.nz) {
-        const Op<T, DIM> op(h, cld);
         const int m0 = grp * N;
         const int64_t gk = g.z0 + k;
         const int o = color ^ (int)((j + gk) & 1);  // x parity of this row's colour-c cells
@@ -260,8 +265,8 @@ __global__ __launch_bounds__(kBlock) void k_half(const T* __restrict__ other, co
 template <typename T, int DIM, bool ERR>
 __global__ __launch_bounds__(kBlock) void k_half_s(const T* __restrict__ other, const T* __restrict__ f,
                                                    T* __restrict__ dst, const T* __restrict__ old,
-                                                   double* __restrict__ partials, Geo g, int color, double h,
-                                                   double cld)
+                                                   double* __restrict__ partials, Geo g, int color,
+                                                   Op<T, DIM> op)
 {
     const int64_t it = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     const int m = (int)(it & (g.hw - 1));
@@ -273,8 +278,7 @@ __global__ __launch_bounds__(kBlock) void k_half_s(const T* __restrict__ other, 
         const int o = color ^ (int)((j + gk) & 1);
         const int i = 2 * m + o;
         if (i < g.nx) {
-            const Op<T, DIM> op(h, cld);
-            const int64_t own = k * g.P + color * g.H + (int64_t)j * g.hw + m;
+                const int64_t own = k * g.P + color * g.H + (int64_t)j * g.hw + m;
             const int64_t oth = k * g.P + (color ^ 1) * g.H + (int64_t)j * g.hw + m;
             const T xl = i > 0 ? other[oth - 1 + o] : (T)0;
             const T xr = i < g.nx - 1 ? other[oth + o] : (T)0;
@@ -326,7 +330,7 @@ __device__ __forceinline__ T residual_at(const T* __restrict__ u, const T* __res
 // Scalar form: a thread per coarse cell (any sizes).
 template <typename T, int DIM>
 __global__ __launch_bounds__(kBlock) void k_resrestrict_s(const T* __restrict__ u, const T* __restrict__ f,
-                                                          T* __restrict__ R, Geo g, Geo gc, double h, double cld)
+                                                          T* __restrict__ R, Geo g, Geo gc, Op<T, DIM> op)
 {
     const int cx = g.nx >> 1, cy = g.ny >> 1;
     const int lcx = g.lx - 1, lcy = g.ly - 1;
@@ -336,7 +340,6 @@ __global__ __launch_bounds__(kBlock) void k_resrestrict_s(const T* __restrict__ 
     const int I = (int)(it & (cx - 1));
     const int J = (int)((it >> lcx) & (cy - 1));
     const int64_t K = it >> (lcx + lcy);
-    const Op<T, DIM> op(h, cld);
     const int i = 2 * I, j = 2 * J;
     const int64_t k = DIM == 3 ? 2 * K : 0;
     T s = residual_at<T, DIM>(u, f, g, op, i, j, k) + residual_at<T, DIM>(u, f, g, op, i + 1, j, k);
@@ -354,15 +357,17 @@ __global__ __launch_bounds__(kBlock) void k_resrestrict_s(const T* __restrict__ 
 }
 
 // Vector form: a thread owns N consecutive coarse cells I0 .. I0+N-1 of one coarse row.  Their
-// fine children are, in every fine row, the N cells m = I0 .. of BOTH colours; the thread loads
-// each fine row / colour it needs once (N reals per access) and keeps the reference order
+// fine children are, in every fine row, the N cells m = I0 .. of BOTH colours.  The thread loads
+// each fine (plane, row, colour) vector it needs exactly once into registers — planes 2K, 2K+1
+// with rows 2J-1 .. 2J+2, planes 2K-1, 2K+2 with rows 2J, 2J+1 — and keeps the reference order
 //   R = 1/8 (((((((r000 + r100) + r010) + r110) + r001) + r101) + r011) + r111).
 template <typename T, int DIM>
 __global__ __launch_bounds__(kBlock) void k_resrestrict(const T* __restrict__ u, const T* __restrict__ f,
-                                                        T* __restrict__ R, Geo g, Geo gc, double h, double cld)
+                                                        T* __restrict__ R, Geo g, Geo gc, Op<T, DIM> op)
 {
     constexpr int N = VN<T>::n;
     constexpr int LN = N == 4 ? 2 : 1;
+    constexpr int NZ = DIM == 3 ? 2 : 1;  // fine planes per coarse plane
     const int cy = g.ny >> 1;
     const int lgpr = (g.lx - 1) - LN;  // log2 groups of N per coarse row
     const int64_t ncz = DIM == 3 ? (g.nz >> 1) : 1;
@@ -372,52 +377,81 @@ __global__ __launch_bounds__(kBlock) void k_resrestrict(const T* __restrict__ u,
     const int J = (int)((it >> lgpr) & (cy - 1));
     const int64_t K = it >> (lgpr + g.ly - 1);
     if (K >= ncz) return;
-    const Op<T, DIM> op(h, cld);
-    const int m0 = grp * N;  // = I0
+    const int m0 = grp * N;
     const int j0 = 2 * J;
     const int64_t k0 = DIM == 3 ? 2 * K : 0;
-    constexpr int NZ = DIM == 3 ? 2 : 1;
-    // r[dz][dy][x parity][e]
-    T r[NZ][2][2][N];
+
+    const bool xlo = m0 == 0, xhi = m0 + N == g.hw;
+    auto row = [&](int64_t k, int j, int c) {
+        return (j >= 0 && j < g.ny) ? vload<T, N>(u + k * g.P + c * g.H + (int64_t)j * g.hw + m0) : vzero<T, N>();
+    };
+    // running sum in the reference order: the children of fine plane 2K, then of 2K+1
+    T acc[N];
 #pragma unroll
     for (int dz = 0; dz < NZ; ++dz) {
         const int64_t k = k0 + dz;
         const int64_t gk = g.z0 + k;
+        // this plane's rows j0-1 .. j0+2 (both colours) and, in 3D, rows j0, j0+1 of planes k-1, k+1
+        Vec<T, N> M[4][2], Z[2][2][2];
+#pragma unroll
+        for (int yi = 0; yi < 4; ++yi)
+#pragma unroll
+            for (int c = 0; c < 2; ++c) M[yi][c] = row(k, j0 - 1 + yi, c);
+        if (DIM == 3) {
+#pragma unroll
+            for (int zz = 0; zz < 2; ++zz)
+#pragma unroll
+                for (int yi = 0; yi < 2; ++yi)
+#pragma unroll
+                    for (int c = 0; c < 2; ++c) Z[zz][yi][c] = row(k - 1 + 2 * zz, j0 + yi, c);
+        }
 #pragma unroll
         for (int dy = 0; dy < 2; ++dy) {
             const int j = j0 + dy;
             const int p = (int)((j + gk) & 1);
             const int nbyz = (j == 0) + (j == g.ny - 1) + (DIM == 3 ? (gk == 0) + (gk == g.gnz - 1) : 0);
+            const bool fast = op.cl == (T)0 || (nbyz == 0 && !xlo && !xhi);
+            T rr[2][N];  // [x parity][e]
 #pragma unroll
             for (int c = 0; c < 2; ++c) {
                 const int o = c ^ p;
+                const int oc = c ^ 1;
+                const Vec<T, N>& cen = M[dy + 1][oc];
+                const Vec<T, N>& uc = M[dy + 1][c];
                 const int64_t own = k * g.P + c * g.H + (int64_t)j * g.hw + m0;
-                const int64_t oth = k * g.P + (c ^ 1) * g.H + (int64_t)j * g.hw + m0;
-                const Vec<T, N> cen = vload<T, N>(u + oth);
-                const T edge = o == 0 ? (m0 > 0 ? u[oth - 1] : (T)0) : (m0 + N < g.hw ? u[oth + N] : (T)0);
-                const Vec<T, N> yl = j > 0 ? vload<T, N>(u + oth - g.hw) : vzero<T, N>();
-                const Vec<T, N> yr = j < g.ny - 1 ? vload<T, N>(u + oth + g.hw) : vzero<T, N>();
-                Vec<T, N> zl, zr;
-                if (DIM == 3) {
-                    zl = vload<T, N>(u + oth - g.P);
-                    zr = vload<T, N>(u + oth + g.P);
-                }
-                const Vec<T, N> uc = vload<T, N>(u + own);
+                const int64_t oth = k * g.P + oc * g.H + (int64_t)j * g.hw + m0;
                 const Vec<T, N> fv = vload<T, N>(f + own);
+                const T edge = o == 0 ? (xlo ? (T)0 : u[oth - 1]) : (xhi ? (T)0 : u[oth + N]);
 #pragma unroll
                 for (int e = 0; e < N; ++e) {
-                    const int i = 2 * (m0 + e) + o;
                     const T xl = o == 0 ? (e == 0 ? edge : cen.v[e - 1]) : cen.v[e];
                     const T xr = o == 0 ? cen.v[e] : (e == N - 1 ? edge : cen.v[e + 1]);
                     T s = xl + xr;
-                    s = s + yl.v[e];
-                    s = s + yr.v[e];
+                    s = s + M[dy][oc].v[e];
+                    s = s + M[dy + 2][oc].v[e];
                     if (DIM == 3) {
-                        s = s + zl.v[e];
-                        s = s + zr.v[e];
+                        s = s + Z[0][dy][oc].v[e];
+                        s = s + Z[1][dy][oc].v[e];
                     }
-                    const int nb = nbyz + (i == 0) + (i == g.nx - 1);
-                    r[dz][dy][o][e] = op.residual(s, fv.v[e], uc.v[e], nb);
+                    T res;
+                    if (fast) {
+                        const T askew = s * op.inv_hSq;
+                        const T a_u = askew + op.adiag * uc.v[e];
+                        res = fv.v[e] - a_u;
+                    } else {
+                        const int i = 2 * (m0 + e) + o;
+                        res = op.residual(s, fv.v[e], uc.v[e], nbyz + (i == 0) + (i == g.nx - 1));
+                    }
+                    rr[o][e] = res;
+                }
+            }
+#pragma unroll
+            for (int e = 0; e < N; ++e) {
+                if (dz == 0 && dy == 0) {
+                    acc[e] = rr[0][e] + rr[1][e];
+                } else {
+                    acc[e] = acc[e] + rr[0][e];
+                    acc[e] = acc[e] + rr[1][e];
                 }
             }
         }
@@ -425,24 +459,14 @@ __global__ __launch_bounds__(kBlock) void k_resrestrict(const T* __restrict__ u,
     // coarse cells I0 + e: colour (I0 + e + J + gK) & 1, packed position (I0 + e) >> 1
     const int64_t gK = gc.z0 + K;
     const int pc = (int)((J + gK) & 1);
+    T val[N];
+#pragma unroll
+    for (int e = 0; e < N; ++e) val[e] = (DIM == 3 ? (T)0.125 : (T)0.25) * acc[e];
+    const int64_t rowc = K * gc.P + (int64_t)J * gc.hw;
 #pragma unroll
     for (int e = 0; e < N; ++e) {
-        T s = r[0][0][0][e] + r[0][0][1][e];
-        s = s + r[0][1][0][e];
-        s = s + r[0][1][1][e];
-        T val;
-        if (DIM == 3) {
-            s = s + r[1][0][0][e];
-            s = s + r[1][0][1][e];
-            s = s + r[1][1][0][e];
-            s = s + r[1][1][1][e];
-            val = (T)0.125 * s;
-        } else {
-            val = (T)0.25 * s;
-        }
         const int I = m0 + e;
-        const int cc = (I + pc) & 1;
-        R[K * gc.P + cc * gc.H + (int64_t)J * gc.hw + (I >> 1)] = val;
+        R[rowc + ((I + pc) & 1) * gc.H + (I >> 1)] = val[e];
     }
 }
 
@@ -510,100 +534,132 @@ __global__ __launch_bounds__(kBlock) void k_prolong(T* __restrict__ u, const T* 
     u[own] = u[own] + v;
 }
 
-// Vector form (fine hw % N == 0, coarse nx >= N): a thread owns N consecutive fine cells of one
-// colour in one row; their parents are the N consecutive coarse cells I = m0 .. m0+N-1 of coarse
-// row (J, K), whose packed positions alternate colour, and the linear neighbours In = I - 1 + 2o.
+// Coarse samples x = I0-1 .. I0+N of coarse row (Jr, Kr) (Kr relative to the V pointer) into
+// c[0 .. N+1]; samples outside the row are 0 (never used: the caller clamps to the parent).
+// In the packed layout I0 .. I0+N-1 sit pairwise in the two halves at (I0 >> 1) ..: two 2-wide
+// loads for fp32, plus the two edge samples.
+template <typename T, int N>
+__device__ __forceinline__ void coarse_row(const T* __restrict__ V, const Geo& gc, int Jr, int64_t Kr, int I0,
+                                           T (&c)[N + 2])
+{
+    const int pc = (int)((Jr + gc.z0 + Kr) & 1);  // colour of even x in this row
+    const int64_t row = Kr * gc.P + (int64_t)Jr * gc.hw;
+    const T* hp = V + row + pc * gc.H;        // colour of I0, I0+2, ...
+    const T* hq = V + row + (pc ^ 1) * gc.H;  // colour of I0+1, I0+3, ...
+    const int cm = I0 >> 1;
+    if (N == 4) {
+        const Vec<T, 2> a = vload<T, 2>(hp + cm);
+        const Vec<T, 2> b = vload<T, 2>(hq + cm);
+        c[1] = a.v[0];
+        c[2] = b.v[0];
+        c[3] = a.v[1];
+        c[4] = b.v[1];
+    } else {
+#pragma unroll
+        for (int e = 0; e < N; ++e) c[e + 1] = ((e & 1) ? hq : hp)[cm + (e >> 1)];
+    }
+    c[0] = I0 > 0 ? hq[cm - 1] : (T)0;
+    c[N + 1] = I0 + N < gc.nx ? hp[cm + N / 2] : (T)0;
+}
+
+// Vector form (coarse nx >= N): a thread owns the fine cells of one fine row (j, k) above N
+// consecutive coarse cells I0 .. — fine m = I0 .. in BOTH colours (one N-wide access of u each).
+// It needs the coarse rows J, Jn and planes K, Kn only (Jn, Kn clamped to the parent row/plane
+// outside the box, where the oracle's cval() factor applies) and evaluates exactly the oracle's
+// per-cell expression.
 template <typename T, int DIM, int LINEAR>
 __global__ __launch_bounds__(kBlock) void k_prolong_v(T* __restrict__ u, const T* __restrict__ V, Geo g, Geo gc,
-                                                      double clc, int color)
+                                                      T cl)
 {
     constexpr int N = VN<T>::n;
     constexpr int LN = N == 4 ? 2 : 1;
+    const int cx = gc.nx, cy = gc.ny;
+    const int lgpr = gc.lx - LN;
     const int b = xcd_remap(blockIdx.x, gridDim.x);
     const int64_t it = (int64_t)b * kBlock + threadIdx.x;
-    const int lgpr = g.lhw - LN;
     const int grp = (int)(it & ((1 << lgpr) - 1));
     const int j = (int)((it >> lgpr) & (g.ny - 1));
-    const int64_t k = it >> (lgpr + g.ly);
+    const int64_t k = DIM == 3 ? it >> (lgpr + g.ly) : 0;
     if (k >= g.nz) return;
-    const int m0 = grp * N;
-    const int o = color ^ (int)((j + g.z0 + k) & 1);
-    const int64_t own = k * g.P + color * g.H + (int64_t)j * g.hw + m0;
+    const int I0 = grp * N;
     const int J = j >> 1;
     const int64_t K = DIM == 3 ? (k >> 1) : 0;
-    // coarse row (Jr, Kr): values at I = m0 - 1 + e for e = 0 .. N + 1 (out-of-row entries 0)
-    auto crow = [&](int Jr, int64_t Kr, T (&c)[N + 2]) {
-        const int pc = (int)((Jr + gc.z0 + Kr) & 1);
-        const int64_t base = Kr * gc.P + (int64_t)Jr * gc.hw;
-#pragma unroll
-        for (int e = 0; e < N + 2; ++e) {
-            const int I = m0 - 1 + e;
-            if (I < 0 || I >= gc.nx) {
-                c[e] = (T)0;
-            } else {
-                const int cc = (I + pc) & 1;
-                c[e] = V[base + cc * gc.H + (I >> 1)];
-            }
+    int Jn = (j & 1) ? J + 1 : J - 1;
+    const bool oy = Jn < 0 || Jn >= cy;
+    if (oy) Jn = J;
+    int64_t Kn = K;
+    bool oz = false;
+    if (DIM == 3) {
+        Kn = (k & 1) ? K + 1 : K - 1;
+        oz = gc.z0 + Kn < 0 || gc.z0 + Kn >= gc.gnz;
+        if (oz) Kn = K;
+    }
+    T c00[N + 2], c10[N + 2], c01[N + 2], c11[N + 2];  // [z: K / Kn][y: J / Jn]
+    coarse_row<T, N>(V, gc, J, K, I0, c00);
+    if (LINEAR) {
+        coarse_row<T, N>(V, gc, Jn, K, I0, c10);
+        if (DIM == 3) {
+            coarse_row<T, N>(V, gc, J, Kn, I0, c01);
+            coarse_row<T, N>(V, gc, Jn, Kn, I0, c11);
         }
+    }
+    const T w0 = (T)0.75, w1 = (T)0.25;
+    auto sv = [&](T val, bool fx, bool fy, bool fz) {
+        T s = (T)1;
+        if (fx) s = -cl * s;
+        if (fy) s = -cl * s;
+        if (fz) s = -cl * s;
+        return s == (T)1 ? val : s * val;
     };
-    Vec<T, N> uv = vload<T, N>(u + own);
-    if (!LINEAR) {
-        T c[N + 2];
-        crow(J, K, c);
+    const int p = (int)((j + g.z0 + k) & 1);
+    const bool interior = !oy && !oz && I0 > 0 && I0 + N < cx;
 #pragma unroll
-        for (int e = 0; e < N; ++e) uv.v[e] = uv.v[e] + c[e + 1];
-    } else {
-        const T w0 = (T)0.75, w1 = (T)0.25, cl = (T)clc;
-        int Jn = (j & 1) ? J + 1 : J - 1;
-        const bool oy = Jn < 0 || Jn >= gc.ny;
-        if (oy) Jn = J;
-        int64_t Kn = K;
-        bool oz = false;
-        if (DIM == 3) {
-            Kn = (k & 1) ? K + 1 : K - 1;
-            const int64_t Kng = gc.z0 + Kn;
-            oz = Kng < 0 || Kng >= gc.gnz;
-            if (oz) Kn = K;
-        }
-        T c00[N + 2], c10[N + 2], c01[N + 2], c11[N + 2];
-        crow(J, K, c00);
-        crow(Jn, K, c10);
-        if (DIM == 3) {
-            crow(J, Kn, c01);
-            crow(Jn, Kn, c11);
-        }
-        auto sv = [&](T v, bool ox, bool yy, bool zz) {
-            T s = (T)1;
-            if (ox) s = -cl * s;
-            if (yy) s = -cl * s;
-            if (zz) s = -cl * s;
-            return s == (T)1 ? v : s * v;
-        };
+    for (int c = 0; c < 2; ++c) {
+        const int o = c ^ p;  // x parity of this colour's cells in row j
+        const int64_t own = k * g.P + c * g.H + (int64_t)j * g.hw + I0;
+        Vec<T, N> uv = vload<T, N>(u + own);
 #pragma unroll
         for (int e = 0; e < N; ++e) {
-            const int I = m0 + e;
-            const int In = I - 1 + 2 * o;
-            const bool ox = In < 0 || In >= gc.nx;
-            const int pe = e + 1;                    // parent column in c[]
-            const int ne = ox ? pe : e + 2 * o;      // neighbour column (clamped to the parent)
+            const int pe = e + 1;  // parent I0 + e
             T v;
-            if (DIM == 2) {
-                const T a0 = w0 * sv(c00[pe], false, false, false) + w1 * sv(c00[ne], ox, false, false);
-                const T a1 = w0 * sv(c10[pe], false, oy, false) + w1 * sv(c10[ne], ox, oy, false);
-                v = w0 * a0 + w1 * a1;
+            if (!LINEAR) {
+                v = c00[pe];
+            } else if (interior) {  // no neighbour leaves the box: every factor is 1
+                const T nb00 = o ? c00[e + 2] : c00[e];
+                const T nb10 = o ? c10[e + 2] : c10[e];
+                const T a00 = w0 * c00[pe] + w1 * nb00;
+                const T a10 = w0 * c10[pe] + w1 * nb10;
+                if (DIM == 2) {
+                    v = w0 * a00 + w1 * a10;
+                } else {
+                    const T nb01 = o ? c01[e + 2] : c01[e];
+                    const T nb11 = o ? c11[e + 2] : c11[e];
+                    const T a01 = w0 * c01[pe] + w1 * nb01;
+                    const T a11 = w0 * c11[pe] + w1 * nb11;
+                    const T b0 = w0 * a00 + w1 * a10;
+                    const T b1 = w0 * a01 + w1 * a11;
+                    v = w0 * b0 + w1 * b1;
+                }
             } else {
-                const T a00 = w0 * sv(c00[pe], false, false, false) + w1 * sv(c00[ne], ox, false, false);
-                const T a10 = w0 * sv(c10[pe], false, oy, false) + w1 * sv(c10[ne], ox, oy, false);
-                const T a01 = w0 * sv(c01[pe], false, false, oz) + w1 * sv(c01[ne], ox, false, oz);
-                const T a11 = w0 * sv(c11[pe], false, oy, oz) + w1 * sv(c11[ne], ox, oy, oz);
-                const T b0 = w0 * a00 + w1 * a10;
-                const T b1 = w0 * a01 + w1 * a11;
-                v = w0 * b0 + w1 * b1;
+                const bool ox = (o == 0 && I0 + e == 0) || (o == 1 && I0 + e == cx - 1);
+                // neighbour column: e (o = 0) or e + 2 (o = 1); the parent when out of the box
+                auto col = [&](const T (&cc)[N + 2]) { return ox ? cc[pe] : (o ? cc[e + 2] : cc[e]); };
+                const T a00 = w0 * c00[pe] + w1 * sv(col(c00), ox, false, false);
+                const T a10 = w0 * sv(c10[pe], false, oy, false) + w1 * sv(col(c10), ox, oy, false);
+                if (DIM == 2) {
+                    v = w0 * a00 + w1 * a10;
+                } else {
+                    const T a01 = w0 * sv(c01[pe], false, false, oz) + w1 * sv(col(c01), ox, false, oz);
+                    const T a11 = w0 * sv(c11[pe], false, oy, oz) + w1 * sv(col(c11), ox, oy, oz);
+                    const T b0 = w0 * a00 + w1 * a10;
+                    const T b1 = w0 * a01 + w1 * a11;
+                    v = w0 * b0 + w1 * b1;
+                }
             }
             uv.v[e] = uv.v[e] + v;
         }
+        vstore<T, N>(u + own, uv);
     }
-    vstore<T, N>(u + own, uv);
 }
 
 // ---- reductions -----------------------------------------------------------------------------
@@ -618,6 +674,23 @@ __global__ __launch_bounds__(kBlock) void k_sqdiff_partial(const T* __restrict__
         acc += d * d;
     }
     block_partial<T>(acc, partials);
+}
+
+// First level of a two-level fixed-order sum: block b sums partials [b*chunk, (b+1)*chunk).
+__global__ __launch_bounds__(1024) void k_sum_chunks(const double* __restrict__ partials, int n, int chunk,
+                                                     double* __restrict__ out)
+{
+    __shared__ double sh[1024];
+    const int lo = blockIdx.x * chunk, hi = lo + chunk < n ? lo + chunk : n;
+    double a = 0.0;
+    for (int i = lo + threadIdx.x; i < hi; i += 1024) a += partials[i];
+    sh[threadIdx.x] = a;
+    __syncthreads();
+    for (int w = 512; w > 0; w >>= 1) {
+        if ((int)threadIdx.x < w) sh[threadIdx.x] += sh[threadIdx.x + w];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) out[blockIdx.x] = sh[0];
 }
 
 __global__ __launch_bounds__(1024) void k_sum_n(const double* __restrict__ partials, int n, double* __restrict__ out)
@@ -685,79 +758,98 @@ int half_blocks(int rb, Geo g)
     return (int)nblk(items);
 }
 
+template <typename T, int D>
+static void half_t(bool fine, bool err, bool vec, unsigned nb, int color, const void* other, const void* f, void* dst,
+                   const void* old, double* partials, Geo g, double h, double cl, hipStream_t s)
+{
+    const Op<T, D> op = make_op<T, D>(h, cl);
+    const T* o_ = (const T*)other;
+    const T* f_ = (const T*)f;
+    T* d_ = (T*)dst;
+    const T* w_ = (const T*)old;
+    if (vec) {
+        if (fine) {
+            if (err) k_half<T, D, 1, true><<<nb, kBlock, 0, s>>>(o_, f_, d_, w_, partials, g, color, op);
+            else k_half<T, D, 1, false><<<nb, kBlock, 0, s>>>(o_, f_, d_, w_, partials, g, color, op);
+        } else {
+            if (err) k_half<T, D, 0, true><<<nb, kBlock, 0, s>>>(o_, f_, d_, w_, partials, g, color, op);
+            else k_half<T, D, 0, false><<<nb, kBlock, 0, s>>>(o_, f_, d_, w_, partials, g, color, op);
+        }
+    } else {
+        if (err) k_half_s<T, D, true><<<nb, kBlock, 0, s>>>(o_, f_, d_, w_, partials, g, color, op);
+        else k_half_s<T, D, false><<<nb, kBlock, 0, s>>>(o_, f_, d_, w_, partials, g, color, op);
+    }
+}
+
 hipError_t launch_half_sweep(int rb, int dim, bool fine, int color, const void* other, const void* f, void* dst,
                              const void* old, double* partials, Geo g, double h, double cl, hipStream_t s)
 {
     const unsigned nb = (unsigned)half_blocks(rb, g);
-    const bool err = old != nullptr;
-    if (half_vector(rb, g)) {
-#define HALF(D, TAG, E)                                                                                      \
-    MGP_REAL(rb, (k_half<T, D, TAG, E><<<nb, kBlock, 0, s>>>((const T*)other, (const T*)f, (T*)dst, (const T*)old, \
-                                                             partials, g, color, h, cl)))
-        if (dim == 3) {
-            if (fine) { if (err) HALF(3, 1, true); else HALF(3, 1, false); }
-            else { if (err) HALF(3, 0, true); else HALF(3, 0, false); }
-        } else {
-            if (fine) { if (err) HALF(2, 1, true); else HALF(2, 1, false); }
-            else { if (err) HALF(2, 0, true); else HALF(2, 0, false); }
-        }
-#undef HALF
+    const bool err = old != nullptr, vec = half_vector(rb, g);
+    if (rb == 8) {
+        if (dim == 3) half_t<double, 3>(fine, err, vec, nb, color, other, f, dst, old, partials, g, h, cl, s);
+        else half_t<double, 2>(fine, err, vec, nb, color, other, f, dst, old, partials, g, h, cl, s);
     } else {
-#define HALFS(D, E)                                                                                          \
-    MGP_REAL(rb, (k_half_s<T, D, E><<<nb, kBlock, 0, s>>>((const T*)other, (const T*)f, (T*)dst, (const T*)old, \
-                                                          partials, g, color, h, cl)))
-        if (dim == 3) { if (err) HALFS(3, true); else HALFS(3, false); }
-        else { if (err) HALFS(2, true); else HALFS(2, false); }
-#undef HALFS
+        if (dim == 3) half_t<float, 3>(fine, err, vec, nb, color, other, f, dst, old, partials, g, h, cl, s);
+        else half_t<float, 2>(fine, err, vec, nb, color, other, f, dst, old, partials, g, h, cl, s);
     }
     return hipGetLastError();
+}
+
+template <typename T, int D>
+static void rr_t(const void* u, const void* f, void* R, Geo g, Geo gc, double h, double cl, hipStream_t s)
+{
+    const Op<T, D> op = make_op<T, D>(h, cl);
+    constexpr int n = VN<T>::n;
+    const int cx = g.nx / 2;
+    const int64_t ncz = D == 3 ? g.nz / 2 : 1;
+    if (cx >= n) {
+        const int64_t items = (int64_t)(cx / n) * (g.ny / 2) * ncz;
+        k_resrestrict<T, D><<<nblk(items), kBlock, 0, s>>>((const T*)u, (const T*)f, (T*)R, g, gc, op);
+    } else {
+        const int64_t items = (int64_t)cx * (g.ny / 2) * ncz;
+        k_resrestrict_s<T, D><<<nblk(items), kBlock, 0, s>>>((const T*)u, (const T*)f, (T*)R, g, gc, op);
+    }
 }
 
 hipError_t launch_residual_restrict(int rb, int dim, const void* u, const void* f, void* R, Geo g, Geo gc, double h,
                                     double cl, hipStream_t s)
 {
-    const int n = 16 / rb;
-    const int cx = g.nx / 2;
-    const int64_t ncz = dim == 3 ? g.nz / 2 : 1;
-    if (cx >= n && g.nx >= 2 * n) {
-        const int64_t items = (int64_t)(cx / n) * (g.ny / 2) * ncz;
-        if (dim == 3)
-            MGP_REAL(rb, (k_resrestrict<T, 3><<<nblk(items), kBlock, 0, s>>>((const T*)u, (const T*)f, (T*)R, g, gc, h, cl)));
-        else
-            MGP_REAL(rb, (k_resrestrict<T, 2><<<nblk(items), kBlock, 0, s>>>((const T*)u, (const T*)f, (T*)R, g, gc, h, cl)));
+    if (rb == 8) {
+        if (dim == 3) rr_t<double, 3>(u, f, R, g, gc, h, cl, s);
+        else rr_t<double, 2>(u, f, R, g, gc, h, cl, s);
     } else {
-        const int64_t items = (int64_t)cx * (g.ny / 2) * ncz;
-        if (dim == 3)
-            MGP_REAL(rb, (k_resrestrict_s<T, 3><<<nblk(items), kBlock, 0, s>>>((const T*)u, (const T*)f, (T*)R, g, gc, h, cl)));
-        else
-            MGP_REAL(rb, (k_resrestrict_s<T, 2><<<nblk(items), kBlock, 0, s>>>((const T*)u, (const T*)f, (T*)R, g, gc, h, cl)));
+        if (dim == 3) rr_t<float, 3>(u, f, R, g, gc, h, cl, s);
+        else rr_t<float, 2>(u, f, R, g, gc, h, cl, s);
     }
     return hipGetLastError();
+}
+
+template <typename T, int D>
+static hipError_t pr_t(int linear, void* u, const void* V, Geo g, Geo gc, double clc, hipStream_t s)
+{
+    constexpr int n = VN<T>::n;
+    if (gc.nx >= n) {
+        const int64_t items = (int64_t)(gc.nx / n) * g.ny * g.nz;
+        if (linear) k_prolong_v<T, D, 1><<<nblk(items), kBlock, 0, s>>>((T*)u, (const T*)V, g, gc, (T)clc);
+        else k_prolong_v<T, D, 0><<<nblk(items), kBlock, 0, s>>>((T*)u, (const T*)V, g, gc, (T)clc);
+        return hipGetLastError();
+    }
+    for (int color = 0; color < 2; ++color) {
+        const unsigned nb = nblk(g.H * g.nz);
+        if (linear) k_prolong<T, D, 1><<<nb, kBlock, 0, s>>>((T*)u, (const T*)V, g, gc, clc, color);
+        else k_prolong<T, D, 0><<<nb, kBlock, 0, s>>>((T*)u, (const T*)V, g, gc, clc, color);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
 }
 
 hipError_t launch_prolong_correct(int rb, int dim, int linear, void* u, const void* V, Geo g, Geo gc, double clc,
                                   hipStream_t s)
 {
-    const int n = 16 / rb;
-    const bool vec = g.hw >= n && g.nx >= 2;
-    for (int color = 0; color < 2; ++color) {
-        if (vec) {
-            const unsigned nb = nblk((g.H / n) * g.nz);
-#define PV(D, L) MGP_REAL(rb, (k_prolong_v<T, D, L><<<nb, kBlock, 0, s>>>((T*)u, (const T*)V, g, gc, clc, color)))
-            if (dim == 3) { if (linear) PV(3, 1); else PV(3, 0); }
-            else { if (linear) PV(2, 1); else PV(2, 0); }
-#undef PV
-        } else {
-            const unsigned nb = nblk(g.H * g.nz);
-#define PS(D, L) MGP_REAL(rb, (k_prolong<T, D, L><<<nb, kBlock, 0, s>>>((T*)u, (const T*)V, g, gc, clc, color)))
-            if (dim == 3) { if (linear) PS(3, 1); else PS(3, 0); }
-            else { if (linear) PS(2, 1); else PS(2, 0); }
-#undef PS
-        }
-        hipError_t e = hipGetLastError();
-        if (e != hipSuccess) return e;
-    }
-    return hipSuccess;
+    if (rb == 8) return dim == 3 ? pr_t<double, 3>(linear, u, V, g, gc, clc, s) : pr_t<double, 2>(linear, u, V, g, gc, clc, s);
+    return dim == 3 ? pr_t<float, 3>(linear, u, V, g, gc, clc, s) : pr_t<float, 2>(linear, u, V, g, gc, clc, s);
 }
 
 hipError_t launch_sqdiff_sum(int rb, const void* a, const void* b, int64_t n, double* partials, double* out,
@@ -768,9 +860,19 @@ hipError_t launch_sqdiff_sum(int rb, const void* a, const void* b, int64_t n, do
     return hipGetLastError();
 }
 
+int sum_scratch(int n) { return n <= 8192 ? 0 : (n + 8191) / 8192; }
+
 hipError_t launch_sum_partials(const double* partials, int n, double* out, hipStream_t s)
 {
-    k_sum_n<<<1, 1024, 0, s>>>(partials, n, out);
+    const int nb = sum_scratch(n);
+    if (nb == 0) {
+        k_sum_n<<<1, 1024, 0, s>>>(partials, n, out);
+    } else {
+        // two fixed-order levels; the first level's sums go right after the partials
+        double* mid = const_cast<double*>(partials) + n;
+        k_sum_chunks<<<nb, 1024, 0, s>>>(partials, n, 8192, mid);
+        k_sum_n<<<1, 1024, 0, s>>>(mid, nb, out);
+    }
     return hipGetLastError();
 }
 

@@ -1,0 +1,133 @@
+"""CPU tests of the drop-in boundary: libmgpoisson.so loads, exports every function that
+include/mgpoisson.h declares, agrees on the mgp_opts layout, plans level hierarchies on the host,
+and fails loudly (never silently on a CPU path) when no GPU is present."""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "mgpoisson.h")
+LIB = os.path.join(ROOT, "lua-multigrid-poisson_amd", "mgpoisson", "libmgpoisson.so")
+
+
+def _declared():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(mgp_[a-z_0-9]+)\s*\(", text)))
+
+
+def test_header_declares_the_boundary():
+    names = _declared()
+    for must in ("mgp_create", "mgp_destroy", "mgp_cycle", "mgp_cycles", "mgp_two_grid", "mgp_set_field",
+                 "mgp_get_field", "mgp_init_point_charge", "mgp_last_error", "mgp_plan", "mgp_smooth",
+                 "mgp_residual_restrict", "mgp_prolong_correct", "mgp_coarse_solve", "mgp_comm_unique_id"):
+        assert must in names
+
+
+def test_library_exports_every_declared_symbol():
+    assert os.path.exists(LIB), "build first: python -c 'import __graft_entry__ as g; g.build()'"
+    out = subprocess.run(["nm", "-D", "--defined-only", LIB], capture_output=True, text=True, check=True).stdout
+    exported = set(re.findall(r"\bT (mgp_[a-z_0-9]+)$", out, flags=re.M))
+    missing = [n for n in _declared() if n not in exported]
+    assert not missing, missing
+    lib = ctypes.CDLL(LIB)
+    for n in _declared():
+        assert getattr(lib, n) is not None
+
+
+def test_library_targets_gfx950(tmp_path):
+    """The .hip_fatbin section carries exactly one device code object, for gfx950."""
+    fat = tmp_path / "fat.bin"
+    subprocess.run(["objcopy", "-O", "binary", "--only-section=.hip_fatbin", LIB, str(fat)], check=True)
+    out = subprocess.run(["/opt/rocm/llvm/bin/clang-offload-bundler", "--list", "--type=o", f"--input={fat}"],
+                         capture_output=True, text=True, check=True).stdout.split()
+    dev = [t for t in out if t.startswith("hipv4-")]
+    assert dev == ["hipv4-amdgcn-amd-amdhsa--gfx950"], out
+
+
+def _mg():
+    import mgpoisson
+
+    return mgpoisson
+
+
+def test_opts_struct_layout_matches_header():
+    mg = _mg()
+    o = mg.default_opts()
+    assert o.struct_size == ctypes.sizeof(mg._lib.MGPOpts) == 224
+    # defaults = the reference cpu.lua configuration
+    assert (o.dim, o.real_bytes, o.nu1, o.nu2) == (2, 8, 7, 7)
+    assert (o.smoother, o.cycle, o.prolong, o.coarse_init, o.coarse_bc) == (0, 0, 0, 0, 0)
+    assert mg._lib.lib.mgp_version() == 1
+
+
+def test_plan_single_cube():
+    mg = _mg()
+    rows = mg.plan(mg.make_opts(dim=3, n=(512, 512, 512)))
+    assert [r["nx"] for r in rows] == [512 >> l for l in range(10)]
+    assert rows[-1]["nx"] == rows[-1]["ny"] == rows[-1]["nz_global"] == 1
+    assert not any(r["distributed"] for r in rows)
+
+
+def test_plan_2d_reference_size():
+    mg = _mg()
+    rows = mg.plan(mg.make_opts(dim=2, n=(256, 256, 1)))
+    assert len(rows) == 9 and rows[-1]["nx"] == 1 and all(r["nz_global"] == 1 for r in rows)
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_plan_slab_decomposition(world):
+    """Weak-scaling box 512 x 512 x 512N: slabs of equal planes, agglomeration once a level
+    has <= gather_cells cells, replicated down to the coarsest 1 x 1 x N line."""
+    mg = _mg()
+    plans = [mg.plan(mg.make_opts(dim=3, n=(512, 512, 512 * world), rank=r, world=world, comm_id=b"\0" * 128))
+             for r in range(world)]
+    for r, rows in enumerate(plans):
+        for lv in rows:
+            if lv["distributed"]:
+                assert lv["nz_local"] * world == lv["nz_global"]
+                assert lv["z0"] == r * lv["nz_local"]
+                assert lv["nz_local"] >= 2
+            else:
+                assert lv["nz_local"] == lv["nz_global"] and lv["z0"] == 0
+        dist = [lv["distributed"] for lv in rows]
+        assert dist[0] and not dist[-1]
+        assert dist == sorted(dist, reverse=True)  # once replicated, always replicated
+        first_rep = dist.index(False)
+        lv = rows[first_rep]
+        assert lv["nx"] * lv["ny"] * lv["nz_global"] <= 32768
+        assert rows[-1]["nx"] == 1 and rows[-1]["nz_global"] == world
+    # all ranks agree on the level shapes
+    shapes = {tuple((lv["nx"], lv["ny"], lv["nz_global"]) for lv in rows) for rows in plans}
+    assert len(shapes) == 1
+
+
+@pytest.mark.parametrize("kw,msg", [
+    (dict(dim=2, n=(12, 12, 1)), "powers of two"),
+    (dict(dim=4, n=(8, 8, 8)), "dim"),
+    (dict(dim=3, n=(8, 8, 8), real=3), "real_bytes"),
+    (dict(dim=2, n=(8, 8, 1), world=2, rank=0), "3D"),
+    (dict(dim=3, n=(8, 8, 8), world=8, rank=0), "planes per rank"),
+    (dict(dim=3, n=(8, 8, 8), rank=2, world=2), "rank"),
+])
+def test_plan_rejects_bad_options(kw, msg):
+    mg = _mg()
+    with pytest.raises(mg.MGPError) as ei:
+        mg.plan(mg.make_opts(**kw))
+    assert msg in str(ei.value)
+
+
+def test_create_without_gpu_fails_loudly():
+    import torch
+
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present")
+    mg = _mg()
+    with pytest.raises(mg.MGPError) as ei:
+        mg.Context(mg.make_opts(dim=2, n=(8, 8, 1)))
+    assert "MGP_ERR_HIP" in str(ei.value)
+    with pytest.raises(mg.MGPError):
+        mg.MultigridHIP(size=8)

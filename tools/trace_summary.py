@@ -1,0 +1,30 @@
+#!/usr/bin/env python3
+"""Summarise a rocprofv3 kernel_trace.csv: time per (kernel, grid) and per-cycle wall/busy."""
+import collections
+import csv
+import re
+import sys
+
+path = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/prof/run_kernel_trace.csv"
+rows = list(csv.DictReader(open(path)))
+
+
+def name(r):
+    m = re.search(r"(k_\w+(<[^>]*>)?)", r["Kernel_Name"])
+    return m.group(1) if m else r["Kernel_Name"][:40]
+
+
+d = collections.defaultdict(list)
+for r in rows:
+    d[(name(r), int(r["Grid_Size_X"]))].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+tot = sum(sum(v) for v in d.values())
+for k, v in sorted(d.items(), key=lambda kv: -sum(kv[1]))[:int(sys.argv[2]) if len(sys.argv) > 2 else 30]:
+    print(f"{k[0][:46]:46s} {k[1]:>10d} {len(v):>5d} {sum(v)/len(v):9.1f} us {100*sum(v)/tot:5.1f}%")
+rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+ends = [i for i, r in enumerate(rows) if "k_sum_n" in r["Kernel_Name"]]
+if len(ends) > 6:
+    a, b = ends[-6], ends[-1]
+    seg = rows[a + 1:b + 1]
+    t0, t1 = int(seg[0]["Start_Timestamp"]), int(seg[-1]["End_Timestamp"])
+    busy = sum(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in seg)
+    print(f"per cycle: wall {(t1-t0)/5e6:.3f} ms, busy {busy/5e6:.3f} ms, launches {len(seg)/5:.0f}")
