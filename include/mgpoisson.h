@@ -113,9 +113,11 @@ int         mgp_coarse_solve(mgp_ctx* c);                           /* L == 1 br
 
 int         mgp_sync(mgp_ctx* c);
 /* Finest-level smoother kernel timing with HIP events on the context's stream.  mgp_timing(c, 1)
- * resets and enables; mgp_timing_read returns the summed kernel milliseconds, the number of
- * timed launches and the number of full sweeps they performed (cells * sweeps * 3 * real_bytes
- * is the algorithmic byte count). */
+ * resets and enables (cycles then run eagerly, without hipGraph replay, so each launch can be
+ * bracketed); mgp_timing_read returns the summed kernel milliseconds, the number of timed
+ * launches and the number of full sweeps they performed (cells * sweeps * 3 * real_bytes is the
+ * algorithmic byte count).  Timed launches are the plain finest-level smoother half-sweeps; the
+ * err-fused last half-sweeps of a cycle (which also read psiOld) are not timed. */
 int         mgp_timing(mgp_ctx* c, int enable);
 int         mgp_timing_read(mgp_ctx* c, double* ms_total, int64_t* launches, double* sweeps);
 

@@ -131,7 +131,16 @@ struct mgp_ctx {
     bool in_cycle = false;  // a one_cycle() is running (level-0 first sweep goes out of place)
     bool first_done = false;
     bool err_done = false;
-    int err_slot = 0;
+    // hipGraph replay of whole cycles (single GPU): one instantiated graph per pointer state of
+    // the level buffers (the finest level alternates u/t every cycle), err written to d_err_cur
+    struct GraphEntry {
+        std::vector<char*> pre, post;
+        hipGraphExec_t exec = nullptr;
+    };
+    bool use_graph = false;
+    std::vector<GraphEntry> graphs;
+    double* d_err_cur = nullptr;
+    double* err_dst = nullptr;  // where this cycle's sum of squares goes
     std::string err;
     // finest-smoother timing
     bool timing = false;
@@ -264,8 +273,10 @@ int timed_end(mgp_ctx* c, hipEvent_t e1, double sweeps)
 int half(mgp_ctx* c, int l, int color, char* other, char* dst, const char* old, double h, double cl, int part_off)
 {
     Level& L = c->lev[l];
+    // only the plain finest half-sweep (k_half<T, dim, 1, false>) is timed, so the event total
+    // matches that kernel's rocprofv3 row; the err-fused variant reads psiOld as well
     hipEvent_t e;
-    TRY(timed_begin(c, l, &e));
+    TRY(timed_begin(c, old ? -1 : l, &e));
     HIP_TRY(c, mgp::launch_half_sweep(c->rb, c->o.dim, l == 0, color, c->ui(L, other), c->ui(L, L.f), c->ui(L, dst),
                                       old ? c->ui(L, (char*)old) : nullptr, c->d_part + part_off, L.g, h, cl, c->s));
     TRY(timed_end(c, e, 0.5));
@@ -303,7 +314,7 @@ int smooth(mgp_ctx* c, int l, int sweeps, double h, bool want_err = false)
         }
         L.ghost_ok = !L.p.dist;
         if (last_err) {
-            HIP_TRY(c, mgp::launch_sum_partials(c->d_part, 2 * nb, c->d_errs + c->err_slot, c->s));
+            HIP_TRY(c, mgp::launch_sum_partials(c->d_part, 2 * nb, c->err_dst, c->s));
             c->err_done = true;
         }
     }
@@ -380,12 +391,13 @@ int cycle_rec(mgp_ctx* c, int l, double h, bool fcycle)
     return MGP_OK;
 }
 
-int one_cycle(mgp_ctx* c, int slot)
+// One outer iteration; err (sum of squares) goes to *dst.
+int one_cycle(mgp_ctx* c, double* dst)
 {
     Level& L = c->lev[0];
     const size_t bytes = (size_t)(L.g.P * L.g.nz) * c->rb;
     const bool fuse = c->o.err_mode && c->err_fuse;
-    c->err_slot = slot;
+    c->err_dst = dst;
     c->err_done = false;
     c->first_done = false;
     if (c->o.err_mode && !fuse)
@@ -398,11 +410,64 @@ int one_cycle(mgp_ctx* c, int slot)
     if (fuse && !c->err_done) return c->fail(MGP_ERR_STATE, "internal: fused err launch did not run");
     if (c->o.err_mode && !fuse) {
         Level& L0 = c->lev[0];
-        HIP_TRY(c, mgp::launch_sqdiff_sum(c->rb, c->ui(L0, L0.u), c->psi_old, L0.g.P * L0.g.nz, c->d_part,
-                                          c->d_errs + slot, c->s));
+        HIP_TRY(c, mgp::launch_sqdiff_sum(c->rb, c->ui(L0, L0.u), c->psi_old, L0.g.P * L0.g.nz, c->d_part, dst,
+                                          c->s));
     }
     if (c->o.err_mode && c->o.world > 1)
-        NCCL_TRY(c, ncclAllReduce(c->d_errs + slot, c->d_errs + slot, 1, ncclDouble, ncclSum, c->comm, c->s));
+        NCCL_TRY(c, ncclAllReduce(dst, dst, 1, ncclDouble, ncclSum, c->comm, c->s));
+    return MGP_OK;
+}
+
+std::vector<char*> level_state(const mgp_ctx* c)
+{
+    std::vector<char*> v;
+    for (const auto& L : c->lev) {
+        v.push_back(L.u);
+        v.push_back(L.t);
+    }
+    return v;
+}
+
+void set_level_state(mgp_ctx* c, const std::vector<char*>& v)
+{
+    for (size_t l = 0; l < c->lev.size(); ++l) {
+        c->lev[l].u = v[2 * l];
+        c->lev[l].t = v[2 * l + 1];
+    }
+}
+
+// One cycle through a cached hipGraph (captured on first use of a buffer-pointer state).
+int graph_cycle(mgp_ctx* c, int slot)
+{
+    const std::vector<char*> pre = level_state(c);
+    mgp_ctx::GraphEntry* hit = nullptr;
+    for (auto& e : c->graphs)
+        if (e.pre == pre) hit = &e;
+    if (!hit) {
+        if (c->graphs.size() >= 8) return one_cycle(c, c->d_errs + slot);  // unusual state churn: eager
+        HIP_TRY(c, hipStreamBeginCapture(c->s, hipStreamCaptureModeThreadLocal));
+        const int rc = one_cycle(c, c->d_err_cur);
+        hipGraph_t graph = nullptr;
+        const hipError_t ec = hipStreamEndCapture(c->s, &graph);
+        if (rc != MGP_OK) {
+            if (graph) (void)hipGraphDestroy(graph);
+            set_level_state(c, pre);
+            return rc;
+        }
+        HIP_TRY(c, ec);
+        mgp_ctx::GraphEntry e;
+        e.pre = pre;
+        e.post = level_state(c);
+        const hipError_t ei = hipGraphInstantiate(&e.exec, graph, nullptr, nullptr, 0);
+        (void)hipGraphDestroy(graph);
+        HIP_TRY(c, ei);
+        c->graphs.push_back(e);
+        hit = &c->graphs.back();
+    }
+    set_level_state(c, hit->post);
+    HIP_TRY(c, hipGraphLaunch(hit->exec, c->s));
+    if (c->o.err_mode)
+        HIP_TRY(c, hipMemcpyAsync(c->d_errs + slot, c->d_err_cur, sizeof(double), hipMemcpyDeviceToDevice, c->s));
     return MGP_OK;
 }
 
@@ -514,6 +579,8 @@ static void destroy_impl(mgp_ctx* c)
     if (c->stage) (void)hipFree(c->stage);
     if (c->d_part) (void)hipFree(c->d_part);
     if (c->d_errs) (void)hipFree(c->d_errs);
+    if (c->d_err_cur) (void)hipFree(c->d_err_cur);
+    for (auto& g : c->graphs) (void)hipGraphExecDestroy(g.exec);
     for (auto e : c->ev) (void)hipEventDestroy(e);
     if (c->comm) (void)ncclCommDestroy(c->comm);
     if (c->s) (void)hipStreamDestroy(c->s);
@@ -605,7 +672,14 @@ int mgp_create(mgp_ctx** out, const mgp_opts* o)
         c->err = "hipMalloc failed for reduction partials";
         return bail(MGP_ERR_OOM);
     }
-    if (ensure_errs(c, 64) != MGP_OK) return bail(MGP_ERR_OOM);
+    if (ensure_errs(c, 64) != MGP_OK || hipMalloc(&c->d_err_cur, sizeof(double)) != hipSuccess) {
+        c->err = "hipMalloc failed for err slots";
+        return bail(MGP_ERR_OOM);
+    }
+    {
+        const char* v = std::getenv("MGP_GRAPH");
+        c->use_graph = c->o.world == 1 && !(v && std::atoi(v) == 0);
+    }
     if (c->o.world > 1) {
         ncclUniqueId id;
         std::memcpy(&id, o->comm_id, sizeof(id));
@@ -695,7 +769,8 @@ int mgp_cycles(mgp_ctx* c, int32_t k, double* errs)
 {
     if (!c || k < 0) return MGP_ERR_ARG;
     TRY(ensure_errs(c, k));
-    for (int i = 0; i < k; ++i) TRY(one_cycle(c, i));
+    const bool graph = c->use_graph && !c->timing;
+    for (int i = 0; i < k; ++i) TRY(graph ? graph_cycle(c, i) : one_cycle(c, c->d_errs + i));
     TRY(sync_and_check(c));
     if (errs) {
         if (!c->o.err_mode) {

@@ -214,6 +214,20 @@ def test_cycles_batch_equals_single():
     assert np.array_equal(ea, eb)
 
 
+def test_graph_replay_equals_eager(monkeypatch):
+    """hipGraph replay (default on one GPU) and eager launches give identical psi and err."""
+    kw = dict(dim=3, n=_n3(3, 64), real="float", smoother="rbgs", nu1=2, nu2=2, prolong="linear", coarse_bc="consistent")
+    g = _ctx(**kw)
+    monkeypatch.setenv("MGP_GRAPH", "0")
+    e = _ctx(**kw)
+    g.init_point_charge()
+    e.init_point_charge()
+    eg = np.concatenate([g.cycles(3), g.cycles(4)])
+    ee = np.concatenate([e.cycles(3), e.cycles(4)])
+    assert np.array_equal(g.get_psi(), e.get_psi())
+    assert np.array_equal(eg, ee)
+
+
 def test_two_grid_host_buffers():
     """cpu-raw.lua:186 twoGrid(h, u, f, L) on caller buffers == the oracle's mgo_two_grid."""
     import ctypes
