@@ -79,7 +79,8 @@ int         mgp_create(mgp_ctx** out, const mgp_opts* o);
 void        mgp_destroy(mgp_ctx* c);
 const char* mgp_last_error(const mgp_ctx* c);
 
-/* Level hierarchy.  info[0..7] = {nx, ny, nz_global, nz_local, z0, distributed, 0, 0} */
+/* Level hierarchy.  info[0..7] = {nx, ny, nz_global, nz_local, z0, distributed, tail, 0}; tail = 1
+ * when a cycle runs this level inside the single-launch coarse tail (LDS-resident levels). */
 int         mgp_num_levels(const mgp_ctx* c);
 int         mgp_level_info(const mgp_ctx* c, int level, int64_t info[8]);
 /* The same plan without a device (host logic only): fills up to max_levels rows of 8 int64s. */
@@ -112,14 +113,20 @@ int         mgp_prolong_correct(mgp_ctx* c, int level);             /* expandRes
 int         mgp_coarse_solve(mgp_ctx* c);                           /* L == 1 branch of twoGrid */
 
 int         mgp_sync(mgp_ctx* c);
-/* Finest-level smoother kernel timing with HIP events on the context's stream.  mgp_timing(c, 1)
- * resets and enables (cycles then run eagerly, without hipGraph replay, so each launch can be
- * bracketed); mgp_timing_read returns the summed kernel milliseconds, the number of timed
- * launches and the number of full sweeps they performed (cells * sweeps * 3 * real_bytes is the
- * algorithmic byte count).  Timed launches are the plain finest-level smoother half-sweeps; the
- * err-fused last half-sweeps of a cycle (which also read psiOld) are not timed. */
+/* Finest-level kernel timing with HIP events on the context's stream.  mgp_timing(c, 1) resets and
+ * enables (cycles then run eagerly, without hipGraph replay, so each launch can be bracketed).
+ * Timed kinds, level 0 only:
+ *   MGP_TIMING_HALF_SWEEP  plain red/black (or Jacobi) half-sweeps (not the err-fused last ones);
+ *                          1.5 reals per cell per launch
+ *   MGP_TIMING_FUSED_PRE   temporally blocked nu1 sweeps + residual + restriction;
+ *                          (3 nu1 + 2 + 1/8) reals per cell
+ *   MGP_TIMING_FUSED_POST  temporally blocked prolongation + correction + nu2 sweeps (+ err);
+ *                          (3 nu2 + 2 + 1/8 [+ 2]) reals per cell
+ * mgp_timing_read returns, for one kind, the summed kernel milliseconds, the number of launches
+ * and their ALGORITHMIC bytes (SURVEY.md §8d accounting, not measured traffic). */
+enum { MGP_TIMING_HALF_SWEEP = 0, MGP_TIMING_FUSED_PRE = 1, MGP_TIMING_FUSED_POST = 2, MGP_TIMING_KINDS = 3 };
 int         mgp_timing(mgp_ctx* c, int enable);
-int         mgp_timing_read(mgp_ctx* c, double* ms_total, int64_t* launches, double* sweeps);
+int         mgp_timing_read(mgp_ctx* c, int kind, double* ms_total, int64_t* launches, double* bytes);
 
 #ifdef __cplusplus
 }

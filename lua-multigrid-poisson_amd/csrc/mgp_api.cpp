@@ -108,6 +108,8 @@ struct Level {
     char* t = nullptr;      // second u buffer (Jacobi ping-pong; level 0: keeps psiOld during a cycle)
     bool ghost_ok = true;   // u's ghost planes hold the neighbours' current planes
     bool fghost_ok = true;  // f's ghost planes likewise
+    bool fused = false;     // smoothing phases run temporally blocked (k_fused); needs t
+    int zc = 0;             // k_fused z-chunk (planes per workgroup)
 };
 
 struct mgp_ctx {
@@ -139,16 +141,20 @@ struct mgp_ctx {
     };
     bool use_graph = false;
     std::vector<GraphEntry> graphs;
+    // coarse-level tail (k_tail): cycle_rec(tail_level, ...) as one launch; programs for V and F
+    int tail_level = -1;
+    std::vector<uint32_t> tail_v, tail_f;
     double* d_err_cur = nullptr;
     double* err_dst = nullptr;  // where this cycle's sum of squares goes
     std::string err;
-    // finest-smoother timing
+    // finest-level kernel timing: event pairs around level-0 launches of each timed kind
     bool timing = false;
     std::vector<hipEvent_t> ev;
+    std::vector<std::pair<int, double>> ev_meta;  // (kind, algorithmic bytes) per pair
     size_t ev_used = 0;
-    double t_ms = 0.0;
-    int64_t t_launch = 0;
-    double t_sweeps = 0.0;
+    double t_ms[MGP_TIMING_KINDS] = {};
+    int64_t t_launch[MGP_TIMING_KINDS] = {};
+    double t_bytes[MGP_TIMING_KINDS] = {};
 
     int fail(int code, const char* fmt, ...)
     {
@@ -239,33 +245,42 @@ int exchange(mgp_ctx* c, Level& L)
 
 // ---- finest-level smoother timing ----
 
+void timing_collect(mgp_ctx* c)
+{
+    for (size_t e = 0; e + 1 < c->ev_used; e += 2) {
+        float ms = 0.f;
+        if (hipEventElapsedTime(&ms, c->ev[e], c->ev[e + 1]) != hipSuccess) ms = 0.f;
+        const auto& m = c->ev_meta[e / 2];
+        c->t_ms[m.first] += ms;
+        c->t_launch[m.first] += 1;
+        c->t_bytes[m.first] += m.second;
+    }
+    c->ev_used = 0;
+}
+
 int timed_begin(mgp_ctx* c, int l, hipEvent_t* e1)
 {
     *e1 = nullptr;
     if (!c->timing || l != 0) return MGP_OK;
     if (c->ev_used + 2 > c->ev.size()) {
         HIP_TRY(c, hipStreamSynchronize(c->s));
-        for (size_t e = 0; e + 1 < c->ev_used; e += 2) {
-            float ms = 0.f;
-            HIP_TRY(c, hipEventElapsedTime(&ms, c->ev[e], c->ev[e + 1]));
-            c->t_ms += ms;
-        }
-        c->ev_used = 0;
+        timing_collect(c);
     }
     *e1 = c->ev[c->ev_used];
     HIP_TRY(c, hipEventRecord(*e1, c->s));
     return MGP_OK;
 }
 
-int timed_end(mgp_ctx* c, hipEvent_t e1, double sweeps)
+int timed_end(mgp_ctx* c, hipEvent_t e1, int kind, double bytes)
 {
     if (!e1) return MGP_OK;
     HIP_TRY(c, hipEventRecord(c->ev[c->ev_used + 1], c->s));
+    c->ev_meta[c->ev_used / 2] = {kind, bytes};
     c->ev_used += 2;
-    c->t_launch += 1;
-    c->t_sweeps += sweeps;
     return MGP_OK;
 }
+
+int64_t level_cells(const Level& L) { return L.p.nx * L.p.ny * L.p.nz; }
 
 // ---- cycle pieces ----
 
@@ -279,7 +294,7 @@ int half(mgp_ctx* c, int l, int color, char* other, char* dst, const char* old, 
     TRY(timed_begin(c, old ? -1 : l, &e));
     HIP_TRY(c, mgp::launch_half_sweep(c->rb, c->o.dim, l == 0, color, c->ui(L, other), c->ui(L, L.f), c->ui(L, dst),
                                       old ? c->ui(L, (char*)old) : nullptr, c->d_part + part_off, L.g, h, cl, c->s));
-    TRY(timed_end(c, e, 0.5));
+    TRY(timed_end(c, e, MGP_TIMING_HALF_SWEEP, 1.5 * c->rb * (double)level_cells(L)));
     return MGP_OK;
 }
 
@@ -377,17 +392,163 @@ int zero_level(mgp_ctx* c, Level& L)
     return MGP_OK;
 }
 
+double level_h(const mgp_ctx* c, int level) { return std::ldexp(1.0 / (double)c->lev[0].p.nx, level); }
+
+// smooth(l, nu1) + residual_restrict(l) as one temporally blocked pass: u -> t, R -> f of l+1
+int fused_pre(mgp_ctx* c, int l, double h)
+{
+    Level& L = c->lev[l];
+    Level& C = c->lev[l + 1];
+    mgp::FusedArgs a{};
+    a.pre = true;
+    a.src = c->ui(L, L.u);
+    a.f = c->ui(L, L.f);
+    a.dst = c->ui(L, L.t);
+    a.R = c->ui(C, C.f);
+    a.g = L.g;
+    a.gc = C.g;
+    a.h = h;
+    a.cl = coarse_coef(c->o.coarse_bc, l);
+    a.zc = L.zc;
+    hipEvent_t e;
+    TRY(timed_begin(c, l, &e));
+    HIP_TRY(c, mgp::launch_fused(c->rb, a, c->s));
+    // algorithmic bytes: nu1 sweeps x 3 reals + (2 + 1/8) reals of residual/restriction
+    TRY(timed_end(c, e, MGP_TIMING_FUSED_PRE, (3.0 * c->o.nu1 + 2.125) * c->rb * (double)level_cells(L)));
+    std::swap(L.u, L.t);  // u = smoothed; t = the previous iterate (psiOld on level 0)
+    if (l == 0 && c->in_cycle) c->first_done = true;
+    return MGP_OK;
+}
+
+// prolong_correct(l) + smooth(l, nu2) as one temporally blocked pass: u + P V -> t (err vs t)
+int fused_post(mgp_ctx* c, int l, double h, bool want_err)
+{
+    Level& L = c->lev[l];
+    Level& C = c->lev[l + 1];
+    mgp::FusedArgs a{};
+    a.pre = false;
+    a.linear = c->o.prolong == MGP_PROLONG_LINEAR;
+    a.src = c->ui(L, L.u);
+    a.f = c->ui(L, L.f);
+    a.dst = c->ui(L, L.t);
+    a.V = c->ui(C, C.u);
+    a.partials = want_err ? c->d_part : nullptr;
+    a.g = L.g;
+    a.gc = C.g;
+    a.h = h;
+    a.cl = coarse_coef(c->o.coarse_bc, l);
+    a.clc = coarse_coef(c->o.coarse_bc, l + 1);
+    a.zc = L.zc;
+    hipEvent_t e;
+    TRY(timed_begin(c, l, &e));
+    HIP_TRY(c, mgp::launch_fused(c->rb, a, c->s));
+    TRY(timed_end(c, e, MGP_TIMING_FUSED_POST,
+                  (3.0 * c->o.nu2 + 2.125 + (want_err ? 2.0 : 0.0)) * c->rb * (double)level_cells(L)));
+    std::swap(L.u, L.t);
+    if (want_err) {
+        HIP_TRY(c, mgp::launch_sum_partials(c->d_part, mgp::fused_blocks(c->rb, L.g, L.zc), c->err_dst, c->s));
+        c->err_done = true;
+    }
+    return MGP_OK;
+}
+
+// The ops of cycle_rec(l, fcycle) for levels >= T, recorded for k_tail (levels relative to T).
+void tail_gen(const mgp_ctx* c, int T, int l, bool fcycle, std::vector<uint32_t>& ops)
+{
+    auto emit = [&](int op, int lv, int arg) {
+        ops.push_back((uint32_t)op | ((uint32_t)(lv - T) << 4) | ((uint32_t)arg << 8));
+    };
+    const int last = (int)c->lev.size() - 1;
+    if (l == last) {
+        const Level& L = c->lev[l];
+        const int64_t cells = L.p.nx * L.p.ny * L.p.gnz;
+        emit(mgp::TAIL_SMOOTH, l, cells == 1 ? 1 : c->o.coarse_sweeps);
+        return;
+    }
+    emit(mgp::TAIL_SMOOTH, l, c->o.nu1);
+    emit(mgp::TAIL_RR, l, 0);
+    if (c->o.coarse_init == MGP_COARSE_FRESH) emit(mgp::TAIL_ZERO, l + 1, 0);
+    if (fcycle) tail_gen(c, T, l + 1, true, ops);
+    tail_gen(c, T, l + 1, false, ops);
+    emit(mgp::TAIL_PROLONG, l, 0);
+    emit(mgp::TAIL_SMOOTH, l, c->o.nu2);
+}
+
+// First level (>= 1, replicated, <= MGP_TAIL_CELLS cells) whose sub-hierarchy fits one
+// workgroup's LDS and the op budget; -1 = no tail (MGP_TAIL=0 disables it).
+void plan_tail(mgp_ctx* c)
+{
+    c->tail_level = -1;
+    const char* v = std::getenv("MGP_TAIL");
+    if (v && std::atoi(v) == 0) return;
+    const char* vc = std::getenv("MGP_TAIL_CELLS");
+    const int64_t max_cells = vc ? std::atoll(vc) : 4096;
+    const int last = (int)c->lev.size() - 1;
+    for (int T = 1; T <= last; ++T) {
+        const Level& L = c->lev[T];
+        if (L.p.dist || L.p.nx * L.p.ny * L.p.gnz > max_cells) continue;
+        const int nlev = last - T + 1;
+        if (nlev > mgp::kTailMaxLevels) continue;
+        std::vector<Geo> g;
+        for (int l = T; l <= last; ++l) g.push_back(c->lev[l].g);
+        if (mgp::tail_lds_bytes(c->rb, c->o.dim, c->o.smoother == MGP_JACOBI, g.data(), nlev) > mgp::kTailMaxLds)
+            continue;
+        std::vector<uint32_t> pv, pf;
+        tail_gen(c, T, T, false, pv);
+        tail_gen(c, T, T, true, pf);
+        if ((int)pv.size() > mgp::kTailMaxOps || (int)pf.size() > mgp::kTailMaxOps) continue;
+        c->tail_level = T;
+        c->tail_v = pv;
+        c->tail_f = pf;
+        return;
+    }
+}
+
+int run_tail(mgp_ctx* c, bool fcycle)
+{
+    mgp::TailSpec t{};
+    const int T = c->tail_level, last = (int)c->lev.size() - 1;
+    t.nlev = last - T + 1;
+    t.jacobi = c->o.smoother == MGP_JACOBI;
+    t.linear = c->o.prolong == MGP_PROLONG_LINEAR;
+    for (int i = 0; i < t.nlev; ++i) {
+        Level& L = c->lev[T + i];
+        t.u[i] = c->ui(L, L.u);
+        t.f[i] = c->ui(L, L.f);
+        t.g[i] = L.g;
+        t.h[i] = level_h(c, T + i);
+        t.cl[i] = coarse_coef(c->o.coarse_bc, T + i);
+        L.ghost_ok = true;
+    }
+    const std::vector<uint32_t>& p = fcycle ? c->tail_f : c->tail_v;
+    t.nops = (int)p.size();
+    std::copy(p.begin(), p.end(), t.ops);
+    HIP_TRY(c, mgp::launch_tail(c->rb, c->o.dim, t, c->s));
+    return MGP_OK;
+}
+
 int cycle_rec(mgp_ctx* c, int l, double h, bool fcycle)
 {
     const int last = (int)c->lev.size() - 1;
+    if (l == c->tail_level && h == level_h(c, l)) return run_tail(c, fcycle);
     if (l == last) return coarse_solve_at(c, l, h);
-    TRY(smooth(c, l, c->o.nu1, h));
-    TRY(residual_restrict(c, l, h));
+    const bool fused = c->lev[l].fused && h == level_h(c, l);
+    if (fused) {
+        TRY(fused_pre(c, l, h));
+    } else {
+        TRY(smooth(c, l, c->o.nu1, h));
+        TRY(residual_restrict(c, l, h));
+    }
     if (c->o.coarse_init == MGP_COARSE_FRESH) TRY(zero_level(c, c->lev[l + 1]));
     if (fcycle) TRY(cycle_rec(c, l + 1, 2 * h, true));
     TRY(cycle_rec(c, l + 1, 2 * h, false));
-    TRY(prolong_correct(c, l));
-    TRY(smooth(c, l, c->o.nu2, h, l == 0 && c->in_cycle && c->err_fuse));
+    const bool want_err = l == 0 && c->in_cycle && c->err_fuse;
+    if (fused) {
+        TRY(fused_post(c, l, h, want_err));
+    } else {
+        TRY(prolong_correct(c, l));
+        TRY(smooth(c, l, c->o.nu2, h, want_err));
+    }
     return MGP_OK;
 }
 
@@ -640,10 +801,23 @@ int mgp_create(mgp_ctx** out, const mgp_opts* o)
         c->lev.push_back(L);
     }
     c->err_fuse = c->o.err_mode && c->o.smoother == MGP_RBGS && c->o.nu1 >= 1 && c->o.nu2 >= 1 && c->lev.size() > 1;
+    {
+        // temporally blocked phases: RB-GS 2+2 on replicated 3D levels of >= MGP_FUSED_MIN_CELLS
+        const char* v = std::getenv("MGP_FUSED");
+        const char* vm = std::getenv("MGP_FUSED_MIN_CELLS");
+        const int64_t min_cells = vm ? std::atoll(vm) : (int64_t(1) << 25);
+        // opt-in (MGP_FUSED=1) until it beats one launch per half-sweep
+        const bool on = v && std::atoi(v) != 0 && c->o.smoother == MGP_RBGS && c->o.nu1 == 2 && c->o.nu2 == 2;
+        for (size_t l = 0; l + 1 < c->lev.size(); ++l) {
+            Level& L = c->lev[l];
+            L.fused = on && !L.p.dist && level_cells(L) >= min_cells && mgp::fused_supported(c->rb, c->o.dim, 2, L.g);
+            if (L.fused) L.zc = mgp::fused_zc(c->rb, L.g);
+        }
+    }
     for (size_t l = 0; l < c->lev.size(); ++l) {
         Level& L = c->lev[l];
         const size_t bytes = (size_t)L.alloc * rb;
-        const bool need_t = c->o.smoother == MGP_JACOBI || (l == 0 && c->err_fuse);
+        const bool need_t = c->o.smoother == MGP_JACOBI || (l == 0 && c->err_fuse) || L.fused;
         if (hipMalloc(&L.u, bytes) != hipSuccess || hipMalloc(&L.f, bytes) != hipSuccess ||
             (need_t && hipMalloc(&L.t, bytes) != hipSuccess)) {
             c->err = "hipMalloc failed for level " + std::to_string(l) + " (" + std::to_string(bytes) + " bytes)";
@@ -666,7 +840,8 @@ int mgp_create(mgp_ctx** out, const mgp_opts* o)
         c->err = "hipMalloc failed for the staging buffer";
         return bail(MGP_ERR_OOM);
     }
-    const int nb2 = 2 * mgp::half_blocks(c->rb, L0.g);
+    int nb2 = 2 * mgp::half_blocks(c->rb, L0.g);
+    if (L0.fused) nb2 = std::max(nb2, mgp::fused_blocks(c->rb, L0.g, L0.zc));
     c->part_cap = std::max<int64_t>(mgp::kSumBlocks, nb2 + mgp::sum_scratch(nb2));
     if (hipMalloc(&c->d_part, sizeof(double) * c->part_cap) != hipSuccess) {
         c->err = "hipMalloc failed for reduction partials";
@@ -679,6 +854,12 @@ int mgp_create(mgp_ctx** out, const mgp_opts* o)
     {
         const char* v = std::getenv("MGP_GRAPH");
         c->use_graph = c->o.world == 1 && !(v && std::atoi(v) == 0);
+    }
+    plan_tail(c);
+    he = mgp::prepare_kernels(c->rb);
+    if (he != hipSuccess) {
+        c->err = std::string("hipFuncSetAttribute (dynamic LDS): ") + hipGetErrorString(he);
+        return bail(MGP_ERR_HIP);
     }
     if (c->o.world > 1) {
         ncclUniqueId id;
@@ -714,7 +895,8 @@ int mgp_level_info(const mgp_ctx* c, int level, int64_t info[8])
     info[3] = p.nz;
     info[4] = p.z0;
     info[5] = p.dist;
-    info[6] = info[7] = 0;
+    info[6] = c->tail_level >= 0 && level >= c->tail_level;  // run inside the one-launch coarse tail
+    info[7] = 0;
     return MGP_OK;
 }
 
@@ -809,7 +991,6 @@ int mgp_two_grid(mgp_ctx* c, double h, void* u, const void* f, int64_t L, int me
     return c->fail(MGP_ERR_ARG, "mgp_two_grid: no level of size %lld", (long long)L);
 }
 
-static double level_h(const mgp_ctx* c, int level) { return std::ldexp(1.0 / (double)c->lev[0].p.nx, level); }
 
 int mgp_smooth(mgp_ctx* c, int level, int sweeps)
 {
@@ -848,29 +1029,27 @@ int mgp_timing(mgp_ctx* c, int enable)
     TRY(sync_and_check(c));
     if (enable && c->ev.empty()) {
         c->ev.resize(4096);
+        c->ev_meta.resize(2048);
         for (auto& e : c->ev) HIP_TRY(c, hipEventCreate(&e));
     }
     c->timing = enable != 0;
     c->ev_used = 0;
-    c->t_ms = 0.0;
-    c->t_launch = 0;
-    c->t_sweeps = 0.0;
+    for (int k = 0; k < MGP_TIMING_KINDS; ++k) {
+        c->t_ms[k] = 0.0;
+        c->t_launch[k] = 0;
+        c->t_bytes[k] = 0.0;
+    }
     return MGP_OK;
 }
 
-int mgp_timing_read(mgp_ctx* c, double* ms_total, int64_t* launches, double* sweeps)
+int mgp_timing_read(mgp_ctx* c, int kind, double* ms_total, int64_t* launches, double* bytes)
 {
-    if (!c) return MGP_ERR_ARG;
+    if (!c || kind < 0 || kind >= MGP_TIMING_KINDS) return MGP_ERR_ARG;
     TRY(sync_and_check(c));
-    for (size_t e = 0; e + 1 < c->ev_used; e += 2) {
-        float ms = 0.f;
-        HIP_TRY(c, hipEventElapsedTime(&ms, c->ev[e], c->ev[e + 1]));
-        c->t_ms += ms;
-    }
-    c->ev_used = 0;
-    if (ms_total) *ms_total = c->t_ms;
-    if (launches) *launches = c->t_launch;
-    if (sweeps) *sweeps = c->t_sweeps;
+    timing_collect(c);
+    if (ms_total) *ms_total = c->t_ms[kind];
+    if (launches) *launches = c->t_launch[kind];
+    if (bytes) *bytes = c->t_bytes[kind];
     return MGP_OK;
 }
 

@@ -6,6 +6,8 @@
 
 namespace mgp {
 
+constexpr int kGhost3D = 1;  // ghost planes per side of every 3D level
+
 // Device layout of one level ("red/black packed").  A level is a stack of planes (one plane in
 // 2D).  Each plane holds its red cells ((i + j + gk) even) in the first half and its black cells
 // in the second half; a half is ny rows of hw = max(1, nx/2) cells and cell (i, j) sits at
@@ -59,7 +61,48 @@ hipError_t launch_sqdiff_sum(int rb, const void* a, const void* b, int64_t n, do
 int sum_scratch(int n);
 hipError_t launch_sum_partials(const double* partials, int n, double* out, hipStream_t s);
 
+// Temporally blocked smoothing phases of a replicated 3D red/black level (ns = 2 sweeps):
+//   pre : dst = nu1 sweeps of src; R (coarse packed, Geo gc) = restrict(residual(dst))
+//   post: dst = nu2 sweeps of (src + P V); with partials, sum (dst - dst_before)^2 per workgroup
+// src and dst are different buffers (tiles read each other's halos of src).
+struct FusedArgs {
+    bool pre;
+    int linear;
+    const void* src;
+    const void* f;
+    void* dst;
+    void* R;
+    const void* V;
+    double* partials;
+    Geo g, gc;
+    double h, cl, clc;
+    int zc;
+};
+bool fused_supported(int rb, int dim, int ns, const Geo& g);
+// Raise the dynamic-LDS limit of the fused and tail kernels (once per context, before any capture).
+hipError_t prepare_kernels(int rb);
+int fused_zc(int rb, const Geo& g);
+int fused_blocks(int rb, const Geo& g, int zc);
+hipError_t launch_fused(int rb, const FusedArgs& a, hipStream_t s);
+
+// Coarse-level tail: the sub-cycle below one level as a single one-workgroup launch with every
+// level in LDS.  ops[] = (op | level << 4 | arg << 8), levels relative to the tail's first level.
+constexpr int kTailMaxLevels = 8;
+constexpr int kTailMaxOps = 192;
+constexpr size_t kTailMaxLds = 160 * 1024;  // gfx950 LDS per workgroup
+enum TailOp { TAIL_SMOOTH = 1, TAIL_RR = 2, TAIL_ZERO = 3, TAIL_PROLONG = 4 };
+struct TailSpec {
+    int nlev, nops, jacobi, linear;
+    void* u[kTailMaxLevels];  // interior plane 0 of each level's u / f (global)
+    void* f[kTailMaxLevels];
+    Geo g[kTailMaxLevels];
+    double h[kTailMaxLevels];
+    double cl[kTailMaxLevels];
+    uint32_t ops[kTailMaxOps];
+};
+size_t tail_lds_bytes(int rb, int dim, int jacobi, const Geo* g, int nlev);
+hipError_t launch_tail(int rb, int dim, const TailSpec& t, hipStream_t s);
+
 constexpr int kSumBlocks = 1024;
-constexpr int kGhost3D = 1;  // ghost planes per side of every 3D level
 
 }  // namespace mgp

@@ -261,6 +261,37 @@ __global__ __launch_bounds__(kBlock) void k_half(const T* __restrict__ other, co
     if (ERR) block_partial<T>(acc, partials);
 }
 
+// One colour-c slot of a half-sweep (scalar; any level size, nx = 1 included).  Returns the
+// packed index written, or -1 for the empty slot of an nx = 1 row; *v = the new value.
+template <typename T, int DIM>
+__device__ __forceinline__ int64_t half_item(const T* other, const T* __restrict__ f, T* dst, const Geo& g,
+                                             int color, const Op<T, DIM>& op, int64_t it, T* v)
+{
+    const int m = (int)(it & (g.hw - 1));
+    const int j = (int)((it >> g.lhw) & (g.ny - 1));
+    const int64_t k = it >> (g.lhw + g.ly);
+    const int64_t gk = g.z0 + k;
+    const int o = color ^ (int)((j + gk) & 1);
+    const int i = 2 * m + o;
+    if (i >= g.nx) return -1;
+    const int64_t own = k * g.P + color * g.H + (int64_t)j * g.hw + m;
+    const int64_t oth = k * g.P + (color ^ 1) * g.H + (int64_t)j * g.hw + m;
+    const T xl = i > 0 ? other[oth - 1 + o] : (T)0;
+    const T xr = i < g.nx - 1 ? other[oth + o] : (T)0;
+    T s = xl + xr;
+    s = s + (j > 0 ? other[oth - g.hw] : (T)0);
+    s = s + (j < g.ny - 1 ? other[oth + g.hw] : (T)0);
+    if (DIM == 3) {
+        s = s + other[oth - g.P];
+        s = s + other[oth + g.P];
+    }
+    const int nb = (i == 0) + (i == g.nx - 1) + (j == 0) + (j == g.ny - 1) +
+                   (DIM == 3 ? (gk == 0) + (gk == g.gnz - 1) : 0);
+    *v = op.relax(s, f[own], nb);
+    dst[own] = *v;
+    return own;
+}
+
 // Scalar form for small levels (hw < N, nx = 1 included): a thread per colour-c slot.
 template <typename T, int DIM, bool ERR>
 __global__ __launch_bounds__(kBlock) void k_half_s(const T* __restrict__ other, const T* __restrict__ f,
@@ -269,34 +300,13 @@ __global__ __launch_bounds__(kBlock) void k_half_s(const T* __restrict__ other, 
                                                    Op<T, DIM> op)
 {
     const int64_t it = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    const int m = (int)(it & (g.hw - 1));
-    const int j = (int)((it >> g.lhw) & (g.ny - 1));
-    const int64_t k = it >> (g.lhw + g.ly);
     double acc = 0.0;
-    if (k < g.nz) {
-        const int64_t gk = g.z0 + k;
-        const int o = color ^ (int)((j + gk) & 1);
-        const int i = 2 * m + o;
-        if (i < g.nx) {
-                const int64_t own = k * g.P + color * g.H + (int64_t)j * g.hw + m;
-            const int64_t oth = k * g.P + (color ^ 1) * g.H + (int64_t)j * g.hw + m;
-            const T xl = i > 0 ? other[oth - 1 + o] : (T)0;
-            const T xr = i < g.nx - 1 ? other[oth + o] : (T)0;
-            T s = xl + xr;
-            s = s + (j > 0 ? other[oth - g.hw] : (T)0);
-            s = s + (j < g.ny - 1 ? other[oth + g.hw] : (T)0);
-            if (DIM == 3) {
-                s = s + other[oth - g.P];
-                s = s + other[oth + g.P];
-            }
-            const int nb = (i == 0) + (i == g.nx - 1) + (j == 0) + (j == g.ny - 1) +
-                           (DIM == 3 ? (gk == 0) + (gk == g.gnz - 1) : 0);
-            const T v = op.relax(s, f[own], nb);
-            dst[own] = v;
-            if (ERR) {
-                const double d = (double)v - (double)old[own];
-                acc += d * d;
-            }
+    if (it < g.H * g.nz) {
+        T v;
+        const int64_t own = half_item<T, DIM>(other, f, dst, g, color, op, it, &v);
+        if (ERR && own >= 0) {
+            const double d = (double)v - (double)old[own];
+            acc += d * d;
         }
     }
     if (ERR) block_partial<T>(acc, partials);
@@ -327,16 +337,13 @@ __device__ __forceinline__ T residual_at(const T* __restrict__ u, const T* __res
     return op.residual(s, f[c], u[c], nb);
 }
 
-// Scalar form: a thread per coarse cell (any sizes).
+// One coarse cell of the fused residual + restriction (scalar; any sizes).
 template <typename T, int DIM>
-__global__ __launch_bounds__(kBlock) void k_resrestrict_s(const T* __restrict__ u, const T* __restrict__ f,
-                                                          T* __restrict__ R, Geo g, Geo gc, Op<T, DIM> op)
+__device__ __forceinline__ void resrestrict_item(const T* u, const T* f, T* R, const Geo& g, const Geo& gc,
+                                                 const Op<T, DIM>& op, int64_t it)
 {
     const int cx = g.nx >> 1, cy = g.ny >> 1;
     const int lcx = g.lx - 1, lcy = g.ly - 1;
-    const int64_t ncz = DIM == 3 ? (g.nz >> 1) : 1;
-    const int64_t it = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (it >= ((int64_t)cx * cy) * ncz) return;
     const int I = (int)(it & (cx - 1));
     const int J = (int)((it >> lcx) & (cy - 1));
     const int64_t K = it >> (lcx + lcy);
@@ -354,6 +361,22 @@ __global__ __launch_bounds__(kBlock) void k_resrestrict_s(const T* __restrict__ 
     } else {
         R[pidx(gc, I, J, 0)] = (T)0.25 * s;
     }
+}
+
+template <typename T, int DIM>
+__device__ __forceinline__ int64_t resrestrict_items(const Geo& g)
+{
+    return (int64_t)(g.nx >> 1) * (g.ny >> 1) * (DIM == 3 ? (g.nz >> 1) : 1);
+}
+
+// Scalar form: a thread per coarse cell (any sizes).
+template <typename T, int DIM>
+__global__ __launch_bounds__(kBlock) void k_resrestrict_s(const T* __restrict__ u, const T* __restrict__ f,
+                                                          T* __restrict__ R, Geo g, Geo gc, Op<T, DIM> op)
+{
+    const int64_t it = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (it >= resrestrict_items<T, DIM>(g)) return;
+    resrestrict_item<T, DIM>(u, f, R, g, gc, op, it);
 }
 
 // Vector form: a thread owns N consecutive coarse cells I0 .. I0+N-1 of one coarse row.  Their
@@ -486,16 +509,14 @@ __device__ __forceinline__ T cval(const T* __restrict__ V, const Geo& gc, int I,
     return s == (T)1 ? v : s * v;
 }
 
-// a thread per fine slot of colour `color` (any sizes)
+// One fine slot of colour `color` of the prolongation + correction (scalar; any sizes).
 template <typename T, int DIM, int LINEAR>
-__global__ __launch_bounds__(kBlock) void k_prolong(T* __restrict__ u, const T* __restrict__ V, Geo g, Geo gc,
-                                                    double clc, int color)
+__device__ __forceinline__ void prolong_item(T* u, const T* V, const Geo& g, const Geo& gc, T cl, int color,
+                                             int64_t it)
 {
-    const int64_t it = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     const int m = (int)(it & (g.hw - 1));
     const int j = (int)((it >> g.lhw) & (g.ny - 1));
     const int64_t k = it >> (g.lhw + g.ly);
-    if (k >= g.nz) return;
     const int o = color ^ (int)((j + g.z0 + k) & 1);
     const int i = 2 * m + o;
     if (i >= g.nx) return;
@@ -506,7 +527,7 @@ __global__ __launch_bounds__(kBlock) void k_prolong(T* __restrict__ u, const T* 
     if (!LINEAR) {
         v = V[pidx(gc, I, J, K)];
     } else {
-        const T w0 = (T)0.75, w1 = (T)0.25, cl = (T)clc;
+        const T w0 = (T)0.75, w1 = (T)0.25;
         int In = (i & 1) ? I + 1 : I - 1;
         int Jn = (j & 1) ? J + 1 : J - 1;
         const bool ox = In < 0 || In >= gc.nx;
@@ -532,6 +553,16 @@ __global__ __launch_bounds__(kBlock) void k_prolong(T* __restrict__ u, const T* 
         }
     }
     u[own] = u[own] + v;
+}
+
+// a thread per fine slot of colour `color` (any sizes)
+template <typename T, int DIM, int LINEAR>
+__global__ __launch_bounds__(kBlock) void k_prolong(T* __restrict__ u, const T* __restrict__ V, Geo g, Geo gc,
+                                                    double clc, int color)
+{
+    const int64_t it = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (it >= g.H * g.nz) return;
+    prolong_item<T, DIM, LINEAR>(u, V, g, gc, (T)clc, color, it);
 }
 
 // Coarse samples x = I0-1 .. I0+N of coarse row (Jr, Kr) (Kr relative to the V pointer) into
@@ -659,6 +690,545 @@ __global__ __launch_bounds__(kBlock) void k_prolong_v(T* __restrict__ u, const T
             uv.v[e] = uv.v[e] + v;
         }
         vstore<T, N>(u + own, uv);
+    }
+}
+
+// ---- temporally blocked smoothing (3D, red/black, replicated level) --------------------------
+//
+// The unfused cycle moves every fine cell through HBM once per half-sweep: 2+2 RB-GS plus the
+// residual/restriction and prolongation/correction passes cost (4 x 1.5 + 2.125 + 2.125 + 1) reals
+// per cell.  k_fused streams a z-slab of one x-y tile through a ring of packed planes in LDS and
+// applies ALL the half-sweeps of a smoothing phase to each plane as it passes, in wavefront order:
+// at step p plane p is loaded (PRE) or loaded and corrected by the prolongation (POST), half-sweep
+// k runs on plane p - k, and the last stage (PRE: residual + restriction, POST: store + err) on
+// plane p - NST.  Stage k only trusts rows that lie k rows inside the extended tile, so the tile
+// carries a y/z halo of NST planes/rows and an x halo of 8 cells; halo cells are recomputed by
+// every tile that needs them.  HBM traffic per cell drops to read u, f, write u (+ R) for PRE and
+// read u, V, f, psiOld, write u for POST.  The arithmetic of every cell is the unfused kernels'
+// (same expressions, same order), so results are bit-identical.
+//
+// Thread layout per stage: one item = N consecutive same-colour cells of one LDS row (16 bytes),
+// as in k_half; rows of the plane ring are laid out like a global packed plane (two colour
+// halves, HWE cells per half-row), so every neighbour access is the global one re-based.
+
+template <typename T>
+struct FusedTile;
+template <>
+struct FusedTile<float> {
+    static constexpr int TX = 64, TY = 32;
+};
+template <>
+struct FusedTile<double> {
+    static constexpr int TX = 32, TY = 16;
+};
+constexpr int kFusedThreads = 512;
+constexpr int kFusedHX = 8;  // x halo (cells): >= NST, and keeps the tile's x origin 16-byte aligned
+
+// Stage k = 1 .. 2 NS (half-sweep k) runs on plane p - (2k - 1) at step p and the last stage
+// (PRE: residual + restriction, POST: store + err) on plane p - LAST: the stages of one step touch
+// disjoint planes whose inputs were finished in earlier steps, so a step needs just two barriers
+// (after the load, after the stages).
+template <typename T, int NS, bool PRE>
+struct FusedShape {
+    static constexpr int N = VN<T>::n;
+    static constexpr int TX = FusedTile<T>::TX, TY = FusedTile<T>::TY;
+    static constexpr int H = 2 * NS + (PRE ? 1 : 0);    // y and z halo: stages that read neighbours
+    static constexpr int LAST = 4 * NS + 1;             // lag of the last stage
+    static constexpr int XE = TX + 2 * kFusedHX;
+    static constexpr int HWE = XE / 2;                  // cells per LDS half-row
+    static constexpr int G = HWE / N;                   // vector groups per LDS half-row
+    static constexpr int YE = TY + 2 * H;
+    static constexpr int RU = LAST + 2;                 // planes in the ring (last reader: LAST + 1)
+    static constexpr int PS = 2 * YE * HWE;             // reals per plane slot
+    static constexpr int OG = TX / 2 / N;               // output groups per half-row (= coarse groups per coarse row)
+    static constexpr size_t lds_bytes = (size_t)RU * PS * sizeof(T);
+    // every phase is at most one item per thread (the prefetch registers rely on it)
+    static_assert(YE * G <= kFusedThreads, "load phase exceeds one item per thread");
+    static_assert(TY * 2 * OG <= kFusedThreads, "output phase exceeds one item per thread");
+    static_assert(H <= kFusedHX, "x halo too small");
+};
+
+template <typename T>
+__device__ __forceinline__ void block_partial_n(double acc, double* partials, int nthreads)
+{
+    __shared__ double red[kFusedThreads];
+    red[threadIdx.x] = acc;
+    __syncthreads();
+    for (int w = nthreads / 2; w > 0; w >>= 1) {
+        if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) partials[blockIdx.x] = red[0];
+}
+
+// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS operations, not for its
+// outstanding global loads (the next step's prefetch stays in flight across the barrier).
+__device__ __forceinline__ void lds_barrier()
+{
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+// Global operands of one z-step for this thread, loaded one step ahead.
+template <typename T, int NS>
+struct FusedPrefetch {
+    static constexpr int N = VN<T>::n;
+    static constexpr int W = N > 1 ? N / 2 : 1;  // residual item width (coarse cells)
+    Vec<T, N> u0, u1;                                  // stage 0: the plane's u, both colours
+    T c00[N + 2], c10[N + 2], c01[N + 2], c11[N + 2];  // stage 0 (POST): coarse rows for P V
+    Vec<T, N> fk[2 * NS];                              // f of the half-sweep items
+    T fr[2][2][W];                                     // f of the residual item: [row dy][colour][e]
+    Vec<T, N> old;                                     // psiOld of the output item (POST, ERR)
+};
+
+// src: the level's u before the phase; dst: the phase's output (POST with ERR reads psiOld from
+// dst first).  V/gc: coarse correction (POST); R/gc: restricted residual (PRE).  zc: planes per
+// z-chunk.  CLZ: the level operator has no boundary modification (cl == 0, e.g. level 0).
+template <typename T, int NS, bool PRE, int LINEAR, bool ERR, bool CLZ>
+__global__ __launch_bounds__(kFusedThreads) void k_fused(const T* __restrict__ src, const T* __restrict__ f,
+                                                         T* __restrict__ dst, T* __restrict__ R,
+                                                         const T* __restrict__ V, double* __restrict__ partials,
+                                                         Geo g, Geo gc, Op<T, 3> op, T clc, int zc)
+{
+    using S = FusedShape<T, NS, PRE>;
+    constexpr int N = S::N, H = S::H, LAST = S::LAST, HWE = S::HWE, G = S::G, YE = S::YE, RU = S::RU,
+                  PS = S::PS, TX = S::TX, TY = S::TY, OG = S::OG;
+    constexpr int W = FusedPrefetch<T, NS>::W;
+    constexpr int RG = TX / 2 / W;  // residual items per coarse row
+    constexpr int CH = YE * HWE;    // reals per colour half of a plane slot
+    static_assert((TY / 2) * RG <= kFusedThreads, "residual phase exceeds one item per thread");
+    extern __shared__ __align__(16) unsigned char fused_smem[];
+    T* const ring = reinterpret_cast<T*>(fused_smem);
+    const int tid = threadIdx.x;
+
+    const int tiles_x = g.nx / TX, tiles_y = g.ny / TY;
+    const int b = xcd_remap(blockIdx.x, gridDim.x);
+    const int tile = b % (tiles_x * tiles_y);
+    const int Z0 = (b / (tiles_x * tiles_y)) * zc;
+    const int X0 = (tile % tiles_x) * TX, Y0 = (tile / tiles_x) * TY;
+    const int YS = Y0 - H;               // global row of LDS row 0
+    const int MS = (X0 - kFusedHX) / 2;  // global packed m of LDS m = 0
+    const int nz = (int)g.nz;
+    const int hw = g.hw;
+    const int Hh = (int)g.H;
+    auto plane = [&](int q) { return (int64_t)q * g.P; };
+    // ring slot of plane q (q >= -RU)
+    auto slot = [&](int q) { return ring + ((q + 4 * RU) % RU) * PS; };
+    auto zrange = [&](int q, int k) {  // plane q gets half-sweep k
+        return q >= 0 && q < nz && q >= Z0 - (H - k) && q <= Z0 + zc - 1 + (H - k);
+    };
+    const int p_first = Z0 - H, p_last = Z0 + zc - 1 + LAST;
+
+    // ---- per-thread geometry, fixed for the whole stream ----
+    // load item: LDS row l_ye, group l_m0 (both colours)
+    const int l_ye = tid / G, l_m0 = (tid % G) * N;
+    const int l_gy = YS + l_ye, l_gm = MS + l_m0;
+    const bool l_on = tid < YE * G;
+    const bool l_xy = l_on && l_gy >= 0 && l_gy < g.ny && l_gm >= 0 && 2 * l_gm < g.nx;
+    const int l_g = l_gy * hw + l_gm;  // in-plane offset, colour 0
+    const int l_s = l_ye * HWE + l_m0;
+    // half-sweep item of stage k: LDS row k + tid / G, same group for every stage
+    const int s_m0 = (tid % G) * N, s_gm = MS + s_m0;
+    const bool s_x = s_gm >= 0 && 2 * s_gm < g.nx;
+    const bool s_lo = s_m0 > 0, s_hi = s_m0 + N < HWE;
+    // residual item: coarse row r_jt, W coarse cells from r_m0 (LDS m of the fine cells)
+    const int r_jt = tid / RG, r_m0 = kFusedHX / 2 + (tid % RG) * W;
+    const bool r_on = PRE && tid < (TY / 2) * RG;
+    const int r_gm = MS + r_m0;
+    // output item
+    const int o_r = tid / (2 * OG), o_c = (tid / OG) & 1, o_m0 = kFusedHX / 2 + (tid % OG) * N;
+    const bool o_on = tid < TY * 2 * OG;
+    const int o_g = o_c * Hh + (Y0 + o_r) * hw + MS + o_m0;
+    const int o_s = o_c * CH + (H + o_r) * HWE + o_m0;
+
+    auto prefetch = [&](FusedPrefetch<T, NS>& r, int p) {
+        r.u0 = vzero<T, N>();
+        r.u1 = vzero<T, N>();
+        if (l_xy && p >= 0 && p < nz && p <= Z0 + zc - 1 + H) {
+            const T* sp = src + plane(p);
+            r.u0 = vload<T, N>(sp + l_g);
+            r.u1 = vload<T, N>(sp + Hh + l_g);
+            if (!PRE) {
+                const int J = l_gy >> 1, K = p >> 1;
+                int Jn = (l_gy & 1) ? J + 1 : J - 1;
+                if (Jn < 0 || Jn >= gc.ny) Jn = J;
+                int Kn = (p & 1) ? K + 1 : K - 1;
+                if (Kn < 0 || Kn >= gc.gnz) Kn = K;
+                coarse_row<T, N>(V, gc, J, K, l_gm, r.c00);
+                if (LINEAR) {
+                    coarse_row<T, N>(V, gc, Jn, K, l_gm, r.c10);
+                    coarse_row<T, N>(V, gc, J, Kn, l_gm, r.c01);
+                    coarse_row<T, N>(V, gc, Jn, Kn, l_gm, r.c11);
+                }
+            }
+        }
+#pragma unroll
+        for (int k = 1; k <= 2 * NS; ++k) {
+            r.fk[k - 1] = vzero<T, N>();
+            const int q = p - (2 * k - 1);
+            const int gy = YS + k + tid / G;
+            if (zrange(q, k) && tid < (YE - 2 * k) * G && s_x && gy >= 0 && gy < g.ny)
+                r.fk[k - 1] = vload<T, N>(f + plane(q) + ((k - 1) & 1) * Hh + gy * hw + s_gm);
+        }
+        const int q = p - LAST;
+        const bool last = q >= Z0 && q < Z0 + zc;
+        if (PRE) {
+#pragma unroll
+            for (int dy = 0; dy < 2; ++dy)
+#pragma unroll
+                for (int c = 0; c < 2; ++c) {
+                    if (r_on && last) {
+                        const T* fp = f + plane(q) + c * Hh + (Y0 + 2 * r_jt + dy) * hw + r_gm;
+                        if (W == 2) {
+                            const Vec<T, 2> v = vload<T, 2>(fp);
+                            r.fr[dy][c][0] = v.v[0];
+                            r.fr[dy][c][W - 1] = v.v[1];
+                        } else {
+#pragma unroll
+                            for (int e = 0; e < W; ++e) r.fr[dy][c][e] = fp[e];
+                        }
+                    } else {
+#pragma unroll
+                        for (int e = 0; e < W; ++e) r.fr[dy][c][e] = (T)0;
+                    }
+                }
+        }
+        if (ERR) {
+            r.old = vzero<T, N>();
+            if (last && o_on) r.old = vload<T, N>(dst + plane(q) + o_g);
+        }
+    };
+
+    T acc[W];  // PRE: running restriction sums of this thread's coarse cells
+#pragma unroll
+    for (int e = 0; e < W; ++e) acc[e] = (T)0;
+    double err = 0.0;
+
+    FusedPrefetch<T, NS> nxt;
+    prefetch(nxt, p_first);
+    for (int p = p_first; p <= p_last; ++p) {
+        const FusedPrefetch<T, NS> cur = nxt;
+        if (p < p_last) prefetch(nxt, p + 1);
+
+        // ---- stage 0: plane p into the ring (POST: u + P V, k_prolong_v's expressions) ----
+        if (l_on) {
+            Vec<T, N> v0 = cur.u0, v1 = cur.u1;
+            if (!PRE && l_xy && p >= 0 && p < nz && p <= Z0 + zc - 1 + H) {
+                const int I0 = l_gm, cx = gc.nx;
+                const int J = l_gy >> 1, K = p >> 1;
+                const int Jn = (l_gy & 1) ? J + 1 : J - 1;
+                const bool oy = Jn < 0 || Jn >= gc.ny;
+                const int Kn = (p & 1) ? K + 1 : K - 1;
+                const bool oz = Kn < 0 || Kn >= gc.gnz;
+                const T w0 = (T)0.75, w1 = (T)0.25, cl = clc;
+                auto sv = [&](T val, bool fx, bool fy, bool fz) {
+                    T s = (T)1;
+                    if (fx) s = -cl * s;
+                    if (fy) s = -cl * s;
+                    if (fz) s = -cl * s;
+                    return s == (T)1 ? val : s * val;
+                };
+                const int pp = (l_gy + p) & 1;
+                const bool interior = !oy && !oz && I0 > 0 && I0 + N < cx;
+#pragma unroll
+                for (int c = 0; c < 2; ++c) {
+                    const int o = c ^ pp;
+                    Vec<T, N>& uv = c ? v1 : v0;
+#pragma unroll
+                    for (int e = 0; e < N; ++e) {
+                        const int pe = e + 1;
+                        T v;
+                        if (!LINEAR) {
+                            v = cur.c00[pe];
+                        } else if (interior) {
+                            const T nb00 = o ? cur.c00[e + 2] : cur.c00[e];
+                            const T nb10 = o ? cur.c10[e + 2] : cur.c10[e];
+                            const T nb01 = o ? cur.c01[e + 2] : cur.c01[e];
+                            const T nb11 = o ? cur.c11[e + 2] : cur.c11[e];
+                            const T a00 = w0 * cur.c00[pe] + w1 * nb00;
+                            const T a10 = w0 * cur.c10[pe] + w1 * nb10;
+                            const T a01 = w0 * cur.c01[pe] + w1 * nb01;
+                            const T a11 = w0 * cur.c11[pe] + w1 * nb11;
+                            const T b0 = w0 * a00 + w1 * a10;
+                            const T b1 = w0 * a01 + w1 * a11;
+                            v = w0 * b0 + w1 * b1;
+                        } else {
+                            const bool ox = (o == 0 && I0 + e == 0) || (o == 1 && I0 + e == cx - 1);
+                            auto col = [&](const T (&cc)[N + 2]) { return ox ? cc[pe] : (o ? cc[e + 2] : cc[e]); };
+                            const T a00 = w0 * cur.c00[pe] + w1 * sv(col(cur.c00), ox, false, false);
+                            const T a10 = w0 * sv(cur.c10[pe], false, oy, false) + w1 * sv(col(cur.c10), ox, oy, false);
+                            const T a01 = w0 * sv(cur.c01[pe], false, false, oz) + w1 * sv(col(cur.c01), ox, false, oz);
+                            const T a11 = w0 * sv(cur.c11[pe], false, oy, oz) + w1 * sv(col(cur.c11), ox, oy, oz);
+                            const T b0 = w0 * a00 + w1 * a10;
+                            const T b1 = w0 * a01 + w1 * a11;
+                            v = w0 * b0 + w1 * b1;
+                        }
+                        uv.v[e] = uv.v[e] + v;
+                    }
+                }
+            }
+            T* P = slot(p);
+            vstore<T, N>(P + l_s, v0);
+            vstore<T, N>(P + CH + l_s, v1);
+        }
+        lds_barrier();
+
+        // ---- stages 1 .. 2 NS: red/black half-sweeps on planes p - (2k - 1), independent ----
+#pragma unroll
+        for (int k = 1; k <= 2 * NS; ++k) {
+            const int q = p - (2 * k - 1);
+            const int c = (k - 1) & 1;  // red first
+            const int ye = k + tid / G;
+            const int gy = YS + ye;
+            if (zrange(q, k) && tid < (YE - 2 * k) * G && s_x && gy >= 0 && gy < g.ny) {
+                T* P = slot(q);
+                const T* Pm = slot(q - 1);
+                const T* Pp = slot(q + 1);
+                const int o = c ^ ((gy + q) & 1);
+                const int own = c * CH + ye * HWE + s_m0;
+                const int oth = (c ^ 1) * CH + ye * HWE + s_m0;
+                const Vec<T, N> cen = vload<T, N>(P + oth);
+                T edge;
+                if (o == 0)
+                    edge = s_lo ? P[oth - 1] : (T)0;
+                else
+                    edge = s_hi ? P[oth + N] : (T)0;
+                const Vec<T, N> yl = vload<T, N>(P + oth - HWE);  // ye >= 1
+                const Vec<T, N> yr = vload<T, N>(P + oth + HWE);  // ye <= YE - 2
+                const Vec<T, N> zl = vload<T, N>(Pm + oth);
+                const Vec<T, N> zr = vload<T, N>(Pp + oth);
+                const Vec<T, N>& fv = cur.fk[k - 1];
+                int nbyz = 0;
+                if (!CLZ) nbyz = (gy == 0) + (gy == g.ny - 1) + (q == 0) + (q == g.gnz - 1);
+                Vec<T, N> out;
+#pragma unroll
+                for (int e = 0; e < N; ++e) {
+                    const T xl = o == 0 ? (e == 0 ? edge : cen.v[e - 1]) : cen.v[e];
+                    const T xr = o == 0 ? cen.v[e] : (e == N - 1 ? edge : cen.v[e + 1]);
+                    T s = xl + xr;
+                    s = s + yl.v[e];
+                    s = s + yr.v[e];
+                    s = s + zl.v[e];
+                    s = s + zr.v[e];
+                    if (CLZ) {
+                        out.v[e] = div_rn(fv.v[e] - s * op.inv_hSq, op.adiag, op.yadiag);
+                    } else {
+                        const int i = 2 * (s_gm + e) + o;
+                        out.v[e] = op.relax(s, fv.v[e], nbyz + (i == 0) + (i == g.nx - 1));
+                    }
+                }
+                vstore<T, N>(P + own, out);
+            }
+        }
+
+        // ---- last stage on plane q = p - LAST ----
+        const int q = p - LAST;
+        if (q >= Z0 && q < Z0 + zc) {
+            const T* P = slot(q);
+            if (o_on) {  // the smoothed tile region -> dst (POST with ERR: against psiOld)
+                const Vec<T, N> v = vload<T, N>(P + o_s);
+                if (ERR) {
+#pragma unroll
+                    for (int e = 0; e < N; ++e) {
+                        const double df = (double)v.v[e] - (double)cur.old.v[e];
+                        err += df * df;
+                    }
+                }
+                vstore<T, N>(dst + plane(q) + o_g, v);
+            }
+            if (r_on) {
+                // residual + restriction (k_resrestrict's expressions): thread -> W coarse cells
+                const int qz = (q - Z0) & 1;
+                const int j0e = H + 2 * r_jt, j0 = Y0 + 2 * r_jt;
+                const T* Pm = slot(q - 1);
+                const T* Pp = slot(q + 1);
+                const bool xlo = r_gm == 0, xhi = r_gm + W == hw;
+                auto ld = [&](const T* base) {
+                    Vec<T, W> v;
+                    if (W == 2) {
+                        v = vload<T, W>(base);
+                    } else {
+#pragma unroll
+                        for (int e = 0; e < W; ++e) v.v[e] = base[e];
+                    }
+                    return v;
+                };
+                Vec<T, W> M[4][2], Z[2][2][2];
+#pragma unroll
+                for (int yi = 0; yi < 4; ++yi)
+#pragma unroll
+                    for (int c = 0; c < 2; ++c) M[yi][c] = ld(P + c * CH + (j0e - 1 + yi) * HWE + r_m0);
+#pragma unroll
+                for (int yi = 0; yi < 2; ++yi)
+#pragma unroll
+                    for (int c = 0; c < 2; ++c) {
+                        Z[0][yi][c] = ld(Pm + c * CH + (j0e + yi) * HWE + r_m0);
+                        Z[1][yi][c] = ld(Pp + c * CH + (j0e + yi) * HWE + r_m0);
+                    }
+#pragma unroll
+                for (int dy = 0; dy < 2; ++dy) {
+                    const int j = j0 + dy;
+                    const int pj = (j + q) & 1;
+                    const int nbyz = (j == 0) + (j == g.ny - 1) + (q == 0) + (q == g.gnz - 1);
+                    const bool fast = CLZ || (nbyz == 0 && !xlo && !xhi);
+                    T rr[2][W];
+#pragma unroll
+                    for (int c = 0; c < 2; ++c) {
+                        const int o = c ^ pj;
+                        const int oc = c ^ 1;
+                        const Vec<T, W>& cen = M[dy + 1][oc];
+                        const Vec<T, W>& uc = M[dy + 1][c];
+                        const int othe = oc * CH + (j0e + dy) * HWE + r_m0;
+                        const T edge = o == 0 ? (xlo ? (T)0 : P[othe - 1]) : (xhi ? (T)0 : P[othe + W]);
+#pragma unroll
+                        for (int e = 0; e < W; ++e) {
+                            const T xl = o == 0 ? (e == 0 ? edge : cen.v[e - 1]) : cen.v[e];
+                            const T xr = o == 0 ? cen.v[e] : (e == W - 1 ? edge : cen.v[e + 1]);
+                            T s = xl + xr;
+                            s = s + M[dy][oc].v[e];
+                            s = s + M[dy + 2][oc].v[e];
+                            s = s + Z[0][dy][oc].v[e];
+                            s = s + Z[1][dy][oc].v[e];
+                            const T fc = cur.fr[dy][c][e];
+                            T res;
+                            if (fast) {
+                                const T askew = s * op.inv_hSq;
+                                const T a_u = askew + op.adiag * uc.v[e];
+                                res = fc - a_u;
+                            } else {
+                                const int i = 2 * (r_gm + e) + o;
+                                res = op.residual(s, fc, uc.v[e], nbyz + (i == 0) + (i == g.nx - 1));
+                            }
+                            rr[o][e] = res;
+                        }
+                    }
+#pragma unroll
+                    for (int e = 0; e < W; ++e) {
+                        if (qz == 0 && dy == 0) {
+                            acc[e] = rr[0][e] + rr[1][e];
+                        } else {
+                            acc[e] = acc[e] + rr[0][e];
+                            acc[e] = acc[e] + rr[1][e];
+                        }
+                    }
+                }
+                if (qz == 1) {
+                    const int J = j0 >> 1, K = q >> 1;
+                    const int pc = (J + K) & 1;
+                    T* rowc = R + (int64_t)K * gc.P + (int64_t)J * gc.hw;
+#pragma unroll
+                    for (int e = 0; e < W; ++e) {
+                        const int I = r_gm + e;
+                        rowc[((I + pc) & 1) * gc.H + (I >> 1)] = (T)0.125 * acc[e];
+                    }
+                }
+            }
+        }
+        lds_barrier();
+    }
+    if (ERR) block_partial_n<T>(err, partials, kFusedThreads);
+}
+
+// ---- coarse-level tail ----------------------------------------------------------------------
+//
+// The levels at and below ~16^3 cost one launch (3-5 us) per piece while their work is a few
+// thousand cells.  k_tail runs the whole sub-cycle below level T — the ops of cycle_rec(T, ...)
+// that the host recorded into TailSpec::ops — in ONE workgroup with every level resident in LDS
+// (same packed layout, ghost planes zero), a __syncthreads() between dependent phases.  The
+// per-cell arithmetic is the scalar kernels' (half_item / resrestrict_item / prolong_item), so
+// results are bit-identical to the launch-per-piece path.
+
+// 1024 threads = 16 waves on the CU; fp64 gets 512 so the kernel keeps 256 VGPRs without spills
+template <typename T>
+constexpr int tail_threads() { return sizeof(T) == 4 ? 1024 : 512; }
+
+template <typename T, int DIM>
+struct TailArgs {
+    int nlev, nops, jacobi, pad;
+    int64_t off[kTailMaxLevels];     // element offset of the level's LDS region
+    int64_t region[kTailMaxLevels];  // elements of one LDS array of the level (ghost planes included)
+    T* u[kTailMaxLevels];            // global interior plane 0 of u / f
+    T* f[kTailMaxLevels];
+    Geo g[kTailMaxLevels];
+    Op<T, DIM> op[kTailMaxLevels];
+    uint32_t ops[kTailMaxOps];
+};
+
+template <typename T, int DIM, int LINEAR>
+__global__ __launch_bounds__(tail_threads<T>()) void k_tail(const TailArgs<T, DIM> a)
+{
+    constexpr int kTailThreads = tail_threads<T>();
+    extern __shared__ __align__(16) unsigned char tail_smem[];
+    T* const lds = reinterpret_cast<T*>(tail_smem);
+    constexpr int G = DIM == 3 ? kGhost3D : 0;
+    const int tid = threadIdx.x;
+    // level l: u at off, f at off + region, Jacobi target at off + 2 region
+    for (int l = 0; l < a.nlev; ++l) {
+        const Geo& g = a.g[l];
+        T* U = lds + a.off[l];
+        T* F = U + a.region[l];
+        const int64_t lo = G * g.P, n = g.nz * g.P;
+        for (int64_t e = tid; e < a.region[l]; e += kTailThreads) {
+            const int64_t ie = e - lo;
+            const bool in = ie >= 0 && ie < n;
+            U[e] = in ? a.u[l][ie] : (T)0;
+            F[e] = in ? a.f[l][ie] : (T)0;
+            if (a.jacobi) U[e + 2 * a.region[l]] = (T)0;
+        }
+    }
+    __syncthreads();
+    unsigned alt = 0;  // Jacobi: bit l = level l's iterate currently lives in its second array
+    auto cur = [&](int l) { return lds + a.off[l] + G * a.g[l].P + (((alt >> l) & 1) ? 2 * a.region[l] : 0); };
+    auto rhs = [&](int l) { return lds + a.off[l] + a.region[l] + G * a.g[l].P; };
+    for (int pc = 0; pc < a.nops; ++pc) {
+        const uint32_t w = a.ops[pc];
+        const int op = (int)(w & 15), l = (int)((w >> 4) & 15), arg = (int)(w >> 8);
+        const Geo g = a.g[l];
+        const int64_t half = g.H * g.nz;
+        if (op == TAIL_SMOOTH) {
+            for (int sw = 0; sw < arg; ++sw) {
+                T* U = cur(l);
+                const T* F = rhs(l);
+                T v;
+                if (a.jacobi) {  // both colours from the old iterate into the other array
+                    T* D = lds + a.off[l] + G * g.P + (((alt >> l) & 1) ? 0 : 2 * a.region[l]);
+                    for (int64_t it = tid; it < 2 * half; it += kTailThreads) {
+                        const int c = it >= half;
+                        half_item<T, DIM>(U, F, D, g, c, a.op[l], it - c * half, &v);
+                    }
+                    alt ^= 1u << l;
+                    __syncthreads();
+                } else {
+                    for (int c = 0; c < 2; ++c) {
+                        for (int64_t it = tid; it < half; it += kTailThreads) half_item<T, DIM>(U, F, U, g, c, a.op[l], it, &v);
+                        __syncthreads();
+                    }
+                }
+            }
+        } else if (op == TAIL_RR) {
+            const int64_t n = resrestrict_items<T, DIM>(g);
+            for (int64_t it = tid; it < n; it += kTailThreads)
+                resrestrict_item<T, DIM>(cur(l), rhs(l), rhs(l + 1), g, a.g[l + 1], a.op[l], it);
+            __syncthreads();
+        } else if (op == TAIL_ZERO) {
+            T* U = cur(l);
+            for (int64_t e = tid; e < g.nz * g.P; e += kTailThreads) U[e] = (T)0;
+            __syncthreads();
+        } else if (op == TAIL_PROLONG) {
+            for (int64_t it = tid; it < 2 * half; it += kTailThreads) {
+                const int c = it >= half;
+                prolong_item<T, DIM, LINEAR>(cur(l), cur(l + 1), g, a.g[l + 1], a.op[l + 1].cl, c, it - c * half);
+            }
+            __syncthreads();
+        }
+    }
+    for (int l = 0; l < a.nlev; ++l) {
+        const T* U = cur(l);
+        const T* F = rhs(l);
+        const int64_t n = a.g[l].nz * a.g[l].P;
+        for (int64_t e = tid; e < n; e += kTailThreads) {
+            a.u[l][e] = U[e];
+            a.f[l][e] = F[e];
+        }
     }
 }
 
@@ -850,6 +1420,145 @@ hipError_t launch_prolong_correct(int rb, int dim, int linear, void* u, const vo
 {
     if (rb == 8) return dim == 3 ? pr_t<double, 3>(linear, u, V, g, gc, clc, s) : pr_t<double, 2>(linear, u, V, g, gc, clc, s);
     return dim == 3 ? pr_t<float, 3>(linear, u, V, g, gc, clc, s) : pr_t<float, 2>(linear, u, V, g, gc, clc, s);
+}
+
+// ---- fused smoothing phases ----
+
+template <typename T, int NS, bool PRE, int LINEAR, bool ERR, bool CLZ>
+static hipError_t fused_launch(const FusedArgs& a, hipStream_t s)
+{
+    using S = FusedShape<T, NS, PRE>;
+    auto kern = k_fused<T, NS, PRE, LINEAR, ERR, CLZ>;
+    const Op<T, 3> op = make_op<T, 3>(a.h, a.cl);
+    const unsigned nb = (unsigned)fused_blocks(sizeof(T), a.g, a.zc);
+    kern<<<nb, kFusedThreads, S::lds_bytes, s>>>((const T*)a.src, (const T*)a.f, (T*)a.dst, (T*)a.R, (const T*)a.V,
+                                                  a.partials, a.g, a.gc, op, (T)a.clc, a.zc);
+    return hipGetLastError();
+}
+
+template <typename T, bool CLZ>
+static hipError_t fused_dispatch(const FusedArgs& a, hipStream_t s)
+{
+    const bool err = a.partials != nullptr;
+    if (a.pre) return fused_launch<T, 2, true, 0, false, CLZ>(a, s);
+    if (a.linear) return err ? fused_launch<T, 2, false, 1, true, CLZ>(a, s) : fused_launch<T, 2, false, 1, false, CLZ>(a, s);
+    return err ? fused_launch<T, 2, false, 0, true, CLZ>(a, s) : fused_launch<T, 2, false, 0, false, CLZ>(a, s);
+}
+
+bool fused_supported(int rb, int dim, int ns, const Geo& g)
+{
+    if (dim != 3 || ns != 2) return false;
+    const int TX = rb == 4 ? FusedTile<float>::TX : FusedTile<double>::TX;
+    const int TY = rb == 4 ? FusedTile<float>::TY : FusedTile<double>::TY;
+    return g.nx % TX == 0 && g.ny % TY == 0 && g.nz >= 16 && (g.nz & 1) == 0 && g.z0 == 0 && g.gnz == g.nz;
+}
+
+int fused_zc(int rb, const Geo& g)
+{
+    const int TX = rb == 4 ? FusedTile<float>::TX : FusedTile<double>::TX;
+    const int TY = rb == 4 ? FusedTile<float>::TY : FusedTile<double>::TY;
+    const int64_t tiles = (int64_t)(g.nx / TX) * (g.ny / TY);
+    int64_t chunks = 1;
+    while (tiles * chunks < 512 && g.nz / (chunks * 2) >= 16) chunks *= 2;
+    return (int)(g.nz / chunks);
+}
+
+int fused_blocks(int rb, const Geo& g, int zc)
+{
+    const int TX = rb == 4 ? FusedTile<float>::TX : FusedTile<double>::TX;
+    const int TY = rb == 4 ? FusedTile<float>::TY : FusedTile<double>::TY;
+    return (int)((int64_t)(g.nx / TX) * (g.ny / TY) * (g.nz / zc));
+}
+
+template <typename T, bool CLZ>
+static hipError_t fused_attr()
+{
+    const int pre = (int)FusedShape<T, 2, true>::lds_bytes, post = (int)FusedShape<T, 2, false>::lds_bytes;
+    const auto A = hipFuncAttributeMaxDynamicSharedMemorySize;
+    hipError_t e = hipFuncSetAttribute((const void*)k_fused<T, 2, true, 0, false, CLZ>, A, pre);
+    if (e == hipSuccess) e = hipFuncSetAttribute((const void*)k_fused<T, 2, false, 0, false, CLZ>, A, post);
+    if (e == hipSuccess) e = hipFuncSetAttribute((const void*)k_fused<T, 2, false, 0, true, CLZ>, A, post);
+    if (e == hipSuccess) e = hipFuncSetAttribute((const void*)k_fused<T, 2, false, 1, false, CLZ>, A, post);
+    if (e == hipSuccess) e = hipFuncSetAttribute((const void*)k_fused<T, 2, false, 1, true, CLZ>, A, post);
+    return e;
+}
+
+template <typename T, int D>
+static hipError_t tail_attr()
+{
+    hipError_t e = hipFuncSetAttribute((const void*)k_tail<T, D, 0>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)kTailMaxLds);
+    if (e == hipSuccess)
+        e = hipFuncSetAttribute((const void*)k_tail<T, D, 1>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)kTailMaxLds);
+    return e;
+}
+
+hipError_t prepare_kernels(int rb)
+{
+    hipError_t e = hipSuccess;
+#define MGP_CHAIN(x) \
+    if (e == hipSuccess) e = (x)
+    if (rb == 4) {
+        MGP_CHAIN((fused_attr<float, true>()));
+        MGP_CHAIN((fused_attr<float, false>()));
+        MGP_CHAIN((tail_attr<float, 2>()));
+        MGP_CHAIN((tail_attr<float, 3>()));
+    } else {
+        MGP_CHAIN((fused_attr<double, true>()));
+        MGP_CHAIN((fused_attr<double, false>()));
+        MGP_CHAIN((tail_attr<double, 2>()));
+        MGP_CHAIN((tail_attr<double, 3>()));
+    }
+#undef MGP_CHAIN
+    return e;
+}
+
+hipError_t launch_fused(int rb, const FusedArgs& a, hipStream_t s)
+{
+    const bool clz = a.cl == 0.0;
+    if (rb == 4) return clz ? fused_dispatch<float, true>(a, s) : fused_dispatch<float, false>(a, s);
+    return clz ? fused_dispatch<double, true>(a, s) : fused_dispatch<double, false>(a, s);
+}
+
+size_t tail_lds_bytes(int rb, int dim, int jacobi, const Geo* g, int nlev)
+{
+    const int G = dim == 3 ? kGhost3D : 0;
+    size_t n = 0;
+    for (int l = 0; l < nlev; ++l) n += (size_t)((g[l].nz + 2 * G) * g[l].P) * (jacobi ? 3 : 2);
+    return n * (size_t)rb;
+}
+
+template <typename T, int D>
+static hipError_t tail_t(const TailSpec& t, hipStream_t s)
+{
+    TailArgs<T, D> a{};
+    a.nlev = t.nlev;
+    a.nops = t.nops;
+    a.jacobi = t.jacobi;
+    const int G = D == 3 ? kGhost3D : 0;
+    int64_t off = 0;
+    for (int l = 0; l < t.nlev; ++l) {
+        a.g[l] = t.g[l];
+        a.u[l] = (T*)t.u[l];
+        a.f[l] = (T*)t.f[l];
+        a.op[l] = make_op<T, D>(t.h[l], t.cl[l]);
+        a.region[l] = (t.g[l].nz + 2 * G) * t.g[l].P;
+        a.off[l] = off;
+        off += a.region[l] * (t.jacobi ? 3 : 2);
+    }
+    for (int i = 0; i < t.nops; ++i) a.ops[i] = t.ops[i];
+    const size_t bytes = (size_t)off * sizeof(T);
+    auto kern = t.linear ? k_tail<T, D, 1> : k_tail<T, D, 0>;
+    kern<<<1, tail_threads<T>(), bytes, s>>>(a);
+    return hipGetLastError();
+}
+
+hipError_t launch_tail(int rb, int dim, const TailSpec& t, hipStream_t s)
+{
+    if (t.nlev < 1 || t.nlev > kTailMaxLevels || t.nops > kTailMaxOps) return hipErrorInvalidValue;
+    if (rb == 8) return dim == 3 ? tail_t<double, 3>(t, s) : tail_t<double, 2>(t, s);
+    return dim == 3 ? tail_t<float, 3>(t, s) : tail_t<float, 2>(t, s);
 }
 
 hipError_t launch_sqdiff_sum(int rb, const void* a, const void* b, int64_t n, double* partials, double* out,

@@ -40,6 +40,8 @@ COARSE_FRESH, COARSE_WARM = 0, 1
 BC_ZERO, BC_CONSISTENT = 0, 1
 FIELD_U, FIELD_F = 0, 1
 MEM_HOST, MEM_DEVICE = 0, 1
+TIMING_HALF_SWEEP, TIMING_FUSED_PRE, TIMING_FUSED_POST = 0, 1, 2
+TIMING_KINDS = {TIMING_HALF_SWEEP: "half_sweep", TIMING_FUSED_PRE: "fused_pre", TIMING_FUSED_POST: "fused_post"}
 COMM_ID_BYTES = 128
 
 
@@ -91,7 +93,7 @@ SIGNATURES = {
     "mgp_coarse_solve": (ctypes.c_int, [_vp]),
     "mgp_sync": (ctypes.c_int, [_vp]),
     "mgp_timing": (ctypes.c_int, [_vp, ctypes.c_int]),
-    "mgp_timing_read": (ctypes.c_int, [_vp, _P(_dbl), _P(_i64), _P(_dbl)]),
+    "mgp_timing_read": (ctypes.c_int, [_vp, ctypes.c_int, _P(_dbl), _P(_i64), _P(_dbl)]),
 }
 
 for _name, (_res, _args) in SIGNATURES.items():

@@ -59,7 +59,7 @@ class Context:
         for l in range(L.lib.mgp_num_levels(self._h)):
             L.check(L.lib.mgp_level_info(self._h, l, info), self._h)
             self.levels.append(dict(nx=info[0], ny=info[1], nz_global=info[2], nz_local=info[3],
-                                    z0=info[4], distributed=bool(info[5])))
+                                    z0=info[4], distributed=bool(info[5]), tail=bool(info[6])))
 
     # -- lifecycle --
     def close(self):
@@ -161,6 +161,10 @@ class Context:
         self._chk(L.lib.mgp_timing(self._h, 1 if enable else 0))
 
     def timing_read(self):
-        ms, n, sw = ctypes.c_double(), ctypes.c_int64(), ctypes.c_double()
-        self._chk(L.lib.mgp_timing_read(self._h, ctypes.byref(ms), ctypes.byref(n), ctypes.byref(sw)))
-        return ms.value, n.value, sw.value
+        """{kind name: (kernel ms, launches, algorithmic bytes)} of the level-0 launches timed so far."""
+        out = {}
+        for kind, name in L.TIMING_KINDS.items():
+            ms, n, by = ctypes.c_double(), ctypes.c_int64(), ctypes.c_double()
+            self._chk(L.lib.mgp_timing_read(self._h, kind, ctypes.byref(ms), ctypes.byref(n), ctypes.byref(by)))
+            out[name] = (ms.value, n.value, by.value)
+        return out

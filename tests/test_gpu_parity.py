@@ -228,6 +228,93 @@ def test_graph_replay_equals_eager(monkeypatch):
     assert np.array_equal(eg, ee)
 
 
+TAIL_CONFIGS = [
+    dict(dim=3, n=64, real="float", smoother="rbgs", nu1=2, nu2=2, prolong="linear", coarse_bc="consistent"),
+    dict(dim=3, n=32, real="double", smoother="rbgs", nu1=2, nu2=2, cycle="F", prolong="linear", coarse_bc="consistent"),
+    dict(dim=3, n=32, real="double", smoother="jacobi", prolong="pc"),
+    dict(dim=3, n=(64, 32, 16), real="float", smoother="jacobi", nu1=3, nu2=2, cycle="F", prolong="linear",
+         coarse_bc="consistent", coarse_init="warm"),
+    dict(dim=2, n=256, real="double"),
+    dict(dim=2, n=128, real="float", smoother="rbgs", nu1=2, nu2=2, cycle="F", prolong="linear", coarse_bc="consistent"),
+    dict(dim=2, n=64, real="double", coarse_init="warm"),
+]
+
+
+@pytest.mark.parametrize("cfg", TAIL_CONFIGS, ids=_cfg_id)
+def test_tail_equals_launch_per_piece(cfg, monkeypatch):
+    """The one-launch LDS coarse tail (k_tail) == one launch per piece, on every level."""
+    cfg = dict(cfg)
+    dim, n = cfg.pop("dim"), cfg.pop("n")
+    box = n if isinstance(n, tuple) else _n3(dim, n)
+    a = _ctx(dim=dim, n=box, **cfg)
+    monkeypatch.setenv("MGP_TAIL", "0")
+    b = _ctx(dim=dim, n=box, **cfg)
+    assert any(lv["tail"] for lv in a.levels) and not any(lv["tail"] for lv in b.levels)
+    assert not a.levels[0]["tail"]
+    a.init_point_charge()
+    b.init_point_charge()
+    for _ in range(3):
+        assert a.cycle() == b.cycle()
+    for level in range(len(a.levels)):
+        assert np.array_equal(a.get_psi(level), b.get_psi(level)), f"psi level {level}"
+        assert np.array_equal(a.get_f(level), b.get_f(level)), f"f level {level}"
+
+
+FUSED_CONFIGS = [
+    dict(n=(128, 128, 128), real="float", prolong="linear", coarse_bc="consistent"),
+    dict(n=(64, 64, 64), real="float", prolong="linear", coarse_bc="consistent", cycle="F"),
+    dict(n=(128, 64, 32), real="double", prolong="pc", coarse_bc="zero"),
+    dict(n=(64, 128, 64), real="double", prolong="linear", coarse_bc="consistent", coarse_init="warm"),
+    dict(n=(64, 32, 128), real="float", prolong="pc", coarse_bc="consistent", err_mode=0),
+]
+
+
+@pytest.mark.parametrize("cfg", FUSED_CONFIGS, ids=_cfg_id)
+def test_fused_phases_match_oracle(cfg, monkeypatch):
+    """Temporally blocked RB-GS 2+2 phases (k_fused, forced down to 64^3 here) vs one launch per
+    half-sweep vs the C oracle: psi bit-identical on every level; err to summation order."""
+    kw = dict(dim=3, smoother="rbgs", nu1=2, nu2=2, **cfg)
+    monkeypatch.setenv("MGP_FUSED_MIN_CELLS", "65536")
+    monkeypatch.setenv("MGP_FUSED", "1")
+    a = _ctx(**kw)
+    monkeypatch.setenv("MGP_FUSED", "0")
+    b = _ctx(**kw)
+    o = Oracle(threads=8, **{k: v for k, v in kw.items() if k != "err_mode"})
+    for x in (a, b, o):
+        x.init_point_charge()
+    for it in range(3):
+        old = o.get(0)
+        ea, eb, eo = a.cycle(), b.cycle(), o.step()
+        new = o.get(0)
+        assert np.array_equal(a.get_psi(), new), f"fused psi differs after cycle {it + 1}"
+        assert np.array_equal(b.get_psi(), new), f"unfused psi differs after cycle {it + 1}"
+        if kw.get("err_mode", 1):
+            _check_err(ea, eo, new, old)
+            assert abs(ea - eb) <= 1e-12 * abs(eb)
+    for level in range(len(a.levels)):
+        assert np.array_equal(a.get_psi(level), b.get_psi(level)), f"psi level {level}"
+
+
+def test_fused_timing_kinds(monkeypatch):
+    """The bench's roofline window sees the fused level-0 kernels with their algorithmic bytes."""
+    monkeypatch.setenv("MGP_FUSED_MIN_CELLS", "65536")
+    monkeypatch.setenv("MGP_FUSED", "1")
+    kw = dict(dim=3, n=(64, 64, 64), real="float", smoother="rbgs", nu1=2, nu2=2, prolong="linear",
+              coarse_bc="consistent")
+    a = _ctx(**kw)
+    a.init_point_charge()
+    a.timing(True)
+    a.cycles(3)
+    t = a.timing_read()
+    a.timing(False)
+    cells = 64 ** 3
+    assert t["half_sweep"][1] == 0
+    assert t["fused_pre"][1] == 3 and t["fused_post"][1] == 3
+    assert t["fused_pre"][2] == 3 * 8.125 * 4 * cells
+    assert t["fused_post"][2] == 3 * 10.125 * 4 * cells
+    assert t["fused_pre"][0] > 0 and t["fused_post"][0] > 0
+
+
 def test_two_grid_host_buffers():
     """cpu-raw.lua:186 twoGrid(h, u, f, L) on caller buffers == the oracle's mgo_two_grid."""
     import ctypes

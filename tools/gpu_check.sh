@@ -17,7 +17,7 @@ for s in $STEPS; do
   case $s in
     tests) step pytest_gpu 900 python -m pytest tests -m gpu -q -x ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
-    bench) step bench 400 python bench.py --steps 20 --warmup 3 ;;
+    bench) step bench 400 python bench.py --steps 50 --warmup 3 ;;
     prof)  step prof 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 20 --warmup 3 --cpu-cycles 0 ;;
   esac
 done
