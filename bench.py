@@ -40,7 +40,9 @@ def parse():
     p.add_argument("--nu", type=int, default=2)
     p.add_argument("--no-timing", action="store_true", help="skip the per-launch smoother events")
     p.add_argument("--cpu-cycles", type=int, default=2, help="oracle cycles timed for cpu_baseline (0 = skip)")
-    p.add_argument("--traffic", default=None, help="JSON with PMC-measured HBM bytes per finest-smoother launch")
+    p.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "r01_pmc_traffic_half_sweep.json"),
+                   help="JSON with the PMC-measured HBM bytes per launch of the dominant kernel (tools/pmc_traffic.py); "
+                        "used only when its kernel name matches")
     return p.parse_args()
 
 
@@ -133,6 +135,10 @@ def main():
                "fused_pre": f"k_fused<{tname}, 2, true, 0, false>",
                "fused_post": f"k_fused<{tname}, 2, false, {lin}, true>"}
     per_kind = {k: v for k, v in timed.items() if v[1] > 0}
+
+    def grid_of(kind):  # threads per launch of the level-0 kernel (rocprofv3 Grid_Size)
+        cells = n * n * n
+        return cells // 2 // (16 // rb) if kind == "half_sweep" else None
     if per_kind:
         line["level0_kernels"] = {
             k: {"kernel": kernels[k], "launches": n, "avg_us": 1e3 * ms / n, "algorithmic_bytes_per_launch": by / n,
@@ -148,8 +154,9 @@ def main():
         if a.traffic and os.path.exists(a.traffic):
             with open(a.traffic) as fh:
                 tr = json.load(fh)
-            if tr.get("kernel") == kernels[dom]:
+            if tr.get("kernel") == kernels[dom] and tr.get("grid") in (None, grid_of(dom)):
                 roof["traffic"] = tr.get("bytes_per_launch")
+                roof["traffic_source"] = os.path.relpath(a.traffic, ROOT)
         line["roofline"] = roof
 
     if rank == 0 and world == 1 and a.cpu_cycles > 0:

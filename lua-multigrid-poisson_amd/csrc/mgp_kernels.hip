@@ -768,6 +768,25 @@ __device__ __forceinline__ void lds_barrier()
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
+// Lane i <- lane i - 1 (shr) / lane i + 1 (shl) across the whole wavefront (DPP wave_shr:1 /
+// wave_shl:1, GFX9 encodings); the edge lanes receive 0 and are patched by the caller.
+__device__ __forceinline__ int dpp_shr1_i(int v) { return __builtin_amdgcn_update_dpp(0, v, 0x138, 0xf, 0xf, false); }
+__device__ __forceinline__ int dpp_shl1_i(int v) { return __builtin_amdgcn_update_dpp(0, v, 0x130, 0xf, 0xf, false); }
+__device__ __forceinline__ float dpp_shr1(float v) { return __int_as_float(dpp_shr1_i(__float_as_int(v))); }
+__device__ __forceinline__ float dpp_shl1(float v) { return __int_as_float(dpp_shl1_i(__float_as_int(v))); }
+__device__ __forceinline__ double dpp_shr1(double v)
+{
+    const long long b = __double_as_longlong(v);
+    const int lo = dpp_shr1_i((int)b), hi = dpp_shr1_i((int)(b >> 32));
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+__device__ __forceinline__ double dpp_shl1(double v)
+{
+    const long long b = __double_as_longlong(v);
+    const int lo = dpp_shl1_i((int)b), hi = dpp_shl1_i((int)(b >> 32));
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+
 // Global operands of one z-step for this thread, loaded one step ahead.
 template <typename T, int NS>
 struct FusedPrefetch {
@@ -794,6 +813,10 @@ __global__ __launch_bounds__(kFusedThreads) void k_fused(const T* __restrict__ s
                   PS = S::PS, TX = S::TX, TY = S::TY, OG = S::OG;
     constexpr int W = FusedPrefetch<T, NS>::W;
     constexpr int RG = TX / 2 / W;  // residual items per coarse row
+    // POST: step p also writes plane p + 1 (its slot holds plane p - LAST - 1, which no stage of
+    // step p reads), so one barrier per step suffices; PRE's residual still reads that plane.
+    constexpr bool MERGE = !PRE;
+    static_assert(!MERGE || RU >= LAST + 2, "ring too small for the merged load");
     constexpr int CH = YE * HWE;    // reals per colour half of a plane slot
     static_assert((TY / 2) * RG <= kFusedThreads, "residual phase exceeds one item per thread");
     extern __shared__ __align__(16) unsigned char fused_smem[];
@@ -843,15 +866,16 @@ __global__ __launch_bounds__(kFusedThreads) void k_fused(const T* __restrict__ s
     auto prefetch = [&](FusedPrefetch<T, NS>& r, int p) {
         r.u0 = vzero<T, N>();
         r.u1 = vzero<T, N>();
-        if (l_xy && p >= 0 && p < nz && p <= Z0 + zc - 1 + H) {
-            const T* sp = src + plane(p);
+        const int lp = MERGE ? p + 1 : p;  // the plane stage 0 of step p writes
+        if (l_xy && lp >= 0 && lp < nz && lp <= Z0 + zc - 1 + H) {
+            const T* sp = src + plane(lp);
             r.u0 = vload<T, N>(sp + l_g);
             r.u1 = vload<T, N>(sp + Hh + l_g);
             if (!PRE) {
-                const int J = l_gy >> 1, K = p >> 1;
+                const int J = l_gy >> 1, K = lp >> 1;
                 int Jn = (l_gy & 1) ? J + 1 : J - 1;
                 if (Jn < 0 || Jn >= gc.ny) Jn = J;
-                int Kn = (p & 1) ? K + 1 : K - 1;
+                int Kn = (lp & 1) ? K + 1 : K - 1;
                 if (Kn < 0 || Kn >= gc.gnz) Kn = K;
                 coarse_row<T, N>(V, gc, J, K, l_gm, r.c00);
                 if (LINEAR) {
@@ -903,74 +927,76 @@ __global__ __launch_bounds__(kFusedThreads) void k_fused(const T* __restrict__ s
     for (int e = 0; e < W; ++e) acc[e] = (T)0;
     double err = 0.0;
 
-    FusedPrefetch<T, NS> nxt;
-    prefetch(nxt, p_first);
-    for (int p = p_first; p <= p_last; ++p) {
-        const FusedPrefetch<T, NS> cur = nxt;
-        if (p < p_last) prefetch(nxt, p + 1);
-
-        // ---- stage 0: plane p into the ring (POST: u + P V, k_prolong_v's expressions) ----
-        if (l_on) {
-            Vec<T, N> v0 = cur.u0, v1 = cur.u1;
-            if (!PRE && l_xy && p >= 0 && p < nz && p <= Z0 + zc - 1 + H) {
-                const int I0 = l_gm, cx = gc.nx;
-                const int J = l_gy >> 1, K = p >> 1;
-                const int Jn = (l_gy & 1) ? J + 1 : J - 1;
-                const bool oy = Jn < 0 || Jn >= gc.ny;
-                const int Kn = (p & 1) ? K + 1 : K - 1;
-                const bool oz = Kn < 0 || Kn >= gc.gnz;
-                const T w0 = (T)0.75, w1 = (T)0.25, cl = clc;
-                auto sv = [&](T val, bool fx, bool fy, bool fz) {
-                    T s = (T)1;
-                    if (fx) s = -cl * s;
-                    if (fy) s = -cl * s;
-                    if (fz) s = -cl * s;
-                    return s == (T)1 ? val : s * val;
-                };
-                const int pp = (l_gy + p) & 1;
-                const bool interior = !oy && !oz && I0 > 0 && I0 + N < cx;
-#pragma unroll
-                for (int c = 0; c < 2; ++c) {
-                    const int o = c ^ pp;
-                    Vec<T, N>& uv = c ? v1 : v0;
-#pragma unroll
-                    for (int e = 0; e < N; ++e) {
-                        const int pe = e + 1;
-                        T v;
-                        if (!LINEAR) {
-                            v = cur.c00[pe];
-                        } else if (interior) {
-                            const T nb00 = o ? cur.c00[e + 2] : cur.c00[e];
-                            const T nb10 = o ? cur.c10[e + 2] : cur.c10[e];
-                            const T nb01 = o ? cur.c01[e + 2] : cur.c01[e];
-                            const T nb11 = o ? cur.c11[e + 2] : cur.c11[e];
-                            const T a00 = w0 * cur.c00[pe] + w1 * nb00;
-                            const T a10 = w0 * cur.c10[pe] + w1 * nb10;
-                            const T a01 = w0 * cur.c01[pe] + w1 * nb01;
-                            const T a11 = w0 * cur.c11[pe] + w1 * nb11;
-                            const T b0 = w0 * a00 + w1 * a10;
-                            const T b1 = w0 * a01 + w1 * a11;
-                            v = w0 * b0 + w1 * b1;
-                        } else {
-                            const bool ox = (o == 0 && I0 + e == 0) || (o == 1 && I0 + e == cx - 1);
-                            auto col = [&](const T (&cc)[N + 2]) { return ox ? cc[pe] : (o ? cc[e + 2] : cc[e]); };
-                            const T a00 = w0 * cur.c00[pe] + w1 * sv(col(cur.c00), ox, false, false);
-                            const T a10 = w0 * sv(cur.c10[pe], false, oy, false) + w1 * sv(col(cur.c10), ox, oy, false);
-                            const T a01 = w0 * sv(cur.c01[pe], false, false, oz) + w1 * sv(col(cur.c01), ox, false, oz);
-                            const T a11 = w0 * sv(cur.c11[pe], false, oy, oz) + w1 * sv(col(cur.c11), ox, oy, oz);
-                            const T b0 = w0 * a00 + w1 * a10;
-                            const T b1 = w0 * a01 + w1 * a11;
-                            v = w0 * b0 + w1 * b1;
+    // stage 0: plane lp into the ring (POST: u + P V, k_prolong_v's expressions)
+    auto stage0 = [&](const FusedPrefetch<T, NS>& cur, int lp) {
+            if (l_on) {
+                Vec<T, N> v0 = cur.u0, v1 = cur.u1;
+                if (!PRE && l_xy && lp >= 0 && lp < nz && lp <= Z0 + zc - 1 + H) {
+                    const int I0 = l_gm, cx = gc.nx;
+                    const int J = l_gy >> 1, K = lp >> 1;
+                    const int Jn = (l_gy & 1) ? J + 1 : J - 1;
+                    const bool oy = Jn < 0 || Jn >= gc.ny;
+                    const int Kn = (lp & 1) ? K + 1 : K - 1;
+                    const bool oz = Kn < 0 || Kn >= gc.gnz;
+                    const T w0 = (T)0.75, w1 = (T)0.25, cl = clc;
+                    auto sv = [&](T val, bool fx, bool fy, bool fz) {
+                        T s = (T)1;
+                        if (fx) s = -cl * s;
+                        if (fy) s = -cl * s;
+                        if (fz) s = -cl * s;
+                        return s == (T)1 ? val : s * val;
+                    };
+                    const int pp = (l_gy + lp) & 1;
+                    const bool interior = !oy && !oz && I0 > 0 && I0 + N < cx;
+    #pragma unroll
+                    for (int c = 0; c < 2; ++c) {
+                        const int o = c ^ pp;
+                        Vec<T, N>& uv = c ? v1 : v0;
+    #pragma unroll
+                        for (int e = 0; e < N; ++e) {
+                            const int pe = e + 1;
+                            T v;
+                            if (!LINEAR) {
+                                v = cur.c00[pe];
+                            } else if (interior) {
+                                const T nb00 = o ? cur.c00[e + 2] : cur.c00[e];
+                                const T nb10 = o ? cur.c10[e + 2] : cur.c10[e];
+                                const T nb01 = o ? cur.c01[e + 2] : cur.c01[e];
+                                const T nb11 = o ? cur.c11[e + 2] : cur.c11[e];
+                                const T a00 = w0 * cur.c00[pe] + w1 * nb00;
+                                const T a10 = w0 * cur.c10[pe] + w1 * nb10;
+                                const T a01 = w0 * cur.c01[pe] + w1 * nb01;
+                                const T a11 = w0 * cur.c11[pe] + w1 * nb11;
+                                const T b0 = w0 * a00 + w1 * a10;
+                                const T b1 = w0 * a01 + w1 * a11;
+                                v = w0 * b0 + w1 * b1;
+                            } else {
+                                const bool ox = (o == 0 && I0 + e == 0) || (o == 1 && I0 + e == cx - 1);
+                                auto col = [&](const T (&cc)[N + 2]) { return ox ? cc[pe] : (o ? cc[e + 2] : cc[e]); };
+                                const T a00 = w0 * cur.c00[pe] + w1 * sv(col(cur.c00), ox, false, false);
+                                const T a10 = w0 * sv(cur.c10[pe], false, oy, false) + w1 * sv(col(cur.c10), ox, oy, false);
+                                const T a01 = w0 * sv(cur.c01[pe], false, false, oz) + w1 * sv(col(cur.c01), ox, false, oz);
+                                const T a11 = w0 * sv(cur.c11[pe], false, oy, oz) + w1 * sv(col(cur.c11), ox, oy, oz);
+                                const T b0 = w0 * a00 + w1 * a10;
+                                const T b1 = w0 * a01 + w1 * a11;
+                                v = w0 * b0 + w1 * b1;
+                            }
+                            uv.v[e] = uv.v[e] + v;
                         }
-                        uv.v[e] = uv.v[e] + v;
                     }
                 }
+                T* P = slot(lp);
+                vstore<T, N>(P + l_s, v0);
+                vstore<T, N>(P + CH + l_s, v1);
             }
-            T* P = slot(p);
-            vstore<T, N>(P + l_s, v0);
-            vstore<T, N>(P + CH + l_s, v1);
+    };
+
+    auto step = [&](const FusedPrefetch<T, NS>& cur, FusedPrefetch<T, NS>& nxt, int p) {
+        if (p < p_last) prefetch(nxt, p + 1);
+        if (!MERGE) {
+            stage0(cur, p);
+            lds_barrier();
         }
-        lds_barrier();
 
         // ---- stages 1 .. 2 NS: red/black half-sweeps on planes p - (2k - 1), independent ----
 #pragma unroll
@@ -979,19 +1005,23 @@ __global__ __launch_bounds__(kFusedThreads) void k_fused(const T* __restrict__ s
             const int c = (k - 1) & 1;  // red first
             const int ye = k + tid / G;
             const int gy = YS + ye;
-            if (zrange(q, k) && tid < (YE - 2 * k) * G && s_x && gy >= 0 && gy < g.ny) {
+            if (zrange(q, k) && tid < (YE - 2 * k) * G) {
                 T* P = slot(q);
+                const int oth = (c ^ 1) * CH + ye * HWE + s_m0;
+                const Vec<T, N> cen = vload<T, N>(P + oth);
+                // x-1 of the first cell / x+1 of the last: the neighbouring lane's group in the row
+                const T e_prev = dpp_shr1(cen.v[N - 1]), e_next = dpp_shl1(cen.v[0]);
+                if (s_x && gy >= 0 && gy < g.ny) {
                 const T* Pm = slot(q - 1);
                 const T* Pp = slot(q + 1);
                 const int o = c ^ ((gy + q) & 1);
                 const int own = c * CH + ye * HWE + s_m0;
-                const int oth = (c ^ 1) * CH + ye * HWE + s_m0;
-                const Vec<T, N> cen = vload<T, N>(P + oth);
+                const int lane = tid & 63;
                 T edge;
                 if (o == 0)
-                    edge = s_lo ? P[oth - 1] : (T)0;
+                    edge = s_lo ? (lane != 0 ? e_prev : P[oth - 1]) : (T)0;
                 else
-                    edge = s_hi ? P[oth + N] : (T)0;
+                    edge = s_hi ? (lane != 63 ? e_next : P[oth + N]) : (T)0;
                 const Vec<T, N> yl = vload<T, N>(P + oth - HWE);  // ye >= 1
                 const Vec<T, N> yr = vload<T, N>(P + oth + HWE);  // ye <= YE - 2
                 const Vec<T, N> zl = vload<T, N>(Pm + oth);
@@ -1017,6 +1047,7 @@ __global__ __launch_bounds__(kFusedThreads) void k_fused(const T* __restrict__ s
                     }
                 }
                 vstore<T, N>(P + own, out);
+                }
             }
         }
 
@@ -1123,7 +1154,15 @@ __global__ __launch_bounds__(kFusedThreads) void k_fused(const T* __restrict__ s
                 }
             }
         }
+        if (MERGE) stage0(cur, p + 1);
         lds_barrier();
+    };
+    const int p_begin = MERGE ? p_first - 1 : p_first;
+    FusedPrefetch<T, NS> nxt;
+    prefetch(nxt, p_begin);
+    for (int p = p_begin; p <= p_last; ++p) {
+        const FusedPrefetch<T, NS> cur = nxt;
+        step(cur, nxt, p);
     }
     if (ERR) block_partial_n<T>(err, partials, kFusedThreads);
 }
