@@ -140,6 +140,7 @@ struct mgp_ctx {
         hipGraphExec_t exec = nullptr;
     };
     bool use_graph = false;
+    bool use_gs = false;  // grid-stride half-sweeps on large levels (MGP_GS=1; measured slower at 512^3)
     std::vector<GraphEntry> graphs;
     // coarse-level tail (k_tail): cycle_rec(tail_level, ...) as one launch; programs for V and F
     int tail_level = -1;
@@ -293,7 +294,8 @@ int half(mgp_ctx* c, int l, int color, char* other, char* dst, const char* old, 
     hipEvent_t e;
     TRY(timed_begin(c, old ? -1 : l, &e));
     HIP_TRY(c, mgp::launch_half_sweep(c->rb, c->o.dim, l == 0, color, c->ui(L, other), c->ui(L, L.f), c->ui(L, dst),
-                                      old ? c->ui(L, (char*)old) : nullptr, c->d_part + part_off, L.g, h, cl, c->s));
+                                      old ? c->ui(L, (char*)old) : nullptr, c->d_part + part_off, L.g, h, cl,
+                                      c->use_gs, c->s));
     TRY(timed_end(c, e, MGP_TIMING_HALF_SWEEP, 1.5 * c->rb * (double)level_cells(L)));
     return MGP_OK;
 }
@@ -315,7 +317,7 @@ int smooth(mgp_ctx* c, int l, int sweeps, double h, bool want_err = false)
         const bool oop = l == 0 && c->in_cycle && c->err_fuse && !c->first_done;  // keep psiOld in t
         const bool last_err = want_err && sw == sweeps - 1;
         const char* old = last_err ? L.t : nullptr;
-        const int nb = mgp::half_blocks(c->rb, L.g);
+        const int nb = mgp::half_blocks(c->rb, L.g, c->use_gs);
         char* dst = oop ? L.t : L.u;
         TRY(exchange(c, L));
         TRY(half(c, l, 0, L.u, dst, old, h, cl, 0));  // red from black
@@ -840,7 +842,11 @@ int mgp_create(mgp_ctx** out, const mgp_opts* o)
         c->err = "hipMalloc failed for the staging buffer";
         return bail(MGP_ERR_OOM);
     }
-    int nb2 = 2 * mgp::half_blocks(c->rb, L0.g);
+    {
+        const char* v = std::getenv("MGP_GS");
+        c->use_gs = v && std::atoi(v) != 0;
+    }
+    int nb2 = 2 * mgp::half_blocks(c->rb, L0.g, c->use_gs);
     if (L0.fused) nb2 = std::max(nb2, mgp::fused_blocks(c->rb, L0.g, L0.zc));
     c->part_cap = std::max<int64_t>(mgp::kSumBlocks, nb2 + mgp::sum_scratch(nb2));
     if (hipMalloc(&c->d_part, sizeof(double) * c->part_cap) != hipSuccess) {

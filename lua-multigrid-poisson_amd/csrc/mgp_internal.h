@@ -42,9 +42,10 @@ hipError_t launch_unpack(int rb, const void* packed, void* lex, Geo g, hipStream
 // other and dst may be the same buffer (in place) or different (out of place: Jacobi, the first
 // sweep of a cycle).  With old != nullptr, sum (dst - old)^2 over colour c goes to one fp64
 // partial per workgroup in partials[0 .. half_blocks()).
-int half_blocks(int rb, Geo g);
+// gs: large levels use the grid-stride form (kGsBlocks workgroups, XCD-banded)
+int half_blocks(int rb, Geo g, bool gs);
 hipError_t launch_half_sweep(int rb, int dim, bool fine, int color, const void* other, const void* f, void* dst,
-                             const void* old, double* partials, Geo g, double h, double cl, hipStream_t s);
+                             const void* old, double* partials, Geo g, double h, double cl, bool gs, hipStream_t s);
 // Fused residual + restriction (calcResidual + reduceResidual): R (coarse packed, pointing at the
 // coarse plane of this rank's fine plane 0; its Geo is gc) from u, f of the fine level.
 hipError_t launch_residual_restrict(int rb, int dim, const void* u, const void* f, void* R, Geo g, Geo gc, double h,

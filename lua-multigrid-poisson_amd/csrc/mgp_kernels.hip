@@ -196,67 +196,126 @@ __global__ __launch_bounds__(kBlock) void k_unpack(const T* __restrict__ in, T* 
 // ---- red/black half-sweep -------------------------------------------------------------------
 
 // Vector form: a thread owns N consecutive cells of colour `color` in one row (hw % N == 0).
+// half_load gathers an item's operands (all loads issued), half_store computes and stores it, so
+// a thread can keep several items' loads in flight.
+template <typename T, int N>
+struct HalfIn {
+    Vec<T, N> cen, yl, yr, zl, zr, fv;
+    T edge;
+    int64_t own;
+    int o, j, nbyz, m0;
+    int64_t gk;
+};
+
+template <typename T, int DIM>
+__device__ __forceinline__ void half_load(HalfIn<T, VN<T>::n>& in, const T* __restrict__ other, const T* __restrict__ f,
+                                          const Geo& g, int color, int64_t it)
+{
+    constexpr int N = VN<T>::n;
+    constexpr int LN = N == 4 ? 2 : 1;
+    const int lgpr = g.lhw - LN;  // log2 groups per row
+    const int grp = (int)(it & ((1 << lgpr) - 1));
+    const int j = (int)((it >> lgpr) & (g.ny - 1));
+    const int64_t k = it >> (lgpr + g.ly);
+    const int m0 = grp * N;
+    const int64_t gk = g.z0 + k;
+    const int o = color ^ (int)((j + gk) & 1);  // x parity of this row's colour-c cells
+    const int64_t own = k * g.P + color * g.H + (int64_t)j * g.hw + m0;
+    const int64_t oth = k * g.P + (color ^ 1) * g.H + (int64_t)j * g.hw + m0;
+    in.cen = vload<T, N>(other + oth);
+    if (o == 0)
+        in.edge = m0 > 0 ? other[oth - 1] : (T)0;      // x-1 of the first cell
+    else
+        in.edge = m0 + N < g.hw ? other[oth + N] : (T)0;  // x+1 of the last cell
+    in.yl = j > 0 ? vload<T, N>(other + oth - g.hw) : vzero<T, N>();
+    in.yr = j < g.ny - 1 ? vload<T, N>(other + oth + g.hw) : vzero<T, N>();
+    if (DIM == 3) {
+        in.zl = vload<T, N>(other + oth - g.P);
+        in.zr = vload<T, N>(other + oth + g.P);
+    }
+    in.fv = vload<T, N>(f + own);
+    in.own = own;
+    in.o = o;
+    in.j = j;
+    in.m0 = m0;
+    in.gk = gk;
+    in.nbyz = (j == 0) + (j == g.ny - 1) + (DIM == 3 ? (gk == 0) + (gk == g.gnz - 1) : 0);
+}
+
+template <typename T, int DIM, bool ERR>
+__device__ __forceinline__ void half_store(const HalfIn<T, VN<T>::n>& in, T* __restrict__ dst, const T* __restrict__ old,
+                                           const Geo& g, const Op<T, DIM>& op, double& acc)
+{
+    constexpr int N = VN<T>::n;
+    const int o = in.o;
+    Vec<T, N> out;
+#pragma unroll
+    for (int e = 0; e < N; ++e) {
+        const int i = 2 * (in.m0 + e) + o;
+        const T xl = o == 0 ? (e == 0 ? in.edge : in.cen.v[e - 1]) : in.cen.v[e];
+        const T xr = o == 0 ? in.cen.v[e] : (e == N - 1 ? in.edge : in.cen.v[e + 1]);
+        T s = xl + xr;
+        s = s + in.yl.v[e];
+        s = s + in.yr.v[e];
+        if (DIM == 3) {
+            s = s + in.zl.v[e];
+            s = s + in.zr.v[e];
+        }
+        const int nb = in.nbyz + (i == 0) + (i == g.nx - 1);
+        out.v[e] = op.relax(s, in.fv.v[e], nb);
+    }
+    vstore<T, N>(dst + in.own, out);
+    if (ERR) {
+        const Vec<T, N> w = vload<T, N>(old + in.own);
+#pragma unroll
+        for (int e = 0; e < N; ++e) {
+            const double d = (double)out.v[e] - (double)w.v[e];
+            acc += d * d;
+        }
+    }
+}
+
 template <typename T, int DIM, int TAG, bool ERR>
 __global__ __launch_bounds__(kBlock) void k_half(const T* __restrict__ other, const T* __restrict__ f,
                                                  T* __restrict__ dst, const T* __restrict__ old,
                                                  double* __restrict__ partials, Geo g, int color,
                                                  Op<T, DIM> op)
 {
-    constexpr int N = VN<T>::n;
-    constexpr int LN = N == 4 ? 2 : 1;
     const int b = xcd_remap(blockIdx.x, gridDim.x);
     const int64_t it = (int64_t)b * kBlock + threadIdx.x;
-    const int lgpr = g.lhw - LN;  // log2 groups per row
-    const int grp = (int)(it & ((1 << lgpr) - 1));
-    const int j = (int)((it >> lgpr) & (g.ny - 1));
-    const int64_t k = it >> (lgpr + g.ly);
     double acc = 0.0;
-    if (k < g.nz) {
-        const int m0 = grp * N;
-        const int64_t gk = g.z0 + k;
-        const int o = color ^ (int)((j + gk) & 1);  // x parity of this row's colour-c cells
-        const int64_t own = k * g.P + color * g.H + (int64_t)j * g.hw + m0;
-        const int64_t oth = k * g.P + (color ^ 1) * g.H + (int64_t)j * g.hw + m0;
-        const Vec<T, N> cen = vload<T, N>(other + oth);
-        T edge;
-        if (o == 0)
-            edge = m0 > 0 ? other[oth - 1] : (T)0;      // x-1 of the first cell
-        else
-            edge = m0 + N < g.hw ? other[oth + N] : (T)0;  // x+1 of the last cell
-        const Vec<T, N> yl = j > 0 ? vload<T, N>(other + oth - g.hw) : vzero<T, N>();
-        const Vec<T, N> yr = j < g.ny - 1 ? vload<T, N>(other + oth + g.hw) : vzero<T, N>();
-        Vec<T, N> zl, zr;
-        if (DIM == 3) {
-            zl = vload<T, N>(other + oth - g.P);
-            zr = vload<T, N>(other + oth + g.P);
-        }
-        const Vec<T, N> fv = vload<T, N>(f + own);
-        const int nbyz = (j == 0) + (j == g.ny - 1) + (DIM == 3 ? (gk == 0) + (gk == g.gnz - 1) : 0);
-        Vec<T, N> out;
-#pragma unroll
-        for (int e = 0; e < N; ++e) {
-            const int i = 2 * (m0 + e) + o;
-            const T xl = o == 0 ? (e == 0 ? edge : cen.v[e - 1]) : cen.v[e];
-            const T xr = o == 0 ? cen.v[e] : (e == N - 1 ? edge : cen.v[e + 1]);
-            T s = xl + xr;
-            s = s + yl.v[e];
-            s = s + yr.v[e];
-            if (DIM == 3) {
-                s = s + zl.v[e];
-                s = s + zr.v[e];
-            }
-            const int nb = nbyz + (i == 0) + (i == g.nx - 1);
-            out.v[e] = op.relax(s, fv.v[e], nb);
-        }
-        vstore<T, N>(dst + own, out);
-        if (ERR) {
-            const Vec<T, N> w = vload<T, N>(old + own);
-#pragma unroll
-            for (int e = 0; e < N; ++e) {
-                const double d = (double)out.v[e] - (double)w.v[e];
-                acc += d * d;
-            }
-        }
+    if ((it >> (g.lhw - (VN<T>::n == 4 ? 2 : 1) + g.ly)) < g.nz) {
+        HalfIn<T, VN<T>::n> in;
+        half_load<T, DIM>(in, other, f, g, color, it);
+        half_store<T, DIM, ERR>(in, dst, old, g, op, acc);
+    }
+    if (ERR) block_partial<T>(acc, partials);
+}
+
+// Grid-stride form for large levels (kGsBlocks workgroups): the workgroups of XCD x (b % 8 == x)
+// sweep the contiguous band x of the items, so y/z neighbours meet in that XCD's L2, and each
+// thread keeps two items' loads in flight.
+constexpr int kGsBlocks = 2048;
+
+template <typename T, int DIM, int TAG, bool ERR>
+__global__ __launch_bounds__(kBlock) void k_half_gs(const T* __restrict__ other, const T* __restrict__ f,
+                                                    T* __restrict__ dst, const T* __restrict__ old,
+                                                    double* __restrict__ partials, Geo g, int color,
+                                                    Op<T, DIM> op, int64_t items)
+{
+    const int nlb = gridDim.x >> 3;
+    const int64_t band = (items + 7) >> 3;
+    const int64_t base = (int64_t)(blockIdx.x & 7) * band;
+    const int64_t end = base + band < items ? base + band : items;
+    const int64_t step = (int64_t)nlb * kBlock;
+    double acc = 0.0;
+    for (int64_t i0 = base + (int64_t)(blockIdx.x >> 3) * kBlock + threadIdx.x; i0 < end; i0 += 2 * step) {
+        const int64_t i1 = i0 + step;
+        HalfIn<T, VN<T>::n> a, c;
+        half_load<T, DIM>(a, other, f, g, color, i0);
+        if (i1 < end) half_load<T, DIM>(c, other, f, g, color, i1);
+        half_store<T, DIM, ERR>(a, dst, old, g, op, acc);
+        if (i1 < end) half_store<T, DIM, ERR>(c, dst, old, g, op, acc);
     }
     if (ERR) block_partial<T>(acc, partials);
 }
@@ -1360,15 +1419,24 @@ hipError_t launch_unpack(int rb, const void* packed, void* lex, Geo g, hipStream
 
 static bool half_vector(int rb, const Geo& g) { return g.hw >= 16 / rb && g.nx >= 2; }
 
-int half_blocks(int rb, Geo g)
+static int64_t half_items(int rb, const Geo& g)
 {
     const int n = 16 / rb;
-    const int64_t items = half_vector(rb, g) ? (g.H / n) * g.nz : g.H * g.nz;
-    return (int)nblk(items);
+    return half_vector(rb, g) ? (g.H / n) * g.nz : g.H * g.nz;
+}
+
+static bool half_gs(int rb, const Geo& g, bool gs)
+{
+    return gs && half_vector(rb, g) && half_items(rb, g) >= (int64_t)kGsBlocks * kBlock * 2;
+}
+
+int half_blocks(int rb, Geo g, bool gs)
+{
+    return half_gs(rb, g, gs) ? kGsBlocks : (int)nblk(half_items(rb, g));
 }
 
 template <typename T, int D>
-static void half_t(bool fine, bool err, bool vec, unsigned nb, int color, const void* other, const void* f, void* dst,
+static void half_t(bool fine, bool err, bool vec, bool gs, unsigned nb, int color, const void* other, const void* f, void* dst,
                    const void* old, double* partials, Geo g, double h, double cl, hipStream_t s)
 {
     const Op<T, D> op = make_op<T, D>(h, cl);
@@ -1376,7 +1444,16 @@ static void half_t(bool fine, bool err, bool vec, unsigned nb, int color, const 
     const T* f_ = (const T*)f;
     T* d_ = (T*)dst;
     const T* w_ = (const T*)old;
-    if (vec) {
+    if (vec && gs && half_gs(sizeof(T), g, gs)) {
+        const int64_t items = half_items(sizeof(T), g);
+        if (fine) {
+            if (err) k_half_gs<T, D, 1, true><<<nb, kBlock, 0, s>>>(o_, f_, d_, w_, partials, g, color, op, items);
+            else k_half_gs<T, D, 1, false><<<nb, kBlock, 0, s>>>(o_, f_, d_, w_, partials, g, color, op, items);
+        } else {
+            if (err) k_half_gs<T, D, 0, true><<<nb, kBlock, 0, s>>>(o_, f_, d_, w_, partials, g, color, op, items);
+            else k_half_gs<T, D, 0, false><<<nb, kBlock, 0, s>>>(o_, f_, d_, w_, partials, g, color, op, items);
+        }
+    } else if (vec) {
         if (fine) {
             if (err) k_half<T, D, 1, true><<<nb, kBlock, 0, s>>>(o_, f_, d_, w_, partials, g, color, op);
             else k_half<T, D, 1, false><<<nb, kBlock, 0, s>>>(o_, f_, d_, w_, partials, g, color, op);
@@ -1391,16 +1468,16 @@ static void half_t(bool fine, bool err, bool vec, unsigned nb, int color, const 
 }
 
 hipError_t launch_half_sweep(int rb, int dim, bool fine, int color, const void* other, const void* f, void* dst,
-                             const void* old, double* partials, Geo g, double h, double cl, hipStream_t s)
+                             const void* old, double* partials, Geo g, double h, double cl, bool gs, hipStream_t s)
 {
-    const unsigned nb = (unsigned)half_blocks(rb, g);
+    const unsigned nb = (unsigned)half_blocks(rb, g, gs);
     const bool err = old != nullptr, vec = half_vector(rb, g);
     if (rb == 8) {
-        if (dim == 3) half_t<double, 3>(fine, err, vec, nb, color, other, f, dst, old, partials, g, h, cl, s);
-        else half_t<double, 2>(fine, err, vec, nb, color, other, f, dst, old, partials, g, h, cl, s);
+        if (dim == 3) half_t<double, 3>(fine, err, vec, gs, nb, color, other, f, dst, old, partials, g, h, cl, s);
+        else half_t<double, 2>(fine, err, vec, gs, nb, color, other, f, dst, old, partials, g, h, cl, s);
     } else {
-        if (dim == 3) half_t<float, 3>(fine, err, vec, nb, color, other, f, dst, old, partials, g, h, cl, s);
-        else half_t<float, 2>(fine, err, vec, nb, color, other, f, dst, old, partials, g, h, cl, s);
+        if (dim == 3) half_t<float, 3>(fine, err, vec, gs, nb, color, other, f, dst, old, partials, g, h, cl, s);
+        else half_t<float, 2>(fine, err, vec, gs, nb, color, other, f, dst, old, partials, g, h, cl, s);
     }
     return hipGetLastError();
 }

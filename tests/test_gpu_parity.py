@@ -315,6 +315,23 @@ def test_fused_timing_kinds(monkeypatch):
     assert t["fused_pre"][0] > 0 and t["fused_post"][0] > 0
 
 
+@pytest.mark.parametrize("kw", [
+    dict(real="float", smoother="rbgs", nu1=2, nu2=2, prolong="linear", coarse_bc="consistent"),
+    dict(real="double", smoother="jacobi", nu1=2, nu2=2, prolong="pc"),
+], ids=["rbgs-f32", "jacobi-f64"])
+def test_grid_stride_half_sweep_equals_one_shot(kw, monkeypatch):
+    """The grid-stride half-sweep (opt-in, large levels: 256^3 here) == one item per thread."""
+    monkeypatch.setenv("MGP_GS", "1")
+    a = _ctx(dim=3, n=(256, 256, 256), **kw)
+    monkeypatch.setenv("MGP_GS", "0")
+    b = _ctx(dim=3, n=(256, 256, 256), **kw)
+    a.init_point_charge()
+    b.init_point_charge()
+    ea, eb = a.cycles(2), b.cycles(2)
+    assert np.array_equal(a.get_psi(), b.get_psi())
+    np.testing.assert_allclose(ea, eb, rtol=1e-12, atol=0)
+
+
 def test_two_grid_host_buffers():
     """cpu-raw.lua:186 twoGrid(h, u, f, L) on caller buffers == the oracle's mgo_two_grid."""
     import ctypes
