@@ -113,6 +113,16 @@ int         mgp_prolong_correct(mgp_ctx* c, int level);             /* expandRes
 int         mgp_coarse_solve(mgp_ctx* c);                           /* L == 1 branch of twoGrid */
 
 int         mgp_sync(mgp_ctx* c);
+
+/* Loopback transport (tests only): the `world` ranks of a slab decomposition as contexts of ONE
+ * process on one GPU, each driven by its own host thread.  Halo exchanges, the all-gather and the
+ * err all-reduce become device copies ordered by events and a host barrier instead of RCCL calls;
+ * everything else runs the multi-GPU code path unchanged.  A rank that stops calling makes the
+ * others fail with MGP_ERR_STATE after 120 s instead of hanging. */
+typedef struct mgp_loopback mgp_loopback;
+int         mgp_loopback_create(mgp_loopback** out, int world);
+void        mgp_loopback_destroy(mgp_loopback* lb);
+int         mgp_create_loopback(mgp_ctx** out, const mgp_opts* o, mgp_loopback* lb);
 /* Finest-level kernel timing with HIP events on the context's stream.  mgp_timing(c, 1) resets and
  * enables (cycles then run eagerly, without hipGraph replay, so each launch can be bracketed).
  * Timed kinds, level 0 only:

@@ -12,6 +12,9 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <chrono>
+#include <condition_variable>
+#include <mutex>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -112,6 +115,34 @@ struct Level {
     int zc = 0;             // k_fused z-chunk (planes per workgroup)
 };
 
+// Loopback transport (tests): the ranks of a slab decomposition as contexts of one process on
+// one GPU, one host thread each; exchanges are device copies ordered by events and a host barrier.
+struct mgp_loopback {
+    int world = 0;
+    std::mutex m;
+    std::condition_variable cv;
+    int arrived = 0;
+    uint64_t gen = 0;
+    bool broken = false;
+    std::vector<mgp_ctx*> ranks;
+    // false after a 120 s wait (a rank failed or stopped calling): the group is then unusable
+    bool barrier()
+    {
+        std::unique_lock<std::mutex> lk(m);
+        if (broken) return false;
+        const uint64_t g = gen;
+        if (++arrived == world) {
+            arrived = 0;
+            ++gen;
+            cv.notify_all();
+            return true;
+        }
+        if (!cv.wait_for(lk, std::chrono::seconds(120), [&] { return gen != g || broken; })) broken = true;
+        if (broken) cv.notify_all();
+        return !broken;
+    }
+};
+
 struct mgp_ctx {
     mgp_opts o{};
     int rb = 8;
@@ -120,6 +151,10 @@ struct mgp_ctx {
     hipStream_t s = nullptr;
     int device = 0;
     ncclComm_t comm = nullptr;
+    mgp_loopback* lb = nullptr;  // loopback transport instead of RCCL (tests)
+    hipEvent_t lb_ev = nullptr, lb_ev2 = nullptr;
+    char* lb_buf = nullptr;
+    double* lb_red = nullptr;
     char* psi_old = nullptr;  // snapshot buffer (Jacobi path)
     char* stage = nullptr;    // lexicographic staging buffer for set/get (level-0 size)
     double* d_part = nullptr;
@@ -215,11 +250,82 @@ Geo make_geo(const LevelPlan& p, int dim)
 
 // ---- halo exchange over RCCL (grouped send/recv to the z-neighbours) ----
 
+// ---- loopback transport (same collective semantics as the RCCL calls below) ----
+
+int lb_fail(mgp_ctx* c) { return c->fail(MGP_ERR_STATE, "loopback group barrier timed out or broken"); }
+
+int lb_exchange(mgp_ctx* c, int l, char* buf)
+{
+    mgp_loopback* g = c->lb;
+    const size_t rb = (size_t)c->rb;
+    const Level& L = c->lev[l];
+    const size_t bytes = (size_t)L.g.P * rb;
+    auto at = [&](char* b, int64_t k) { return b + (size_t)((k + c->G) * L.g.P) * rb; };
+    c->lb_buf = buf;
+    HIP_TRY(c, hipEventRecord(c->lb_ev, c->s));  // my boundary planes are final here
+    if (!g->barrier()) return lb_fail(c);
+    const int r = c->o.rank;
+    for (int nb : {r - 1, r + 1}) {
+        if (nb < 0 || nb >= c->o.world) continue;
+        mgp_ctx* o = g->ranks[nb];
+        HIP_TRY(c, hipStreamWaitEvent(c->s, o->lb_ev, 0));
+        const char* src = nb < r ? at(o->lb_buf, L.g.nz - 1) : at(o->lb_buf, 0);
+        HIP_TRY(c, hipMemcpyAsync(nb < r ? at(buf, -1) : at(buf, L.g.nz), src, bytes, hipMemcpyDeviceToDevice, c->s));
+    }
+    HIP_TRY(c, hipEventRecord(c->lb_ev2, c->s));  // my pulls are done here
+    if (!g->barrier()) return lb_fail(c);
+    for (int nb : {r - 1, r + 1})  // neighbours may overwrite their planes only after my pull
+        if (nb >= 0 && nb < c->o.world) HIP_TRY(c, hipStreamWaitEvent(c->s, g->ranks[nb]->lb_ev2, 0));
+    return MGP_OK;
+}
+
+// in-place all-gather: rank q's slab is at buf + q * count reals on every rank
+int lb_allgather(mgp_ctx* c, char* buf, size_t count)
+{
+    mgp_loopback* g = c->lb;
+    const size_t bytes = count * (size_t)c->rb;
+    c->lb_buf = buf;
+    HIP_TRY(c, hipEventRecord(c->lb_ev, c->s));
+    if (!g->barrier()) return lb_fail(c);
+    for (int q = 0; q < c->o.world; ++q) {
+        if (q == c->o.rank) continue;
+        mgp_ctx* o = g->ranks[q];
+        HIP_TRY(c, hipStreamWaitEvent(c->s, o->lb_ev, 0));
+        HIP_TRY(c, hipMemcpyAsync(buf + q * bytes, o->lb_buf + q * bytes, bytes, hipMemcpyDeviceToDevice, c->s));
+    }
+    HIP_TRY(c, hipEventRecord(c->lb_ev2, c->s));
+    if (!g->barrier()) return lb_fail(c);
+    for (int q = 0; q < c->o.world; ++q)
+        if (q != c->o.rank) HIP_TRY(c, hipStreamWaitEvent(c->s, g->ranks[q]->lb_ev2, 0));
+    return MGP_OK;
+}
+
+// in-place sum of one double over the ranks, added in rank order
+int lb_allreduce(mgp_ctx* c, double* v)
+{
+    mgp_loopback* g = c->lb;
+    c->lb_buf = (char*)v;
+    HIP_TRY(c, hipEventRecord(c->lb_ev, c->s));
+    if (!g->barrier()) return lb_fail(c);
+    for (int q = 0; q < c->o.world; ++q) {
+        mgp_ctx* o = g->ranks[q];
+        if (q != c->o.rank) HIP_TRY(c, hipStreamWaitEvent(c->s, o->lb_ev, 0));
+        HIP_TRY(c, hipMemcpyAsync(c->lb_red + q, o->lb_buf, sizeof(double), hipMemcpyDeviceToDevice, c->s));
+    }
+    HIP_TRY(c, hipEventRecord(c->lb_ev2, c->s));
+    if (!g->barrier()) return lb_fail(c);
+    for (int q = 0; q < c->o.world; ++q)
+        if (q != c->o.rank) HIP_TRY(c, hipStreamWaitEvent(c->s, g->ranks[q]->lb_ev2, 0));
+    HIP_TRY(c, mgp::launch_sum_partials(c->lb_red, c->o.world, v, c->s));
+    return MGP_OK;
+}
+
 // Exchange one boundary plane of `buf` with each z-neighbour: my first interior plane goes to
 // rank-1's upper ghost, my last to rank+1's lower ghost.  A plane is contiguous in the packed
 // layout, so each direction is one ncclSend/ncclRecv pair on that neighbour's xGMI link.
 int exchange_buf(mgp_ctx* c, Level& L, char* buf)
 {
+    if (c->lb) return lb_exchange(c, (int)(&L - c->lev.data()), buf);
     const size_t rb = (size_t)c->rb;
     const size_t cnt = (size_t)L.g.P;
     auto at = [&](int64_t k) { return buf + (size_t)((k + c->G) * L.g.P) * rb; };
@@ -360,7 +466,10 @@ int residual_restrict(mgp_ctx* c, int l, double h)
     if (L.p.dist && !C.p.dist) {
         // agglomerate: every rank gets the whole coarse right-hand side (cf. cpu-gpu.lua:22-32)
         const size_t count = (size_t)((L.g.nz / 2) * C.g.P);
-        NCCL_TRY(c, ncclAllGather(R, c->ui(C, C.f), count, c->nccl_real(), c->comm, c->s));
+        if (c->lb)
+            TRY(lb_allgather(c, c->ui(C, C.f), count));
+        else
+            NCCL_TRY(c, ncclAllGather(R, c->ui(C, C.f), count, c->nccl_real(), c->comm, c->s));
     }
     return MGP_OK;
 }
@@ -576,8 +685,12 @@ int one_cycle(mgp_ctx* c, double* dst)
         HIP_TRY(c, mgp::launch_sqdiff_sum(c->rb, c->ui(L0, L0.u), c->psi_old, L0.g.P * L0.g.nz, c->d_part, dst,
                                           c->s));
     }
-    if (c->o.err_mode && c->o.world > 1)
-        NCCL_TRY(c, ncclAllReduce(dst, dst, 1, ncclDouble, ncclSum, c->comm, c->s));
+    if (c->o.err_mode && c->o.world > 1) {
+        if (c->lb)
+            TRY(lb_allreduce(c, dst));
+        else
+            NCCL_TRY(c, ncclAllReduce(dst, dst, 1, ncclDouble, ncclSum, c->comm, c->s));
+    }
     return MGP_OK;
 }
 
@@ -746,11 +859,44 @@ static void destroy_impl(mgp_ctx* c)
     for (auto& g : c->graphs) (void)hipGraphExecDestroy(g.exec);
     for (auto e : c->ev) (void)hipEventDestroy(e);
     if (c->comm) (void)ncclCommDestroy(c->comm);
+    if (c->lb) {
+        std::lock_guard<std::mutex> lk(c->lb->m);
+        if (c->o.rank >= 0 && c->o.rank < (int)c->lb->ranks.size() && c->lb->ranks[c->o.rank] == c)
+            c->lb->ranks[c->o.rank] = nullptr;
+    }
+    if (c->lb_ev) (void)hipEventDestroy(c->lb_ev);
+    if (c->lb_ev2) (void)hipEventDestroy(c->lb_ev2);
+    if (c->lb_red) (void)hipFree(c->lb_red);
     if (c->s) (void)hipStreamDestroy(c->s);
     delete c;
 }
 
-int mgp_create(mgp_ctx** out, const mgp_opts* o)
+static int create_impl(mgp_ctx** out, const mgp_opts* o, mgp_loopback* lb);
+
+int mgp_create(mgp_ctx** out, const mgp_opts* o) { return create_impl(out, o, nullptr); }
+
+int mgp_loopback_create(mgp_loopback** out, int world)
+{
+    if (!out || world < 1) return MGP_ERR_ARG;
+    mgp_loopback* g = new mgp_loopback();
+    g->world = world;
+    g->ranks.assign((size_t)world, nullptr);
+    *out = g;
+    return MGP_OK;
+}
+
+void mgp_loopback_destroy(mgp_loopback* lb) { delete lb; }
+
+int mgp_create_loopback(mgp_ctx** out, const mgp_opts* o, mgp_loopback* lb)
+{
+    if (!lb || !o || o->world != lb->world) {
+        g_create_error = "mgp_create_loopback: group size != opts.world";
+        return MGP_ERR_ARG;
+    }
+    return create_impl(out, o, lb);
+}
+
+static int create_impl(mgp_ctx** out, const mgp_opts* o, mgp_loopback* lb)
 {
     if (!out || !o) {
         g_create_error = "mgp_create: null argument";
@@ -867,7 +1013,23 @@ int mgp_create(mgp_ctx** out, const mgp_opts* o)
         c->err = std::string("hipFuncSetAttribute (dynamic LDS): ") + hipGetErrorString(he);
         return bail(MGP_ERR_HIP);
     }
-    if (c->o.world > 1) {
+    if (c->o.world > 1 && lb) {
+        c->lb = lb;
+        if (hipEventCreateWithFlags(&c->lb_ev, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&c->lb_ev2, hipEventDisableTiming) != hipSuccess ||
+            hipMalloc(&c->lb_red, sizeof(double) * c->o.world) != hipSuccess) {
+            c->err = "loopback transport setup failed";
+            c->lb = nullptr;
+            return bail(MGP_ERR_HIP);
+        }
+        std::lock_guard<std::mutex> lk(lb->m);
+        if (lb->ranks[c->o.rank]) {
+            c->err = "loopback rank already registered";
+            c->lb = nullptr;
+            return bail(MGP_ERR_ARG);
+        }
+        lb->ranks[c->o.rank] = c;
+    } else if (c->o.world > 1) {
         ncclUniqueId id;
         std::memcpy(&id, o->comm_id, sizeof(id));
         ncclResult_t r = ncclCommInitRank(&c->comm, c->o.world, id, c->o.rank);

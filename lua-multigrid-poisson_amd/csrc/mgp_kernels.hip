@@ -24,6 +24,8 @@
 // parity tests check every piece bit for bit against the C oracle's plain divisions.
 #include "mgp_internal.h"
 
+#include <cstdlib>
+
 namespace mgp {
 namespace {
 
@@ -51,6 +53,26 @@ __device__ __forceinline__ void vstore(T* p, const Vec<T, N>& a)
 {
     *reinterpret_cast<Vec<T, N>*>(p) = a;
 }
+// Nontemporal (streaming) 16-byte access: data touched once by this kernel
+template <typename T, int N>
+__device__ __forceinline__ Vec<T, N> vload_nt(const T* p)
+{
+    using V4 = float __attribute__((ext_vector_type(4)));
+    static_assert(sizeof(Vec<T, N>) == 16, "16-byte vectors only");
+    const V4 r = __builtin_nontemporal_load(reinterpret_cast<const V4*>(p));
+    Vec<T, N> a;
+    __builtin_memcpy(&a, &r, 16);
+    return a;
+}
+template <typename T, int N>
+__device__ __forceinline__ void vstore_nt(T* p, const Vec<T, N>& a)
+{
+    using V4 = float __attribute__((ext_vector_type(4)));
+    V4 r;
+    __builtin_memcpy(&r, &a, 16);
+    __builtin_nontemporal_store(r, reinterpret_cast<V4*>(p));
+}
+
 template <typename T, int N>
 __device__ __forceinline__ Vec<T, N> vzero()
 {
@@ -207,7 +229,7 @@ struct HalfIn {
     int64_t gk;
 };
 
-template <typename T, int DIM>
+template <typename T, int DIM, bool NT = false>
 __device__ __forceinline__ void half_load(HalfIn<T, VN<T>::n>& in, const T* __restrict__ other, const T* __restrict__ f,
                                           const Geo& g, int color, int64_t it)
 {
@@ -233,7 +255,7 @@ __device__ __forceinline__ void half_load(HalfIn<T, VN<T>::n>& in, const T* __re
         in.zl = vload<T, N>(other + oth - g.P);
         in.zr = vload<T, N>(other + oth + g.P);
     }
-    in.fv = vload<T, N>(f + own);
+    in.fv = NT ? vload_nt<T, N>(f + own) : vload<T, N>(f + own);
     in.own = own;
     in.o = o;
     in.j = j;
@@ -242,7 +264,7 @@ __device__ __forceinline__ void half_load(HalfIn<T, VN<T>::n>& in, const T* __re
     in.nbyz = (j == 0) + (j == g.ny - 1) + (DIM == 3 ? (gk == 0) + (gk == g.gnz - 1) : 0);
 }
 
-template <typename T, int DIM, bool ERR>
+template <typename T, int DIM, bool ERR, bool NT = false>
 __device__ __forceinline__ void half_store(const HalfIn<T, VN<T>::n>& in, T* __restrict__ dst, const T* __restrict__ old,
                                            const Geo& g, const Op<T, DIM>& op, double& acc)
 {
@@ -264,9 +286,12 @@ __device__ __forceinline__ void half_store(const HalfIn<T, VN<T>::n>& in, T* __r
         const int nb = in.nbyz + (i == 0) + (i == g.nx - 1);
         out.v[e] = op.relax(s, in.fv.v[e], nb);
     }
-    vstore<T, N>(dst + in.own, out);
+    if (NT)
+        vstore_nt<T, N>(dst + in.own, out);
+    else
+        vstore<T, N>(dst + in.own, out);
     if (ERR) {
-        const Vec<T, N> w = vload<T, N>(old + in.own);
+        const Vec<T, N> w = NT ? vload_nt<T, N>(old + in.own) : vload<T, N>(old + in.own);
 #pragma unroll
         for (int e = 0; e < N; ++e) {
             const double d = (double)out.v[e] - (double)w.v[e];
@@ -286,8 +311,8 @@ __global__ __launch_bounds__(kBlock) void k_half(const T* __restrict__ other, co
     double acc = 0.0;
     if ((it >> (g.lhw - (VN<T>::n == 4 ? 2 : 1) + g.ly)) < g.nz) {
         HalfIn<T, VN<T>::n> in;
-        half_load<T, DIM>(in, other, f, g, color, it);
-        half_store<T, DIM, ERR>(in, dst, old, g, op, acc);
+        half_load<T, DIM, TAG == 2>(in, other, f, g, color, it);
+        half_store<T, DIM, ERR, TAG == 2>(in, dst, old, g, op, acc);
     }
     if (ERR) block_partial<T>(acc, partials);
 }
@@ -1454,7 +1479,14 @@ static void half_t(bool fine, bool err, bool vec, bool gs, unsigned nb, int colo
             else k_half_gs<T, D, 0, false><<<nb, kBlock, 0, s>>>(o_, f_, d_, w_, partials, g, color, op, items);
         }
     } else if (vec) {
-        if (fine) {
+        static const bool nt = [] {
+            const char* v = std::getenv("MGP_NT");
+            return v && std::atoi(v) != 0;
+        }();
+        if (fine && nt) {
+            if (err) k_half<T, D, 2, true><<<nb, kBlock, 0, s>>>(o_, f_, d_, w_, partials, g, color, op);
+            else k_half<T, D, 2, false><<<nb, kBlock, 0, s>>>(o_, f_, d_, w_, partials, g, color, op);
+        } else if (fine) {
             if (err) k_half<T, D, 1, true><<<nb, kBlock, 0, s>>>(o_, f_, d_, w_, partials, g, color, op);
             else k_half<T, D, 1, false><<<nb, kBlock, 0, s>>>(o_, f_, d_, w_, partials, g, color, op);
         } else {

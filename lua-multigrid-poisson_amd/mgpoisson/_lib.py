@@ -76,6 +76,9 @@ SIGNATURES = {
     "mgp_opts_default": (None, [_P(MGPOpts)]),
     "mgp_comm_unique_id": (ctypes.c_int, [_vp, _i64]),
     "mgp_create": (ctypes.c_int, [_P(_vp), _P(MGPOpts)]),
+    "mgp_loopback_create": (ctypes.c_int, [_P(_vp), ctypes.c_int]),
+    "mgp_loopback_destroy": (None, [_vp]),
+    "mgp_create_loopback": (ctypes.c_int, [_P(_vp), _P(MGPOpts), _vp]),
     "mgp_destroy": (None, [_vp]),
     "mgp_last_error": (ctypes.c_char_p, [_vp]),
     "mgp_num_levels": (ctypes.c_int, [_vp]),

@@ -45,14 +45,33 @@ def make_opts(dim=2, n=(8, 8, 1), real="double", nu1=7, nu2=7, smoother="jacobi"
     return o
 
 
+class Loopback:
+    """A loopback transport group (tests): `world` ranks as contexts of this process on one GPU,
+    each driven from its own thread (see mgp_create_loopback)."""
+
+    def __init__(self, world: int):
+        h = ctypes.c_void_p()
+        L.check(L.lib.mgp_loopback_create(ctypes.byref(h), world))
+        self._h = h
+        self.world = world
+
+    def close(self):
+        if getattr(self, "_h", None):
+            L.lib.mgp_loopback_destroy(self._h)
+            self._h = None
+
+
 class Context:
     """Owns one mgp_ctx: the level hierarchy, its device buffers and stream."""
 
-    def __init__(self, opts: L.MGPOpts):
+    def __init__(self, opts: L.MGPOpts, loopback: "Loopback | None" = None):
         self.opts = opts
         self.dtype = np.dtype(np.float64 if opts.real_bytes == 8 else np.float32)
         h = ctypes.c_void_p()
-        L.check(L.lib.mgp_create(ctypes.byref(h), ctypes.byref(opts)))
+        if loopback is not None:
+            L.check(L.lib.mgp_create_loopback(ctypes.byref(h), ctypes.byref(opts), loopback._h))
+        else:
+            L.check(L.lib.mgp_create(ctypes.byref(h), ctypes.byref(opts)))
         self._h = h
         self.levels = []
         info = (ctypes.c_int64 * 8)()

@@ -332,6 +332,56 @@ def test_grid_stride_half_sweep_equals_one_shot(kw, monkeypatch):
     np.testing.assert_allclose(ea, eb, rtol=1e-12, atol=0)
 
 
+LOOPBACK_CASES = [
+    # box, world, gather_cells, config
+    ((64, 64, 128), 2, 4096, dict(real="float", smoother="rbgs", nu1=2, nu2=2, prolong="linear", coarse_bc="consistent")),
+    ((64, 64, 128), 4, 4096, dict(real="double", smoother="rbgs", nu1=2, nu2=2, prolong="linear", coarse_bc="consistent",
+                                  cycle="F")),
+    ((32, 64, 64), 2, 512, dict(real="double", smoother="jacobi", nu1=3, nu2=3, prolong="pc", coarse_init="warm")),
+    ((128, 64, 64), 8, 32768, dict(real="float", smoother="rbgs", nu1=2, nu2=2, prolong="pc", coarse_bc="zero")),
+]
+
+
+@pytest.mark.parametrize("box,world,gather,cfg", LOOPBACK_CASES, ids=["w2-rbgs-lin-f32", "w4-F-f64", "w2-jacobi-warm",
+                                                                       "w8-rbgs-pc"])
+def test_slab_decomposition_loopback(box, world, gather, cfg):
+    """The library's multi-GPU code path (slab planes, ghost exchange after every half-sweep, coarse
+    ghost planes for linear P, all-gather agglomeration, err all-reduce) with the loopback transport:
+    `world` ranks on one GPU, one thread each.  Gathered psi == the single-domain run bit for bit."""
+    import threading
+
+    mg = _mg()
+    lb = mg.Loopback(world)
+    results, errors = [None] * world, []
+
+    def rank_main(r):
+        try:
+            ctx = mg.Context(mg.make_opts(dim=3, n=box, rank=r, world=world, gather_cells=gather, device=0,
+                                          comm_id=b"\0" * 128, **cfg), loopback=lb)
+            assert sum(lv["distributed"] for lv in ctx.levels) >= 2
+            ctx.init_point_charge()
+            errs = ctx.cycles(3)
+            results[r] = (ctx.get_psi(), errs)
+            ctx.close()
+        except Exception as e:  # noqa: BLE001 - surfaced below
+            errors.append((r, repr(e)))
+
+    threads = [threading.Thread(target=rank_main, args=(r,)) for r in range(world)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join(timeout=600)
+    lb.close()
+    assert not errors, errors
+    ref = _ctx(dim=3, n=box, gather_cells=gather, **cfg)
+    ref.init_point_charge()
+    e_ref = ref.cycles(3)
+    psi = np.concatenate([results[r][0] for r in range(world)], axis=0)
+    assert np.array_equal(psi, ref.get_psi()), float(np.max(np.abs(psi - ref.get_psi())))
+    for r in range(world):
+        np.testing.assert_allclose(results[r][1], e_ref, rtol=1e-12, atol=0)
+
+
 def test_two_grid_host_buffers():
     """cpu-raw.lua:186 twoGrid(h, u, f, L) on caller buffers == the oracle's mgo_two_grid."""
     import ctypes
