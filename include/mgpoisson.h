@@ -114,6 +114,12 @@ int         mgp_coarse_solve(mgp_ctx* c);                           /* L == 1 br
 
 int         mgp_sync(mgp_ctx* c);
 
+/* The reference's convergence metrics of the last outer iteration, on the device
+ * (gpu.lua:173-200 calcRelErr / calcFrobErr, test-gpu-obj.lua:216-247 relErr / count / frobErr):
+ * rel_err = mean of |1 - psi/psiOld| over the cells where it is nonzero, count = their number,
+ * frob = sqrt(sum (psi - psiOld)^2 / N).  Needs err_mode 1. */
+int         mgp_metrics(mgp_ctx* c, double* rel_err, int64_t* count, double* frob);
+
 /* Loopback transport (tests only): the `world` ranks of a slab decomposition as contexts of ONE
  * process on one GPU, each driven by its own host thread.  Halo exchanges, the all-gather and the
  * err all-reduce become device copies ordered by events and a host barrier instead of RCCL calls;

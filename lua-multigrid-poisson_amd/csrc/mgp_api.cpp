@@ -155,6 +155,9 @@ struct mgp_ctx {
     hipEvent_t lb_ev = nullptr, lb_ev2 = nullptr;
     char* lb_buf = nullptr;
     double* lb_red = nullptr;
+    // psiOld of the last outer iteration (for mgp_metrics), nullptr when not kept
+    const char* metrics_old = nullptr;
+    double* d_metrics = nullptr;  // 3 * kSumBlocks partials + 3 results
     char* psi_old = nullptr;  // snapshot buffer (Jacobi path)
     char* stage = nullptr;    // lexicographic staging buffer for set/get (level-0 size)
     double* d_part = nullptr;
@@ -300,8 +303,8 @@ int lb_allgather(mgp_ctx* c, char* buf, size_t count)
     return MGP_OK;
 }
 
-// in-place sum of one double over the ranks, added in rank order
-int lb_allreduce(mgp_ctx* c, double* v)
+// in-place sum of n doubles over the ranks, added in rank order
+int lb_allreduce(mgp_ctx* c, double* v, int n = 1)
 {
     mgp_loopback* g = c->lb;
     c->lb_buf = (char*)v;
@@ -310,13 +313,15 @@ int lb_allreduce(mgp_ctx* c, double* v)
     for (int q = 0; q < c->o.world; ++q) {
         mgp_ctx* o = g->ranks[q];
         if (q != c->o.rank) HIP_TRY(c, hipStreamWaitEvent(c->s, o->lb_ev, 0));
-        HIP_TRY(c, hipMemcpyAsync(c->lb_red + q, o->lb_buf, sizeof(double), hipMemcpyDeviceToDevice, c->s));
+        for (int i = 0; i < n; ++i)
+            HIP_TRY(c, hipMemcpyAsync(c->lb_red + i * c->o.world + q, (const double*)o->lb_buf + i, sizeof(double),
+                                      hipMemcpyDeviceToDevice, c->s));
     }
     HIP_TRY(c, hipEventRecord(c->lb_ev2, c->s));
     if (!g->barrier()) return lb_fail(c);
     for (int q = 0; q < c->o.world; ++q)
         if (q != c->o.rank) HIP_TRY(c, hipStreamWaitEvent(c->s, g->ranks[q]->lb_ev2, 0));
-    HIP_TRY(c, mgp::launch_sum_partials(c->lb_red, c->o.world, v, c->s));
+    for (int i = 0; i < n; ++i) HIP_TRY(c, mgp::launch_sum_partials(c->lb_red + i * c->o.world, c->o.world, v + i, c->s));
     return MGP_OK;
 }
 
@@ -663,6 +668,20 @@ int cycle_rec(mgp_ctx* c, int l, double h, bool fcycle)
     return MGP_OK;
 }
 
+// Where the last outer iteration's psiOld lives: the level-0 t buffer with the fused err (the
+// first sweep ran out of place), the snapshot otherwise; lost when the temporally blocked phase
+// overwrote it, absent without err_mode.
+void update_metrics_old(mgp_ctx* c)
+{
+    const Level& L0 = c->lev[0];
+    c->metrics_old = nullptr;
+    if (!c->o.err_mode) return;
+    if (!c->err_fuse)
+        c->metrics_old = c->psi_old;
+    else if (!L0.fused)
+        c->metrics_old = c->ui(L0, L0.t);
+}
+
 // One outer iteration; err (sum of squares) goes to *dst.
 int one_cycle(mgp_ctx* c, double* dst)
 {
@@ -691,6 +710,7 @@ int one_cycle(mgp_ctx* c, double* dst)
         else
             NCCL_TRY(c, ncclAllReduce(dst, dst, 1, ncclDouble, ncclSum, c->comm, c->s));
     }
+    update_metrics_old(c);
     return MGP_OK;
 }
 
@@ -741,6 +761,7 @@ int graph_cycle(mgp_ctx* c, int slot)
         hit = &c->graphs.back();
     }
     set_level_state(c, hit->post);
+    update_metrics_old(c);
     HIP_TRY(c, hipGraphLaunch(hit->exec, c->s));
     if (c->o.err_mode)
         HIP_TRY(c, hipMemcpyAsync(c->d_errs + slot, c->d_err_cur, sizeof(double), hipMemcpyDeviceToDevice, c->s));
@@ -867,6 +888,7 @@ static void destroy_impl(mgp_ctx* c)
     if (c->lb_ev) (void)hipEventDestroy(c->lb_ev);
     if (c->lb_ev2) (void)hipEventDestroy(c->lb_ev2);
     if (c->lb_red) (void)hipFree(c->lb_red);
+    if (c->d_metrics) (void)hipFree(c->d_metrics);
     if (c->s) (void)hipStreamDestroy(c->s);
     delete c;
 }
@@ -1017,7 +1039,7 @@ static int create_impl(mgp_ctx** out, const mgp_opts* o, mgp_loopback* lb)
         c->lb = lb;
         if (hipEventCreateWithFlags(&c->lb_ev, hipEventDisableTiming) != hipSuccess ||
             hipEventCreateWithFlags(&c->lb_ev2, hipEventDisableTiming) != hipSuccess ||
-            hipMalloc(&c->lb_red, sizeof(double) * c->o.world) != hipSuccess) {
+            hipMalloc(&c->lb_red, sizeof(double) * 3 * c->o.world) != hipSuccess) {
             c->err = "loopback transport setup failed";
             c->lb = nullptr;
             return bail(MGP_ERR_HIP);
@@ -1190,6 +1212,32 @@ int mgp_coarse_solve(mgp_ctx* c)
 }
 
 int mgp_sync(mgp_ctx* c) { return c ? sync_and_check(c) : MGP_ERR_ARG; }
+
+int mgp_metrics(mgp_ctx* c, double* rel_err, int64_t* count, double* frob)
+{
+    if (!c) return MGP_ERR_ARG;
+    if (!c->metrics_old)
+        return c->fail(MGP_ERR_STATE, "mgp_metrics: no psiOld of a last outer iteration (run mgp_cycle with err_mode 1; "
+                                      "not available with the temporally blocked phases)");
+    if (!c->d_metrics) HIP_TRY(c, hipMalloc(&c->d_metrics, sizeof(double) * (3 * mgp::kSumBlocks + 3)));
+    const Level& L0 = c->lev[0];
+    double* out = c->d_metrics + 3 * mgp::kSumBlocks;
+    HIP_TRY(c, mgp::launch_metrics(c->rb, c->ui(L0, L0.u), c->metrics_old, L0.g.P * L0.g.nz, c->d_metrics, out, c->s));
+    if (c->o.world > 1) {
+        if (c->lb)
+            TRY(lb_allreduce(c, out, 3));
+        else
+            NCCL_TRY(c, ncclAllReduce(out, out, 3, ncclDouble, ncclSum, c->comm, c->s));
+    }
+    double h[3];
+    HIP_TRY(c, hipMemcpyAsync(h, out, sizeof h, hipMemcpyDeviceToHost, c->s));
+    TRY(sync_and_check(c));
+    const int64_t n = (int64_t)h[1];
+    if (rel_err) *rel_err = n > 0 ? h[0] / (double)n : NAN;    // test-gpu-obj.lua:240-243
+    if (count) *count = n;
+    if (frob) *frob = std::sqrt(h[2] / (double)c->ncells_global());  // gpu.lua:361-366
+    return MGP_OK;
+}
 
 int mgp_timing(mgp_ctx* c, int enable)
 {

@@ -57,6 +57,10 @@ hipError_t launch_prolong_correct(int rb, int dim, int linear, void* u, const vo
 // Deterministic two-pass fp64 sum of (a - b)^2 over n elements into *out.
 hipError_t launch_sqdiff_sum(int rb, const void* a, const void* b, int64_t n, double* partials, double* out,
                              hipStream_t s);
+// out[0..2] = {sum |1 - psi/psiOld| over nonzero entries, their count, sum (psi - psiOld)^2}
+// over n elements; partials needs 3 * kSumBlocks doubles.
+hipError_t launch_metrics(int rb, const void* psi, const void* old, int64_t n, double* partials, double* out,
+                          hipStream_t s);
 // Fixed-order fp64 sum of n partials into *out.  Needs sum_scratch(n) doubles of scratch right
 // after partials[n - 1].
 int sum_scratch(int n);

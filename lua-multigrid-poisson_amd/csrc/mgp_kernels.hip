@@ -1369,6 +1369,38 @@ __global__ __launch_bounds__(kBlock) void k_sqdiff_partial(const T* __restrict__
     block_partial<T>(acc, partials);
 }
 
+// calcRelErr + count + calcFrobErr of gpu.lua:173-200 / test-gpu-obj.lua:96-123, 216-247 in one
+// pass: per workgroup sum |1 - psi/psiOld| (in real, as errorBuf holds it), the number of nonzero
+// errorBuf entries and sum (psi - psiOld)^2, each into its own block of kSumBlocks partials.
+template <typename T>
+__global__ __launch_bounds__(kBlock) void k_metrics_partial(const T* __restrict__ psi, const T* __restrict__ old,
+                                                            int64_t n, double* __restrict__ partials)
+{
+    double rel = 0.0, cnt = 0.0, sq = 0.0;
+    for (int64_t c = (int64_t)blockIdx.x * kBlock + threadIdx.x; c < n; c += (int64_t)gridDim.x * kBlock) {
+        const T p = psi[c], o = old[c];
+        const T e = (o != (T)0 && o != p) ? (T)fabs(1.0 - (double)(p / o)) : (T)0;
+        if (e != (T)0) {
+            rel += (double)e;
+            cnt += 1.0;
+        }
+        const double d = (double)p - (double)o;
+        sq += d * d;
+    }
+    __shared__ double red[3][kBlock];
+    red[0][threadIdx.x] = rel;
+    red[1][threadIdx.x] = cnt;
+    red[2][threadIdx.x] = sq;
+    __syncthreads();
+    for (int w = kBlock / 2; w > 0; w >>= 1) {
+        if ((int)threadIdx.x < w)
+            for (int q = 0; q < 3; ++q) red[q][threadIdx.x] += red[q][threadIdx.x + w];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0)
+        for (int q = 0; q < 3; ++q) partials[q * gridDim.x + blockIdx.x] = red[q][0];
+}
+
 // First level of a two-level fixed-order sum: block b sums partials [b*chunk, (b+1)*chunk).
 __global__ __launch_bounds__(1024) void k_sum_chunks(const double* __restrict__ partials, int n, int chunk,
                                                      double* __restrict__ out)
@@ -1714,6 +1746,14 @@ hipError_t launch_sqdiff_sum(int rb, const void* a, const void* b, int64_t n, do
 {
     MGP_REAL(rb, (k_sqdiff_partial<T><<<kSumBlocks, kBlock, 0, s>>>((const T*)a, (const T*)b, n, partials)));
     k_sum_n<<<1, 1024, 0, s>>>(partials, kSumBlocks, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_metrics(int rb, const void* psi, const void* old, int64_t n, double* partials, double* out,
+                          hipStream_t s)
+{
+    MGP_REAL(rb, (k_metrics_partial<T><<<kSumBlocks, kBlock, 0, s>>>((const T*)psi, (const T*)old, n, partials)));
+    for (int q = 0; q < 3; ++q) k_sum_n<<<1, 1024, 0, s>>>(partials + q * kSumBlocks, kSumBlocks, out + q);
     return hipGetLastError();
 }
 

@@ -95,6 +95,7 @@ SIGNATURES = {
     "mgp_prolong_correct": (ctypes.c_int, [_vp, ctypes.c_int]),
     "mgp_coarse_solve": (ctypes.c_int, [_vp]),
     "mgp_sync": (ctypes.c_int, [_vp]),
+    "mgp_metrics": (ctypes.c_int, [_vp, _P(_dbl), _P(_i64), _P(_dbl)]),
     "mgp_timing": (ctypes.c_int, [_vp, ctypes.c_int]),
     "mgp_timing_read": (ctypes.c_int, [_vp, ctypes.c_int, _P(_dbl), _P(_i64), _P(_dbl)]),
 }

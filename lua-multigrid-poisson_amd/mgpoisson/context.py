@@ -172,6 +172,12 @@ class Context:
     def coarse_solve(self):
         self._chk(L.lib.mgp_coarse_solve(self._h))
 
+    def metrics(self):
+        """(rel_err, count, frob) of the last outer iteration (gpu.lua:173-200, test-gpu-obj.lua:216-247)."""
+        rel, n, frob = ctypes.c_double(), ctypes.c_int64(), ctypes.c_double()
+        self._chk(L.lib.mgp_metrics(self._h, ctypes.byref(rel), ctypes.byref(n), ctypes.byref(frob)))
+        return rel.value, n.value, frob.value
+
     def sync(self):
         self._chk(L.lib.mgp_sync(self._h))
 

@@ -361,7 +361,7 @@ def test_slab_decomposition_loopback(box, world, gather, cfg):
             assert sum(lv["distributed"] for lv in ctx.levels) >= 2
             ctx.init_point_charge()
             errs = ctx.cycles(3)
-            results[r] = (ctx.get_psi(), errs)
+            results[r] = (ctx.get_psi(), errs, ctx.metrics())
             ctx.close()
         except Exception as e:  # noqa: BLE001 - surfaced below
             errors.append((r, repr(e)))
@@ -378,8 +378,48 @@ def test_slab_decomposition_loopback(box, world, gather, cfg):
     e_ref = ref.cycles(3)
     psi = np.concatenate([results[r][0] for r in range(world)], axis=0)
     assert np.array_equal(psi, ref.get_psi()), float(np.max(np.abs(psi - ref.get_psi())))
+    m_ref = ref.metrics()
     for r in range(world):
         np.testing.assert_allclose(results[r][1], e_ref, rtol=1e-12, atol=0)
+        assert results[r][2][1] == m_ref[1]
+        np.testing.assert_allclose(results[r][2], m_ref, rtol=1e-12, atol=0)
+
+
+def _ref_metrics(psi, old):
+    """gpu.lua:173-200 / test-gpu-obj.lua:216-247 restated in numpy (errorBuf in real, sums fp64)."""
+    dt = psi.dtype.type
+    with np.errstate(divide="ignore", invalid="ignore"):
+        e = np.where((old != 0) & (old != psi), np.abs(1.0 - (psi / old).astype(np.float64)).astype(psi.dtype), dt(0))
+    nz = e != 0
+    d = psi.astype(np.float64) - old.astype(np.float64)
+    n = int(nz.sum())
+    return float(e[nz].astype(np.float64).sum()) / n, n, float(np.sqrt((d * d).sum() / d.size))
+
+
+@pytest.mark.parametrize("kw", [
+    dict(dim=2, n=(64, 64, 1), real="double"),
+    dict(dim=2, n=(128, 128, 1), real="float", smoother="rbgs", nu1=2, nu2=2),
+    dict(dim=3, n=(64, 64, 64), real="float", smoother="rbgs", nu1=2, nu2=2, prolong="linear", coarse_bc="consistent"),
+], ids=["2d-jacobi-f64", "2d-rbgs-f32", "3d-rbgs-f32"])
+def test_metrics_match_reference_formulas(kw):
+    ctx = _ctx(**kw)
+    ctx.init_point_charge()
+    ctx.cycles(2)
+    old = ctx.get_psi()
+    e = ctx.cycle()
+    rel, n, frob = ctx.metrics()
+    r_rel, r_n, r_frob = _ref_metrics(ctx.get_psi(), old)
+    assert n == r_n
+    assert abs(rel - r_rel) <= 1e-12 * abs(r_rel)
+    assert abs(frob - r_frob) <= 1e-12 * r_frob and abs(frob - e) <= 1e-12 * e
+
+
+def test_metrics_need_err_mode():
+    ctx = _ctx(dim=2, n=(16, 16, 1), err_mode=0)
+    ctx.init_point_charge()
+    ctx.cycle()
+    with pytest.raises(_mg().MGPError):
+        ctx.metrics()
 
 
 def test_two_grid_host_buffers():
