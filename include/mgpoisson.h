@@ -114,6 +114,19 @@ int         mgp_coarse_solve(mgp_ctx* c);                           /* L == 1 br
 
 int         mgp_sync(mgp_ctx* c);
 
+/* Coarse-engine switch, the MI355X form of cpu-gpu.lua's cpuDepth (cpu-gpu.lua:61): the levels of
+ * nx <= size run as ONE launch of the LDS-resident coarse engine (levels of <= 4096 cells by
+ * default).  size 0 turns the engine off.  MGP_ERR_ARG if that sub-hierarchy does not fit one
+ * workgroup's LDS. */
+int         mgp_set_coarse_level(mgp_ctx* c, int64_t size);
+/* Hybrid hand-off (cpu-gpu.lua:17-52).  When the cycle reaches the level of nx = size it copies
+ * that level's u and f to host buffers (lexicographic, size^dim reals), calls fn(user, h, u, f,
+ * size), which runs the coarse cycle in place on u (e.g. the reference's MultigridCPURaw:twoGrid),
+ * and copies u and f back.  fn returns 0 on success.  fn == NULL removes the hand-off.  Replicated
+ * levels >= 1 only; hipGraph replay is off while a hand-off is set. */
+typedef int (*mgp_coarse_fn)(void* user, double h, void* u, const void* f, int64_t size);
+int         mgp_set_coarse_handoff(mgp_ctx* c, int64_t size, mgp_coarse_fn fn, void* user);
+
 /* The reference's convergence metrics of the last outer iteration, on the device
  * (gpu.lua:173-200 calcRelErr / calcFrobErr, test-gpu-obj.lua:216-247 relErr / count / frobErr):
  * rel_err = mean of |1 - psi/psiOld| over the cells where it is nonzero, count = their number,

@@ -183,6 +183,11 @@ struct mgp_ctx {
     // coarse-level tail (k_tail): cycle_rec(tail_level, ...) as one launch; programs for V and F
     int tail_level = -1;
     std::vector<uint32_t> tail_v, tail_f;
+    // hybrid hand-off (cpu-gpu.lua:17-52): the level of size handoff_size goes to a host callback
+    int handoff_level = -1;
+    mgp_coarse_fn handoff_fn = nullptr;
+    void* handoff_user = nullptr;
+    std::vector<char> hbuf_u, hbuf_f;
     double* d_err_cur = nullptr;
     double* err_dst = nullptr;  // where this cycle's sum of squares goes
     std::string err;
@@ -393,6 +398,7 @@ int timed_end(mgp_ctx* c, hipEvent_t e1, int kind, double bytes)
 }
 
 int64_t level_cells(const Level& L) { return L.p.nx * L.p.ny * L.p.nz; }
+int64_t level_count(const Level& L) { return L.p.nx * L.p.ny * (L.g.nz); }
 
 // ---- cycle pieces ----
 
@@ -592,6 +598,29 @@ void tail_gen(const mgp_ctx* c, int T, int l, bool fcycle, std::vector<uint32_t>
 
 // First level (>= 1, replicated, <= MGP_TAIL_CELLS cells) whose sub-hierarchy fits one
 // workgroup's LDS and the op budget; -1 = no tail (MGP_TAIL=0 disables it).
+// Make level T (>= 1, replicated) the first level of the coarse tail if its sub-hierarchy fits
+// one workgroup's LDS and the op budget.
+bool try_tail(mgp_ctx* c, int T)
+{
+    const int last = (int)c->lev.size() - 1;
+    if (T < 1 || T > last || c->lev[T].p.dist) return false;
+    const int nlev = last - T + 1;
+    if (nlev > mgp::kTailMaxLevels) return false;
+    std::vector<Geo> g;
+    for (int l = T; l <= last; ++l) g.push_back(c->lev[l].g);
+    if (mgp::tail_lds_bytes(c->rb, c->o.dim, c->o.smoother == MGP_JACOBI, g.data(), nlev) > mgp::kTailMaxLds)
+        return false;
+    std::vector<uint32_t> pv, pf;
+    tail_gen(c, T, T, false, pv);
+    tail_gen(c, T, T, true, pf);
+    if ((int)pv.size() > mgp::kTailMaxOps || (int)pf.size() > mgp::kTailMaxOps) return false;
+    c->tail_level = T;
+    c->tail_v = pv;
+    c->tail_f = pf;
+    return true;
+}
+
+// Default: the first level with <= MGP_TAIL_CELLS (4096) cells that fits (MGP_TAIL=0: none).
 void plan_tail(mgp_ctx* c)
 {
     c->tail_level = -1;
@@ -599,25 +628,33 @@ void plan_tail(mgp_ctx* c)
     if (v && std::atoi(v) == 0) return;
     const char* vc = std::getenv("MGP_TAIL_CELLS");
     const int64_t max_cells = vc ? std::atoll(vc) : 4096;
-    const int last = (int)c->lev.size() - 1;
-    for (int T = 1; T <= last; ++T) {
+    for (int T = 1; T < (int)c->lev.size(); ++T) {
         const Level& L = c->lev[T];
-        if (L.p.dist || L.p.nx * L.p.ny * L.p.gnz > max_cells) continue;
-        const int nlev = last - T + 1;
-        if (nlev > mgp::kTailMaxLevels) continue;
-        std::vector<Geo> g;
-        for (int l = T; l <= last; ++l) g.push_back(c->lev[l].g);
-        if (mgp::tail_lds_bytes(c->rb, c->o.dim, c->o.smoother == MGP_JACOBI, g.data(), nlev) > mgp::kTailMaxLds)
-            continue;
-        std::vector<uint32_t> pv, pf;
-        tail_gen(c, T, T, false, pv);
-        tail_gen(c, T, T, true, pf);
-        if ((int)pv.size() > mgp::kTailMaxOps || (int)pf.size() > mgp::kTailMaxOps) continue;
-        c->tail_level = T;
-        c->tail_v = pv;
-        c->tail_f = pf;
-        return;
+        if (L.p.nx * L.p.ny * L.p.gnz <= max_cells && try_tail(c, T)) return;
     }
+}
+
+void drop_graphs(mgp_ctx* c)
+{
+    for (auto& g : c->graphs) (void)hipGraphExecDestroy(g.exec);
+    c->graphs.clear();
+}
+
+// cpu-gpu.lua:17-52: level l's u and f to the host, the callback's coarse cycle, and back
+int run_handoff(mgp_ctx* c, int l, double h)
+{
+    Level& L = c->lev[l];
+    const int64_t n = level_count(L);
+    c->hbuf_u.resize((size_t)n * c->rb);
+    c->hbuf_f.resize((size_t)n * c->rb);
+    TRY(mgp_get_field(c, l, MGP_FIELD_U, c->hbuf_u.data(), n, MGP_MEM_HOST));
+    TRY(mgp_get_field(c, l, MGP_FIELD_F, c->hbuf_f.data(), n, MGP_MEM_HOST));
+    const int rc = c->handoff_fn(c->handoff_user, h, c->hbuf_u.data(), c->hbuf_f.data(), L.p.nx);
+    if (rc != 0) return c->fail(MGP_ERR_STATE, "coarse hand-off callback returned %d", rc);
+    TRY(mgp_set_field(c, l, MGP_FIELD_U, c->hbuf_u.data(), n, MGP_MEM_HOST));
+    TRY(mgp_set_field(c, l, MGP_FIELD_F, c->hbuf_f.data(), n, MGP_MEM_HOST));
+    L.ghost_ok = !L.p.dist;
+    return MGP_OK;
 }
 
 int run_tail(mgp_ctx* c, bool fcycle)
@@ -646,6 +683,7 @@ int run_tail(mgp_ctx* c, bool fcycle)
 int cycle_rec(mgp_ctx* c, int l, double h, bool fcycle)
 {
     const int last = (int)c->lev.size() - 1;
+    if (l == c->handoff_level && c->handoff_fn) return run_handoff(c, l, h);
     if (l == c->tail_level && h == level_h(c, l)) return run_tail(c, fcycle);
     if (l == last) return coarse_solve_at(c, l, h);
     const bool fused = c->lev[l].fused && h == level_h(c, l);
@@ -1102,7 +1140,6 @@ int mgp_init_point_charge(mgp_ctx* c)
     return sync_and_check(c);
 }
 
-static int64_t level_count(const Level& L) { return L.p.nx * L.p.ny * (L.g.nz); }
 
 int mgp_set_field(mgp_ctx* c, int level, int which, const void* src, int64_t count, int mem)
 {
@@ -1141,7 +1178,7 @@ int mgp_cycles(mgp_ctx* c, int32_t k, double* errs)
 {
     if (!c || k < 0) return MGP_ERR_ARG;
     TRY(ensure_errs(c, k));
-    const bool graph = c->use_graph && !c->timing;
+    const bool graph = c->use_graph && !c->timing && !c->handoff_fn;
     for (int i = 0; i < k; ++i) TRY(graph ? graph_cycle(c, i) : one_cycle(c, c->d_errs + i));
     TRY(sync_and_check(c));
     if (errs) {
@@ -1212,6 +1249,55 @@ int mgp_coarse_solve(mgp_ctx* c)
 }
 
 int mgp_sync(mgp_ctx* c) { return c ? sync_and_check(c) : MGP_ERR_ARG; }
+
+static int level_of_size(const mgp_ctx* c, int64_t size)
+{
+    for (int l = 1; l < (int)c->lev.size(); ++l)
+        if (c->lev[l].p.nx == size) return l;
+    return -1;
+}
+
+int mgp_set_coarse_level(mgp_ctx* c, int64_t size)
+{
+    if (!c) return MGP_ERR_ARG;
+    TRY(sync_and_check(c));
+    drop_graphs(c);
+    if (size == 0) {
+        c->tail_level = -1;
+        return MGP_OK;
+    }
+    const int l = level_of_size(c, size);
+    if (l < 0) return c->fail(MGP_ERR_ARG, "mgp_set_coarse_level: no level >= 1 with nx = %lld", (long long)size);
+    const int prev = c->tail_level;
+    if (!try_tail(c, l)) {
+        c->tail_level = prev;
+        return c->fail(MGP_ERR_ARG, "mgp_set_coarse_level: levels from nx = %lld do not fit the one-workgroup coarse engine",
+                       (long long)size);
+    }
+    return MGP_OK;
+}
+
+int mgp_set_coarse_handoff(mgp_ctx* c, int64_t size, mgp_coarse_fn fn, void* user)
+{
+    if (!c) return MGP_ERR_ARG;
+    TRY(sync_and_check(c));
+    drop_graphs(c);
+    if (!fn) {
+        c->handoff_level = -1;
+        c->handoff_fn = nullptr;
+        c->handoff_user = nullptr;
+        plan_tail(c);
+        return MGP_OK;
+    }
+    const int l = level_of_size(c, size);
+    if (l < 0 || c->lev[l].p.dist)
+        return c->fail(MGP_ERR_ARG, "mgp_set_coarse_handoff: no replicated level >= 1 with nx = %lld", (long long)size);
+    c->handoff_level = l;
+    c->handoff_fn = fn;
+    c->handoff_user = user;
+    if (c->tail_level >= 0 && c->tail_level <= l) c->tail_level = -1;  // the levels below l are the callback's
+    return MGP_OK;
+}
 
 int mgp_metrics(mgp_ctx* c, double* rel_err, int64_t* count, double* frob)
 {

@@ -11,6 +11,11 @@ It accepts both constructor protocols of the reference:
         local mg = MG(size, real)    -- real = 'double' (default) or 'float'
         mg:run()              -- two outer iterations, prints '#iter err'
         mg:twoGrid(h, uPtr, fPtr, L) -- raw real* host buffers of an L x L grid (cpu-raw.lua:186)
+  * cpu-gpu.lua protocol (cpu-gpu.lua:55-72): MG(size, real, cpuDepth[, engine]) switches to the
+    GPU's one-launch coarse engine at size 2^cpuDepth, or, given an engine with
+    engine:twoGrid(h, uPtr, fPtr, L) (e.g. require'multigrid-poisson.cpu-raw'(2^cpuDepth)), hands
+    that level's u and f to it and back, exactly as MultigridGPUSubset:twoGrid does.
+mg:metrics() returns relErr, count, frobErr of the last outer iteration (gpu.lua:173-200).
 Extra table fields select the build's configurations: dim (2|3), real, smoother ('jacobi'|'rbgs'),
 cycle ('V'|'F'), prolong ('pc'|'linear'), coarse_init ('fresh'|'warm'), coarse_bc
 ('zero'|'consistent'), device.  Defaults reproduce cpu.lua (2D, double, Jacobi 7+7, V-cycle,
@@ -24,6 +29,7 @@ Not executable in this repository's CI (no Lua runtime in the image); the Python
 ../mgpoisson/solver.py is the tested twin of this file.
 --]]
 local ffi = require 'ffi'
+local bit = require 'bit'
 
 ffi.cdef[[
 typedef struct mgp_ctx mgp_ctx;
@@ -55,6 +61,10 @@ int         mgp_set_field(mgp_ctx* c, int level, int which, const void* src, int
 int         mgp_get_field(const mgp_ctx* c, int level, int which, void* dst, int64_t count, int mem);
 int         mgp_cycle(mgp_ctx* c, double* err_out);
 int         mgp_two_grid(mgp_ctx* c, double h, void* u, const void* f, int64_t L, int mem);
+int         mgp_set_coarse_level(mgp_ctx* c, int64_t size);
+typedef int (*mgp_coarse_fn)(void* user, double h, void* u, const void* f, int64_t size);
+int         mgp_set_coarse_handoff(mgp_ctx* c, int64_t size, mgp_coarse_fn fn, void* user);
+int         mgp_metrics(mgp_ctx* c, double* rel_err, int64_t* count, double* frob);
 ]]
 
 local lib = ffi.load(os.getenv('MGP_LIBRARY') or 'mgpoisson')
@@ -96,7 +106,7 @@ setmetatable(MultigridHIP, {
 	end,
 })
 
-function MultigridHIP:init(a, real, cpuDepth)
+function MultigridHIP:init(a, real, cpuDepth, engine)
 	local args
 	if type(a) == 'table' then
 		args = a
@@ -130,7 +140,28 @@ function MultigridHIP:init(a, real, cpuDepth)
 	rawset(self, 'ctx', ffi.gc(pp[0], lib.mgp_destroy))
 	rawset(self, 'count', n * n * (dim == 3 and n or 1))
 	rawset(self, 'ctype', (self.real == 'float') and 'float[?]' or 'double[?]')
+	if cpuDepth then
+		local L = bit.lshift(1, cpuDepth)
+		if engine then
+			-- cpu-gpu.lua:17-52: the callback runs engine:twoGrid on the level's host copies
+			local cb = ffi.cast('mgp_coarse_fn', function(user, h, u, f, size)
+				local ok = pcall(engine.twoGrid, engine, h, ffi.cast(self.ctype:gsub('%[%?%]', '*'), u),
+					ffi.cast(self.ctype:gsub('%[%?%]', '*'), f), tonumber(size))
+				return ok and 0 or 1
+			end)
+			rawset(self, 'handoff', cb)  -- keep the callback alive
+			check(lib.mgp_set_coarse_handoff(self.ctx, L, cb, nil), self.ctx)
+		else
+			lib.mgp_set_coarse_level(self.ctx, L)  -- keeps the default switch when it does not fit
+		end
+	end
 	check(lib.mgp_init_point_charge(self.ctx), self.ctx)  -- cpu.lua:180-193
+end
+
+function MultigridHIP:metrics()
+	local rel, n, frob = ffi.new('double[1]'), ffi.new('int64_t[1]'), ffi.new('double[1]')
+	check(lib.mgp_metrics(self.ctx, rel, n, frob), self.ctx)
+	return rel[0], tonumber(n[0]), frob[0]
 end
 
 function MultigridHIP:getBuffer(which)

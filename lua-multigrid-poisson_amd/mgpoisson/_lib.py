@@ -40,6 +40,9 @@ COARSE_FRESH, COARSE_WARM = 0, 1
 BC_ZERO, BC_CONSISTENT = 0, 1
 FIELD_U, FIELD_F = 0, 1
 MEM_HOST, MEM_DEVICE = 0, 1
+# int fn(void* user, double h, void* u, const void* f, int64_t size)
+COARSE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_double, ctypes.c_void_p, ctypes.c_void_p,
+                             ctypes.c_int64)
 TIMING_HALF_SWEEP, TIMING_FUSED_PRE, TIMING_FUSED_POST = 0, 1, 2
 TIMING_KINDS = {TIMING_HALF_SWEEP: "half_sweep", TIMING_FUSED_PRE: "fused_pre", TIMING_FUSED_POST: "fused_post"}
 COMM_ID_BYTES = 128
@@ -96,6 +99,8 @@ SIGNATURES = {
     "mgp_coarse_solve": (ctypes.c_int, [_vp]),
     "mgp_sync": (ctypes.c_int, [_vp]),
     "mgp_metrics": (ctypes.c_int, [_vp, _P(_dbl), _P(_i64), _P(_dbl)]),
+    "mgp_set_coarse_level": (ctypes.c_int, [_vp, _i64]),
+    "mgp_set_coarse_handoff": (ctypes.c_int, [_vp, _i64, COARSE_FN, _vp]),
     "mgp_timing": (ctypes.c_int, [_vp, ctypes.c_int]),
     "mgp_timing_read": (ctypes.c_int, [_vp, ctypes.c_int, _P(_dbl), _P(_i64), _P(_dbl)]),
 }

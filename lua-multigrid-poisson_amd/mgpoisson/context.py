@@ -73,6 +73,9 @@ class Context:
         else:
             L.check(L.lib.mgp_create(ctypes.byref(h), ctypes.byref(opts)))
         self._h = h
+        self._read_levels()
+
+    def _read_levels(self):
         self.levels = []
         info = (ctypes.c_int64 * 8)()
         for l in range(L.lib.mgp_num_levels(self._h)):
@@ -171,6 +174,35 @@ class Context:
 
     def coarse_solve(self):
         self._chk(L.lib.mgp_coarse_solve(self._h))
+
+    def set_coarse_level(self, size: int):
+        """Levels of nx <= size run in the one-launch LDS coarse engine (cpuDepth, cpu-gpu.lua:61)."""
+        self._chk(L.lib.mgp_set_coarse_level(self._h, int(size)))
+        self._read_levels()
+
+    def set_coarse_handoff(self, size: int, engine):
+        """cpu-gpu.lua:17-52: at the level of nx = size call engine(h, u, f, size) on host numpy views
+        (u updated in place); engine=None removes the hand-off."""
+        if engine is None:
+            self._handoff = None
+            self._chk(L.lib.mgp_set_coarse_handoff(self._h, int(size), L.COARSE_FN(), None))
+            return
+        lvl = next(i for i, lv in enumerate(self.levels) if lv["nx"] == size)
+        shape = self.shape(lvl)
+        count = int(np.prod(shape))
+        dt = self.dtype
+
+        def cb(user, h, u_ptr, f_ptr, n):
+            try:
+                u = np.ctypeslib.as_array((ctypes.c_char * (count * dt.itemsize)).from_address(u_ptr)).view(dt).reshape(shape)
+                f = np.ctypeslib.as_array((ctypes.c_char * (count * dt.itemsize)).from_address(f_ptr)).view(dt).reshape(shape)
+                engine(h, u, f, int(n))
+                return 0
+            except Exception:  # noqa: BLE001 - reported as a library error
+                return 1
+
+        self._handoff = L.COARSE_FN(cb)  # keep the trampoline alive
+        self._chk(L.lib.mgp_set_coarse_handoff(self._h, int(size), self._handoff, None))
 
     def metrics(self):
         """(rel_err, count, frob) of the last outer iteration (gpu.lua:173-200, test-gpu-obj.lua:216-247)."""

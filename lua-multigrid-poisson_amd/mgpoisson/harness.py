@@ -1,0 +1,146 @@
+"""Benchmark harness and convergence report in the reference's formats.
+
+``python -m mgpoisson.harness bench`` reproduces test/test.lua:8-63.  For sizes 2^lo .. 2^hi it
+constructs the solver with the positional protocol ``MG(size, real, cpuDepth)``, times
+``mg:run()`` (two outer iterations, cpu-raw.lua:239-258), keeps the best of ``--tries`` and
+writes ``#size<TAB>col...`` rows to ``cpu-vs-gpu.txt``.  The reference times with ``os.clock``
+(CPU time); this harness uses wall-clock time with a device synchronisation, since the work runs
+on the GPU.  The reference's harness calls ``run`` on ``multigrid-poisson.cpu``, which only has
+``solve``.  Here every column is a solver whose class has ``run``.
+
+``python -m mgpoisson.harness converge`` reproduces the multigrid half of
+test/converge-multigrid-vs-krylov.lua:15-89.  For sizes 4 .. 128 it runs ``solve()`` with
+``epsilon = 1e-20`` and records ``|psi|_inf`` per iteration from the ``errorCallback``.  It adds a
+conjugate-gradient column on the same system (the reference's ``solver.conjgrad`` with
+``x0 = -f``, ``b = f``, ``A`` = the 5-point operator with zero ghosts), computed with SciPy on the
+host as the cross-check.  Both columns are shifted by their common minimum and written to
+``converge/<size>.txt``.
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import sys
+import time
+
+import numpy as np
+
+COLUMNS = {
+    # column name -> (real, build options); 'hip' is the reference configuration on the GPU
+    "hip": ("double", {}),
+    "hip-f32": ("float", {}),
+    "hip-rbgs": ("double", dict(smoother="rbgs", nu1=2, nu2=2, prolong="linear", coarse_bc="consistent")),
+}
+
+
+def bench(lo=5, hi=10, tries=1, cols=("hip",), cpudepth=3, out="cpu-vs-gpu.txt", quiet=False):
+    """test/test.lua: best-of-tries wall time of MG(size, real, cpudepth):run() per size and column."""
+    from .solver import MultigridHIPRaw
+
+    rows = []
+    with open(out, "w") as fh:
+        def write(s):
+            fh.write(s)
+            fh.flush()
+            if not quiet:
+                sys.stdout.write(s)
+                sys.stdout.flush()
+
+        write("#size" + "".join("\t" + c for c in cols) + "\n")
+        for log2size in range(lo, hi + 1):
+            size = 1 << log2size
+            write(str(size))
+            row = [size]
+            for col in cols:
+                real, build = COLUMNS[col]
+                best = float("inf")
+                for _ in range(tries):
+                    mg = MultigridHIPRaw(size, real, cpudepth, **build)
+                    mg.quiet = True
+                    t0 = time.perf_counter()
+                    mg.run()
+                    mg.ctx.sync()
+                    best = min(best, time.perf_counter() - t0)
+                    mg.ctx.close()
+                write(f"\t{best}")
+                row.append(best)
+            write("\n")
+            rows.append(row)
+    return rows
+
+
+def _cg_linf_history(f: np.ndarray, h: float, epsilon: float, maxiter: int = 100000):
+    """|x|_inf per CG iteration on A x = f (5-point, zero ghosts), x0 = -f (converge...lua:37-58)."""
+    import scipy.sparse as sp
+    import scipy.sparse.linalg as spla
+
+    n = f.shape[0]
+    one = sp.diags([np.ones(n - 1), -2 * np.ones(n), np.ones(n - 1)], [-1, 0, 1])
+    eye = sp.identity(n)
+    A = (sp.kron(eye, one) + sp.kron(one, eye)) / (h * h)
+    hist = []
+    b = f.reshape(-1)
+    bsq = float(b @ b)
+
+    def cb(xk):
+        hist.append(float(np.max(np.abs(xk))))
+
+    # the reference stops when err = rSq / bSq < epsilon; scipy's rtol is on |r| / |b|
+    spla.cg(A, b, x0=-b.copy(), rtol=max(np.sqrt(epsilon), 1e-15), atol=0.0, maxiter=maxiter, callback=cb)
+    del bsq
+    return hist
+
+
+def converge(sizes=(4, 8, 16, 32, 64, 128), epsilon=1e-20, outdir="converge", maxiter=1000, quiet=False):
+    """converge-multigrid-vs-krylov.lua: |psi|_inf per multigrid iteration next to CG's."""
+    from .solver import MultigridHIP
+
+    os.makedirs(outdir, exist_ok=True)
+    report = {}
+    for size in sizes:
+        if not quiet:
+            print(f"solving for size {size}")
+        data = []
+        mg = None
+
+        def cb(it, err):
+            data.append(float(np.max(np.abs(mg.psi))))
+            return False
+
+        mg = MultigridHIP(size=size, epsilon=epsilon, errorCallback=cb, maxiter=maxiter)
+        mg.solve()
+        f = np.asarray(mg.f, dtype=np.float64)
+        cg = _cg_linf_history(f, 1.0 / size, epsilon)
+        n = max(len(data), len(cg))
+        cols = [data + [float("nan")] * (n - len(data)), cg + [float("nan")] * (n - len(cg))]
+        finite = [v for c in cols for v in c if np.isfinite(v)]
+        lo = min(finite) if finite else 0.0
+        with open(os.path.join(outdir, f"{size}.txt"), "w") as fh:
+            fh.write("\n".join("\t".join(repr(c[i] - lo) for c in cols) for i in range(n)))
+        report[size] = (data, cg)
+    return report
+
+
+def main(argv=None):
+    p = argparse.ArgumentParser(prog="python -m mgpoisson.harness")
+    sub = p.add_subparsers(dest="cmd", required=True)
+    b = sub.add_parser("bench", help="test/test.lua: TSV of best-of-tries run() times")
+    b.add_argument("--lo", type=int, default=5)
+    b.add_argument("--hi", type=int, default=10)
+    b.add_argument("--tries", type=int, default=1)
+    b.add_argument("--cols", default="hip", help="comma list of " + ",".join(COLUMNS))
+    b.add_argument("--cpudepth", type=int, default=3)
+    b.add_argument("--out", default="cpu-vs-gpu.txt")
+    c = sub.add_parser("converge", help="converge-multigrid-vs-krylov.lua: |psi|_inf histories")
+    c.add_argument("--sizes", default="4,8,16,32,64,128")
+    c.add_argument("--epsilon", type=float, default=1e-20)
+    c.add_argument("--outdir", default="converge")
+    a = p.parse_args(argv)
+    if a.cmd == "bench":
+        bench(a.lo, a.hi, a.tries, tuple(a.cols.split(",")), a.cpudepth, a.out)
+    else:
+        converge(tuple(int(s) for s in a.sizes.split(",")), a.epsilon, a.outdir)
+
+
+if __name__ == "__main__":
+    main()

@@ -139,10 +139,20 @@ class MultigridHIPRaw:
         self.cpuDepth = cpuDepth
         dim = int(build.pop("dim", 2))
         n = self.size
-        opts = make_opts(dim=dim, n=(n, n, n if dim == 3 else 1), real=self.real, nu1=self.smooth,
-                         nu2=self.smooth, coarse_init=build.pop("coarse_init", "warm"), **build)
+        opts = make_opts(dim=dim, n=(n, n, n if dim == 3 else 1), real=self.real, nu1=build.pop("nu1", self.smooth),
+                         nu2=build.pop("nu2", self.smooth), coarse_init=build.pop("coarse_init", "warm"), **build)
         self._ctx = Context(opts)
+        if cpuDepth:  # cpu-gpu.lua:61: switch to the coarse engine at size 2^cpuDepth when it fits
+            try:
+                self._ctx.set_coarse_level(1 << int(cpuDepth))
+            except Exception:  # noqa: BLE001 - the default switch stays
+                pass
         self._ctx.init_point_charge()  # call2D(initCells) (cpu-raw.lua:173)
+        self.quiet = False
+
+    @property
+    def ctx(self):
+        return self._ctx
 
     @property
     def psi(self):
@@ -160,12 +170,26 @@ class MultigridHIPRaw:
 
     def run(self, iters: int = 2):
         """cpu-raw.lua:239-258 / gpu.lua:348-373 (2 outer iterations, printed)."""
-        print("#iter", "err")
+        if not self.quiet:
+            print("#iter", "err")
         errs = []
         for it in range(1, iters + 1):
             err = self._ctx.cycle()
             errs.append(err)
-            print(it, err)
+            if not self.quiet:
+                print(it, err)
             if err < self.accuracy or not math.isfinite(err):
                 break
         return errs
+
+
+class MultigridHIPHybrid(MultigridHIPRaw):
+    """Drop-in for ``MultigridCPUGPU`` (cpu-gpu.lua:55-72): ``MultigridHIPHybrid(size, real,
+    cpuDepth, engine)`` runs the fine levels on the GPU and hands the level of size 2^cpuDepth to
+    ``engine(h, u, f, L)`` (a coarse twoGrid on host arrays, e.g. a CPU solver), then continues.
+    Without an engine the hand-off goes to the GPU's own one-launch coarse engine."""
+
+    def __init__(self, size, real="double", cpuDepth=3, engine=None, **build):
+        super().__init__(size, real, cpuDepth if engine is None else None, **build)
+        if engine is not None:
+            self._ctx.set_coarse_handoff(1 << int(cpuDepth), engine)

@@ -422,6 +422,30 @@ def test_metrics_need_err_mode():
         ctx.metrics()
 
 
+def test_harness_bench_tsv(tmp_path):
+    """test/test.lua's TSV: '#size<TAB>col' header, one row per size with the best run() time."""
+    from mgpoisson import harness
+
+    out = tmp_path / "cpu-vs-gpu.txt"
+    rows = harness.bench(5, 7, tries=2, cols=("hip", "hip-rbgs"), out=str(out), quiet=True)
+    lines = out.read_text().splitlines()
+    assert lines[0] == "#size\thip\thip-rbgs"
+    assert [int(l.split("\t")[0]) for l in lines[1:]] == [32, 64, 128]
+    assert all(len(r) == 3 and all(t > 0 for t in r[1:]) for r in rows)
+
+
+def test_harness_converge_matches_cg(tmp_path):
+    """converge-multigrid-vs-krylov.lua: multigrid and CG histories of |psi|_inf end at the same
+    discrete solution (the converged values agree to 1e-8 relative)."""
+    from mgpoisson import harness
+
+    rep = harness.converge((8, 16), epsilon=1e-20, outdir=str(tmp_path), maxiter=200, quiet=True)
+    for size, (mgh, cgh) in rep.items():
+        assert len(mgh) > 3 and len(cgh) > 3
+        assert abs(mgh[-1] - cgh[-1]) <= 1e-8 * abs(cgh[-1])
+        assert (tmp_path / f"{size}.txt").exists()
+
+
 def test_two_grid_host_buffers():
     """cpu-raw.lua:186 twoGrid(h, u, f, L) on caller buffers == the oracle's mgo_two_grid."""
     import ctypes
@@ -438,6 +462,53 @@ def test_two_grid_host_buffers():
     u_ref = u.copy()
     assert olib.mgo_two_grid(o.h, ctypes.c_double(2.0 / n), u_ref.ctypes.data, f.ctypes.data, 16) == 0
     assert np.array_equal(u_gpu, u_ref)
+
+
+@pytest.mark.parametrize("kw", [
+    dict(dim=2, n=(256, 256, 1), real="double"),
+    dict(dim=3, n=(64, 64, 64), real="float", smoother="rbgs", nu1=2, nu2=2, prolong="linear", coarse_bc="consistent"),
+], ids=["2d-jacobi", "3d-rbgs"])
+def test_coarse_level_switch_is_exact(kw):
+    """cpuDepth's MI355X form: moving the coarse-engine switch changes nothing in the results."""
+    runs = []
+    for size in (0, 16, 8, 4):
+        ctx = _ctx(**kw)
+        ctx.set_coarse_level(size)
+        if size:
+            assert [lv["nx"] for lv in ctx.levels if lv["tail"]][0] == size or not any(lv["tail"] for lv in ctx.levels)
+        ctx.init_point_charge()
+        runs.append((ctx.cycles(3), ctx.get_psi()))
+    for e, p in runs[1:]:
+        assert np.array_equal(p, runs[0][1]) and np.array_equal(e, runs[0][0])
+
+
+@pytest.mark.parametrize("init", ["fresh", "warm"])
+def test_hybrid_handoff_to_reference_engine(init):
+    """cpu-gpu.lua:17-52: the GPU runs the fine levels and hands level 16 (u, f) to another engine's
+    twoGrid (here the C restatement of cpu-raw.lua's twoGrid) and back; psi == the all-GPU cycle."""
+    import ctypes
+
+    from oracle_lib import lib as olib
+
+    kw = dict(dim=2, n=_n3(2, 64), real="double", coarse_init=init)
+    a, b = _ctx(**kw), _ctx(**kw)
+    o = Oracle(dim=2, n=_n3(2, 64), real="double", coarse_init=init)
+    calls = []
+
+    def engine(h, u, f, size):
+        calls.append(size)
+        assert olib.mgo_two_grid(o.h, ctypes.c_double(h), u.ctypes.data, f.ctypes.data, size) == 0
+
+    a.set_coarse_handoff(16, engine)
+    a.init_point_charge()
+    b.init_point_charge()
+    for _ in range(3):
+        ea, eb = a.cycle(), b.cycle()
+        assert np.array_equal(a.get_psi(), b.get_psi())
+        assert abs(ea - eb) <= 1e-12 * abs(eb)
+    assert calls == [16, 16, 16]
+    a.set_coarse_handoff(16, None)
+    a.cycle()
 
 
 def test_solver_protocol_cpu_lua():
