@@ -111,8 +111,8 @@ struct Level {
     char* t = nullptr;      // second u buffer (Jacobi ping-pong; level 0: keeps psiOld during a cycle)
     bool ghost_ok = true;   // u's ghost planes hold the neighbours' current planes
     bool fghost_ok = true;  // f's ghost planes likewise
-    bool fused = false;     // smoothing phases run temporally blocked (k_fused); needs t
-    int zc = 0;             // k_fused z-chunk (planes per workgroup)
+    bool fused = false;     // smoothing phases run temporally blocked (k_zs); needs t
+    int zc = 0;             // k_zs z-chunk (planes per workgroup)
 };
 
 // Loopback transport (tests): the ranks of a slab decomposition as contexts of one process on

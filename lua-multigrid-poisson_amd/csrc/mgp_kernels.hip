@@ -662,7 +662,7 @@ __device__ __forceinline__ void coarse_row(const T* __restrict__ V, const Geo& g
     const T* hp = V + row + pc * gc.H;        // colour of I0, I0+2, ...
     const T* hq = V + row + (pc ^ 1) * gc.H;  // colour of I0+1, I0+3, ...
     const int cm = I0 >> 1;
-    if (N == 4) {
+    if constexpr (N == 4) {
         const Vec<T, 2> a = vload<T, 2>(hp + cm);
         const Vec<T, 2> b = vload<T, 2>(hq + cm);
         c[1] = a.v[0];
@@ -777,80 +777,46 @@ __global__ __launch_bounds__(kBlock) void k_prolong_v(T* __restrict__ u, const T
     }
 }
 
-// ---- temporally blocked smoothing (3D, red/black, replicated level) --------------------------
+// ---- z-streamed temporally blocked smoothing (3D, red/black 2+2) -------------------------------
 //
-// The unfused cycle moves every fine cell through HBM once per half-sweep: 2+2 RB-GS plus the
-// residual/restriction and prolongation/correction passes cost (4 x 1.5 + 2.125 + 2.125 + 1) reals
-// per cell.  k_fused streams a z-slab of one x-y tile through a ring of packed planes in LDS and
-// applies ALL the half-sweeps of a smoothing phase to each plane as it passes, in wavefront order:
-// at step p plane p is loaded (PRE) or loaded and corrected by the prolongation (POST), half-sweep
-// k runs on plane p - k, and the last stage (PRE: residual + restriction, POST: store + err) on
-// plane p - NST.  Stage k only trusts rows that lie k rows inside the extended tile, so the tile
-// carries a y/z halo of NST planes/rows and an x halo of 8 cells; halo cells are recomputed by
-// every tile that needs them.  HBM traffic per cell drops to read u, f, write u (+ R) for PRE and
-// read u, V, f, psiOld, write u for POST.  The arithmetic of every cell is the unfused kernels'
-// (same expressions, same order), so results are bit-identical.
-//
-// Thread layout per stage: one item = N consecutive same-colour cells of one LDS row (16 bytes),
-// as in k_half; rows of the plane ring are laid out like a global packed plane (two colour
-// halves, HWE cells per half-row), so every neighbour access is the global one re-based.
-
-template <typename T>
-struct FusedTile;
-template <>
-struct FusedTile<float> {
-    static constexpr int TX = 64, TY = 32;
-};
-template <>
-struct FusedTile<double> {
-    static constexpr int TX = 32, TY = 16;
-};
-constexpr int kFusedThreads = 512;
-constexpr int kFusedHX = 8;  // x halo (cells): >= NST, and keeps the tile's x origin 16-byte aligned
-
-// Stage k = 1 .. 2 NS (half-sweep k) runs on plane p - (2k - 1) at step p and the last stage
-// (PRE: residual + restriction, POST: store + err) on plane p - LAST: the stages of one step touch
-// disjoint planes whose inputs were finished in earlier steps, so a step needs just two barriers
-// (after the load, after the stages).
-template <typename T, int NS, bool PRE>
-struct FusedShape {
-    static constexpr int N = VN<T>::n;
-    static constexpr int TX = FusedTile<T>::TX, TY = FusedTile<T>::TY;
-    static constexpr int H = 2 * NS + (PRE ? 1 : 0);    // y and z halo: stages that read neighbours
-    static constexpr int LAST = 4 * NS + 1;             // lag of the last stage
-    static constexpr int XE = TX + 2 * kFusedHX;
-    static constexpr int HWE = XE / 2;                  // cells per LDS half-row
-    static constexpr int G = HWE / N;                   // vector groups per LDS half-row
-    static constexpr int YE = TY + 2 * H;
-    static constexpr int RU = LAST + 2;                 // planes in the ring (last reader: LAST + 1)
-    static constexpr int PS = 2 * YE * HWE;             // reals per plane slot
-    static constexpr int OG = TX / 2 / N;               // output groups per half-row (= coarse groups per coarse row)
-    static constexpr size_t lds_bytes = (size_t)RU * PS * sizeof(T);
-    // every phase is at most one item per thread (the prefetch registers rely on it)
-    static_assert(YE * G <= kFusedThreads, "load phase exceeds one item per thread");
-    static_assert(TY * 2 * OG <= kFusedThreads, "output phase exceeds one item per thread");
-    static_assert(H <= kFusedHX, "x halo too small");
-};
-
-template <typename T>
-__device__ __forceinline__ void block_partial_n(double acc, double* partials, int nthreads)
-{
-    __shared__ double red[kFusedThreads];
-    red[threadIdx.x] = acc;
-    __syncthreads();
-    for (int w = nthreads / 2; w > 0; w >>= 1) {
-        if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) partials[blockIdx.x] = red[0];
-}
+// k_zs applies a whole smoothing phase of a level in ONE pass over HBM:
+//   PRE : 2 RB-GS sweeps, then residual + restriction (smooth(l, 2) + residual_restrict(l))
+//   POST: prolongation + correction, then 2 RB-GS sweeps (+ err) (prolong_correct + smooth(l, 2))
+// A workgroup owns an x-y tile (plus a halo of H rows and kZsHX cells per side) and a chunk of zc
+// planes and streams through z.  Every thread owns one column of the extended tile: N consecutive
+// cells of each colour (16 bytes each) of one row.  At step p:
+//   stage 0   plane p of the input's BLACK cells (POST: plus the prolongation, k_prolong_v's
+//             expressions).  Red cells are never loaded: half-sweep 1 overwrites them, and a
+//             Gauss-Seidel update does not read the value it replaces.
+//   stage k   half-sweep k (k = 1..4, red first) on plane p - k.
+//   last      the smoothed plane p - 4 is stored; PRE: residual + restriction of plane p - 5
+//             (k_resrestrict's expressions, children summed in the reference order, the odd row's
+//             residuals handed to the even row through LDS); POST: (psi - psiOld)^2 partials.
+// The z-neighbours of stage k's inputs are the thread's own registers (a window of 3-4 planes per
+// stage).  The in-plane neighbours come from LDS, where every stage leaves the plane it computed
+// (2-3 slots per stage: stage k reads the plane stage k-1 wrote one step earlier), and x-edges
+// from the neighbouring lane (DPP; LDS at wave boundaries), so a step needs one barrier.  Cells
+// outside the box stay 0 at every stage (the Dirichlet ghost); halo cells are recomputed by every
+// tile that needs them (the trapezoid shrinks by one cell per stage).  On a slab-distributed
+// level the z-halo comes from H ghost planes per side (u: black cells, f).  HBM traffic per cell:
+// PRE reads black u and f and writes u and R/8 (2.625 reals), POST reads black u, V/8, f and
+// psiOld and writes u (3.625 reals), against 8.125 and 9.125 for the launch-per-piece path.
 
 // Workgroup barrier for LDS hand-offs only: waits for this wave's LDS operations, not for its
 // outstanding global loads (the next step's prefetch stays in flight across the barrier).
 __device__ __forceinline__ void lds_barrier()
 {
+#ifdef ZS_NOBAR  // timing experiment only: results are wrong
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#else
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+#endif
 }
+#ifdef ZS_NOLOAD  // timing experiment only: every plane reads plane 0 (cache-resident)
+#define ZS_PLANE(q) 0
+#else
+#define ZS_PLANE(q) (q)
+#endif
 
 // Lane i <- lane i - 1 (shr) / lane i + 1 (shl) across the whole wavefront (DPP wave_shr:1 /
 // wave_shl:1, GFX9 encodings); the edge lanes receive 0 and are patched by the caller.
@@ -871,40 +837,230 @@ __device__ __forceinline__ double dpp_shl1(double v)
     return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
 }
 
-// Global operands of one z-step for this thread, loaded one step ahead.
-template <typename T, int NS>
-struct FusedPrefetch {
+template <typename T>
+struct ZsTile;
+template <>
+struct ZsTile<float> {
+    static constexpr int TX = 64, TY = 32;
+};
+template <>
+struct ZsTile<double> {
+    static constexpr int TX = 64, TY = 16;
+};
+constexpr int kZsHX = 8;  // x halo cells per side (>= the trapezoid depth, whole 16-byte groups)
+
+template <typename T, bool PRE>
+struct ZsShape {
     static constexpr int N = VN<T>::n;
-    static constexpr int W = N > 1 ? N / 2 : 1;  // residual item width (coarse cells)
-    Vec<T, N> u0, u1;                                  // stage 0: the plane's u, both colours
-    T c00[N + 2], c10[N + 2], c01[N + 2], c11[N + 2];  // stage 0 (POST): coarse rows for P V
-    Vec<T, N> fk[2 * NS];                              // f of the half-sweep items
-    T fr[2][2][W];                                     // f of the residual item: [row dy][colour][e]
-    Vec<T, N> old;                                     // psiOld of the output item (POST, ERR)
+    static constexpr int TX = ZsTile<T>::TX, TY = ZsTile<T>::TY;
+    static constexpr int H = PRE ? 5 : 4;              // y/z halo = stages that read neighbours
+    static constexpr int HWE = (TX + 2 * kZsHX) / 2;   // reals per LDS half-row
+    static constexpr int G = HWE / N;                  // column groups per row
+    static constexpr int HXG = kZsHX / 2 / N;          // halo groups per side
+    static constexpr int YE = TY + 2 * H;
+    static constexpr int NT = G * YE;                  // threads with a column
+    static constexpr int NTL = (NT + 63) / 64 * 64;    // launched threads
+    static constexpr int SLOT = YE * HWE;              // reals per LDS slot (one colour of a plane)
+    static constexpr int NS3 = PRE ? 3 : 2;            // stage-3 slots (PRE's residual reads 2 back)
+    static constexpr int OFF1 = 2 * SLOT, OFF2 = 4 * SLOT, OFF3 = 6 * SLOT, OFF4 = OFF3 + NS3 * SLOT;
+    static constexpr int OFFX = OFF4 + (PRE ? 2 * SLOT : 0);
+    static constexpr int XPAIRS = YE / 2 + 1;          // row pairs of the residual hand-off
+    static constexpr int XSLOT = PRE ? XPAIRS * G * 2 * N : 0;
+    static constexpr size_t lds_bytes = (size_t)(OFFX + 2 * XSLOT) * sizeof(T);
+    static_assert(NTL <= 1024, "too many threads");
+    static_assert(2 * N * HXG >= H, "x halo too small");
+    static_assert(HWE % N == 0, "LDS row must hold whole groups");
 };
 
-// src: the level's u before the phase; dst: the phase's output (POST with ERR reads psiOld from
-// dst first).  V/gc: coarse correction (POST); R/gc: restricted residual (PRE).  zc: planes per
-// z-chunk.  CLZ: the level operator has no boundary modification (cl == 0, e.g. level 0).
-template <typename T, int NS, bool PRE, int LINEAR, bool ERR, bool CLZ>
-__global__ __launch_bounds__(kFusedThreads) void k_fused(const T* __restrict__ src, const T* __restrict__ f,
-                                                         T* __restrict__ dst, T* __restrict__ R,
-                                                         const T* __restrict__ V, double* __restrict__ partials,
-                                                         Geo g, Geo gc, Op<T, 3> op, T clc, int zc)
+template <typename T, int N>
+struct ZsPrefetch {
+    Vec<T, N> u;                                       // stage 0: black cells of the input at plane p
+    T c00[N + 2], c10[N + 2], c01[N + 2], c11[N + 2];  // POST: coarse rows of P V at plane p
+    Vec<T, N> fk[4];                                   // f of half-sweep k at plane p - k
+    Vec<T, N> old0, old1;                              // POST + ERR: psiOld at plane p - 4
+};
+
+struct ZsCol {
+    int lrow, lym, lyp, lane, gm;
+    bool x_first, x_last;
+};
+
+// In-plane operands of one stage's cells: the other colour in the rows above / below and the x
+// neighbours beyond my group (last cell of the left group, first of the right group).  Stage k
+// reads them from the LDS slot stage k-1 filled one step earlier, so a step issues all its LDS
+// reads up front.
+template <typename T, int N>
+struct ZsNb {
+    Vec<T, N> yl, yr;
+    T ep, en;
+};
+
+template <typename T, int N>
+__device__ __forceinline__ void zs_nb_load(ZsNb<T, N>& nb, const T* s_in, const ZsCol& c)
 {
-    using S = FusedShape<T, NS, PRE>;
-    constexpr int N = S::N, H = S::H, LAST = S::LAST, HWE = S::HWE, G = S::G, YE = S::YE, RU = S::RU,
-                  PS = S::PS, TX = S::TX, TY = S::TY, OG = S::OG;
-    constexpr int W = FusedPrefetch<T, NS>::W;
-    constexpr int RG = TX / 2 / W;  // residual items per coarse row
-    // POST: step p also writes plane p + 1 (its slot holds plane p - LAST - 1, which no stage of
-    // step p reads), so one barrier per step suffices; PRE's residual still reads that plane.
-    constexpr bool MERGE = !PRE;
-    static_assert(!MERGE || RU >= LAST + 2, "ring too small for the merged load");
-    constexpr int CH = YE * HWE;    // reals per colour half of a plane slot
-    static_assert((TY / 2) * RG <= kFusedThreads, "residual phase exceeds one item per thread");
-    extern __shared__ __align__(16) unsigned char fused_smem[];
-    T* const ring = reinterpret_cast<T*>(fused_smem);
+    nb.yl = vload<T, N>(s_in + c.lym);
+    nb.yr = vload<T, N>(s_in + c.lyp);
+    // lanes at a wave boundary take their x-edge from LDS, the others from the neighbouring lane
+    nb.ep = (c.lane == 0 && !c.x_first) ? s_in[c.lrow - 1] : (T)0;
+    nb.en = (c.lane == 63 && !c.x_last) ? s_in[c.lrow + N] : (T)0;
+}
+
+// cen: the other colour of my own row (the plane the neighbouring lanes hold too)
+template <typename T, int N>
+__device__ __forceinline__ void zs_nb_edges(ZsNb<T, N>& nb, const Vec<T, N>& cen, const ZsCol& c)
+{
+    const T dl = dpp_shr1(cen.v[N - 1]), dr = dpp_shl1(cen.v[0]);
+    if (c.lane != 0) nb.ep = dl;
+    if (c.lane != 63) nb.en = dr;
+    if (c.x_first) nb.ep = (T)0;
+    if (c.x_last) nb.en = (T)0;
+}
+
+// xl + xr of my N cells of x parity o (IEEE addition commutes, so the pair sums are shared
+// between the two parities)
+template <typename T, int N>
+__device__ __forceinline__ void zs_xsum(const Vec<T, N>& cen, const ZsNb<T, N>& nb, int o, T (&s)[N])
+{
+    const T edge = o == 0 ? nb.ep : nb.en;
+    T m[N + 1];
+    m[0] = edge + cen.v[0];
+#pragma unroll
+    for (int e = 0; e + 1 < N; ++e) m[e + 1] = cen.v[e] + cen.v[e + 1];
+    m[N] = cen.v[N - 1] + edge;
+#pragma unroll
+    for (int e = 0; e < N; ++e) s[e] = o == 0 ? m[e] : m[e + 1];
+}
+
+// One half-sweep of my N cells of one colour (x parity o) from the other colour's window
+// (zl, cen, zr) and its in-plane operands: k_half's expressions.
+template <typename T, int N, bool CLZ>
+__device__ __forceinline__ Vec<T, N> zs_relax(const Vec<T, N>& zl, const Vec<T, N>& cen, const Vec<T, N>& zr,
+                                              const ZsNb<T, N>& nb, const Vec<T, N>& fv, const ZsCol& c, int o,
+                                              int nbyz, int nx, const Op<T, 3>& op)
+{
+    T s[N];
+    zs_xsum<T, N>(cen, nb, o, s);
+    Vec<T, N> out;
+#pragma unroll
+    for (int e = 0; e < N; ++e) {
+        T t = s[e] + nb.yl.v[e];
+        t = t + nb.yr.v[e];
+        t = t + zl.v[e];
+        t = t + zr.v[e];
+        if (CLZ) {
+            out.v[e] = div_rn(fv.v[e] - t * op.inv_hSq, op.adiag, op.yadiag);
+        } else {
+            const int i = 2 * (c.gm + e) + o;
+            out.v[e] = op.relax(t, fv.v[e], nbyz + (i == 0) + (i == nx - 1));
+        }
+    }
+    return out;
+}
+
+// Residual of my N cells of one colour (x parity o) at one plane: k_resrestrict's expressions.
+template <typename T, int N, bool CLZ>
+__device__ __forceinline__ void zs_residual(const Vec<T, N>& zl, const Vec<T, N>& cen, const Vec<T, N>& zr,
+                                            const ZsNb<T, N>& nb, const Vec<T, N>& uc, const Vec<T, N>& fv,
+                                            const ZsCol& c, int o, int nbyz, int nx, const Op<T, 3>& op, T (&rr)[N])
+{
+    T s[N];
+    zs_xsum<T, N>(cen, nb, o, s);
+#pragma unroll
+    for (int e = 0; e < N; ++e) {
+        T t = s[e] + nb.yl.v[e];
+        t = t + nb.yr.v[e];
+        t = t + zl.v[e];
+        t = t + zr.v[e];
+        if (CLZ) {
+            const T askew = t * op.inv_hSq;
+            const T a_u = askew + op.adiag * uc.v[e];
+            rr[e] = fv.v[e] - a_u;
+        } else {
+            const int i = 2 * (c.gm + e) + o;
+            rr[e] = op.residual(t, fv.v[e], uc.v[e], nbyz + (i == 0) + (i == nx - 1));
+        }
+    }
+}
+
+// uv += P V for my N cells of x parity o in one fine row (k_prolong_v's expressions).
+template <typename T, int N, int LINEAR>
+__device__ __forceinline__ void zs_correct(Vec<T, N>& uv, const ZsPrefetch<T, N>& cur, int o, int I0, int cx, bool oy,
+                                           bool oz, T cl)
+{
+    const T w0 = (T)0.75, w1 = (T)0.25;
+    auto sv = [&](T val, bool fx, bool fy, bool fz) {
+        T s = (T)1;
+        if (fx) s = -cl * s;
+        if (fy) s = -cl * s;
+        if (fz) s = -cl * s;
+        return s == (T)1 ? val : s * val;
+    };
+    const bool interior = !oy && !oz && I0 > 0 && I0 + N < cx;
+#pragma unroll
+    for (int e = 0; e < N; ++e) {
+        const int pe = e + 1;
+        T v;
+        if (!LINEAR) {
+            v = cur.c00[pe];
+        } else if (interior) {
+            const T nb00 = o ? cur.c00[e + 2] : cur.c00[e];
+            const T nb10 = o ? cur.c10[e + 2] : cur.c10[e];
+            const T nb01 = o ? cur.c01[e + 2] : cur.c01[e];
+            const T nb11 = o ? cur.c11[e + 2] : cur.c11[e];
+            const T a00 = w0 * cur.c00[pe] + w1 * nb00;
+            const T a10 = w0 * cur.c10[pe] + w1 * nb10;
+            const T a01 = w0 * cur.c01[pe] + w1 * nb01;
+            const T a11 = w0 * cur.c11[pe] + w1 * nb11;
+            const T b0 = w0 * a00 + w1 * a10;
+            const T b1 = w0 * a01 + w1 * a11;
+            v = w0 * b0 + w1 * b1;
+        } else {
+            const bool ox = (o == 0 && I0 + e == 0) || (o == 1 && I0 + e == cx - 1);
+            auto col = [&](const T (&cc)[N + 2]) { return ox ? cc[pe] : (o ? cc[e + 2] : cc[e]); };
+            const T a00 = w0 * cur.c00[pe] + w1 * sv(col(cur.c00), ox, false, false);
+            const T a10 = w0 * sv(cur.c10[pe], false, oy, false) + w1 * sv(col(cur.c10), ox, oy, false);
+            const T a01 = w0 * sv(cur.c01[pe], false, false, oz) + w1 * sv(col(cur.c01), ox, false, oz);
+            const T a11 = w0 * sv(cur.c11[pe], false, oy, oz) + w1 * sv(col(cur.c11), ox, oy, oz);
+            const T b0 = w0 * a00 + w1 * a10;
+            const T b1 = w0 * a01 + w1 * a11;
+            v = w0 * b0 + w1 * b1;
+        }
+        uv.v[e] = uv.v[e] + v;
+    }
+}
+
+// Fixed-order workgroup sum of one double per thread (NTL threads, any count <= 1024).
+template <int NTL>
+__device__ __forceinline__ void block_partial_t(double acc, double* partials)
+{
+    __shared__ double red[NTL];
+    red[threadIdx.x] = acc;
+    __syncthreads();
+    for (int w = 512; w > 0; w >>= 1) {
+        if ((int)threadIdx.x < w && (int)threadIdx.x + w < NTL) red[threadIdx.x] += red[threadIdx.x + w];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) partials[blockIdx.x] = red[0];
+}
+
+// src: the level's u before the phase; dst: the phase's output (POST with ERR reads psiOld from
+// dst first).  V/gc: coarse correction (POST); R/gc: restricted residual (PRE); both point at the
+// coarse plane of local fine plane 0 (gc.z0 = g.z0 / 2).  zc: planes per z-chunk.  On a
+// distributed level, src and f must hold H current ghost planes per side.  CLZ: the level operator
+// has no boundary modification (cl == 0, e.g. level 0).
+template <typename T, bool PRE, int LINEAR, bool ERR, bool CLZ>
+__global__ __launch_bounds__((ZsShape<T, PRE>::NTL)) void k_zs(const T* __restrict__ src, const T* __restrict__ f,
+                                                                T* __restrict__ dst, T* __restrict__ R,
+                                                                const T* __restrict__ V, double* __restrict__ partials,
+                                                                Geo g, Geo gc, Op<T, 3> op, T clc, int zc)
+{
+    using S = ZsShape<T, PRE>;
+    constexpr int N = S::N, H = S::H, HWE = S::HWE, G = S::G, YE = S::YE, SLOT = S::SLOT, TX = S::TX,
+                  TY = S::TY, NS3 = S::NS3, NTL = S::NTL;
+    using VT = Vec<T, N>;
+    using PF = ZsPrefetch<T, N>;
+    extern __shared__ __align__(16) unsigned char zs_smem[];
+    T* const lds = reinterpret_cast<T*>(zs_smem);
     const int tid = threadIdx.x;
 
     const int tiles_x = g.nx / TX, tiles_y = g.ny / TY;
@@ -912,343 +1068,248 @@ __global__ __launch_bounds__(kFusedThreads) void k_fused(const T* __restrict__ s
     const int tile = b % (tiles_x * tiles_y);
     const int Z0 = (b / (tiles_x * tiles_y)) * zc;
     const int X0 = (tile % tiles_x) * TX, Y0 = (tile / tiles_x) * TY;
-    const int YS = Y0 - H;               // global row of LDS row 0
-    const int MS = (X0 - kFusedHX) / 2;  // global packed m of LDS m = 0
-    const int nz = (int)g.nz;
-    const int hw = g.hw;
-    const int Hh = (int)g.H;
-    auto plane = [&](int q) { return (int64_t)q * g.P; };
-    // ring slot of plane q (q >= -RU)
-    auto slot = [&](int q) { return ring + ((q + 4 * RU) % RU) * PS; };
-    auto zrange = [&](int q, int k) {  // plane q gets half-sweep k
-        return q >= 0 && q < nz && q >= Z0 - (H - k) && q <= Z0 + zc - 1 + (H - k);
+    const int hw = g.hw, Hh = (int)g.H;
+    const int z0 = (int)g.z0, gnz = (int)g.gnz, cz0 = (int)gc.z0;
+    const int64_t P = g.P;
+
+    // my column of the extended tile
+    const bool on = tid < S::NT;
+    const int gx = on ? tid % G : 0, ye = on ? tid / G : 0;
+    const int gy = Y0 - H + ye;
+    const int m0 = gx * N;
+    ZsCol col;
+    col.lrow = ye * HWE + m0;
+    col.lym = (ye > 0 ? ye - 1 : ye) * HWE + m0;
+    col.lyp = (ye < YE - 1 ? ye + 1 : ye) * HWE + m0;
+    col.lane = tid & 63;
+    col.gm = (X0 - kZsHX) / 2 + m0;  // global packed m of my first cell
+    col.x_first = gx == 0;
+    col.x_last = gx == G - 1;
+    const bool in_xy = on && gy >= 0 && gy < g.ny && col.gm >= 0 && col.gm < hw;
+    const int goff = in_xy ? gy * hw + col.gm : 0;  // in-plane offset (nx * ny < 2^31)
+    const bool tile_xy = on && ye >= H && ye < H + TY && gx >= S::HXG && gx < G - S::HXG;
+    const int zlo = Z0 - H, zhi = Z0 + zc - 1 + H;  // local planes stage 0 must cover
+    const int p_end = Z0 + zc + (PRE ? 5 : 3);
+    auto inz = [&](int q) { return z0 + q >= 0 && z0 + q < gnz; };  // inside the global box
+    // stage k (0..4) matters on planes [zlo + k, zhi - k]
+    auto live = [&](int q, int k) { return inz(q) && q >= zlo + k && q <= zhi - k; };
+    auto slot = [&](int off, int ns, int q) { return lds + off + ((q + 64 * ns) % ns) * SLOT; };
+    auto nbyz = [&](int q) {
+        return CLZ ? 0 : (gy == 0) + (gy == g.ny - 1) + (z0 + q == 0) + (z0 + q == gnz - 1);
     };
-    const int p_first = Z0 - H, p_last = Z0 + zc - 1 + LAST;
+    auto par = [&](int q) { return (gy + z0 + q) & 1; };
+    const T* const src_black = src + Hh;
 
-    // ---- per-thread geometry, fixed for the whole stream ----
-    // load item: LDS row l_ye, group l_m0 (both colours)
-    const int l_ye = tid / G, l_m0 = (tid % G) * N;
-    const int l_gy = YS + l_ye, l_gm = MS + l_m0;
-    const bool l_on = tid < YE * G;
-    const bool l_xy = l_on && l_gy >= 0 && l_gy < g.ny && l_gm >= 0 && 2 * l_gm < g.nx;
-    const int l_g = l_gy * hw + l_gm;  // in-plane offset, colour 0
-    const int l_s = l_ye * HWE + l_m0;
-    // half-sweep item of stage k: LDS row k + tid / G, same group for every stage
-    const int s_m0 = (tid % G) * N, s_gm = MS + s_m0;
-    const bool s_x = s_gm >= 0 && 2 * s_gm < g.nx;
-    const bool s_lo = s_m0 > 0, s_hi = s_m0 + N < HWE;
-    // residual item: coarse row r_jt, W coarse cells from r_m0 (LDS m of the fine cells)
-    const int r_jt = tid / RG, r_m0 = kFusedHX / 2 + (tid % RG) * W;
-    const bool r_on = PRE && tid < (TY / 2) * RG;
-    const int r_gm = MS + r_m0;
-    // output item
-    const int o_r = tid / (2 * OG), o_c = (tid / OG) & 1, o_m0 = kFusedHX / 2 + (tid % OG) * N;
-    const bool o_on = tid < TY * 2 * OG;
-    const int o_g = o_c * Hh + (Y0 + o_r) * hw + MS + o_m0;
-    const int o_s = o_c * CH + (H + o_r) * HWE + o_m0;
+    for (int i = tid; i < (int)(S::lds_bytes / sizeof(T)); i += NTL) lds[i] = (T)0;
+    __syncthreads();
 
-    auto prefetch = [&](FusedPrefetch<T, NS>& r, int p) {
-        r.u0 = vzero<T, N>();
-        r.u1 = vzero<T, N>();
-        const int lp = MERGE ? p + 1 : p;  // the plane stage 0 of step p writes
-        if (l_xy && lp >= 0 && lp < nz && lp <= Z0 + zc - 1 + H) {
-            const T* sp = src + plane(lp);
-            r.u0 = vload<T, N>(sp + l_g);
-            r.u1 = vload<T, N>(sp + Hh + l_g);
+    auto prefetch = [&](PF& r, int p) {
+        r.u = vzero<T, N>();
+        if (in_xy && live(p, 0)) {
+            r.u = vload<T, N>(src_black + (int64_t)ZS_PLANE(p) * P + goff);
             if (!PRE) {
-                const int J = l_gy >> 1, K = lp >> 1;
-                int Jn = (l_gy & 1) ? J + 1 : J - 1;
+                const int J = gy >> 1, K = (z0 + p) >> 1;  // global coarse row / plane
+                int Jn = (gy & 1) ? J + 1 : J - 1;
                 if (Jn < 0 || Jn >= gc.ny) Jn = J;
-                int Kn = (lp & 1) ? K + 1 : K - 1;
+                int Kn = ((z0 + p) & 1) ? K + 1 : K - 1;
                 if (Kn < 0 || Kn >= gc.gnz) Kn = K;
-                coarse_row<T, N>(V, gc, J, K, l_gm, r.c00);
+                coarse_row<T, N>(V, gc, J, K - cz0, col.gm, r.c00);
                 if (LINEAR) {
-                    coarse_row<T, N>(V, gc, Jn, K, l_gm, r.c10);
-                    coarse_row<T, N>(V, gc, J, Kn, l_gm, r.c01);
-                    coarse_row<T, N>(V, gc, Jn, Kn, l_gm, r.c11);
+                    coarse_row<T, N>(V, gc, Jn, K - cz0, col.gm, r.c10);
+                    coarse_row<T, N>(V, gc, J, Kn - cz0, col.gm, r.c01);
+                    coarse_row<T, N>(V, gc, Jn, Kn - cz0, col.gm, r.c11);
                 }
             }
         }
 #pragma unroll
-        for (int k = 1; k <= 2 * NS; ++k) {
-            r.fk[k - 1] = vzero<T, N>();
-            const int q = p - (2 * k - 1);
-            const int gy = YS + k + tid / G;
-            if (zrange(q, k) && tid < (YE - 2 * k) * G && s_x && gy >= 0 && gy < g.ny)
-                r.fk[k - 1] = vload<T, N>(f + plane(q) + ((k - 1) & 1) * Hh + gy * hw + s_gm);
+        for (int k = 1; k <= 4; ++k) {
+            const int q = p - k;
+            const T* fp = f + (int64_t)ZS_PLANE(q) * P + ((k - 1) & 1) * Hh;
+            r.fk[k - 1] = (in_xy && live(q, k)) ? vload<T, N>(fp + goff) : vzero<T, N>();
         }
-        const int q = p - LAST;
-        const bool last = q >= Z0 && q < Z0 + zc;
-        if (PRE) {
-#pragma unroll
-            for (int dy = 0; dy < 2; ++dy)
-#pragma unroll
-                for (int c = 0; c < 2; ++c) {
-                    if (r_on && last) {
-                        const T* fp = f + plane(q) + c * Hh + (Y0 + 2 * r_jt + dy) * hw + r_gm;
-                        if (W == 2) {
-                            const Vec<T, 2> v = vload<T, 2>(fp);
-                            r.fr[dy][c][0] = v.v[0];
-                            r.fr[dy][c][W - 1] = v.v[1];
-                        } else {
-#pragma unroll
-                            for (int e = 0; e < W; ++e) r.fr[dy][c][e] = fp[e];
-                        }
-                    } else {
-#pragma unroll
-                        for (int e = 0; e < W; ++e) r.fr[dy][c][e] = (T)0;
-                    }
-                }
-        }
-        if (ERR) {
-            r.old = vzero<T, N>();
-            if (last && o_on) r.old = vload<T, N>(dst + plane(q) + o_g);
+        if (!PRE && ERR) {
+            const int q = p - 4;
+            r.old0 = vzero<T, N>();
+            r.old1 = vzero<T, N>();
+            if (tile_xy && q >= Z0 && q < Z0 + zc) {
+                const T* dp = dst + (int64_t)q * P;
+                r.old0 = vload<T, N>(dp + goff);
+                r.old1 = vload<T, N>(dp + Hh + goff);
+            }
         }
     };
 
-    T acc[W];  // PRE: running restriction sums of this thread's coarse cells
+    const VT vz = vzero<T, N>();
+    VT w0a = vz, w0b = vz, w0c = vz;             // A0 black at p-2, p-1, p
+    VT w1a = vz, w1b = vz, w1c = vz;             // A1 red   at p-3, p-2, p-1
+    VT w2a = vz, w2b = vz, w2c = vz;             // A2 black at p-4, p-3, p-2
+    VT w3a = vz, w3b = vz, w3c = vz, w3d = vz;   // A3 red   at p-6, p-5, p-4, p-3
+    VT w4a = vz, w4b = vz, w4c = vz;             // A4 black at p-6, p-5, p-4
+    VT f3_1 = vz, f3_2 = vz, f4_1 = vz;          // PRE: f of stages 3 / 4 one and two steps back
+    T acc[N];
 #pragma unroll
-    for (int e = 0; e < W; ++e) acc[e] = (T)0;
+    for (int e = 0; e < N; ++e) acc[e] = (T)0;
     double err = 0.0;
+    const bool even_row = (gy & 1) == 0;
+    T* const xbase = lds + S::OFFX + (((ye + (H & 1)) >> 1) * G + gx) * 2 * N;
+    auto xs = [&](int q) { return xbase + (q & 1) * (S::XPAIRS * G * 2 * N); };
 
-    // stage 0: plane lp into the ring (POST: u + P V, k_prolong_v's expressions)
-    auto stage0 = [&](const FusedPrefetch<T, NS>& cur, int lp) {
-            if (l_on) {
-                Vec<T, N> v0 = cur.u0, v1 = cur.u1;
-                if (!PRE && l_xy && lp >= 0 && lp < nz && lp <= Z0 + zc - 1 + H) {
-                    const int I0 = l_gm, cx = gc.nx;
-                    const int J = l_gy >> 1, K = lp >> 1;
-                    const int Jn = (l_gy & 1) ? J + 1 : J - 1;
-                    const bool oy = Jn < 0 || Jn >= gc.ny;
-                    const int Kn = (lp & 1) ? K + 1 : K - 1;
-                    const bool oz = Kn < 0 || Kn >= gc.gnz;
-                    const T w0 = (T)0.75, w1 = (T)0.25, cl = clc;
-                    auto sv = [&](T val, bool fx, bool fy, bool fz) {
-                        T s = (T)1;
-                        if (fx) s = -cl * s;
-                        if (fy) s = -cl * s;
-                        if (fz) s = -cl * s;
-                        return s == (T)1 ? val : s * val;
-                    };
-                    const int pp = (l_gy + lp) & 1;
-                    const bool interior = !oy && !oz && I0 > 0 && I0 + N < cx;
-    #pragma unroll
-                    for (int c = 0; c < 2; ++c) {
-                        const int o = c ^ pp;
-                        Vec<T, N>& uv = c ? v1 : v0;
-    #pragma unroll
-                        for (int e = 0; e < N; ++e) {
-                            const int pe = e + 1;
-                            T v;
-                            if (!LINEAR) {
-                                v = cur.c00[pe];
-                            } else if (interior) {
-                                const T nb00 = o ? cur.c00[e + 2] : cur.c00[e];
-                                const T nb10 = o ? cur.c10[e + 2] : cur.c10[e];
-                                const T nb01 = o ? cur.c01[e + 2] : cur.c01[e];
-                                const T nb11 = o ? cur.c11[e + 2] : cur.c11[e];
-                                const T a00 = w0 * cur.c00[pe] + w1 * nb00;
-                                const T a10 = w0 * cur.c10[pe] + w1 * nb10;
-                                const T a01 = w0 * cur.c01[pe] + w1 * nb01;
-                                const T a11 = w0 * cur.c11[pe] + w1 * nb11;
-                                const T b0 = w0 * a00 + w1 * a10;
-                                const T b1 = w0 * a01 + w1 * a11;
-                                v = w0 * b0 + w1 * b1;
-                            } else {
-                                const bool ox = (o == 0 && I0 + e == 0) || (o == 1 && I0 + e == cx - 1);
-                                auto col = [&](const T (&cc)[N + 2]) { return ox ? cc[pe] : (o ? cc[e + 2] : cc[e]); };
-                                const T a00 = w0 * cur.c00[pe] + w1 * sv(col(cur.c00), ox, false, false);
-                                const T a10 = w0 * sv(cur.c10[pe], false, oy, false) + w1 * sv(col(cur.c10), ox, oy, false);
-                                const T a01 = w0 * sv(cur.c01[pe], false, false, oz) + w1 * sv(col(cur.c01), ox, false, oz);
-                                const T a11 = w0 * sv(cur.c11[pe], false, oy, oz) + w1 * sv(col(cur.c11), ox, oy, oz);
-                                const T b0 = w0 * a00 + w1 * a10;
-                                const T b1 = w0 * a01 + w1 * a11;
-                                v = w0 * b0 + w1 * b1;
-                            }
-                            uv.v[e] = uv.v[e] + v;
-                        }
-                    }
-                }
-                T* P = slot(lp);
-                vstore<T, N>(P + l_s, v0);
-                vstore<T, N>(P + CH + l_s, v1);
-            }
-    };
+    auto step = [&](const PF& cur, PF& nxt, int p) {
+        if (p < p_end) prefetch(nxt, p + 1);
 
-    auto step = [&](const FusedPrefetch<T, NS>& cur, FusedPrefetch<T, NS>& nxt, int p) {
-        if (p < p_last) prefetch(nxt, p + 1);
-        if (!MERGE) {
-            stage0(cur, p);
-            lds_barrier();
+        // ---- every LDS read of the step (slots filled in the previous step) and the x-edges ----
+        ZsNb<T, N> n1, n2, n3, n4, nr, nk;
+        zs_nb_load<T, N>(n1, slot(0, 2, p - 1), col);
+        zs_nb_load<T, N>(n2, slot(S::OFF1, 2, p - 2), col);
+        zs_nb_load<T, N>(n3, slot(S::OFF2, 2, p - 3), col);
+        zs_nb_load<T, N>(n4, slot(S::OFF3, NS3, p - 4), col);
+        T xr[2 * N];
+        if (PRE) {
+            zs_nb_load<T, N>(nr, slot(S::OFF3, NS3, p - 5), col);  // red of A4 at p - 5
+            zs_nb_load<T, N>(nk, slot(S::OFF4, 2, p - 5), col);    // black of A4 at p - 5
+            const T* x = xs(p - 6);  // the odd row's residuals of plane p - 6 (even rows read them)
+#pragma unroll
+            for (int e = 0; e < 2 * N; ++e) xr[e] = x[e];
+        }
+        // the centres are last step's planes, held by the neighbouring lanes too
+        zs_nb_edges<T, N>(n1, w0c, col);
+        zs_nb_edges<T, N>(n2, w1c, col);
+        zs_nb_edges<T, N>(n3, w2c, col);
+        zs_nb_edges<T, N>(n4, w3d, col);
+        if (PRE) {
+            zs_nb_edges<T, N>(nr, w3c, col);
+            zs_nb_edges<T, N>(nk, w4c, col);
         }
 
-        // ---- stages 1 .. 2 NS: red/black half-sweeps on planes p - (2k - 1), independent ----
-#pragma unroll
-        for (int k = 1; k <= 2 * NS; ++k) {
-            const int q = p - (2 * k - 1);
-            const int c = (k - 1) & 1;  // red first
-            const int ye = k + tid / G;
-            const int gy = YS + ye;
-            if (zrange(q, k) && tid < (YE - 2 * k) * G) {
-                T* P = slot(q);
-                const int oth = (c ^ 1) * CH + ye * HWE + s_m0;
-                const Vec<T, N> cen = vload<T, N>(P + oth);
-                // x-1 of the first cell / x+1 of the last: the neighbouring lane's group in the row
-                const T e_prev = dpp_shr1(cen.v[N - 1]), e_next = dpp_shl1(cen.v[0]);
-                if (s_x && gy >= 0 && gy < g.ny) {
-                const T* Pm = slot(q - 1);
-                const T* Pp = slot(q + 1);
-                const int o = c ^ ((gy + q) & 1);
-                const int own = c * CH + ye * HWE + s_m0;
-                const int lane = tid & 63;
-                T edge;
-                if (o == 0)
-                    edge = s_lo ? (lane != 0 ? e_prev : P[oth - 1]) : (T)0;
-                else
-                    edge = s_hi ? (lane != 63 ? e_next : P[oth + N]) : (T)0;
-                const Vec<T, N> yl = vload<T, N>(P + oth - HWE);  // ye >= 1
-                const Vec<T, N> yr = vload<T, N>(P + oth + HWE);  // ye <= YE - 2
-                const Vec<T, N> zl = vload<T, N>(Pm + oth);
-                const Vec<T, N> zr = vload<T, N>(Pp + oth);
-                const Vec<T, N>& fv = cur.fk[k - 1];
-                int nbyz = 0;
-                if (!CLZ) nbyz = (gy == 0) + (gy == g.ny - 1) + (q == 0) + (q == g.gnz - 1);
-                Vec<T, N> out;
-#pragma unroll
-                for (int e = 0; e < N; ++e) {
-                    const T xl = o == 0 ? (e == 0 ? edge : cen.v[e - 1]) : cen.v[e];
-                    const T xr = o == 0 ? cen.v[e] : (e == N - 1 ? edge : cen.v[e + 1]);
-                    T s = xl + xr;
-                    s = s + yl.v[e];
-                    s = s + yr.v[e];
-                    s = s + zl.v[e];
-                    s = s + zr.v[e];
-                    if (CLZ) {
-                        out.v[e] = div_rn(fv.v[e] - s * op.inv_hSq, op.adiag, op.yadiag);
-                    } else {
-                        const int i = 2 * (s_gm + e) + o;
-                        out.v[e] = op.relax(s, fv.v[e], nbyz + (i == 0) + (i == g.nx - 1));
-                    }
-                }
-                vstore<T, N>(P + own, out);
-                }
-            }
+        // ---- stage 0: black cells of plane p ----
+        VT a0 = cur.u;
+        if (!PRE && in_xy && live(p, 0)) {
+            const int J = gy >> 1, K = (z0 + p) >> 1;
+            const int Jn = (gy & 1) ? J + 1 : J - 1;
+            const int Kn = ((z0 + p) & 1) ? K + 1 : K - 1;
+            zs_correct<T, N, LINEAR>(a0, cur, 1 ^ par(p), col.gm, gc.nx, Jn < 0 || Jn >= gc.ny, Kn < 0 || Kn >= gc.gnz,
+                                     clc);
+        }
+        w0a = w0b;
+        w0b = w0c;
+        w0c = a0;
+
+        // ---- stages 1..4: half-sweep k on plane p - k (red, black, red, black) ----
+        VT o1 = zs_relax<T, N, CLZ>(w0a, w0b, w0c, n1, cur.fk[0], col, par(p - 1), nbyz(p - 1), g.nx, op);
+        if (!(in_xy && inz(p - 1))) o1 = vz;
+        w1a = w1b;
+        w1b = w1c;
+        w1c = o1;
+        VT o2 = zs_relax<T, N, CLZ>(w1a, w1b, w1c, n2, cur.fk[1], col, 1 ^ par(p - 2), nbyz(p - 2), g.nx, op);
+        if (!(in_xy && inz(p - 2))) o2 = vz;
+        w2a = w2b;
+        w2b = w2c;
+        w2c = o2;
+        VT o3 = zs_relax<T, N, CLZ>(w2a, w2b, w2c, n3, cur.fk[2], col, par(p - 3), nbyz(p - 3), g.nx, op);
+        if (!(in_xy && inz(p - 3))) o3 = vz;
+        w3a = w3b;
+        w3b = w3c;
+        w3c = w3d;
+        w3d = o3;
+        VT o4 = zs_relax<T, N, CLZ>(w3b, w3c, w3d, n4, cur.fk[3], col, 1 ^ par(p - 4), nbyz(p - 4), g.nx, op);
+        if (!(in_xy && inz(p - 4))) o4 = vz;
+        w4a = w4b;
+        w4b = w4c;
+        w4c = o4;
+
+        // ---- LDS writes (slots no stage of this step reads) ----
+        if (on) {
+            vstore<T, N>(slot(0, 2, p) + col.lrow, a0);
+            vstore<T, N>(slot(S::OFF1, 2, p - 1) + col.lrow, o1);
+            vstore<T, N>(slot(S::OFF2, 2, p - 2) + col.lrow, o2);
+            vstore<T, N>(slot(S::OFF3, NS3, p - 3) + col.lrow, o3);
+            if (PRE) vstore<T, N>(slot(S::OFF4, 2, p - 4) + col.lrow, o4);
         }
 
-        // ---- last stage on plane q = p - LAST ----
-        const int q = p - LAST;
-        if (q >= Z0 && q < Z0 + zc) {
-            const T* P = slot(q);
-            if (o_on) {  // the smoothed tile region -> dst (POST with ERR: against psiOld)
-                const Vec<T, N> v = vload<T, N>(P + o_s);
-                if (ERR) {
+        // ---- the smoothed plane p - 4: red final after stage 3, black after stage 4 ----
+        {
+            const int q = p - 4;
+            if (tile_xy && q >= Z0 && q < Z0 + zc) {
+                if (!PRE && ERR) {
 #pragma unroll
                     for (int e = 0; e < N; ++e) {
-                        const double df = (double)v.v[e] - (double)cur.old.v[e];
-                        err += df * df;
+                        const double d0 = (double)w3c.v[e] - (double)cur.old0.v[e];
+                        const double d1 = (double)o4.v[e] - (double)cur.old1.v[e];
+                        err += d0 * d0;
+                        err += d1 * d1;
                     }
                 }
-                vstore<T, N>(dst + plane(q) + o_g, v);
+                T* dp = dst + (int64_t)q * P;
+                vstore<T, N>(dp + goff, w3c);
+                vstore<T, N>(dp + Hh + goff, o4);
             }
-            if (r_on) {
-                // residual + restriction (k_resrestrict's expressions): thread -> W coarse cells
-                const int qz = (q - Z0) & 1;
-                const int j0e = H + 2 * r_jt, j0 = Y0 + 2 * r_jt;
-                const T* Pm = slot(q - 1);
-                const T* Pp = slot(q + 1);
-                const bool xlo = r_gm == 0, xhi = r_gm + W == hw;
-                auto ld = [&](const T* base) {
-                    Vec<T, W> v;
-                    if (W == 2) {
-                        v = vload<T, W>(base);
-                    } else {
+        }
+
+        // ---- PRE: residual + restriction of plane p - 5 ----
+        if (PRE) {
+            const int q = p - 5;
+            T rr[2][N];  // [x parity][e]
+            const int pq = par(q);
+            // red cells (x parity pq) see black neighbours, black cells (x parity 1 - pq) red ones
+            zs_residual<T, N, CLZ>(w4a, w4b, w4c, nk, w3b, f3_2, col, pq, nbyz(q), g.nx, op, rr[pq]);
+            zs_residual<T, N, CLZ>(w3a, w3b, w3c, nr, w4b, f4_1, col, 1 ^ pq, nbyz(q), g.nx, op, rr[1 ^ pq]);
+            f3_2 = f3_1;
+            f3_1 = cur.fk[2];
+            f4_1 = cur.fk[3];
+            if (tile_xy) {
+                const int dq = q - Z0;
+                const bool rin = dq >= 0 && dq < zc;
+                if (!even_row) {
+                    if (rin) {
+                        T* x = xs(q);
 #pragma unroll
-                        for (int e = 0; e < W; ++e) v.v[e] = base[e];
+                        for (int e = 0; e < N; ++e) {
+                            x[e] = rr[0][e];
+                            x[N + e] = rr[1][e];
+                        }
                     }
-                    return v;
-                };
-                Vec<T, W> M[4][2], Z[2][2][2];
+                } else {
+                    if (dq >= 1 && dq <= zc) {  // the odd row's children of plane q - 1
 #pragma unroll
-                for (int yi = 0; yi < 4; ++yi)
+                        for (int e = 0; e < N; ++e) {
+                            acc[e] = acc[e] + xr[e];
+                            acc[e] = acc[e] + xr[N + e];
+                        }
+                        if ((dq & 1) == 0) {  // coarse plane (q - 1) / 2 complete
+                            const int K = (z0 + q - 1) >> 1, J = gy >> 1;  // global
+                            T* rowc = R + (int64_t)(K - cz0) * gc.P + (int64_t)J * gc.hw;
 #pragma unroll
-                    for (int c = 0; c < 2; ++c) M[yi][c] = ld(P + c * CH + (j0e - 1 + yi) * HWE + r_m0);
-#pragma unroll
-                for (int yi = 0; yi < 2; ++yi)
-#pragma unroll
-                    for (int c = 0; c < 2; ++c) {
-                        Z[0][yi][c] = ld(Pm + c * CH + (j0e + yi) * HWE + r_m0);
-                        Z[1][yi][c] = ld(Pp + c * CH + (j0e + yi) * HWE + r_m0);
-                    }
-#pragma unroll
-                for (int dy = 0; dy < 2; ++dy) {
-                    const int j = j0 + dy;
-                    const int pj = (j + q) & 1;
-                    const int nbyz = (j == 0) + (j == g.ny - 1) + (q == 0) + (q == g.gnz - 1);
-                    const bool fast = CLZ || (nbyz == 0 && !xlo && !xhi);
-                    T rr[2][W];
-#pragma unroll
-                    for (int c = 0; c < 2; ++c) {
-                        const int o = c ^ pj;
-                        const int oc = c ^ 1;
-                        const Vec<T, W>& cen = M[dy + 1][oc];
-                        const Vec<T, W>& uc = M[dy + 1][c];
-                        const int othe = oc * CH + (j0e + dy) * HWE + r_m0;
-                        const T edge = o == 0 ? (xlo ? (T)0 : P[othe - 1]) : (xhi ? (T)0 : P[othe + W]);
-#pragma unroll
-                        for (int e = 0; e < W; ++e) {
-                            const T xl = o == 0 ? (e == 0 ? edge : cen.v[e - 1]) : cen.v[e];
-                            const T xr = o == 0 ? cen.v[e] : (e == W - 1 ? edge : cen.v[e + 1]);
-                            T s = xl + xr;
-                            s = s + M[dy][oc].v[e];
-                            s = s + M[dy + 2][oc].v[e];
-                            s = s + Z[0][dy][oc].v[e];
-                            s = s + Z[1][dy][oc].v[e];
-                            const T fc = cur.fr[dy][c][e];
-                            T res;
-                            if (fast) {
-                                const T askew = s * op.inv_hSq;
-                                const T a_u = askew + op.adiag * uc.v[e];
-                                res = fc - a_u;
-                            } else {
-                                const int i = 2 * (r_gm + e) + o;
-                                res = op.residual(s, fc, uc.v[e], nbyz + (i == 0) + (i == g.nx - 1));
+                            for (int e = 0; e < N; ++e) {
+                                const int I = col.gm + e;
+                                rowc[((I + J + K) & 1) * gc.H + (I >> 1)] = (T)0.125 * acc[e];
                             }
-                            rr[o][e] = res;
                         }
                     }
+                    if (rin) {
 #pragma unroll
-                    for (int e = 0; e < W; ++e) {
-                        if (qz == 0 && dy == 0) {
-                            acc[e] = rr[0][e] + rr[1][e];
-                        } else {
-                            acc[e] = acc[e] + rr[0][e];
-                            acc[e] = acc[e] + rr[1][e];
+                        for (int e = 0; e < N; ++e) {
+                            if ((dq & 1) == 0) {
+                                acc[e] = rr[0][e] + rr[1][e];
+                            } else {
+                                acc[e] = acc[e] + rr[0][e];
+                                acc[e] = acc[e] + rr[1][e];
+                            }
                         }
-                    }
-                }
-                if (qz == 1) {
-                    const int J = j0 >> 1, K = q >> 1;
-                    const int pc = (J + K) & 1;
-                    T* rowc = R + (int64_t)K * gc.P + (int64_t)J * gc.hw;
-#pragma unroll
-                    for (int e = 0; e < W; ++e) {
-                        const int I = r_gm + e;
-                        rowc[((I + pc) & 1) * gc.H + (I >> 1)] = (T)0.125 * acc[e];
                     }
                 }
             }
         }
-        if (MERGE) stage0(cur, p + 1);
         lds_barrier();
     };
-    const int p_begin = MERGE ? p_first - 1 : p_first;
-    FusedPrefetch<T, NS> nxt;
-    prefetch(nxt, p_begin);
-    for (int p = p_begin; p <= p_last; ++p) {
-        const FusedPrefetch<T, NS> cur = nxt;
-        step(cur, nxt, p);
+
+    // two prefetch buffers, alternating (no copy of the in-flight registers)
+    PF pa, pb;
+    prefetch(pa, zlo);
+    for (int p = zlo; p <= p_end; p += 2) {
+        step(pa, pb, p);
+        if (p + 1 <= p_end) step(pb, pa, p + 1);
     }
-    if (ERR) block_partial_n<T>(err, partials, kFusedThreads);
+    if (ERR) block_partial_t<NTL>(err, partials);
 }
 
 // ---- coarse-level tail ----------------------------------------------------------------------
@@ -1604,15 +1665,15 @@ hipError_t launch_prolong_correct(int rb, int dim, int linear, void* u, const vo
 
 // ---- fused smoothing phases ----
 
-template <typename T, int NS, bool PRE, int LINEAR, bool ERR, bool CLZ>
-static hipError_t fused_launch(const FusedArgs& a, hipStream_t s)
+template <typename T, bool PRE, int LINEAR, bool ERR, bool CLZ>
+static hipError_t zs_launch(const FusedArgs& a, hipStream_t s)
 {
-    using S = FusedShape<T, NS, PRE>;
-    auto kern = k_fused<T, NS, PRE, LINEAR, ERR, CLZ>;
+    using S = ZsShape<T, PRE>;
     const Op<T, 3> op = make_op<T, 3>(a.h, a.cl);
     const unsigned nb = (unsigned)fused_blocks(sizeof(T), a.g, a.zc);
-    kern<<<nb, kFusedThreads, S::lds_bytes, s>>>((const T*)a.src, (const T*)a.f, (T*)a.dst, (T*)a.R, (const T*)a.V,
-                                                  a.partials, a.g, a.gc, op, (T)a.clc, a.zc);
+    k_zs<T, PRE, LINEAR, ERR, CLZ><<<nb, S::NTL, S::lds_bytes, s>>>((const T*)a.src, (const T*)a.f, (T*)a.dst,
+                                                                     (T*)a.R, (const T*)a.V, a.partials, a.g, a.gc,
+                                                                     op, (T)a.clc, a.zc);
     return hipGetLastError();
 }
 
@@ -1620,46 +1681,60 @@ template <typename T, bool CLZ>
 static hipError_t fused_dispatch(const FusedArgs& a, hipStream_t s)
 {
     const bool err = a.partials != nullptr;
-    if (a.pre) return fused_launch<T, 2, true, 0, false, CLZ>(a, s);
-    if (a.linear) return err ? fused_launch<T, 2, false, 1, true, CLZ>(a, s) : fused_launch<T, 2, false, 1, false, CLZ>(a, s);
-    return err ? fused_launch<T, 2, false, 0, true, CLZ>(a, s) : fused_launch<T, 2, false, 0, false, CLZ>(a, s);
+    if (a.pre) return zs_launch<T, true, 0, false, CLZ>(a, s);
+    if (a.linear) return err ? zs_launch<T, false, 1, true, CLZ>(a, s) : zs_launch<T, false, 1, false, CLZ>(a, s);
+    return err ? zs_launch<T, false, 0, true, CLZ>(a, s) : zs_launch<T, false, 0, false, CLZ>(a, s);
+}
+
+static void zs_tile(int rb, int& tx, int& ty)
+{
+    tx = rb == 4 ? ZsTile<float>::TX : ZsTile<double>::TX;
+    ty = rb == 4 ? ZsTile<float>::TY : ZsTile<double>::TY;
 }
 
 bool fused_supported(int rb, int dim, int ns, const Geo& g)
 {
     if (dim != 3 || ns != 2) return false;
-    const int TX = rb == 4 ? FusedTile<float>::TX : FusedTile<double>::TX;
-    const int TY = rb == 4 ? FusedTile<float>::TY : FusedTile<double>::TY;
-    return g.nx % TX == 0 && g.ny % TY == 0 && g.nz >= 16 && (g.nz & 1) == 0 && g.z0 == 0 && g.gnz == g.nz;
+    int TX, TY;
+    zs_tile(rb, TX, TY);
+    return g.nx % TX == 0 && g.ny % TY == 0 && g.nz >= 16 && (g.nz & 1) == 0;
 }
 
+// planes per workgroup: halve the z-chunk until there are >= MGP_ZS_WGS (default 256, one per CU)
+// workgroups or a chunk would drop below 16 planes
 int fused_zc(int rb, const Geo& g)
 {
-    const int TX = rb == 4 ? FusedTile<float>::TX : FusedTile<double>::TX;
-    const int TY = rb == 4 ? FusedTile<float>::TY : FusedTile<double>::TY;
+    int TX, TY;
+    zs_tile(rb, TX, TY);
+    static const int64_t target = [] {
+        const char* v = std::getenv("MGP_ZS_WGS");
+        return v ? std::atoll(v) : (int64_t)256;
+    }();
     const int64_t tiles = (int64_t)(g.nx / TX) * (g.ny / TY);
     int64_t chunks = 1;
-    while (tiles * chunks < 512 && g.nz / (chunks * 2) >= 16) chunks *= 2;
+    while (tiles * chunks < target && g.nz / (chunks * 2) >= 16) chunks *= 2;
     return (int)(g.nz / chunks);
 }
 
 int fused_blocks(int rb, const Geo& g, int zc)
 {
-    const int TX = rb == 4 ? FusedTile<float>::TX : FusedTile<double>::TX;
-    const int TY = rb == 4 ? FusedTile<float>::TY : FusedTile<double>::TY;
+    int TX, TY;
+    zs_tile(rb, TX, TY);
     return (int)((int64_t)(g.nx / TX) * (g.ny / TY) * (g.nz / zc));
 }
+
+int fused_halo(bool pre) { return pre ? 5 : 4; }
 
 template <typename T, bool CLZ>
 static hipError_t fused_attr()
 {
-    const int pre = (int)FusedShape<T, 2, true>::lds_bytes, post = (int)FusedShape<T, 2, false>::lds_bytes;
+    const int pre = (int)ZsShape<T, true>::lds_bytes, post = (int)ZsShape<T, false>::lds_bytes;
     const auto A = hipFuncAttributeMaxDynamicSharedMemorySize;
-    hipError_t e = hipFuncSetAttribute((const void*)k_fused<T, 2, true, 0, false, CLZ>, A, pre);
-    if (e == hipSuccess) e = hipFuncSetAttribute((const void*)k_fused<T, 2, false, 0, false, CLZ>, A, post);
-    if (e == hipSuccess) e = hipFuncSetAttribute((const void*)k_fused<T, 2, false, 0, true, CLZ>, A, post);
-    if (e == hipSuccess) e = hipFuncSetAttribute((const void*)k_fused<T, 2, false, 1, false, CLZ>, A, post);
-    if (e == hipSuccess) e = hipFuncSetAttribute((const void*)k_fused<T, 2, false, 1, true, CLZ>, A, post);
+    hipError_t e = hipFuncSetAttribute((const void*)k_zs<T, true, 0, false, CLZ>, A, pre);
+    if (e == hipSuccess) e = hipFuncSetAttribute((const void*)k_zs<T, false, 0, false, CLZ>, A, post);
+    if (e == hipSuccess) e = hipFuncSetAttribute((const void*)k_zs<T, false, 0, true, CLZ>, A, post);
+    if (e == hipSuccess) e = hipFuncSetAttribute((const void*)k_zs<T, false, 1, false, CLZ>, A, post);
+    if (e == hipSuccess) e = hipFuncSetAttribute((const void*)k_zs<T, false, 1, true, CLZ>, A, post);
     return e;
 }
 
