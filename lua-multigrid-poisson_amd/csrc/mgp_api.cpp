@@ -532,6 +532,7 @@ int fused_pre(mgp_ctx* c, int l, double h)
     a.h = h;
     a.cl = coarse_coef(c->o.coarse_bc, l);
     a.zc = L.zc;
+    a.ghost = c->G;
     hipEvent_t e;
     TRY(timed_begin(c, l, &e));
     HIP_TRY(c, mgp::launch_fused(c->rb, a, c->s));
@@ -561,6 +562,7 @@ int fused_post(mgp_ctx* c, int l, double h, bool want_err)
     a.cl = coarse_coef(c->o.coarse_bc, l);
     a.clc = coarse_coef(c->o.coarse_bc, l + 1);
     a.zc = L.zc;
+    a.ghost = c->G;
     hipEvent_t e;
     TRY(timed_begin(c, l, &e));
     HIP_TRY(c, mgp::launch_fused(c->rb, a, c->s));

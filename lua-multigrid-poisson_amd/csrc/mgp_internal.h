@@ -82,6 +82,7 @@ struct FusedArgs {
     Geo g, gc;
     double h, cl, clc;
     int zc;
+    int ghost;  // readable ghost planes per side of src / f / dst
 };
 bool fused_supported(int rb, int dim, int ns, const Geo& g);
 // Raise the dynamic-LDS limit of the fused and tail kernels (once per context, before any capture).

@@ -39,7 +39,7 @@ struct VN {
 };
 
 template <typename T, int N>
-struct alignas(16) Vec {
+struct alignas(sizeof(T) * N) Vec {
     T v[N];
 };
 
@@ -784,7 +784,7 @@ __global__ __launch_bounds__(kBlock) void k_prolong_v(T* __restrict__ u, const T
 //   POST: prolongation + correction, then 2 RB-GS sweeps (+ err) (prolong_correct + smooth(l, 2))
 // A workgroup owns an x-y tile (plus a halo of H rows and kZsHX cells per side) and a chunk of zc
 // planes and streams through z.  Every thread owns one column of the extended tile: N consecutive
-// cells of each colour (16 bytes each) of one row.  At step p:
+// cells of each colour of one row.  At step p:
 //   stage 0   plane p of the input's BLACK cells (POST: plus the prolongation, k_prolong_v's
 //             expressions).  Red cells are never loaded: half-sweep 1 overwrites them, and a
 //             Gauss-Seidel update does not read the value it replaces.
@@ -793,14 +793,16 @@ __global__ __launch_bounds__(kBlock) void k_prolong_v(T* __restrict__ u, const T
 //             (k_resrestrict's expressions, children summed in the reference order, the odd row's
 //             residuals handed to the even row through LDS); POST: (psi - psiOld)^2 partials.
 // The z-neighbours of stage k's inputs are the thread's own registers (a window of 3-4 planes per
-// stage).  The in-plane neighbours come from LDS, where every stage leaves the plane it computed
-// (2-3 slots per stage: stage k reads the plane stage k-1 wrote one step earlier), and x-edges
-// from the neighbouring lane (DPP; LDS at wave boundaries), so a step needs one barrier.  Cells
-// outside the box stay 0 at every stage (the Dirichlet ghost); halo cells are recomputed by every
-// tile that needs them (the trapezoid shrinks by one cell per stage).  On a slab-distributed
-// level the z-halo comes from H ghost planes per side (u: black cells, f).  HBM traffic per cell:
-// PRE reads black u and f and writes u and R/8 (2.625 reals), POST reads black u, V/8, f and
-// psiOld and writes u (3.625 reals), against 8.125 and 9.125 for the launch-per-piece path.
+// stage).  The in-plane neighbours (rows above / below, the neighbouring groups of the row) come
+// from LDS, where every stage leaves the plane it computed; stage k reads the plane stage k-1
+// wrote one step earlier, so a step issues its LDS reads up front and needs one barrier.  Cells
+// outside the box are never written to LDS (they read as 0 there: the Dirichlet ghost) and
+// planes outside it are forced to 0; halo cells are recomputed by every tile that needs them (the
+// trapezoid shrinks by one cell per stage).  Plane indices are clamped to the readable planes, so
+// the loads need no branches.  On a slab-distributed level the z-halo comes from H ghost planes per
+// side (u: black cells, f).  HBM traffic per cell: PRE reads black u and f and writes u and R/8
+// (2.625 reals), POST reads black u, V/8, f and psiOld and writes u (3.625 reals), against 8.125
+// and 9.125 for the launch-per-piece path.
 
 // Workgroup barrier for LDS hand-offs only: waits for this wave's LDS operations, not for its
 // outstanding global loads (the next step's prefetch stays in flight across the barrier).
@@ -818,40 +820,26 @@ __device__ __forceinline__ void lds_barrier()
 #define ZS_PLANE(q) (q)
 #endif
 
-// Lane i <- lane i - 1 (shr) / lane i + 1 (shl) across the whole wavefront (DPP wave_shr:1 /
-// wave_shl:1, GFX9 encodings); the edge lanes receive 0 and are patched by the caller.
-__device__ __forceinline__ int dpp_shr1_i(int v) { return __builtin_amdgcn_update_dpp(0, v, 0x138, 0xf, 0xf, false); }
-__device__ __forceinline__ int dpp_shl1_i(int v) { return __builtin_amdgcn_update_dpp(0, v, 0x130, 0xf, 0xf, false); }
-__device__ __forceinline__ float dpp_shr1(float v) { return __int_as_float(dpp_shr1_i(__float_as_int(v))); }
-__device__ __forceinline__ float dpp_shl1(float v) { return __int_as_float(dpp_shl1_i(__float_as_int(v))); }
-__device__ __forceinline__ double dpp_shr1(double v)
-{
-    const long long b = __double_as_longlong(v);
-    const int lo = dpp_shr1_i((int)b), hi = dpp_shr1_i((int)(b >> 32));
-    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
-}
-__device__ __forceinline__ double dpp_shl1(double v)
-{
-    const long long b = __double_as_longlong(v);
-    const int lo = dpp_shl1_i((int)b), hi = dpp_shl1_i((int)(b >> 32));
-    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
-}
-
+// Tile and column width: N cells of each colour per thread (8 bytes for fp32 keeps a thread's
+// registers near 128, so 3-4 waves share a SIMD).
+#ifndef ZS_N_F32
+#define ZS_N_F32 2
+#endif
 template <typename T>
 struct ZsTile;
 template <>
 struct ZsTile<float> {
-    static constexpr int TX = 64, TY = 32;
+    static constexpr int TX = 64, TY = 32, N = ZS_N_F32;
 };
 template <>
 struct ZsTile<double> {
-    static constexpr int TX = 64, TY = 16;
+    static constexpr int TX = 64, TY = 16, N = 2;
 };
-constexpr int kZsHX = 8;  // x halo cells per side (>= the trapezoid depth, whole 16-byte groups)
+constexpr int kZsHX = 8;  // x halo cells per side (>= the trapezoid depth, whole groups)
 
 template <typename T, bool PRE>
 struct ZsShape {
-    static constexpr int N = VN<T>::n;
+    static constexpr int N = ZsTile<T>::N;
     static constexpr int TX = ZsTile<T>::TX, TY = ZsTile<T>::TY;
     static constexpr int H = PRE ? 5 : 4;              // y/z halo = stages that read neighbours
     static constexpr int HWE = (TX + 2 * kZsHX) / 2;   // reals per LDS half-row
@@ -861,7 +849,7 @@ struct ZsShape {
     static constexpr int NT = G * YE;                  // threads with a column
     static constexpr int NTL = (NT + 63) / 64 * 64;    // launched threads
     static constexpr int SLOT = YE * HWE;              // reals per LDS slot (one colour of a plane)
-    static constexpr int NS3 = PRE ? 3 : 2;            // stage-3 slots (PRE's residual reads 2 back)
+    static constexpr int NS3 = PRE ? 4 : 2;            // stage-3 slots (PRE's residual reads 2 back)
     static constexpr int OFF1 = 2 * SLOT, OFF2 = 4 * SLOT, OFF3 = 6 * SLOT, OFF4 = OFF3 + NS3 * SLOT;
     static constexpr int OFFX = OFF4 + (PRE ? 2 * SLOT : 0);
     static constexpr int XPAIRS = YE / 2 + 1;          // row pairs of the residual hand-off
@@ -881,14 +869,14 @@ struct ZsPrefetch {
 };
 
 struct ZsCol {
-    int lrow, lym, lyp, lane, gm;
+    int lrow, lym, lyp, lxm, lxp, gm;
     bool x_first, x_last;
+    bool xin;  // no cell of the group touches the x faces of the box (or the column is outside it)
 };
 
 // In-plane operands of one stage's cells: the other colour in the rows above / below and the x
 // neighbours beyond my group (last cell of the left group, first of the right group).  Stage k
-// reads them from the LDS slot stage k-1 filled one step earlier, so a step issues all its LDS
-// reads up front.
+// reads them from the LDS slot stage k-1 filled one step earlier.
 template <typename T, int N>
 struct ZsNb {
     Vec<T, N> yl, yr;
@@ -900,20 +888,10 @@ __device__ __forceinline__ void zs_nb_load(ZsNb<T, N>& nb, const T* s_in, const 
 {
     nb.yl = vload<T, N>(s_in + c.lym);
     nb.yr = vload<T, N>(s_in + c.lyp);
-    // lanes at a wave boundary take their x-edge from LDS, the others from the neighbouring lane
-    nb.ep = (c.lane == 0 && !c.x_first) ? s_in[c.lrow - 1] : (T)0;
-    nb.en = (c.lane == 63 && !c.x_last) ? s_in[c.lrow + N] : (T)0;
-}
-
-// cen: the other colour of my own row (the plane the neighbouring lanes hold too)
-template <typename T, int N>
-__device__ __forceinline__ void zs_nb_edges(ZsNb<T, N>& nb, const Vec<T, N>& cen, const ZsCol& c)
-{
-    const T dl = dpp_shr1(cen.v[N - 1]), dr = dpp_shl1(cen.v[0]);
-    if (c.lane != 0) nb.ep = dl;
-    if (c.lane != 63) nb.en = dr;
-    if (c.x_first) nb.ep = (T)0;
-    if (c.x_last) nb.en = (T)0;
+    // whole neighbouring groups (conflict-free), of which one cell each is used
+    const Vec<T, N> l = vload<T, N>(s_in + c.lxm), r = vload<T, N>(s_in + c.lxp);
+    nb.ep = c.x_first ? (T)0 : l.v[N - 1];
+    nb.en = c.x_last ? (T)0 : r.v[0];
 }
 
 // xl + xr of my N cells of x parity o (IEEE addition commutes, so the pair sums are shared
@@ -931,27 +909,41 @@ __device__ __forceinline__ void zs_xsum(const Vec<T, N>& cen, const ZsNb<T, N>& 
     for (int e = 0; e < N; ++e) s[e] = o == 0 ? m[e] : m[e + 1];
 }
 
+// ((((xl + xr) + yl) + yr) + zl) + zr of my N cells
+template <typename T, int N>
+__device__ __forceinline__ void zs_nbsum(const Vec<T, N>& zl, const Vec<T, N>& cen, const Vec<T, N>& zr,
+                                         const ZsNb<T, N>& nb, int o, T (&t)[N])
+{
+    zs_xsum<T, N>(cen, nb, o, t);
+#pragma unroll
+    for (int e = 0; e < N; ++e) {
+        t[e] = t[e] + nb.yl.v[e];
+        t[e] = t[e] + nb.yr.v[e];
+        t[e] = t[e] + zl.v[e];
+        t[e] = t[e] + zr.v[e];
+    }
+}
+
 // One half-sweep of my N cells of one colour (x parity o) from the other colour's window
-// (zl, cen, zr) and its in-plane operands: k_half's expressions.
+// (zl, cen, zr) and its in-plane operands: k_half's expressions.  Waves whose cells all have the
+// interior diagonal (every wave of a level with cl = 0) take the reciprocal form, which is what
+// Op::relax computes there.
 template <typename T, int N, bool CLZ>
 __device__ __forceinline__ Vec<T, N> zs_relax(const Vec<T, N>& zl, const Vec<T, N>& cen, const Vec<T, N>& zr,
                                               const ZsNb<T, N>& nb, const Vec<T, N>& fv, const ZsCol& c, int o,
                                               int nbyz, int nx, const Op<T, 3>& op)
 {
-    T s[N];
-    zs_xsum<T, N>(cen, nb, o, s);
+    T t[N];
+    zs_nbsum<T, N>(zl, cen, zr, nb, o, t);
     Vec<T, N> out;
+    if (CLZ || __all(nbyz == 0 && c.xin)) {
 #pragma unroll
-    for (int e = 0; e < N; ++e) {
-        T t = s[e] + nb.yl.v[e];
-        t = t + nb.yr.v[e];
-        t = t + zl.v[e];
-        t = t + zr.v[e];
-        if (CLZ) {
-            out.v[e] = div_rn(fv.v[e] - t * op.inv_hSq, op.adiag, op.yadiag);
-        } else {
+        for (int e = 0; e < N; ++e) out.v[e] = div_rn(fv.v[e] - t[e] * op.inv_hSq, op.adiag, op.yadiag);
+    } else {
+#pragma unroll
+        for (int e = 0; e < N; ++e) {
             const int i = 2 * (c.gm + e) + o;
-            out.v[e] = op.relax(t, fv.v[e], nbyz + (i == 0) + (i == nx - 1));
+            out.v[e] = op.relax(t[e], fv.v[e], nbyz + (i == 0) + (i == nx - 1));
         }
     }
     return out;
@@ -963,46 +955,40 @@ __device__ __forceinline__ void zs_residual(const Vec<T, N>& zl, const Vec<T, N>
                                             const ZsNb<T, N>& nb, const Vec<T, N>& uc, const Vec<T, N>& fv,
                                             const ZsCol& c, int o, int nbyz, int nx, const Op<T, 3>& op, T (&rr)[N])
 {
-    T s[N];
-    zs_xsum<T, N>(cen, nb, o, s);
+    T t[N];
+    zs_nbsum<T, N>(zl, cen, zr, nb, o, t);
+    if (CLZ || __all(nbyz == 0 && c.xin)) {
 #pragma unroll
-    for (int e = 0; e < N; ++e) {
-        T t = s[e] + nb.yl.v[e];
-        t = t + nb.yr.v[e];
-        t = t + zl.v[e];
-        t = t + zr.v[e];
-        if (CLZ) {
-            const T askew = t * op.inv_hSq;
+        for (int e = 0; e < N; ++e) {
+            const T askew = t[e] * op.inv_hSq;
             const T a_u = askew + op.adiag * uc.v[e];
             rr[e] = fv.v[e] - a_u;
-        } else {
+        }
+    } else {
+#pragma unroll
+        for (int e = 0; e < N; ++e) {
             const int i = 2 * (c.gm + e) + o;
-            rr[e] = op.residual(t, fv.v[e], uc.v[e], nbyz + (i == 0) + (i == nx - 1));
+            rr[e] = op.residual(t[e], fv.v[e], uc.v[e], nbyz + (i == 0) + (i == nx - 1));
         }
     }
 }
 
-// uv += P V for my N cells of x parity o in one fine row (k_prolong_v's expressions).
+// uv += P V for my N cells of x parity o in one fine row (k_prolong_v's expressions).  Waves with
+// no cell next to a face of the coarse box take the interior form (every factor is 1 there).
 template <typename T, int N, int LINEAR>
 __device__ __forceinline__ void zs_correct(Vec<T, N>& uv, const ZsPrefetch<T, N>& cur, int o, int I0, int cx, bool oy,
                                            bool oz, T cl)
 {
     const T w0 = (T)0.75, w1 = (T)0.25;
-    auto sv = [&](T val, bool fx, bool fy, bool fz) {
-        T s = (T)1;
-        if (fx) s = -cl * s;
-        if (fy) s = -cl * s;
-        if (fz) s = -cl * s;
-        return s == (T)1 ? val : s * val;
-    };
-    const bool interior = !oy && !oz && I0 > 0 && I0 + N < cx;
+    if (!LINEAR) {
 #pragma unroll
-    for (int e = 0; e < N; ++e) {
-        const int pe = e + 1;
-        T v;
-        if (!LINEAR) {
-            v = cur.c00[pe];
-        } else if (interior) {
+        for (int e = 0; e < N; ++e) uv.v[e] = uv.v[e] + cur.c00[e + 1];
+        return;
+    }
+    if (__all(!oy && !oz && I0 > 0 && I0 + N < cx)) {
+#pragma unroll
+        for (int e = 0; e < N; ++e) {
+            const int pe = e + 1;
             const T nb00 = o ? cur.c00[e + 2] : cur.c00[e];
             const T nb10 = o ? cur.c10[e + 2] : cur.c10[e];
             const T nb01 = o ? cur.c01[e + 2] : cur.c01[e];
@@ -1013,19 +999,29 @@ __device__ __forceinline__ void zs_correct(Vec<T, N>& uv, const ZsPrefetch<T, N>
             const T a11 = w0 * cur.c11[pe] + w1 * nb11;
             const T b0 = w0 * a00 + w1 * a10;
             const T b1 = w0 * a01 + w1 * a11;
-            v = w0 * b0 + w1 * b1;
-        } else {
-            const bool ox = (o == 0 && I0 + e == 0) || (o == 1 && I0 + e == cx - 1);
-            auto col = [&](const T (&cc)[N + 2]) { return ox ? cc[pe] : (o ? cc[e + 2] : cc[e]); };
-            const T a00 = w0 * cur.c00[pe] + w1 * sv(col(cur.c00), ox, false, false);
-            const T a10 = w0 * sv(cur.c10[pe], false, oy, false) + w1 * sv(col(cur.c10), ox, oy, false);
-            const T a01 = w0 * sv(cur.c01[pe], false, false, oz) + w1 * sv(col(cur.c01), ox, false, oz);
-            const T a11 = w0 * sv(cur.c11[pe], false, oy, oz) + w1 * sv(col(cur.c11), ox, oy, oz);
-            const T b0 = w0 * a00 + w1 * a10;
-            const T b1 = w0 * a01 + w1 * a11;
-            v = w0 * b0 + w1 * b1;
+            uv.v[e] = uv.v[e] + (w0 * b0 + w1 * b1);
         }
-        uv.v[e] = uv.v[e] + v;
+        return;
+    }
+    auto sv = [&](T val, bool fx, bool fy, bool fz) {
+        T s = (T)1;
+        if (fx) s = -cl * s;
+        if (fy) s = -cl * s;
+        if (fz) s = -cl * s;
+        return s == (T)1 ? val : s * val;
+    };
+#pragma unroll
+    for (int e = 0; e < N; ++e) {
+        const int pe = e + 1;
+        const bool ox = (o == 0 && I0 + e == 0) || (o == 1 && I0 + e == cx - 1);
+        auto col = [&](const T (&cc)[N + 2]) { return ox ? cc[pe] : (o ? cc[e + 2] : cc[e]); };
+        const T a00 = w0 * cur.c00[pe] + w1 * sv(col(cur.c00), ox, false, false);
+        const T a10 = w0 * sv(cur.c10[pe], false, oy, false) + w1 * sv(col(cur.c10), ox, oy, false);
+        const T a01 = w0 * sv(cur.c01[pe], false, false, oz) + w1 * sv(col(cur.c01), ox, false, oz);
+        const T a11 = w0 * sv(cur.c11[pe], false, oy, oz) + w1 * sv(col(cur.c11), ox, oy, oz);
+        const T b0 = w0 * a00 + w1 * a10;
+        const T b1 = w0 * a01 + w1 * a11;
+        uv.v[e] = uv.v[e] + (w0 * b0 + w1 * b1);
     }
 }
 
@@ -1045,14 +1041,14 @@ __device__ __forceinline__ void block_partial_t(double acc, double* partials)
 
 // src: the level's u before the phase; dst: the phase's output (POST with ERR reads psiOld from
 // dst first).  V/gc: coarse correction (POST); R/gc: restricted residual (PRE); both point at the
-// coarse plane of local fine plane 0 (gc.z0 = g.z0 / 2).  zc: planes per z-chunk.  On a
-// distributed level, src and f must hold H current ghost planes per side.  CLZ: the level operator
-// has no boundary modification (cl == 0, e.g. level 0).
+// coarse plane of local fine plane 0 (gc.z0 = g.z0 / 2).  zc: planes per z-chunk.  gz: readable
+// ghost planes per side of src / f / dst (on a distributed level they must hold the neighbours'
+// current H planes).  CLZ: the level operator has no boundary modification (cl == 0, level 0).
 template <typename T, bool PRE, int LINEAR, bool ERR, bool CLZ>
 __global__ __launch_bounds__((ZsShape<T, PRE>::NTL)) void k_zs(const T* __restrict__ src, const T* __restrict__ f,
                                                                 T* __restrict__ dst, T* __restrict__ R,
                                                                 const T* __restrict__ V, double* __restrict__ partials,
-                                                                Geo g, Geo gc, Op<T, 3> op, T clc, int zc)
+                                                                Geo g, Geo gc, Op<T, 3> op, T clc, int zc, int gz)
 {
     using S = ZsShape<T, PRE>;
     constexpr int N = S::N, H = S::H, HWE = S::HWE, G = S::G, YE = S::YE, SLOT = S::SLOT, TX = S::TX,
@@ -1071,6 +1067,7 @@ __global__ __launch_bounds__((ZsShape<T, PRE>::NTL)) void k_zs(const T* __restri
     const int hw = g.hw, Hh = (int)g.H;
     const int z0 = (int)g.z0, gnz = (int)g.gnz, cz0 = (int)gc.z0;
     const int64_t P = g.P;
+    const int qlo = -gz, qhi = (int)g.nz - 1 + gz;  // readable local planes
 
     // my column of the extended tile
     const bool on = tid < S::NT;
@@ -1081,61 +1078,57 @@ __global__ __launch_bounds__((ZsShape<T, PRE>::NTL)) void k_zs(const T* __restri
     col.lrow = ye * HWE + m0;
     col.lym = (ye > 0 ? ye - 1 : ye) * HWE + m0;
     col.lyp = (ye < YE - 1 ? ye + 1 : ye) * HWE + m0;
-    col.lane = tid & 63;
     col.gm = (X0 - kZsHX) / 2 + m0;  // global packed m of my first cell
     col.x_first = gx == 0;
     col.x_last = gx == G - 1;
+    col.lxm = col.x_first ? col.lrow : col.lrow - N;
+    col.lxp = col.x_last ? col.lrow : col.lrow + N;
     const bool in_xy = on && gy >= 0 && gy < g.ny && col.gm >= 0 && col.gm < hw;
-    const int goff = in_xy ? gy * hw + col.gm : 0;  // in-plane offset (nx * ny < 2^31)
+    col.xin = !in_xy || (col.gm > 0 && 2 * (col.gm + N) < g.nx);
+    // columns outside the box load from a clamped in-plane position; their results never reach
+    // LDS or HBM
+    const int cgy = in_xy ? gy : 0, cgm = in_xy ? col.gm : 0;
+    const int goff = cgy * hw + cgm;  // in-plane offset (nx * ny < 2^31)
     const bool tile_xy = on && ye >= H && ye < H + TY && gx >= S::HXG && gx < G - S::HXG;
-    const int zlo = Z0 - H, zhi = Z0 + zc - 1 + H;  // local planes stage 0 must cover
+    const int zlo = Z0 - H;
     const int p_end = Z0 + zc + (PRE ? 5 : 3);
     auto inz = [&](int q) { return z0 + q >= 0 && z0 + q < gnz; };  // inside the global box
-    // stage k (0..4) matters on planes [zlo + k, zhi - k]
-    auto live = [&](int q, int k) { return inz(q) && q >= zlo + k && q <= zhi - k; };
-    auto slot = [&](int off, int ns, int q) { return lds + off + ((q + 64 * ns) % ns) * SLOT; };
+    auto pcl = [&](int q) { return q < qlo ? qlo : (q > qhi ? qhi : q); };
+    auto slot = [&](int off, int ns, int q) { return lds + off + (q & (ns - 1)) * SLOT; };
     auto nbyz = [&](int q) {
         return CLZ ? 0 : (gy == 0) + (gy == g.ny - 1) + (z0 + q == 0) + (z0 + q == gnz - 1);
     };
-    auto par = [&](int q) { return (gy + z0 + q) & 1; };
+    const int rowpar = (gy + z0) & 1;
+    auto par = [&](int q) { return rowpar ^ (q & 1); };
     const T* const src_black = src + Hh;
 
     for (int i = tid; i < (int)(S::lds_bytes / sizeof(T)); i += NTL) lds[i] = (T)0;
     __syncthreads();
 
     auto prefetch = [&](PF& r, int p) {
-        r.u = vzero<T, N>();
-        if (in_xy && live(p, 0)) {
-            r.u = vload<T, N>(src_black + (int64_t)ZS_PLANE(p) * P + goff);
-            if (!PRE) {
-                const int J = gy >> 1, K = (z0 + p) >> 1;  // global coarse row / plane
-                int Jn = (gy & 1) ? J + 1 : J - 1;
-                if (Jn < 0 || Jn >= gc.ny) Jn = J;
-                int Kn = ((z0 + p) & 1) ? K + 1 : K - 1;
-                if (Kn < 0 || Kn >= gc.gnz) Kn = K;
-                coarse_row<T, N>(V, gc, J, K - cz0, col.gm, r.c00);
-                if (LINEAR) {
-                    coarse_row<T, N>(V, gc, Jn, K - cz0, col.gm, r.c10);
-                    coarse_row<T, N>(V, gc, J, Kn - cz0, col.gm, r.c01);
-                    coarse_row<T, N>(V, gc, Jn, Kn - cz0, col.gm, r.c11);
-                }
+        r.u = vload<T, N>(src_black + (int64_t)ZS_PLANE(pcl(p)) * P + goff);
+        if (!PRE) {
+            const int J = cgy >> 1;
+            int K = (z0 + p) >> 1;  // global coarse plane (any in-box plane outside the box)
+            K = K < 0 ? 0 : (K >= gc.gnz ? gc.gnz - 1 : K);
+            int Jn = (cgy & 1) ? J + 1 : J - 1;
+            if (Jn < 0 || Jn >= gc.ny) Jn = J;
+            int Kn = ((z0 + p) & 1) ? K + 1 : K - 1;
+            if (Kn < 0 || Kn >= gc.gnz) Kn = K;
+            coarse_row<T, N>(V, gc, J, K - cz0, cgm, r.c00);
+            if (LINEAR) {
+                coarse_row<T, N>(V, gc, Jn, K - cz0, cgm, r.c10);
+                coarse_row<T, N>(V, gc, J, Kn - cz0, cgm, r.c01);
+                coarse_row<T, N>(V, gc, Jn, Kn - cz0, cgm, r.c11);
             }
         }
 #pragma unroll
-        for (int k = 1; k <= 4; ++k) {
-            const int q = p - k;
-            const T* fp = f + (int64_t)ZS_PLANE(q) * P + ((k - 1) & 1) * Hh;
-            r.fk[k - 1] = (in_xy && live(q, k)) ? vload<T, N>(fp + goff) : vzero<T, N>();
-        }
+        for (int k = 1; k <= 4; ++k)
+            r.fk[k - 1] = vload<T, N>(f + (int64_t)ZS_PLANE(pcl(p - k)) * P + ((k - 1) & 1) * Hh + goff);
         if (!PRE && ERR) {
-            const int q = p - 4;
-            r.old0 = vzero<T, N>();
-            r.old1 = vzero<T, N>();
-            if (tile_xy && q >= Z0 && q < Z0 + zc) {
-                const T* dp = dst + (int64_t)q * P;
-                r.old0 = vload<T, N>(dp + goff);
-                r.old1 = vload<T, N>(dp + Hh + goff);
-            }
+            const T* dp = dst + (int64_t)pcl(p - 4) * P;
+            r.old0 = vload<T, N>(dp + goff);
+            r.old1 = vload<T, N>(dp + Hh + goff);
         }
     };
 
@@ -1157,68 +1150,53 @@ __global__ __launch_bounds__((ZsShape<T, PRE>::NTL)) void k_zs(const T* __restri
     auto step = [&](const PF& cur, PF& nxt, int p) {
         if (p < p_end) prefetch(nxt, p + 1);
 
-        // ---- every LDS read of the step (slots filled in the previous step) and the x-edges ----
+        // Every LDS read of a step hits a slot filled in the previous step (the writes come after
+        // the stages), so the compiler may schedule them as early as registers allow.
         ZsNb<T, N> n1, n2, n3, n4, nr, nk;
-        zs_nb_load<T, N>(n1, slot(0, 2, p - 1), col);
-        zs_nb_load<T, N>(n2, slot(S::OFF1, 2, p - 2), col);
-        zs_nb_load<T, N>(n3, slot(S::OFF2, 2, p - 3), col);
-        zs_nb_load<T, N>(n4, slot(S::OFF3, NS3, p - 4), col);
-        T xr[2 * N];
-        if (PRE) {
-            zs_nb_load<T, N>(nr, slot(S::OFF3, NS3, p - 5), col);  // red of A4 at p - 5
-            zs_nb_load<T, N>(nk, slot(S::OFF4, 2, p - 5), col);    // black of A4 at p - 5
-            const T* x = xs(p - 6);  // the odd row's residuals of plane p - 6 (even rows read them)
-#pragma unroll
-            for (int e = 0; e < 2 * N; ++e) xr[e] = x[e];
-        }
-        // the centres are last step's planes, held by the neighbouring lanes too
-        zs_nb_edges<T, N>(n1, w0c, col);
-        zs_nb_edges<T, N>(n2, w1c, col);
-        zs_nb_edges<T, N>(n3, w2c, col);
-        zs_nb_edges<T, N>(n4, w3d, col);
-        if (PRE) {
-            zs_nb_edges<T, N>(nr, w3c, col);
-            zs_nb_edges<T, N>(nk, w4c, col);
-        }
 
         // ---- stage 0: black cells of plane p ----
         VT a0 = cur.u;
-        if (!PRE && in_xy && live(p, 0)) {
-            const int J = gy >> 1, K = (z0 + p) >> 1;
-            const int Jn = (gy & 1) ? J + 1 : J - 1;
+        if (!PRE && inz(p)) {
+            const int J = cgy >> 1, K = (z0 + p) >> 1;
+            const int Jn = (cgy & 1) ? J + 1 : J - 1;
             const int Kn = ((z0 + p) & 1) ? K + 1 : K - 1;
-            zs_correct<T, N, LINEAR>(a0, cur, 1 ^ par(p), col.gm, gc.nx, Jn < 0 || Jn >= gc.ny, Kn < 0 || Kn >= gc.gnz,
-                                     clc);
+            zs_correct<T, N, LINEAR>(a0, cur, 1 ^ ((cgy + z0 + p) & 1), cgm, gc.nx, Jn < 0 || Jn >= gc.ny,
+                                     Kn < 0 || Kn >= gc.gnz, clc);
         }
+        if (!inz(p)) a0 = vz;
         w0a = w0b;
         w0b = w0c;
         w0c = a0;
 
         // ---- stages 1..4: half-sweep k on plane p - k (red, black, red, black) ----
+        zs_nb_load<T, N>(n1, slot(0, 2, p - 1), col);
         VT o1 = zs_relax<T, N, CLZ>(w0a, w0b, w0c, n1, cur.fk[0], col, par(p - 1), nbyz(p - 1), g.nx, op);
-        if (!(in_xy && inz(p - 1))) o1 = vz;
+        if (!inz(p - 1)) o1 = vz;
         w1a = w1b;
         w1b = w1c;
         w1c = o1;
+        zs_nb_load<T, N>(n2, slot(S::OFF1, 2, p - 2), col);
         VT o2 = zs_relax<T, N, CLZ>(w1a, w1b, w1c, n2, cur.fk[1], col, 1 ^ par(p - 2), nbyz(p - 2), g.nx, op);
-        if (!(in_xy && inz(p - 2))) o2 = vz;
+        if (!inz(p - 2)) o2 = vz;
         w2a = w2b;
         w2b = w2c;
         w2c = o2;
+        zs_nb_load<T, N>(n3, slot(S::OFF2, 2, p - 3), col);
         VT o3 = zs_relax<T, N, CLZ>(w2a, w2b, w2c, n3, cur.fk[2], col, par(p - 3), nbyz(p - 3), g.nx, op);
-        if (!(in_xy && inz(p - 3))) o3 = vz;
+        if (!inz(p - 3)) o3 = vz;
         w3a = w3b;
         w3b = w3c;
         w3c = w3d;
         w3d = o3;
+        zs_nb_load<T, N>(n4, slot(S::OFF3, NS3, p - 4), col);
         VT o4 = zs_relax<T, N, CLZ>(w3b, w3c, w3d, n4, cur.fk[3], col, 1 ^ par(p - 4), nbyz(p - 4), g.nx, op);
-        if (!(in_xy && inz(p - 4))) o4 = vz;
+        if (!inz(p - 4)) o4 = vz;
         w4a = w4b;
         w4b = w4c;
         w4c = o4;
 
-        // ---- LDS writes (slots no stage of this step reads) ----
-        if (on) {
+        // ---- LDS writes (slots no stage of this step reads); columns outside the box stay 0 ----
+        if (in_xy) {
             vstore<T, N>(slot(0, 2, p) + col.lrow, a0);
             vstore<T, N>(slot(S::OFF1, 2, p - 1) + col.lrow, o1);
             vstore<T, N>(slot(S::OFF2, 2, p - 2) + col.lrow, o2);
@@ -1229,7 +1207,7 @@ __global__ __launch_bounds__((ZsShape<T, PRE>::NTL)) void k_zs(const T* __restri
         // ---- the smoothed plane p - 4: red final after stage 3, black after stage 4 ----
         {
             const int q = p - 4;
-            if (tile_xy && q >= Z0 && q < Z0 + zc) {
+            if (q >= Z0 && q < Z0 + zc && tile_xy) {
                 if (!PRE && ERR) {
 #pragma unroll
                     for (int e = 0; e < N; ++e) {
@@ -1248,19 +1226,31 @@ __global__ __launch_bounds__((ZsShape<T, PRE>::NTL)) void k_zs(const T* __restri
         // ---- PRE: residual + restriction of plane p - 5 ----
         if (PRE) {
             const int q = p - 5;
-            T rr[2][N];  // [x parity][e]
             const int pq = par(q);
+            zs_nb_load<T, N>(nr, slot(S::OFF3, NS3, q), col);  // red of A4 at q
+            zs_nb_load<T, N>(nk, slot(S::OFF4, 2, q), col);    // black of A4 at q
+            T xr[2 * N];
+            {
+                const T* x = xs(q - 1);  // the odd row's residuals of plane q - 1 (even rows read them)
+#pragma unroll
+                for (int e = 0; e < 2 * N; ++e) xr[e] = x[e];
+            }
             // red cells (x parity pq) see black neighbours, black cells (x parity 1 - pq) red ones
-            zs_residual<T, N, CLZ>(w4a, w4b, w4c, nk, w3b, f3_2, col, pq, nbyz(q), g.nx, op, rr[pq]);
-            zs_residual<T, N, CLZ>(w3a, w3b, w3c, nr, w4b, f4_1, col, 1 ^ pq, nbyz(q), g.nx, op, rr[1 ^ pq]);
+            T rred[N], rblk[N], rr[2][N];  // rr: [x parity][e]
+            zs_residual<T, N, CLZ>(w4a, w4b, w4c, nk, w3b, f3_2, col, pq, nbyz(q), g.nx, op, rred);
+            zs_residual<T, N, CLZ>(w3a, w3b, w3c, nr, w4b, f4_1, col, 1 ^ pq, nbyz(q), g.nx, op, rblk);
+#pragma unroll
+            for (int e = 0; e < N; ++e) {
+                rr[0][e] = pq == 0 ? rred[e] : rblk[e];
+                rr[1][e] = pq == 0 ? rblk[e] : rred[e];
+            }
             f3_2 = f3_1;
             f3_1 = cur.fk[2];
             f4_1 = cur.fk[3];
-            if (tile_xy) {
-                const int dq = q - Z0;
-                const bool rin = dq >= 0 && dq < zc;
+            const int dq = q - Z0;
+            if (dq >= 0 && dq <= zc && tile_xy) {
                 if (!even_row) {
-                    if (rin) {
+                    if (dq < zc) {
                         T* x = xs(q);
 #pragma unroll
                         for (int e = 0; e < N; ++e) {
@@ -1269,7 +1259,7 @@ __global__ __launch_bounds__((ZsShape<T, PRE>::NTL)) void k_zs(const T* __restri
                         }
                     }
                 } else {
-                    if (dq >= 1 && dq <= zc) {  // the odd row's children of plane q - 1
+                    if (dq >= 1) {  // the odd row's children of plane q - 1
 #pragma unroll
                         for (int e = 0; e < N; ++e) {
                             acc[e] = acc[e] + xr[e];
@@ -1285,7 +1275,7 @@ __global__ __launch_bounds__((ZsShape<T, PRE>::NTL)) void k_zs(const T* __restri
                             }
                         }
                     }
-                    if (rin) {
+                    if (dq < zc) {
 #pragma unroll
                         for (int e = 0; e < N; ++e) {
                             if ((dq & 1) == 0) {
@@ -1673,7 +1663,7 @@ static hipError_t zs_launch(const FusedArgs& a, hipStream_t s)
     const unsigned nb = (unsigned)fused_blocks(sizeof(T), a.g, a.zc);
     k_zs<T, PRE, LINEAR, ERR, CLZ><<<nb, S::NTL, S::lds_bytes, s>>>((const T*)a.src, (const T*)a.f, (T*)a.dst,
                                                                      (T*)a.R, (const T*)a.V, a.partials, a.g, a.gc,
-                                                                     op, (T)a.clc, a.zc);
+                                                                     op, (T)a.clc, a.zc, a.ghost);
     return hipGetLastError();
 }
 
