@@ -40,7 +40,7 @@ def parse():
     p.add_argument("--nu", type=int, default=2)
     p.add_argument("--no-timing", action="store_true", help="skip the per-launch smoother events")
     p.add_argument("--cpu-cycles", type=int, default=2, help="oracle cycles timed for cpu_baseline (0 = skip)")
-    p.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "r01_pmc_traffic_half_sweep.json"),
+    p.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "r01_pmc_traffic.json"),
                    help="JSON with the PMC-measured HBM bytes per launch of the dominant kernel (tools/pmc_traffic.py); "
                         "used only when its kernel name matches")
     return p.parse_args()
@@ -132,30 +132,39 @@ def main():
     tname = "float" if a.real == "float" else "double"
     lin = 1
     kernels = {"half_sweep": f"k_half<{tname}, 3, 1, false>",
-               "fused_pre": f"k_fused<{tname}, 2, true, 0, false>",
-               "fused_post": f"k_fused<{tname}, 2, false, {lin}, true>"}
+               "fused_pre": f"k_zs<{tname}, true, 0, false, true>",
+               "fused_post": f"k_zs<{tname}, false, {lin}, true, true>"}
+    # Algorithmic bytes per level-0 cell of one launch (reals): what the launch must move
+    # to and from HBM.  half_sweep: read the other colour and f, write this colour of half the cells.
+    # fused_pre (k_zs: 2 RB-GS sweeps + residual + restriction): read black u and f, write u and R/8.
+    # fused_post (k_zs: prolongation + correction + 2 sweeps + err): read black u, V/8, f, psiOld; write u.
+    algo_reals = {"half_sweep": 1.5, "fused_pre": 2.625, "fused_post": 3.625}
     per_kind = {k: v for k, v in timed.items() if v[1] > 0}
-
-    def grid_of(kind):  # threads per launch of the level-0 kernel (rocprofv3 Grid_Size)
-        cells = n * n * n
-        return cells // 2 // (16 // rb) if kind == "half_sweep" else None
+    cells = n * n * n
     if per_kind:
+        # per kind: (ms, launches, algorithmic bytes, reference-path bytes as the library counts them:
+        # SURVEY.md §8(d) per-sweep accounting, i.e. what one launch per half-sweep would move)
+        kinds = {k: (ms, cnt, algo_reals[k] * rb * cells * cnt, by) for k, (ms, cnt, by) in per_kind.items()}
         line["level0_kernels"] = {
-            k: {"kernel": kernels[k], "launches": n, "avg_us": 1e3 * ms / n, "algorithmic_bytes_per_launch": by / n,
-                "achieved_GBps": by / (ms * 1e-3) / 1e9}
-            for k, (ms, n, by) in per_kind.items()}
-        dom = max(per_kind, key=lambda k: per_kind[k][0])  # the kernel with the most level-0 time
-        ms, n, by = per_kind[dom]
-        achieved = by / (ms * 1e-3) / 1e9
+            k: {"kernel": kernels[k], "launches": cnt, "avg_us": 1e3 * ms / cnt,
+                "algorithmic_bytes_per_launch": ab / cnt, "achieved_GBps": ab / (ms * 1e-3) / 1e9,
+                "per_sweep_accounting_bytes_per_launch": by / cnt,
+                "effective_GBps_per_sweep_accounting": by / (ms * 1e-3) / 1e9}
+            for k, (ms, cnt, ab, by) in kinds.items()}
+        dom = max(kinds, key=lambda k: kinds[k][0])  # the kernel with the most level-0 time
+        ms, cnt, ab, by = kinds[dom]
+        achieved = ab / (ms * 1e-3) / 1e9
         roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBPS, "traffic": None, "kernel": kernels[dom],
-                "algorithmic_bytes_per_launch": by / n, "avg_launch_us": 1e3 * ms / n,
+                "algorithmic_bytes_per_launch": ab / cnt, "avg_launch_us": 1e3 * ms / cnt,
                 "window": f"{a.steps} cycles after the timed region, HIP events around each launch"}
         if a.traffic and os.path.exists(a.traffic):
             with open(a.traffic) as fh:
                 tr = json.load(fh)
-            if tr.get("kernel") == kernels[dom] and tr.get("grid") in (None, grid_of(dom)):
-                roof["traffic"] = tr.get("bytes_per_launch")
+            ent = tr.get("kernels", {}).get(kernels[dom]) if "kernels" in tr else (
+                tr if tr.get("kernel") == kernels[dom] else None)
+            if ent:
+                roof["traffic"] = ent.get("bytes_per_launch")
                 roof["traffic_source"] = os.path.relpath(a.traffic, ROOT)
         line["roofline"] = roof
 

@@ -1012,12 +1012,12 @@ static int create_impl(mgp_ctx** out, const mgp_opts* o, mgp_loopback* lb)
     }
     c->err_fuse = c->o.err_mode && c->o.smoother == MGP_RBGS && c->o.nu1 >= 1 && c->o.nu2 >= 1 && c->lev.size() > 1;
     {
-        // temporally blocked phases: RB-GS 2+2 on replicated 3D levels of >= MGP_FUSED_MIN_CELLS
+        // temporally blocked phases (k_zs): RB-GS 2+2 on replicated 3D levels of >= MGP_FUSED_MIN_CELLS
+        // cells; MGP_FUSED=0 turns them off (one launch per half-sweep, bit-identical results)
         const char* v = std::getenv("MGP_FUSED");
         const char* vm = std::getenv("MGP_FUSED_MIN_CELLS");
         const int64_t min_cells = vm ? std::atoll(vm) : (int64_t(1) << 25);
-        // opt-in (MGP_FUSED=1) until it beats one launch per half-sweep
-        const bool on = v && std::atoi(v) != 0 && c->o.smoother == MGP_RBGS && c->o.nu1 == 2 && c->o.nu2 == 2;
+        const bool on = !(v && std::atoi(v) == 0) && c->o.smoother == MGP_RBGS && c->o.nu1 == 2 && c->o.nu2 == 2;
         for (size_t l = 0; l + 1 < c->lev.size(); ++l) {
             Level& L = c->lev[l];
             L.fused = on && !L.p.dist && level_cells(L) >= min_cells && mgp::fused_supported(c->rb, c->o.dim, 2, L.g);

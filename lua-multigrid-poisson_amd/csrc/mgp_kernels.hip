@@ -820,10 +820,11 @@ __device__ __forceinline__ void lds_barrier()
 #define ZS_PLANE(q) (q)
 #endif
 
-// Tile and column width: N cells of each colour per thread (8 bytes for fp32 keeps a thread's
-// registers near 128, so 3-4 waves share a SIMD).
+// Tile and column width: N cells of each colour per thread.  16-byte columns (N = 4 for fp32) issue
+// the fewest instructions per cell; 8-byte columns (ZS_N_F32=2) double the waves but spill and
+// were measured slower (exp/run.sh).
 #ifndef ZS_N_F32
-#define ZS_N_F32 2
+#define ZS_N_F32 4
 #endif
 template <typename T>
 struct ZsTile;
