@@ -826,6 +826,12 @@ __device__ __forceinline__ void lds_barrier()
 #ifndef ZS_N_F32
 #define ZS_N_F32 4
 #endif
+// Prefetch distance in steps: the loads of plane p + D are issued while plane p is computed.
+// D = 2 costs 3 register buffers and measured slower than D = 1 at 512^3 (601 / 878 us against
+// 579 / 787 us for PRE / POST).
+#ifndef ZS_DEPTH
+#define ZS_DEPTH 1
+#endif
 template <typename T>
 struct ZsTile;
 template <>
@@ -855,7 +861,14 @@ struct ZsShape {
     static constexpr int OFFX = OFF4 + (PRE ? 2 * SLOT : 0);
     static constexpr int XPAIRS = YE / 2 + 1;          // row pairs of the residual hand-off
     static constexpr int XSLOT = PRE ? XPAIRS * G * 2 * N : 0;
-    static constexpr size_t lds_bytes = (size_t)(OFFX + 2 * XSLOT) * sizeof(T);
+    // POST: coarse rows J in [Y0/2 - 3, Y0/2 + TY/2 + 3) and cells I in [X0/2 - 8, X0/2 + TX/2 + 8)
+    // of 4 coarse planes around the stream position, unpacked (x order, both colours)
+    static constexpr int CJ = PRE ? 0 : TY / 2 + 6, CI = PRE ? N : TX / 2 + 16;
+    static constexpr int CSLOT = CJ * CI, CPAIRS = CSLOT / 2;
+    static constexpr int OFFC = OFFX + 2 * XSLOT;
+    static constexpr size_t lds_bytes = (size_t)(OFFC + 4 * CSLOT) * sizeof(T);
+    static_assert(CPAIRS <= 2 * NTL, "coarse staging: two pairs per thread");
+    static_assert(CI % N == 0 && OFFC % N == 0, "coarse rows must hold aligned groups");
     static_assert(NTL <= 1024, "too many threads");
     static_assert(2 * N * HXG >= H, "x halo too small");
     static_assert(HWE % N == 0, "LDS row must hold whole groups");
@@ -864,9 +877,9 @@ struct ZsShape {
 template <typename T, int N>
 struct ZsPrefetch {
     Vec<T, N> u;                                       // stage 0: black cells of the input at plane p
-    T c00[N + 2], c10[N + 2], c01[N + 2], c11[N + 2];  // POST: coarse rows of P V at plane p
-    Vec<T, N> fk[4];                                   // f of half-sweep k at plane p - k
-    Vec<T, N> old0, old1;                              // POST + ERR: psiOld at plane p - 4
+    Vec<T, 2> cv[2];                                   // POST: this thread's coarse pairs for the ring
+    Vec<T, N> f1, f2;  // f of half-sweeps 1 (red, plane p - 1) and 2 (black, plane p - 2); sweeps 3
+                       // and 4 reuse them two steps later
 };
 
 struct ZsCol {
@@ -976,8 +989,13 @@ __device__ __forceinline__ void zs_residual(const Vec<T, N>& zl, const Vec<T, N>
 
 // uv += P V for my N cells of x parity o in one fine row (k_prolong_v's expressions).  Waves with
 // no cell next to a face of the coarse box take the interior form (every factor is 1 there).
+template <typename T, int N>
+struct ZsCoarse {
+    T c00[N + 2], c10[N + 2], c01[N + 2], c11[N + 2];  // [z: K / Kn][y: J / Jn], cells I0-1 .. I0+N
+};
+
 template <typename T, int N, int LINEAR>
-__device__ __forceinline__ void zs_correct(Vec<T, N>& uv, const ZsPrefetch<T, N>& cur, int o, int I0, int cx, bool oy,
+__device__ __forceinline__ void zs_correct(Vec<T, N>& uv, const ZsCoarse<T, N>& cur, int o, int I0, int cx, bool oy,
                                            bool oz, T cl)
 {
     const T w0 = (T)0.75, w1 = (T)0.25;
@@ -1088,7 +1106,8 @@ __global__ __launch_bounds__((ZsShape<T, PRE>::NTL)) void k_zs(const T* __restri
     col.xin = !in_xy || (col.gm > 0 && 2 * (col.gm + N) < g.nx);
     // columns outside the box load from a clamped in-plane position; their results never reach
     // LDS or HBM
-    const int cgy = in_xy ? gy : 0, cgm = in_xy ? col.gm : 0;
+    const int cgy = gy < 0 ? 0 : (gy >= g.ny ? g.ny - 1 : gy);
+    const int cgm = col.gm < 0 ? 0 : (col.gm > hw - N ? hw - N : col.gm);
     const int goff = cgy * hw + cgm;  // in-plane offset (nx * ny < 2^31)
     const bool tile_xy = on && ye >= H && ye < H + TY && gx >= S::HXG && gx < G - S::HXG;
     const int zlo = Z0 - H;
@@ -1106,30 +1125,58 @@ __global__ __launch_bounds__((ZsShape<T, PRE>::NTL)) void k_zs(const T* __restri
     for (int i = tid; i < (int)(S::lds_bytes / sizeof(T)); i += NTL) lds[i] = (T)0;
     __syncthreads();
 
-    auto prefetch = [&](PF& r, int p) {
-        r.u = vload<T, N>(src_black + (int64_t)ZS_PLANE(pcl(p)) * P + goff);
-        if (!PRE) {
-            const int J = cgy >> 1;
-            int K = (z0 + p) >> 1;  // global coarse plane (any in-box plane outside the box)
-            K = K < 0 ? 0 : (K >= gc.gnz ? gc.gnz - 1 : K);
-            int Jn = (cgy & 1) ? J + 1 : J - 1;
-            if (Jn < 0 || Jn >= gc.ny) Jn = J;
-            int Kn = ((z0 + p) & 1) ? K + 1 : K - 1;
-            if (Kn < 0 || Kn >= gc.gnz) Kn = K;
-            coarse_row<T, N>(V, gc, J, K - cz0, cgm, r.c00);
-            if (LINEAR) {
-                coarse_row<T, N>(V, gc, Jn, K - cz0, cgm, r.c10);
-                coarse_row<T, N>(V, gc, J, Kn - cz0, cgm, r.c01);
-                coarse_row<T, N>(V, gc, Jn, Kn - cz0, cgm, r.c11);
+    // ---- POST: coarse staging ring, plane K in slot K & 3 (planes clamped to the box) ----
+    const int Ia = X0 / 2 - 8, Ja = Y0 / 2 - 3;
+    auto ckl = [&](int K) { return K < 0 ? 0 : (K >= gc.gnz ? gc.gnz - 1 : K); };
+    auto cslot = [&](int K) { return lds + S::OFFC + (K & 3) * S::CSLOT; };
+    auto cload = [&](PF& r, int K) {
+        K = ckl(K);
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int t = tid + i * NTL;
+            const int J = Ja + t / (S::CI / 2), I = Ia + 2 * (t % (S::CI / 2));
+            r.cv[i].v[0] = r.cv[i].v[1] = (T)0;
+            if (t < S::CPAIRS && J >= 0 && J < gc.ny && I >= 0 && I < gc.nx) {
+                // I even: cells I and I + 1 sit at m = I / 2 of the two colour halves
+                const T* row = V + (int64_t)(K - cz0) * gc.P + (int64_t)J * gc.hw + (I >> 1);
+                const int ce = (I + J + K) & 1;
+                r.cv[i].v[0] = row[ce * gc.H];
+                r.cv[i].v[1] = row[(ce ^ 1) * gc.H];
             }
         }
+    };
+    auto cstore = [&](const PF& r, int K) {
+        T* const sl = cslot(ckl(K));
 #pragma unroll
-        for (int k = 1; k <= 4; ++k)
-            r.fk[k - 1] = vload<T, N>(f + (int64_t)ZS_PLANE(pcl(p - k)) * P + ((k - 1) & 1) * Hh + goff);
-        if (!PRE && ERR) {
-            const T* dp = dst + (int64_t)pcl(p - 4) * P;
-            r.old0 = vload<T, N>(dp + goff);
-            r.old1 = vload<T, N>(dp + Hh + goff);
+        for (int i = 0; i < 2; ++i) {
+            const int t = tid + i * NTL;
+            if (t < S::CPAIRS) vstore<T, 2>(sl + 2 * t, r.cv[i]);  // pair t: cells 2t, 2t + 1 of the region
+        }
+    };
+    auto crow = [&](int K, int J, T (&c)[N + 2]) {  // cells cgm - 1 .. cgm + N of coarse row J, plane K
+        const T* const sl = cslot(ckl(K)) + (J - Ja) * S::CI + (cgm - Ia);
+        const Vec<T, N> mid = vload<T, N>(sl);
+        c[0] = sl[-1];
+#pragma unroll
+        for (int e = 0; e < N; ++e) c[e + 1] = mid.v[e];
+        c[N + 1] = sl[N];
+    };
+
+    auto prefetch = [&](PF& r, int p) {
+        // POST: fine plane 2m + 1 is the first to need coarse plane m + 1; it is loaded with the
+        // prefetch of plane 2m (issued first, so waiting for it leaves the rest in flight)
+        if (!PRE && ((z0 + p) & 1) == 0) cload(r, ((z0 + p) >> 1) + 1);
+        r.u = vload<T, N>(src_black + (int64_t)ZS_PLANE(pcl(p)) * P + goff);
+        r.f1 = vload<T, N>(f + (int64_t)ZS_PLANE(pcl(p - 1)) * P + goff);
+        r.f2 = vload<T, N>(f + (int64_t)ZS_PLANE(pcl(p - 2)) * P + Hh + goff);
+    };
+    // POST + ERR: psiOld of plane q (red, black), for the tile's own columns only
+    VT old0, old1;
+    auto load_old = [&](int q) {
+        if (!PRE && ERR && tile_xy) {
+            const T* dp = dst + (int64_t)pcl(q) * P;
+            old0 = vload<T, N>(dp + goff);
+            old1 = vload<T, N>(dp + Hh + goff);
         }
     };
 
@@ -1139,7 +1186,8 @@ __global__ __launch_bounds__((ZsShape<T, PRE>::NTL)) void k_zs(const T* __restri
     VT w2a = vz, w2b = vz, w2c = vz;             // A2 black at p-4, p-3, p-2
     VT w3a = vz, w3b = vz, w3c = vz, w3d = vz;   // A3 red   at p-6, p-5, p-4, p-3
     VT w4a = vz, w4b = vz, w4c = vz;             // A4 black at p-6, p-5, p-4
-    VT f3_1 = vz, f3_2 = vz, f4_1 = vz;          // PRE: f of stages 3 / 4 one and two steps back
+    VT fr1 = vz, fr2 = vz, fr3 = vz, fr4 = vz;   // f1 of 1..4 steps back (red f at p-2 .. p-5)
+    VT fb1 = vz, fb2 = vz, fb3 = vz;             // f2 of 1..3 steps back (black f at p-3 .. p-5)
     T acc[N];
 #pragma unroll
     for (int e = 0; e < N; ++e) acc[e] = (T)0;
@@ -1148,8 +1196,11 @@ __global__ __launch_bounds__((ZsShape<T, PRE>::NTL)) void k_zs(const T* __restri
     T* const xbase = lds + S::OFFX + (((ye + (H & 1)) >> 1) * G + gx) * 2 * N;
     auto xs = [&](int q) { return xbase + (q & 1) * (S::XPAIRS * G * 2 * N); };
 
-    auto step = [&](const PF& cur, PF& nxt, int p) {
-        if (p < p_end) prefetch(nxt, p + 1);
+    constexpr int D = ZS_DEPTH;
+    static_assert(D == 1 || D == 2, "prefetch distance");
+    // cur: plane p (loaded); nxt: plane p + 1 (in flight); nxd: the buffer plane p + D goes to
+    auto step = [&](const PF& cur, PF& nxt, PF& nxd, int p) {
+        if (p + D <= p_end) prefetch(nxd, p + D);
 
         // Every LDS read of a step hits a slot filled in the previous step (the writes come after
         // the stages), so the compiler may schedule them as early as registers allow.
@@ -1159,10 +1210,19 @@ __global__ __launch_bounds__((ZsShape<T, PRE>::NTL)) void k_zs(const T* __restri
         VT a0 = cur.u;
         if (!PRE && inz(p)) {
             const int J = cgy >> 1, K = (z0 + p) >> 1;
-            const int Jn = (cgy & 1) ? J + 1 : J - 1;
-            const int Kn = ((z0 + p) & 1) ? K + 1 : K - 1;
-            zs_correct<T, N, LINEAR>(a0, cur, 1 ^ ((cgy + z0 + p) & 1), cgm, gc.nx, Jn < 0 || Jn >= gc.ny,
-                                     Kn < 0 || Kn >= gc.gnz, clc);
+            int Jn = (cgy & 1) ? J + 1 : J - 1;
+            int Kn = ((z0 + p) & 1) ? K + 1 : K - 1;
+            const bool oy = Jn < 0 || Jn >= gc.ny, oz = Kn < 0 || Kn >= gc.gnz;
+            if (oy) Jn = J;
+            if (oz) Kn = K;
+            ZsCoarse<T, N> cc;
+            crow(K, J, cc.c00);
+            if (LINEAR) {
+                crow(K, Jn, cc.c10);
+                crow(Kn, J, cc.c01);
+                crow(Kn, Jn, cc.c11);
+            }
+            zs_correct<T, N, LINEAR>(a0, cc, 1 ^ ((cgy + z0 + p) & 1), cgm, gc.nx, oy, oz, clc);
         }
         if (!inz(p)) a0 = vz;
         w0a = w0b;
@@ -1171,26 +1231,26 @@ __global__ __launch_bounds__((ZsShape<T, PRE>::NTL)) void k_zs(const T* __restri
 
         // ---- stages 1..4: half-sweep k on plane p - k (red, black, red, black) ----
         zs_nb_load<T, N>(n1, slot(0, 2, p - 1), col);
-        VT o1 = zs_relax<T, N, CLZ>(w0a, w0b, w0c, n1, cur.fk[0], col, par(p - 1), nbyz(p - 1), g.nx, op);
+        VT o1 = zs_relax<T, N, CLZ>(w0a, w0b, w0c, n1, cur.f1, col, par(p - 1), nbyz(p - 1), g.nx, op);
         if (!inz(p - 1)) o1 = vz;
         w1a = w1b;
         w1b = w1c;
         w1c = o1;
         zs_nb_load<T, N>(n2, slot(S::OFF1, 2, p - 2), col);
-        VT o2 = zs_relax<T, N, CLZ>(w1a, w1b, w1c, n2, cur.fk[1], col, 1 ^ par(p - 2), nbyz(p - 2), g.nx, op);
+        VT o2 = zs_relax<T, N, CLZ>(w1a, w1b, w1c, n2, cur.f2, col, 1 ^ par(p - 2), nbyz(p - 2), g.nx, op);
         if (!inz(p - 2)) o2 = vz;
         w2a = w2b;
         w2b = w2c;
         w2c = o2;
         zs_nb_load<T, N>(n3, slot(S::OFF2, 2, p - 3), col);
-        VT o3 = zs_relax<T, N, CLZ>(w2a, w2b, w2c, n3, cur.fk[2], col, par(p - 3), nbyz(p - 3), g.nx, op);
+        VT o3 = zs_relax<T, N, CLZ>(w2a, w2b, w2c, n3, fr2, col, par(p - 3), nbyz(p - 3), g.nx, op);
         if (!inz(p - 3)) o3 = vz;
         w3a = w3b;
         w3b = w3c;
         w3c = w3d;
         w3d = o3;
         zs_nb_load<T, N>(n4, slot(S::OFF3, NS3, p - 4), col);
-        VT o4 = zs_relax<T, N, CLZ>(w3b, w3c, w3d, n4, cur.fk[3], col, 1 ^ par(p - 4), nbyz(p - 4), g.nx, op);
+        VT o4 = zs_relax<T, N, CLZ>(w3b, w3c, w3d, n4, fb2, col, 1 ^ par(p - 4), nbyz(p - 4), g.nx, op);
         if (!inz(p - 4)) o4 = vz;
         w4a = w4b;
         w4b = w4c;
@@ -1204,6 +1264,9 @@ __global__ __launch_bounds__((ZsShape<T, PRE>::NTL)) void k_zs(const T* __restri
             vstore<T, N>(slot(S::OFF3, NS3, p - 3) + col.lrow, o3);
             if (PRE) vstore<T, N>(slot(S::OFF4, 2, p - 4) + col.lrow, o4);
         }
+        // POST: the coarse plane this step's prefetch loaded (first read two steps on; the slot it
+        // replaces was last read three steps back)
+        if (!PRE && p < p_end && ((z0 + p + 1) & 1) == 0) cstore(nxt, ((z0 + p + 1) >> 1) + 1);
 
         // ---- the smoothed plane p - 4: red final after stage 3, black after stage 4 ----
         {
@@ -1212,8 +1275,8 @@ __global__ __launch_bounds__((ZsShape<T, PRE>::NTL)) void k_zs(const T* __restri
                 if (!PRE && ERR) {
 #pragma unroll
                     for (int e = 0; e < N; ++e) {
-                        const double d0 = (double)w3c.v[e] - (double)cur.old0.v[e];
-                        const double d1 = (double)o4.v[e] - (double)cur.old1.v[e];
+                        const double d0 = (double)w3c.v[e] - (double)old0.v[e];
+                        const double d1 = (double)o4.v[e] - (double)old1.v[e];
                         err += d0 * d0;
                         err += d1 * d1;
                     }
@@ -1238,16 +1301,13 @@ __global__ __launch_bounds__((ZsShape<T, PRE>::NTL)) void k_zs(const T* __restri
             }
             // red cells (x parity pq) see black neighbours, black cells (x parity 1 - pq) red ones
             T rred[N], rblk[N], rr[2][N];  // rr: [x parity][e]
-            zs_residual<T, N, CLZ>(w4a, w4b, w4c, nk, w3b, f3_2, col, pq, nbyz(q), g.nx, op, rred);
-            zs_residual<T, N, CLZ>(w3a, w3b, w3c, nr, w4b, f4_1, col, 1 ^ pq, nbyz(q), g.nx, op, rblk);
+            zs_residual<T, N, CLZ>(w4a, w4b, w4c, nk, w3b, fr4, col, pq, nbyz(q), g.nx, op, rred);
+            zs_residual<T, N, CLZ>(w3a, w3b, w3c, nr, w4b, fb3, col, 1 ^ pq, nbyz(q), g.nx, op, rblk);
 #pragma unroll
             for (int e = 0; e < N; ++e) {
                 rr[0][e] = pq == 0 ? rred[e] : rblk[e];
                 rr[1][e] = pq == 0 ? rblk[e] : rred[e];
             }
-            f3_2 = f3_1;
-            f3_1 = cur.fk[2];
-            f4_1 = cur.fk[3];
             const int dq = q - Z0;
             if (dq >= 0 && dq <= zc && tile_xy) {
                 if (!even_row) {
@@ -1290,15 +1350,41 @@ __global__ __launch_bounds__((ZsShape<T, PRE>::NTL)) void k_zs(const T* __restri
                 }
             }
         }
+        fr4 = fr3;
+        fr3 = fr2;
+        fr2 = fr1;
+        fr1 = cur.f1;
+        fb3 = fb2;
+        fb2 = fb1;
+        fb1 = cur.f2;
+        if (p < p_end) load_old(p - 3);  // used at the end of the next step
         lds_barrier();
     };
 
-    // two prefetch buffers, alternating (no copy of the in-flight registers)
-    PF pa, pb;
+    // D + 1 prefetch buffers, rotating (no copy of the in-flight registers)
+    PF pa, pb, pc;
+    if (!PRE) {  // the coarse planes the first fine plane needs
+        const int K = (z0 + zlo) >> 1;
+        for (int k = K - 1; k <= K + 1; ++k) {
+            cload(pa, k);
+            cstore(pa, k);
+        }
+        __syncthreads();
+    }
     prefetch(pa, zlo);
-    for (int p = zlo; p <= p_end; p += 2) {
-        step(pa, pb, p);
-        if (p + 1 <= p_end) step(pb, pa, p + 1);
+    load_old(zlo - 4);
+    if constexpr (D == 1) {
+        for (int p = zlo; p <= p_end; p += 2) {
+            step(pa, pb, pb, p);
+            if (p + 1 <= p_end) step(pb, pa, pa, p + 1);
+        }
+    } else {
+        prefetch(pb, zlo + 1);  // p_end - zlo >= 7
+        for (int p = zlo; p <= p_end; p += 3) {
+            step(pa, pb, pc, p);
+            if (p + 1 <= p_end) step(pb, pc, pa, p + 1);
+            if (p + 2 <= p_end) step(pc, pa, pb, p + 2);
+        }
     }
     if (ERR) block_partial_t<NTL>(err, partials);
 }

@@ -4,7 +4,9 @@
 FETCH_SIZE and WRITE_SIZE are in KiB.  MI355X_MICROARCH.md (HBM / rocprofv3 section): on gfx950
 FETCH_SIZE reports exactly half of the bytes of wide coalesced streaming reads, so it is doubled;
 WRITE_SIZE is exact for 16-B-per-lane streaming stores.  Output: per kernel (name, grid) the mean
-bytes per launch, and for the finest smoother half-sweep a JSON file bench.py --traffic reads.
+bytes per launch; with an output path, a JSON file bench.py --traffic reads:
+{"kernels": {name: {grid, launches, read_bytes, write_bytes, bytes_per_launch}}, "method": ...}
+holding, per kernel name, the launch grid with the most bytes (the finest level's launches).
 
 usage: tools/pmc_traffic.py gpurun_out/pmc [out.json]
 """
@@ -37,11 +39,14 @@ rows.sort(key=lambda r: -(r[2] + r[3]))
 for name, grid, fetch, write, n in rows[:20]:
     print(f"{name[:46]:46s} {grid:>10d} x{n:<4d} read {fetch/1e6:9.2f} MB  write {write/1e6:9.2f} MB")
 
-fine = [r for r in rows if re.match(r"k_half<float, 3, 1, false>", r[0])]
-if fine and out:
-    name, grid, fetch, write, n = max(fine, key=lambda r: r[1])
-    json.dump({"kernel": name, "grid": grid, "launches": n, "read_bytes": fetch, "write_bytes": write,
-               "bytes_per_launch": fetch + write,
-               "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate passes, KiB -> B, FETCH_SIZE x2 "
-                         "(gfx950 wide-load correction, MI355X_MICROARCH.md)"}, open(out, "w"), indent=1)
+if out:
+    kernels = {}
+    for name, grid, fetch, write, n in rows:  # sorted by bytes: the first row per name is the largest
+        if name not in kernels:
+            kernels[name] = {"grid": grid, "launches": n, "read_bytes": fetch, "write_bytes": write,
+                             "bytes_per_launch": fetch + write}
+    json.dump({"kernels": kernels,
+               "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate passes over bench.py, KiB -> B, "
+                         "FETCH_SIZE x2 (gfx950 wide-load correction, MI355X_MICROARCH.md); per kernel the "
+                         "launch grid with the most bytes"}, open(out, "w"), indent=1)
     print("wrote", out)
