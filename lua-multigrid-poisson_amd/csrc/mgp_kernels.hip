@@ -48,6 +48,20 @@ __device__ __forceinline__ Vec<T, N> vload(const T* p)
 {
     return *reinterpret_cast<const Vec<T, N>*>(p);
 }
+// A whole-vector LDS read the compiler may not narrow: one element of a 16-byte ds_read_b128 of
+// consecutive lanes is conflict-free, while the ds_read_b32 it would be narrowed to hits every
+// 4th bank (4-way conflicts).
+template <typename T, int N>
+__device__ __forceinline__ Vec<T, N> vload_lds_whole(const T* p)
+{
+    typedef T vt __attribute__((ext_vector_type(N)));
+    typedef const volatile __attribute__((address_space(3))) vt* lds_ptr;
+    const vt x = *(lds_ptr)(p);
+    Vec<T, N> r;
+#pragma unroll
+    for (int e = 0; e < N; ++e) r.v[e] = x[e];
+    return r;
+}
 template <typename T, int N>
 __device__ __forceinline__ void vstore(T* p, const Vec<T, N>& a)
 {
@@ -903,7 +917,7 @@ __device__ __forceinline__ void zs_nb_load(ZsNb<T, N>& nb, const T* s_in, const 
     nb.yl = vload<T, N>(s_in + c.lym);
     nb.yr = vload<T, N>(s_in + c.lyp);
     // whole neighbouring groups (conflict-free), of which one cell each is used
-    const Vec<T, N> l = vload<T, N>(s_in + c.lxm), r = vload<T, N>(s_in + c.lxp);
+    const Vec<T, N> l = vload_lds_whole<T, N>(s_in + c.lxm), r = vload_lds_whole<T, N>(s_in + c.lxp);
     nb.ep = c.x_first ? (T)0 : l.v[N - 1];
     nb.en = c.x_last ? (T)0 : r.v[0];
 }
@@ -1156,10 +1170,10 @@ __global__ __launch_bounds__((ZsShape<T, PRE>::NTL)) void k_zs(const T* __restri
     auto crow = [&](int K, int J, T (&c)[N + 2]) {  // cells cgm - 1 .. cgm + N of coarse row J, plane K
         const T* const sl = cslot(ckl(K)) + (J - Ja) * S::CI + (cgm - Ia);
         const Vec<T, N> mid = vload<T, N>(sl);
-        c[0] = sl[-1];
+        c[0] = vload_lds_whole<T, N>(sl - N).v[N - 1];
 #pragma unroll
         for (int e = 0; e < N; ++e) c[e + 1] = mid.v[e];
-        c[N + 1] = sl[N];
+        c[N + 1] = vload_lds_whole<T, N>(sl + N).v[0];
     };
 
     auto prefetch = [&](PF& r, int p) {
