@@ -262,12 +262,12 @@ Geo make_geo(const LevelPlan& p, int dim)
 
 int lb_fail(mgp_ctx* c) { return c->fail(MGP_ERR_STATE, "loopback group barrier timed out or broken"); }
 
-int lb_exchange(mgp_ctx* c, int l, char* buf)
+int lb_exchange(mgp_ctx* c, int l, char* buf, int depth)
 {
     mgp_loopback* g = c->lb;
     const size_t rb = (size_t)c->rb;
     const Level& L = c->lev[l];
-    const size_t bytes = (size_t)L.g.P * rb;
+    const size_t bytes = (size_t)(depth * L.g.P) * rb;
     auto at = [&](char* b, int64_t k) { return b + (size_t)((k + c->G) * L.g.P) * rb; };
     c->lb_buf = buf;
     HIP_TRY(c, hipEventRecord(c->lb_ev, c->s));  // my boundary planes are final here
@@ -277,8 +277,9 @@ int lb_exchange(mgp_ctx* c, int l, char* buf)
         if (nb < 0 || nb >= c->o.world) continue;
         mgp_ctx* o = g->ranks[nb];
         HIP_TRY(c, hipStreamWaitEvent(c->s, o->lb_ev, 0));
-        const char* src = nb < r ? at(o->lb_buf, L.g.nz - 1) : at(o->lb_buf, 0);
-        HIP_TRY(c, hipMemcpyAsync(nb < r ? at(buf, -1) : at(buf, L.g.nz), src, bytes, hipMemcpyDeviceToDevice, c->s));
+        const char* src = nb < r ? at(o->lb_buf, L.g.nz - depth) : at(o->lb_buf, 0);
+        HIP_TRY(c, hipMemcpyAsync(nb < r ? at(buf, -depth) : at(buf, L.g.nz), src, bytes, hipMemcpyDeviceToDevice,
+                                  c->s));
     }
     HIP_TRY(c, hipEventRecord(c->lb_ev2, c->s));  // my pulls are done here
     if (!g->barrier()) return lb_fail(c);
@@ -330,22 +331,24 @@ int lb_allreduce(mgp_ctx* c, double* v, int n = 1)
     return MGP_OK;
 }
 
-// Exchange one boundary plane of `buf` with each z-neighbour: my first interior plane goes to
-// rank-1's upper ghost, my last to rank+1's lower ghost.  A plane is contiguous in the packed
+// Exchange `depth` boundary planes of `buf` with each z-neighbour: my first interior planes go to
+// rank-1's upper ghosts, my last to rank+1's lower ghosts.  Planes are contiguous in the packed
 // layout, so each direction is one ncclSend/ncclRecv pair on that neighbour's xGMI link.
-int exchange_buf(mgp_ctx* c, Level& L, char* buf)
+int exchange_buf(mgp_ctx* c, Level& L, char* buf, int depth = 1)
 {
-    if (c->lb) return lb_exchange(c, (int)(&L - c->lev.data()), buf);
+    if (depth > c->G || depth > L.g.nz)
+        return c->fail(MGP_ERR_STATE, "internal: exchange depth %d (ghost %d, slab %d)", depth, c->G, (int)L.g.nz);
+    if (c->lb) return lb_exchange(c, (int)(&L - c->lev.data()), buf, depth);
     const size_t rb = (size_t)c->rb;
-    const size_t cnt = (size_t)L.g.P;
+    const size_t cnt = (size_t)(depth * L.g.P);
     auto at = [&](int64_t k) { return buf + (size_t)((k + c->G) * L.g.P) * rb; };
     NCCL_TRY(c, ncclGroupStart());
     if (c->o.rank > 0) {
         NCCL_TRY(c, ncclSend(at(0), cnt, c->nccl_real(), c->o.rank - 1, c->comm, c->s));
-        NCCL_TRY(c, ncclRecv(at(-1), cnt, c->nccl_real(), c->o.rank - 1, c->comm, c->s));
+        NCCL_TRY(c, ncclRecv(at(-depth), cnt, c->nccl_real(), c->o.rank - 1, c->comm, c->s));
     }
     if (c->o.rank < c->o.world - 1) {
-        NCCL_TRY(c, ncclSend(at(L.g.nz - 1), cnt, c->nccl_real(), c->o.rank + 1, c->comm, c->s));
+        NCCL_TRY(c, ncclSend(at(L.g.nz - depth), cnt, c->nccl_real(), c->o.rank + 1, c->comm, c->s));
         NCCL_TRY(c, ncclRecv(at(L.g.nz), cnt, c->nccl_real(), c->o.rank + 1, c->comm, c->s));
     }
     NCCL_TRY(c, ncclGroupEnd());
@@ -474,6 +477,7 @@ int residual_restrict(mgp_ctx* c, int l, double h)
     char* R = c->ui(C, C.f) + (size_t)(zc * C.g.P) * c->rb;
     HIP_TRY(c, mgp::launch_residual_restrict(c->rb, c->o.dim, c->ui(L, L.u), c->ui(L, L.f), R, L.g, gc, h,
                                              coarse_coef(c->o.coarse_bc, l), c->s));
+    C.fghost_ok = !C.p.dist;
     if (L.p.dist && !C.p.dist) {
         // agglomerate: every rank gets the whole coarse right-hand side (cf. cpu-gpu.lua:22-32)
         const size_t count = (size_t)((L.g.nz / 2) * C.g.P);
@@ -521,14 +525,21 @@ int fused_pre(mgp_ctx* c, int l, double h)
 {
     Level& L = c->lev[l];
     Level& C = c->lev[l + 1];
+    if (L.p.dist) {  // the trapezoid reads kZsHaloPre planes of u and f beyond the slab
+        TRY(exchange_buf(c, L, L.u, mgp::kZsHaloPre));
+        if (!L.fghost_ok) TRY(exchange_buf(c, L, L.f, mgp::kZsHaloPre));
+        L.fghost_ok = true;
+    }
+    int64_t zc = 0;
+    const Geo gc = coarse_view(L, C, &zc);
     mgp::FusedArgs a{};
     a.pre = true;
     a.src = c->ui(L, L.u);
     a.f = c->ui(L, L.f);
     a.dst = c->ui(L, L.t);
-    a.R = c->ui(C, C.f);
+    a.R = c->ui(C, C.f) + (size_t)(zc * C.g.P) * c->rb;
     a.g = L.g;
-    a.gc = C.g;
+    a.gc = gc;
     a.h = h;
     a.cl = coarse_coef(c->o.coarse_bc, l);
     a.zc = L.zc;
@@ -539,6 +550,15 @@ int fused_pre(mgp_ctx* c, int l, double h)
     // algorithmic bytes: nu1 sweeps x 3 reals + (2 + 1/8) reals of residual/restriction
     TRY(timed_end(c, e, MGP_TIMING_FUSED_PRE, (3.0 * c->o.nu1 + 2.125) * c->rb * (double)level_cells(L)));
     std::swap(L.u, L.t);  // u = smoothed; t = the previous iterate (psiOld on level 0)
+    L.ghost_ok = !L.p.dist;
+    C.fghost_ok = !C.p.dist;
+    if (L.p.dist && !C.p.dist) {  // agglomerate the coarse right-hand side, as residual_restrict
+        const size_t count = (size_t)((L.g.nz / 2) * C.g.P);
+        if (c->lb)
+            TRY(lb_allgather(c, c->ui(C, C.f), count));
+        else
+            NCCL_TRY(c, ncclAllGather(a.R, c->ui(C, C.f), count, c->nccl_real(), c->comm, c->s));
+    }
     if (l == 0 && c->in_cycle) c->first_done = true;
     return MGP_OK;
 }
@@ -548,16 +568,24 @@ int fused_post(mgp_ctx* c, int l, double h, bool want_err)
 {
     Level& L = c->lev[l];
     Level& C = c->lev[l + 1];
+    if (L.p.dist) {  // kZsHaloPost planes of u and f, kZsHaloCoarse coarse planes of V
+        TRY(exchange_buf(c, L, L.u, mgp::kZsHaloPost));
+        if (!L.fghost_ok) TRY(exchange_buf(c, L, L.f, mgp::kZsHaloPost));
+        L.fghost_ok = true;
+        if (C.p.dist) TRY(exchange_buf(c, C, C.u, mgp::kZsHaloCoarse));
+    }
+    int64_t zc = 0;
+    const Geo gc = coarse_view(L, C, &zc);
     mgp::FusedArgs a{};
     a.pre = false;
     a.linear = c->o.prolong == MGP_PROLONG_LINEAR;
     a.src = c->ui(L, L.u);
     a.f = c->ui(L, L.f);
     a.dst = c->ui(L, L.t);
-    a.V = c->ui(C, C.u);
+    a.V = c->ui(C, C.u) + (size_t)(zc * C.g.P) * c->rb;
     a.partials = want_err ? c->d_part : nullptr;
     a.g = L.g;
-    a.gc = C.g;
+    a.gc = gc;
     a.h = h;
     a.cl = coarse_coef(c->o.coarse_bc, l);
     a.clc = coarse_coef(c->o.coarse_bc, l + 1);
@@ -569,6 +597,7 @@ int fused_post(mgp_ctx* c, int l, double h, bool want_err)
     TRY(timed_end(c, e, MGP_TIMING_FUSED_POST,
                   (3.0 * c->o.nu2 + 2.125 + (want_err ? 2.0 : 0.0)) * c->rb * (double)level_cells(L)));
     std::swap(L.u, L.t);
+    L.ghost_ok = !L.p.dist;
     if (want_err) {
         HIP_TRY(c, mgp::launch_sum_partials(c->d_part, mgp::fused_blocks(c->rb, L.g, L.zc), c->err_dst, c->s));
         c->err_done = true;
@@ -973,7 +1002,7 @@ static int create_impl(mgp_ctx** out, const mgp_opts* o, mgp_loopback* lb)
     c->o = *o;
     if (c->o.dim == 2) c->o.n[2] = 1;
     c->rb = o->real_bytes;
-    c->G = o->dim == 3 ? mgp::kGhost3D : 0;
+    c->G = o->dim == 3 ? mgp::kGhost3D : 0;  // widened below when a distributed level is fused
     auto bail = [&](int code) {
         g_create_error = c->err;
         destroy_impl(c);
@@ -1007,23 +1036,25 @@ static int create_impl(mgp_ctx** out, const mgp_opts* o, mgp_loopback* lb)
         Level L;
         L.p = p;
         L.g = make_geo(p, c->o.dim);
-        L.alloc = L.g.P * (L.g.nz + 2 * c->G);
         c->lev.push_back(L);
     }
     c->err_fuse = c->o.err_mode && c->o.smoother == MGP_RBGS && c->o.nu1 >= 1 && c->o.nu2 >= 1 && c->lev.size() > 1;
     {
-        // temporally blocked phases (k_zs): RB-GS 2+2 on replicated 3D levels of >= MGP_FUSED_MIN_CELLS
-        // cells; MGP_FUSED=0 turns them off (one launch per half-sweep, bit-identical results)
+        // temporally blocked phases (k_zs): RB-GS 2+2 on 3D levels of >= MGP_FUSED_MIN_CELLS cells (per
+        // rank); MGP_FUSED=0 turns them off (one launch per half-sweep, bit-identical results).  A
+        // distributed fused level exchanges kGhostZs-deep halos, so every level gets that many ghost planes.
         const char* v = std::getenv("MGP_FUSED");
         const char* vm = std::getenv("MGP_FUSED_MIN_CELLS");
         const int64_t min_cells = vm ? std::atoll(vm) : (int64_t(1) << 25);
         const bool on = !(v && std::atoi(v) == 0) && c->o.smoother == MGP_RBGS && c->o.nu1 == 2 && c->o.nu2 == 2;
         for (size_t l = 0; l + 1 < c->lev.size(); ++l) {
             Level& L = c->lev[l];
-            L.fused = on && !L.p.dist && level_cells(L) >= min_cells && mgp::fused_supported(c->rb, c->o.dim, 2, L.g);
+            L.fused = on && level_cells(L) >= min_cells && mgp::fused_supported(c->rb, c->o.dim, 2, L.g);
             if (L.fused) L.zc = mgp::fused_zc(c->rb, L.g);
+            if (L.fused && L.p.dist) c->G = mgp::kGhostZs;
         }
     }
+    for (auto& L : c->lev) L.alloc = L.g.P * (L.g.nz + 2 * c->G);
     for (size_t l = 0; l < c->lev.size(); ++l) {
         Level& L = c->lev[l];
         const size_t bytes = (size_t)L.alloc * rb;

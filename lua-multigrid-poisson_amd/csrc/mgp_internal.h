@@ -7,6 +7,10 @@
 namespace mgp {
 
 constexpr int kGhost3D = 1;  // ghost planes per side of every 3D level
+// ... when a slab-distributed level runs the temporally blocked phases (k_zs): PRE reads 5 planes
+// of u and f beyond its slab, POST 4 of u and f and 3 coarse planes of V
+constexpr int kGhostZs = 5;
+constexpr int kZsHaloPre = 5, kZsHaloPost = 4, kZsHaloCoarse = 3;
 
 // Device layout of one level ("red/black packed").  A level is a stack of planes (one plane in
 // 2D).  Each plane holds its red cells ((i + j + gk) even) in the first half and its black cells

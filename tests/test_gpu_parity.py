@@ -348,6 +348,31 @@ def test_slab_decomposition_loopback(box, world, gather, cfg):
     """The library's multi-GPU code path (slab planes, ghost exchange after every half-sweep, coarse
     ghost planes for linear P, all-gather agglomeration, err all-reduce) with the loopback transport:
     `world` ranks on one GPU, one thread each.  Gathered psi == the single-domain run bit for bit."""
+    _loopback_vs_single(box, world, gather, cfg)
+
+
+FUSED_LOOPBACK_CASES = [
+    # box, world, gather_cells, config: level 0 of every slab runs k_zs (>= 16 planes per rank)
+    ((64, 64, 128), 2, 4096, dict(real="float", prolong="linear", coarse_bc="consistent")),
+    ((64, 64, 128), 4, 65536, dict(real="double", prolong="linear", coarse_bc="consistent", cycle="F")),
+    ((128, 64, 64), 2, 32768, dict(real="float", prolong="pc", coarse_bc="zero", coarse_init="warm")),
+    ((64, 64, 128), 8, 4096, dict(real="float", prolong="linear", coarse_bc="consistent")),
+]
+
+
+@pytest.mark.parametrize("box,world,gather,cfg", FUSED_LOOPBACK_CASES,
+                         ids=["w2-lin-f32", "w4-F-f64-gathered", "w2-pc-warm", "w8-lin-f32"])
+def test_fused_slab_decomposition_loopback(box, world, gather, cfg, monkeypatch):
+    """k_zs on slab-distributed levels: 5-plane halos of u and f before PRE, 4 before POST, 3 coarse
+    planes of V, the restricted residual all-gathered when the coarse level is agglomerated.
+    Gathered psi == the single-domain run bit for bit, and the level-0 phases ran fused."""
+    monkeypatch.setenv("MGP_FUSED", "1")
+    monkeypatch.setenv("MGP_FUSED_MIN_CELLS", "65536")
+    _loopback_vs_single(box, world, gather, dict(smoother="rbgs", nu1=2, nu2=2, **cfg), expect_fused=True,
+                        min_dist=1 if gather >= 65536 else 2)
+
+
+def _loopback_vs_single(box, world, gather, cfg, expect_fused=False, min_dist=2):
     import threading
 
     mg = _mg()
@@ -358,10 +383,19 @@ def test_slab_decomposition_loopback(box, world, gather, cfg):
         try:
             ctx = mg.Context(mg.make_opts(dim=3, n=box, rank=r, world=world, gather_cells=gather, device=0,
                                           comm_id=b"\0" * 128, **cfg), loopback=lb)
-            assert sum(lv["distributed"] for lv in ctx.levels) >= 2
+            assert sum(lv["distributed"] for lv in ctx.levels) >= min_dist
+            if min_dist == 1:  # level 0's coarse level is agglomerated
+                assert ctx.levels[0]["distributed"] and not ctx.levels[1]["distributed"]
             ctx.init_point_charge()
+            if expect_fused:
+                ctx.timing(True)
             errs = ctx.cycles(3)
-            results[r] = (ctx.get_psi(), errs, ctx.metrics())
+            if expect_fused:
+                t = ctx.timing_read()
+                ctx.timing(False)
+                assert t["fused_pre"][1] == 3 and t["fused_post"][1] == 3 and t["half_sweep"][1] == 0, t
+            # the temporally blocked phases overwrite psiOld, so mgp_metrics is unavailable there
+            results[r] = (ctx.get_psi(), errs, None if expect_fused else ctx.metrics())
             ctx.close()
         except Exception as e:  # noqa: BLE001 - surfaced below
             errors.append((r, repr(e)))
@@ -378,9 +412,12 @@ def test_slab_decomposition_loopback(box, world, gather, cfg):
     e_ref = ref.cycles(3)
     psi = np.concatenate([results[r][0] for r in range(world)], axis=0)
     assert np.array_equal(psi, ref.get_psi()), float(np.max(np.abs(psi - ref.get_psi())))
-    m_ref = ref.metrics()
     for r in range(world):
         np.testing.assert_allclose(results[r][1], e_ref, rtol=1e-12, atol=0)
+    if expect_fused:
+        return
+    m_ref = ref.metrics()
+    for r in range(world):
         assert results[r][2][1] == m_ref[1]
         np.testing.assert_allclose(results[r][2], m_ref, rtol=1e-12, atol=0)
 
