@@ -834,11 +834,15 @@ __device__ __forceinline__ void lds_barrier()
 #define ZS_PLANE(q) (q)
 #endif
 
-// Tile and column width: N cells of each colour per thread.  16-byte columns (N = 4 for fp32) issue
-// the fewest instructions per cell; 8-byte columns (ZS_N_F32=2) double the waves but spill and
-// were measured slower (exp/run.sh).
-#ifndef ZS_N_F32
-#define ZS_N_F32 4
+// Tile and column width: N cells of each colour per thread.  fp32 PRE uses 16-byte columns (7 waves,
+// fewest instructions per cell: 576 us against 762 us with 8-byte columns at 512^3); fp32 POST,
+// whose prolongation and err make it VALU-bound, uses 8-byte columns (14 waves: 642 against
+// 756 us).  exp/run.sh A/B; ZS_NPRE_F32 / ZS_NPOST_F32 override.
+#ifndef ZS_NPRE_F32
+#define ZS_NPRE_F32 4
+#endif
+#ifndef ZS_NPOST_F32
+#define ZS_NPOST_F32 2
 #endif
 // Prefetch distance in steps: the loads of plane p + D are issued while plane p is computed.
 // D = 2 costs 3 register buffers and measured slower than D = 1 at 512^3 (601 / 878 us against
@@ -850,17 +854,17 @@ template <typename T>
 struct ZsTile;
 template <>
 struct ZsTile<float> {
-    static constexpr int TX = 64, TY = 32, N = ZS_N_F32;
+    static constexpr int TX = 64, TY = 32, NPRE = ZS_NPRE_F32, NPOST = ZS_NPOST_F32;
 };
 template <>
 struct ZsTile<double> {
-    static constexpr int TX = 64, TY = 16, N = 2;
+    static constexpr int TX = 64, TY = 16, NPRE = 2, NPOST = 2;
 };
 constexpr int kZsHX = 8;  // x halo cells per side (>= the trapezoid depth, whole groups)
 
 template <typename T, bool PRE>
 struct ZsShape {
-    static constexpr int N = ZsTile<T>::N;
+    static constexpr int N = PRE ? ZsTile<T>::NPRE : ZsTile<T>::NPOST;
     static constexpr int TX = ZsTile<T>::TX, TY = ZsTile<T>::TY;
     static constexpr int H = PRE ? 5 : 4;              // y/z halo = stages that read neighbours
     static constexpr int HWE = (TX + 2 * kZsHX) / 2;   // reals per LDS half-row
@@ -914,6 +918,11 @@ struct ZsNb {
 template <typename T, int N>
 __device__ __forceinline__ void zs_nb_load(ZsNb<T, N>& nb, const T* s_in, const ZsCol& c)
 {
+#ifdef ZS_NOLDSREAD  // timing experiment only: results are wrong
+    nb.yl = nb.yr = vzero<T, N>();
+    nb.ep = nb.en = (T)c.lrow;
+    return;
+#endif
     nb.yl = vload<T, N>(s_in + c.lym);
     nb.yr = vload<T, N>(s_in + c.lyp);
     // whole neighbouring groups (conflict-free), of which one cell each is used
