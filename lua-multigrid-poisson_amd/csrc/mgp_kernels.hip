@@ -1214,7 +1214,7 @@ __global__ __launch_bounds__((ZsShape<T, PRE>::NTL)) void k_zs(const T* __restri
     T acc[N];
 #pragma unroll
     for (int e = 0; e < N; ++e) acc[e] = (T)0;
-    double err = 0.0;
+    double err = 0.0, err1 = 0.0;
     const bool even_row = (gy & 1) == 0;
     T* const xbase = lds + S::OFFX + (((ye + (H & 1)) >> 1) * G + gx) * 2 * N;
     auto xs = [&](int q) { return xbase + (q & 1) * (S::XPAIRS * G * 2 * N); };
@@ -1298,10 +1298,12 @@ __global__ __launch_bounds__((ZsShape<T, PRE>::NTL)) void k_zs(const T* __restri
                 if (!PRE && ERR) {
 #pragma unroll
                     for (int e = 0; e < N; ++e) {
+                        // (psi - psiOld)^2 in fp64, fused multiply-add into two accumulators (err
+                        // matches the oracle's sum to summation order, not bit for bit)
                         const double d0 = (double)w3c.v[e] - (double)old0.v[e];
                         const double d1 = (double)o4.v[e] - (double)old1.v[e];
-                        err += d0 * d0;
-                        err += d1 * d1;
+                        err = __builtin_fma(d0, d0, err);
+                        err1 = __builtin_fma(d1, d1, err1);
                     }
                 }
                 T* dp = dst + (int64_t)q * P;
@@ -1409,7 +1411,7 @@ __global__ __launch_bounds__((ZsShape<T, PRE>::NTL)) void k_zs(const T* __restri
             if (p + 2 <= p_end) step(pc, pa, pb, p + 2);
         }
     }
-    if (ERR) block_partial_t<NTL>(err, partials);
+    if (ERR) block_partial_t<NTL>(err + err1, partials);
 }
 
 // ---- coarse-level tail ----------------------------------------------------------------------
