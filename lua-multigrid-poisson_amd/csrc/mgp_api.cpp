@@ -112,6 +112,7 @@ struct Level {
     bool ghost_ok = true;   // u's ghost planes hold the neighbours' current planes
     bool fghost_ok = true;  // f's ghost planes likewise
     bool fused = false;     // smoothing phases run temporally blocked (k_zs); needs t
+    bool zero_pending = false;  // u is logically 0: the next red half-sweep reads c->zbuf instead
     int zc = 0;             // k_zs z-chunk (planes per workgroup)
 };
 
@@ -159,6 +160,10 @@ struct mgp_ctx {
     const char* metrics_old = nullptr;
     double* d_metrics = nullptr;  // 3 * kSumBlocks partials + 3 results
     char* psi_old = nullptr;  // snapshot buffer (Jacobi path)
+    // an all-zero buffer of the largest lazily zeroed level's layout: a fresh coarse guess (cpu.lua:138)
+    // costs no memset, the first red half-sweep reads its black neighbours from here
+    char* zbuf = nullptr;
+    int64_t zbuf_reals = 0;
     char* stage = nullptr;    // lexicographic staging buffer for set/get (level-0 size)
     double* d_part = nullptr;
     int64_t part_cap = 0;
@@ -440,7 +445,8 @@ int smooth(mgp_ctx* c, int l, int sweeps, double h, bool want_err = false)
         const int nb = mgp::half_blocks(c->rb, L.g, c->use_gs);
         char* dst = oop ? L.t : L.u;
         TRY(exchange(c, L));
-        TRY(half(c, l, 0, L.u, dst, old, h, cl, 0));  // red from black
+        TRY(half(c, l, 0, L.zero_pending ? c->zbuf : L.u, dst, old, h, cl, 0));  // red from black
+        L.zero_pending = false;
         if (L.p.dist) {  // black reads the new red planes of dst
             TRY(exchange_buf(c, L, dst));
         }
@@ -511,8 +517,23 @@ int coarse_solve_at(mgp_ctx* c, int l, double h)
     return smooth(c, l, cells == 1 ? 1 : c->o.coarse_sweeps, h);
 }
 
+// RB-GS levels outside the tail / hand-off / fused levels only need u = 0 as the black input of their
+// first red half-sweep (a Gauss-Seidel update never reads the value it replaces, and the black
+// half-sweep then reads the new red cells), so their zeroing is deferred to that sweep.
+bool lazy_zero_ok(const mgp_ctx* c, const Level& L)
+{
+    const int l = (int)(&L - c->lev.data());
+    return c->zbuf && c->o.smoother == MGP_RBGS && !L.fused && l != c->tail_level && l != c->handoff_level &&
+           L.alloc <= c->zbuf_reals;
+}
+
 int zero_level(mgp_ctx* c, Level& L)
 {
+    if (lazy_zero_ok(c, L)) {
+        L.zero_pending = true;
+        L.ghost_ok = true;
+        return MGP_OK;
+    }
     HIP_TRY(c, hipMemsetAsync(L.u, 0, (size_t)L.alloc * c->rb, c->s));
     L.ghost_ok = true;  // every rank's V is zero, so the ghost planes are current
     return MGP_OK;
@@ -941,6 +962,7 @@ static void destroy_impl(mgp_ctx* c)
         if (L.f) (void)hipFree(L.f);
         if (L.t) (void)hipFree(L.t);
     }
+    if (c->zbuf) (void)hipFree(c->zbuf);
     if (c->psi_old) (void)hipFree(c->psi_old);
     if (c->stage) (void)hipFree(c->stage);
     if (c->d_part) (void)hipFree(c->d_part);
@@ -1101,6 +1123,18 @@ static int create_impl(mgp_ctx** out, const mgp_opts* o, mgp_loopback* lb)
         c->use_graph = c->o.world == 1 && !(v && std::atoi(v) == 0);
     }
     plan_tail(c);
+    if (c->o.smoother == MGP_RBGS && c->o.coarse_init == MGP_COARSE_FRESH) {
+        for (size_t l = 1; l < c->lev.size(); ++l)
+            if (!c->lev[l].fused && (c->tail_level < 0 || (int)l < c->tail_level))
+                c->zbuf_reals = std::max(c->zbuf_reals, c->lev[l].alloc);
+        const size_t zb = (size_t)c->zbuf_reals * rb;
+        if (zb && (hipMalloc(&c->zbuf, zb) != hipSuccess || hipMemsetAsync(c->zbuf, 0, zb, c->s) != hipSuccess)) {
+            c->err = "hipMalloc failed for the zero buffer";
+            return bail(MGP_ERR_OOM);
+        }
+        const char* v = std::getenv("MGP_LAZY_ZERO");  // 0: memset every fresh coarse guess instead
+        if (v && std::atoi(v) == 0) c->zbuf_reals = 0;
+    }
     he = mgp::prepare_kernels(c->rb);
     if (he != hipSuccess) {
         c->err = std::string("hipFuncSetAttribute (dynamic LDS): ") + hipGetErrorString(he);

@@ -316,6 +316,28 @@ def test_fused_timing_kinds(monkeypatch):
 
 
 @pytest.mark.parametrize("kw", [
+    dict(dim=3, n=(64, 64, 64), real="float", prolong="linear", coarse_bc="consistent"),
+    dict(dim=3, n=(128, 64, 32), real="double", prolong="pc", cycle="F"),
+    dict(dim=2, n=(256, 256, 1), real="float", prolong="linear", coarse_bc="consistent"),
+], ids=["3d-f32", "3d-F-f64", "2d-f32"])
+def test_lazy_zero_equals_memset(kw, monkeypatch):
+    """A fresh coarse guess read from the shared zero buffer by the first red half-sweep (no memset)
+    == zeroing u with a memset, bit for bit, with the coarse tail on and off."""
+    kw = dict(smoother="rbgs", nu1=2, nu2=2, **kw)
+    for tail in ("1", "0"):
+        monkeypatch.setenv("MGP_TAIL", tail)
+        monkeypatch.setenv("MGP_LAZY_ZERO", "0")
+        a = _ctx(**kw)
+        monkeypatch.delenv("MGP_LAZY_ZERO")
+        b = _ctx(**kw)
+        a.init_point_charge()
+        b.init_point_charge()
+        ea, eb = a.cycles(3), b.cycles(3)
+        assert np.array_equal(a.get_psi(), b.get_psi())
+        assert list(ea) == list(eb)
+
+
+@pytest.mark.parametrize("kw", [
     dict(real="float", smoother="rbgs", nu1=2, nu2=2, prolong="linear", coarse_bc="consistent"),
     dict(real="double", smoother="jacobi", nu1=2, nu2=2, prolong="pc"),
 ], ids=["rbgs-f32", "jacobi-f64"])
