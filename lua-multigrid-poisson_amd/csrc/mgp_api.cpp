@@ -113,7 +113,7 @@ struct Level {
     bool fghost_ok = true;  // f's ghost planes likewise
     bool fused = false;     // smoothing phases run temporally blocked (k_zs); needs t
     bool zero_pending = false;  // u is logically 0: the next red half-sweep reads c->zbuf instead
-    int zc = 0;             // k_zs z-chunk (planes per workgroup)
+    int zc = 0, zc_pre = 0;  // k_zs z-chunks (planes per workgroup) of POST and PRE
 };
 
 // Loopback transport (tests): the ranks of a slab decomposition as contexts of one process on
@@ -563,7 +563,7 @@ int fused_pre(mgp_ctx* c, int l, double h)
     a.gc = gc;
     a.h = h;
     a.cl = coarse_coef(c->o.coarse_bc, l);
-    a.zc = L.zc;
+    a.zc = L.zc_pre;
     a.ghost = c->G;
     hipEvent_t e;
     TRY(timed_begin(c, l, &e));
@@ -1072,7 +1072,10 @@ static int create_impl(mgp_ctx** out, const mgp_opts* o, mgp_loopback* lb)
         for (size_t l = 0; l + 1 < c->lev.size(); ++l) {
             Level& L = c->lev[l];
             L.fused = on && level_cells(L) >= min_cells && mgp::fused_supported(c->rb, c->o.dim, 2, L.g);
-            if (L.fused) L.zc = mgp::fused_zc(c->rb, L.g);
+            if (L.fused) {
+                L.zc = mgp::fused_zc(c->rb, L.g, false);
+                L.zc_pre = mgp::fused_zc(c->rb, L.g, true);
+            }
             if (L.fused && L.p.dist) c->G = mgp::kGhostZs;
         }
     }

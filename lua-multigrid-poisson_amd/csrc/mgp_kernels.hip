@@ -844,6 +844,9 @@ __device__ __forceinline__ void lds_barrier()
 #ifndef ZS_NPOST_F32
 #define ZS_NPOST_F32 2
 #endif
+#ifndef ZS_TYPRE_F32
+#define ZS_TYPRE_F32 32
+#endif
 // Prefetch distance in steps: the loads of plane p + D are issued while plane p is computed.
 // D = 2 costs 3 register buffers and measured slower than D = 1 at 512^3 (601 / 878 us against
 // 579 / 787 us for PRE / POST).
@@ -854,18 +857,18 @@ template <typename T>
 struct ZsTile;
 template <>
 struct ZsTile<float> {
-    static constexpr int TX = 64, TY = 32, NPRE = ZS_NPRE_F32, NPOST = ZS_NPOST_F32;
+    static constexpr int TX = 64, TYPRE = ZS_TYPRE_F32, TYPOST = 32, NPRE = ZS_NPRE_F32, NPOST = ZS_NPOST_F32;
 };
 template <>
 struct ZsTile<double> {
-    static constexpr int TX = 64, TY = 16, NPRE = 2, NPOST = 2;
+    static constexpr int TX = 64, TYPRE = 16, TYPOST = 16, NPRE = 2, NPOST = 2;
 };
 constexpr int kZsHX = 8;  // x halo cells per side (>= the trapezoid depth, whole groups)
 
 template <typename T, bool PRE>
 struct ZsShape {
     static constexpr int N = PRE ? ZsTile<T>::NPRE : ZsTile<T>::NPOST;
-    static constexpr int TX = ZsTile<T>::TX, TY = ZsTile<T>::TY;
+    static constexpr int TX = ZsTile<T>::TX, TY = PRE ? ZsTile<T>::TYPRE : ZsTile<T>::TYPOST;
     static constexpr int H = PRE ? 5 : 4;              // y/z halo = stages that read neighbours
     static constexpr int HWE = (TX + 2 * kZsHX) / 2;   // reals per LDS half-row
     static constexpr int G = HWE / N;                  // column groups per row
@@ -874,7 +877,7 @@ struct ZsShape {
     static constexpr int NT = G * YE;                  // threads with a column
     static constexpr int NTL = (NT + 63) / 64 * 64;    // launched threads
     static constexpr int SLOT = YE * HWE;              // reals per LDS slot (one colour of a plane)
-    static constexpr int NS3 = PRE ? 4 : 2;            // stage-3 slots (PRE's residual reads 2 back)
+    static constexpr int NS3 = PRE ? 3 : 2;            // stage-3 slots (PRE's residual reads 2 back)
     static constexpr int OFF1 = 2 * SLOT, OFF2 = 4 * SLOT, OFF3 = 6 * SLOT, OFF4 = OFF3 + NS3 * SLOT;
     static constexpr int OFFX = OFF4 + (PRE ? 2 * SLOT : 0);
     static constexpr int XPAIRS = YE / 2 + 1;          // row pairs of the residual hand-off
@@ -1137,7 +1140,11 @@ __global__ __launch_bounds__((ZsShape<T, PRE>::NTL)) void k_zs(const T* __restri
     const int p_end = Z0 + zc + (PRE ? 5 : 3);
     auto inz = [&](int q) { return z0 + q >= 0 && z0 + q < gnz; };  // inside the global box
     auto pcl = [&](int q) { return q < qlo ? qlo : (q > qhi ? qhi : q); };
-    auto slot = [&](int off, int ns, int q) { return lds + off + (q & (ns - 1)) * SLOT; };
+    // ring slot of plane q (q may be negative; ns = 3 as q mod 3)
+    auto slot = [&](int off, int ns, int q) {
+        const int r = ns == 3 ? ((q % 3) + 3) % 3 : (q & (ns - 1));
+        return lds + off + r * SLOT;
+    };
     auto nbyz = [&](int q) {
         return CLZ ? 0 : (gy == 0) + (gy == g.ny - 1) + (z0 + q == 0) + (z0 + q == gnz - 1);
     };
@@ -1772,7 +1779,7 @@ static hipError_t zs_launch(const FusedArgs& a, hipStream_t s)
 {
     using S = ZsShape<T, PRE>;
     const Op<T, 3> op = make_op<T, 3>(a.h, a.cl);
-    const unsigned nb = (unsigned)fused_blocks(sizeof(T), a.g, a.zc);
+    const unsigned nb = (unsigned)((a.g.nx / S::TX) * (a.g.ny / S::TY) * (a.g.nz / a.zc));
     k_zs<T, PRE, LINEAR, ERR, CLZ><<<nb, S::NTL, S::lds_bytes, s>>>((const T*)a.src, (const T*)a.f, (T*)a.dst,
                                                                      (T*)a.R, (const T*)a.V, a.partials, a.g, a.gc,
                                                                      op, (T)a.clc, a.zc, a.ghost);
@@ -1788,10 +1795,13 @@ static hipError_t fused_dispatch(const FusedArgs& a, hipStream_t s)
     return err ? zs_launch<T, false, 0, true, CLZ>(a, s) : zs_launch<T, false, 0, false, CLZ>(a, s);
 }
 
-static void zs_tile(int rb, int& tx, int& ty)
+// tile of a phase (pre) or the tallest of both (pre < 0)
+static void zs_tile(int rb, int& tx, int& ty, int pre = -1)
 {
     tx = rb == 4 ? ZsTile<float>::TX : ZsTile<double>::TX;
-    ty = rb == 4 ? ZsTile<float>::TY : ZsTile<double>::TY;
+    const int a = rb == 4 ? ZsTile<float>::TYPRE : ZsTile<double>::TYPRE;
+    const int b = rb == 4 ? ZsTile<float>::TYPOST : ZsTile<double>::TYPOST;
+    ty = pre < 0 ? (a > b ? a : b) : (pre ? a : b);
 }
 
 bool fused_supported(int rb, int dim, int ns, const Geo& g)
@@ -1804,10 +1814,10 @@ bool fused_supported(int rb, int dim, int ns, const Geo& g)
 
 // planes per workgroup: halve the z-chunk until there are >= MGP_ZS_WGS (default 256, one per CU)
 // workgroups or a chunk would drop below 16 planes
-int fused_zc(int rb, const Geo& g)
+int fused_zc(int rb, const Geo& g, bool pre)
 {
     int TX, TY;
-    zs_tile(rb, TX, TY);
+    zs_tile(rb, TX, TY, pre ? 1 : 0);
     static const int64_t target = [] {
         const char* v = std::getenv("MGP_ZS_WGS");
         return v ? std::atoll(v) : (int64_t)256;
@@ -1818,10 +1828,10 @@ int fused_zc(int rb, const Geo& g)
     return (int)(g.nz / chunks);
 }
 
-int fused_blocks(int rb, const Geo& g, int zc)
+int fused_blocks(int rb, const Geo& g, int zc)  // POST's workgroups (one err partial each)
 {
     int TX, TY;
-    zs_tile(rb, TX, TY);
+    zs_tile(rb, TX, TY, 0);
     return (int)((int64_t)(g.nx / TX) * (g.ny / TY) * (g.nz / zc));
 }
 
