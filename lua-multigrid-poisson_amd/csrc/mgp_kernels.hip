@@ -844,6 +844,8 @@ __device__ __forceinline__ void lds_barrier()
 #ifndef ZS_NPOST_F32
 #define ZS_NPOST_F32 2
 #endif
+// PRE tile height: 64 (less y halo, 12 waves) spills at the 168-VGPR cap and measured slower
+// (640 against 578 us)
 #ifndef ZS_TYPRE_F32
 #define ZS_TYPRE_F32 32
 #endif
@@ -877,7 +879,8 @@ struct ZsShape {
     static constexpr int NT = G * YE;                  // threads with a column
     static constexpr int NTL = (NT + 63) / 64 * 64;    // launched threads
     static constexpr int SLOT = YE * HWE;              // reals per LDS slot (one colour of a plane)
-    static constexpr int NS3 = PRE ? 3 : 2;            // stage-3 slots (PRE's residual reads 2 back)
+    // stage-3 slots: PRE's residual reads 2 back (3 needed; 4 while LDS allows: power-of-2 ring)
+    static constexpr int NS3 = PRE ? (TY > 32 ? 3 : 4) : 2;
     static constexpr int OFF1 = 2 * SLOT, OFF2 = 4 * SLOT, OFF3 = 6 * SLOT, OFF4 = OFF3 + NS3 * SLOT;
     static constexpr int OFFX = OFF4 + (PRE ? 2 * SLOT : 0);
     static constexpr int XPAIRS = YE / 2 + 1;          // row pairs of the residual hand-off
