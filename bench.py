@@ -40,7 +40,7 @@ def parse():
     p.add_argument("--nu", type=int, default=2)
     p.add_argument("--no-timing", action="store_true", help="skip the per-launch smoother events")
     p.add_argument("--cpu-cycles", type=int, default=2, help="oracle cycles timed for cpu_baseline (0 = skip)")
-    p.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "r01_pmc_traffic.json"),
+    p.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "r01_final_pmc_traffic.json"),
                    help="JSON with the PMC-measured HBM bytes per launch of the dominant kernel (tools/pmc_traffic.py); "
                         "used only when its kernel name matches")
     return p.parse_args()
