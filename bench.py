@@ -8,10 +8,15 @@ GPU; 4096^3 needs >= 4 GPUs).  fp32, trilinear prolongation, 2x2x
 restriction, consistent coarse boundary, point-charge RHS (cpu.lua:182-193), and the
 reference's per-cycle err = RMS update (cpu.lua:200-203) computed on the device every cycle.
 
-Scaling: weak.  Each rank owns a 512^3 z-slab of a 512 x 512 x (512 N) box; the V-cycle is
-domain-decomposed with RCCL halo exchange after every smoothing half-sweep and an all-gather
-onto every rank once a level has <= 32768 cells.  value = (N slabs x K cycles) / max-rank
-time, i.e. 512^3-cell V-cycles per second for the whole job (= plain V-cycles/s at N=1).
+Scaling (default): weak.  Each rank owns a 512^3 z-slab of a 512 x 512 x (512 N) box; the V-cycle
+is domain-decomposed with RCCL halo exchange (per half-sweep, or once per temporally blocked phase)
+and an all-gather onto every rank once a level has <= 32768 cells.  value = (N slabs x K cycles) /
+max-rank time, i.e. 512^3-cell V-cycles per second for the whole job (= plain V-cycles/s at N=1).
+
+--box NX,NY,NZ: strong scaling of one global box split into N z-slabs (BASELINE configs[3]:
+--box 2048,2048,2048; configs[4]: --box 4096,4096,4096 --cycle F).  On one GPU, --box 2048,2048,256
+and --box 4096,4096,512 run one rank's slab of those configs.  value = cycles/s of the whole box.
+--dim 2 --n 4096: BASELINE configs[1] (2D 4096^2 RB-GS, cache-resident: flagged in the line).
 
 Launch: python bench.py [--gpus N --steps K --warmup W]  (N>1 under torch.distributed.run).
 """
@@ -34,13 +39,17 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
-    p.add_argument("--n", type=int, default=512, help="cells per axis of each rank's cube slab")
+    p.add_argument("--n", type=int, default=512, help="cells per axis of each rank's cube slab (weak scaling)")
+    p.add_argument("--box", default=None, help="NX,NY,NZ global box, strong scaling over the ranks (slab-z)")
+    p.add_argument("--dim", type=int, default=3, choices=[2, 3])
     p.add_argument("--real", default="float", choices=["float", "double"])
     p.add_argument("--cycle", default="V", choices=["V", "F"])
     p.add_argument("--nu", type=int, default=2)
     p.add_argument("--no-timing", action="store_true", help="skip the per-launch smoother events")
     p.add_argument("--cpu-cycles", type=int, default=2, help="oracle cycles timed for cpu_baseline (0 = skip)")
-    p.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "r01_final_pmc_traffic.json"),
+    p.add_argument("--cpu-threads", type=int, default=0,
+                   help="threads of the OpenMP cpu_baseline (0 = OMP_NUM_THREADS or all host cores)")
+    p.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "pmc_traffic_current.json"),
                    help="JSON with the PMC-measured HBM bytes per launch of the dominant kernel (tools/pmc_traffic.py); "
                         "used only when its kernel name matches")
     return p.parse_args()
@@ -67,13 +76,26 @@ def main():
         comm_id = obj[0]
 
     n = a.n
-    cfg = dict(dim=3, n=(n, n, n * world), real=a.real, smoother="rbgs", nu1=a.nu, nu2=a.nu, cycle=a.cycle,
+    if a.box:
+        box = tuple(int(x) for x in a.box.split(","))
+        if len(box) != 3:
+            raise SystemExit("--box takes NX,NY,NZ")
+        strong = True
+    elif a.dim == 2:
+        if world != 1:
+            raise SystemExit("2D runs are single-GPU (the slab decomposition is 3D)")
+        box, strong = (n, n, 1), False
+    else:
+        box, strong = (n, n, n * world), False
+    cfg = dict(dim=a.dim if not a.box else 3, n=box, real=a.real, smoother="rbgs", nu1=a.nu, nu2=a.nu, cycle=a.cycle,
                prolong="linear", coarse_bc="consistent", coarse_init="fresh", err_mode=1, device=local,
                rank=rank, world=world, comm_id=comm_id)
     ctx = mgpoisson.Context(mgpoisson.make_opts(**cfg))
     ctx.init_point_charge()
     rb = 4 if a.real == "float" else 8
-    cells_rank = n * n * n
+    lv0 = ctx.levels[0]
+    cells_rank = lv0["nx"] * lv0["ny"] * (lv0["nz_local"] if cfg["dim"] == 3 else 1)
+    free_b, total_b = torch.cuda.mem_get_info(local)
 
     def barrier_sync():
         ctx.sync()
@@ -106,32 +128,56 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
 
-    value = world * a.steps / dt
+    value = (1 if strong else world) * a.steps / dt
+    kind = "V" if a.cycle == "V" else "F"
+    gcells = box[0] * box[1] * box[2]
+    if strong:
+        named = {(2048, 2048, 2048): "BASELINE configs[3]: 3D Poisson 2048^3",
+                 (4096, 4096, 4096): "BASELINE configs[4]: 3D Poisson 4096^3 fp32 F-cycle"}
+        slab = {(2048, 2048, 256): "one rank's slab of BASELINE configs[3] (2048^3 / 8 ranks)",
+                (4096, 4096, 512): "one rank's slab of BASELINE configs[4] (4096^3 / 8 ranks)"}
+        wl = named.get(box) or (slab.get(box) if world == 1 else None) or f"3D Poisson {box[0]}x{box[1]}x{box[2]}"
+        workload = f"{wl}, 7-point, RB-GS {a.nu}+{a.nu}, {kind}-cycle, trilinear P, 2x2x2-average R, per-cycle RMS-update err"
+        unit = f"{kind}-cycles/s ({box[0]}x{box[1]}x{box[2]} box, whole job)"
+    elif cfg["dim"] == 2:
+        uf_mb = 2 * n * n * rb / 1e6
+        workload = (f"BASELINE configs[1]: 2D Poisson {n}^2, 5-point, RB-GS {a.nu}+{a.nu}, {kind}-cycle, bilinear P, "
+                    f"2x2-average R, per-cycle RMS-update err; u+f = {uf_mb:.0f} MB "
+                    + ("fit the 256 MB Infinity Cache (MALL-resident: GB/s can exceed HBM)" if uf_mb < 256
+                       else "exceed the 256 MB Infinity Cache"))
+        unit = f"{kind}-cycles/s ({n}^2)"
+    else:
+        workload = (f"BASELINE configs[2]: 3D Poisson {n}^3 per GPU, 7-point, RB-GS {a.nu}+{a.nu}, {kind}-cycle, "
+                    "trilinear P, 2x2x2-average R, per-cycle RMS-update err")
+        unit = f"{kind}-cycles/s ({n}^3-cell slabs, whole job)"
+    rnorm, fnorm = ctx.residual_norm()
     line = {
         "metric": "V-cycles/sec + finest-smoother achieved HBM GB/s, 3D Poisson",
         "value": value,
-        "unit": "V-cycles/s (512^3-cell slabs, whole job)" if a.cycle == "V" else "F-cycles/s (512^3-cell slabs, whole job)",
+        "unit": unit,
         "n_gpus": world,
         "steps": a.steps,
         "warmup": a.warmup,
         "ms_per_step": 1e3 * dt / a.steps,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if strong else "weak",
         "vs_baseline": None,
         "dtype": "f32" if a.real == "float" else "f64",
         "data": "synthetic point-charge RHS (cpu.lua:182-193), psi0 = -f",
         "config": {
-            "workload": f"BASELINE configs[2]: 3D Poisson {n}^3 per GPU, 7-point, RB-GS {a.nu}+{a.nu}, {a.cycle}-cycle, "
-                        "trilinear P, 2x2x2-average R, per-cycle RMS-update err",
-            "global_box": [n, n, n * world],
-            "parallelism": f"slab-z x{world} (RCCL halo per half-sweep)" if world > 1 else "single GPU",
+            "workload": workload,
+            "global_box": list(box),
+            "rank_slab": [lv0["nx"], lv0["ny"], lv0["nz_local"]],
+            "parallelism": (f"slab-z x{world} (RCCL halo exchange)" if world > 1 else "single GPU"),
             "levels": len(ctx.levels),
         },
         "final_err": float(errs[-1]),
+        "relative_residual": rnorm / fnorm,
+        "hbm_used_GB_rank0": (total_b - free_b) / 1e9,
     }
     tname = "float" if a.real == "float" else "double"
     lin = 1
-    kernels = {"half_sweep": f"k_half<{tname}, 3, 1, false>",
+    kernels = {"half_sweep": f"k_half<{tname}, {cfg['dim']}, 1, false>",
                "fused_pre": f"k_zs<{tname}, true, 0, false, true>",
                "fused_post": f"k_zs<{tname}, false, {lin}, true, true>"}
     # Algorithmic bytes per level-0 cell of one launch (reals): what the launch must move
@@ -140,7 +186,7 @@ def main():
     # fused_post (k_zs: prolongation + correction + 2 sweeps + err): read black u, V/8, f, psiOld; write u.
     algo_reals = {"half_sweep": 1.5, "fused_pre": 2.625, "fused_post": 3.625}
     per_kind = {k: v for k, v in timed.items() if v[1] > 0}
-    cells = n * n * n
+    cells = cells_rank
     if per_kind:
         # per kind: (ms, launches, algorithmic bytes, reference-path bytes as the library counts them:
         # SURVEY.md §8(d) per-sweep accounting, i.e. what one launch per half-sweep would move)
@@ -158,18 +204,25 @@ def main():
                 "frac": achieved / HBM_PEAK_GBPS, "traffic": None, "kernel": kernels[dom],
                 "algorithmic_bytes_per_launch": ab / cnt, "avg_launch_us": 1e3 * ms / cnt,
                 "window": f"{a.steps} cycles after the timed region, HIP events around each launch"}
+        # PMC traffic is measured by a separate rocprofv3 pass (tools/gpu_round.sh), never in this run; it
+        # is used only when it was measured on this exact kernel source and workload
+        roof["traffic_measured_this_run"] = False
         if a.traffic and os.path.exists(a.traffic):
             with open(a.traffic) as fh:
                 tr = json.load(fh)
-            ent = tr.get("kernels", {}).get(kernels[dom]) if "kernels" in tr else (
-                tr if tr.get("kernel") == kernels[dom] else None)
-            if ent:
+            ent = tr.get("kernels", {}).get(kernels[dom])
+            src_ok = tr.get("source_hash") == source_hash()
+            wl_ok = tr.get("cells_rank") in (None, cells_rank)
+            roof["traffic_source"] = os.path.relpath(a.traffic, ROOT)
+            roof["traffic_source_matches_build"] = bool(src_ok and wl_ok)
+            if ent and src_ok and wl_ok:
                 roof["traffic"] = ent.get("bytes_per_launch")
-                roof["traffic_source"] = os.path.relpath(a.traffic, ROOT)
         line["roofline"] = roof
 
     if rank == 0 and world == 1 and a.cpu_cycles > 0:
-        line["cpu_baseline"] = cpu_baseline(cfg, a.cpu_cycles)
+        thr = a.cpu_threads or int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
+        line["cpu_baseline"] = cpu_baseline(cfg, a.cpu_cycles * 2, thr, gcells)
+        line["cpu_baseline_1thread"] = cpu_baseline(cfg, a.cpu_cycles, 1, gcells)
     if rank == 0:
         print(json.dumps(line), flush=True)
     ctx.close()
@@ -177,22 +230,44 @@ def main():
         dist.destroy_process_group()
 
 
-def cpu_baseline(cfg, cycles):
-    """The C oracle (the build's restatement of the reference CPU path) on this host, 1 thread."""
+def source_hash():
+    """sha256 (16 hex) of the library's kernel and ABI sources: tags PMC traffic to the build it measured."""
+    import hashlib
+
+    h = hashlib.sha256()
+    for f in ("mgp_kernels.hip", "mgp_api.cpp", "mgp_internal.h"):
+        with open(os.path.join(ROOT, "lua-multigrid-poisson_amd", "csrc", f), "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+def cpu_baseline(cfg, cycles, threads, gcells):
+    """The C oracle (the build's restatement of the reference CPU path) on this host.
+
+    Bounded sample: the workload itself when it has <= 512^3 cells, else a 512^3 (3D) box of the same
+    algorithm, scaled to the workload by cells (labelled extrapolated)."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     from oracle_lib import Oracle
 
     kw = {k: cfg[k] for k in ("dim", "n", "real", "smoother", "nu1", "nu2", "cycle", "prolong", "coarse_bc", "coarse_init")}
-    o = Oracle(threads=1, **kw)
+    scale = 1.0
+    if gcells > 512 ** 3:
+        kw["n"] = (512, 512, 512)
+        scale = 512 ** 3 / gcells
+    o = Oracle(threads=threads, **kw)
     o.init_point_charge()
     t0 = time.perf_counter()
     for _ in range(cycles):
         o.step()
     dt = time.perf_counter() - t0
-    return {"value": cycles / dt, "unit": "V-cycles/s (512^3)" if cfg["cycle"] == "V" else "F-cycles/s (512^3)",
-            "cores": 1, "kind": "port",
-            "sample": f"{cycles} full cycles of the same 3D {cfg['n'][0]}^3 workload, oracle/mgp_oracle.c "
-                      f"(gcc -O2, -ffp-contract=off), single thread like the reference, {dt:.1f} s"}
+    n = kw["n"]
+    kind = "V" if cfg["cycle"] == "V" else "F"
+    sample = (f"{cycles} full {kind}-cycles of {n[0]}x{n[1]}x{n[2] if cfg['dim'] == 3 else 1} with the same "
+              f"algorithm, oracle/mgp_oracle.c (gcc -O2, -ffp-contract=off), {threads} thread(s), {dt:.1f} s")
+    if scale != 1.0:
+        sample += "; EXTRAPOLATED to the workload's cells (x %.3g)" % scale
+    return {"value": scale * cycles / dt, "unit": f"{kind}-cycles/s (same workload)", "cores": threads,
+            "kind": "port", "sample": sample}
 
 
 if __name__ == "__main__":

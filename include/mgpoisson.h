@@ -64,6 +64,12 @@ typedef struct mgp_opts {
     int64_t gather_cells;  /* a level with <= this many cells is replicated on every rank */
     uint8_t comm_id[MGP_COMM_ID_BYTES]; /* from mgp_comm_unique_id() on rank 0 (world > 1) */
 } mgp_opts;
+/* The layout is part of the ABI (LuaJIT cdef, ctypes mirror): a change must bump MGP_API_VERSION. */
+#ifdef __cplusplus
+static_assert(sizeof(mgp_opts) == 224, "mgp_opts layout changed");
+#else
+_Static_assert(sizeof(mgp_opts) == 224, "mgp_opts layout changed");
+#endif
 
 typedef struct mgp_ctx mgp_ctx;
 
@@ -92,6 +98,17 @@ int         mgp_init_point_charge(mgp_ctx* c);
  * Replaces direct access to mg.psi / mg.f (cpu.lua) and .psi.buffer / .f.buffer (cpu-raw.lua). */
 int         mgp_set_field(mgp_ctx* c, int level, int which, const void* src, int64_t count, int mem);
 int         mgp_get_field(const mgp_ctx* c, int level, int which, void* dst, int64_t count, int mem);
+
+/* Plane ranges of a level's field: local planes [z_begin, z_begin + nz) of this rank's slab, nz * ny * nx
+ * reals, x fastest.  Host transfers stream through a bounded staging buffer (~256 MiB), so fields
+ * far larger than host-convenient (a 4096 x 4096 x 512 fp32 slab is 34 GB) can be read piecewise. */
+int         mgp_set_planes(mgp_ctx* c, int level, int which, int64_t z_begin, int64_t nz, const void* src, int mem);
+int         mgp_get_planes(const mgp_ctx* c, int level, int which, int64_t z_begin, int64_t nz, void* dst, int mem);
+/* Device-side fingerprint of this rank's part of a field, for comparing runs that cannot come to the
+ * host: *hash = sum mod 2^64 over cells of mix64(bits(x) ^ mix64(global lexicographic index)) (order-
+ * and decomposition-independent: the ranks' hashes add up to the global one, and two fields hash
+ * equal when they are bit-identical), stats = {sum x, sum x^2, max |x|} in fp64. */
+int         mgp_field_stats(const mgp_ctx* c, int level, int which, uint64_t* hash, double stats[3]);
 
 /* One outer iteration = MultigridCPU:step() (cpu.lua:196-206): psiOld = psi; one V/F-cycle from
  * the finest level with h = 1/n; *err_out = sqrt(sum (psi - psiOld)^2 / N) (NaN if err_mode 0). */
@@ -132,6 +149,13 @@ int         mgp_set_coarse_handoff(mgp_ctx* c, int64_t size, mgp_coarse_fn fn, v
  * rel_err = mean of |1 - psi/psiOld| over the cells where it is nonzero, count = their number,
  * frob = sqrt(sum (psi - psiOld)^2 / N).  Needs err_mode 1. */
 int         mgp_metrics(mgp_ctx* c, double* rel_err, int64_t* count, double* frob);
+
+/* Residual norm of a level (north star: "wavefront-level reductions for the residual norm"):
+ * *rnorm = ||f - A u||_2 with the level's operator (calcResidual, cpu.lua:108-123, never materialised),
+ * *fnorm = ||f||_2; squares summed in fp64 per wave (butterfly), per workgroup and then in a fixed
+ * order, all-reduced over the ranks on a distributed level.  Level 0 after a cycle gives the
+ * converged relative residual ||r|| / ||f||. */
+int         mgp_residual_norm(mgp_ctx* c, int level, double* rnorm, double* fnorm);
 
 /* Loopback transport (tests only): the `world` ranks of a slab decomposition as contexts of ONE
  * process on one GPU, each driven by its own host thread.  Halo exchanges, the all-gather and the

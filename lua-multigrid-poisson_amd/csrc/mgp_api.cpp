@@ -159,12 +159,16 @@ struct mgp_ctx {
     // psiOld of the last outer iteration (for mgp_metrics), nullptr when not kept
     const char* metrics_old = nullptr;
     double* d_metrics = nullptr;  // 3 * kSumBlocks partials + 3 results
+    double* d_rn = nullptr;       // residual-norm partials (+ 2 results), d_rn_cap doubles
+    int64_t d_rn_cap = 0;
     char* psi_old = nullptr;  // snapshot buffer (Jacobi path)
     // an all-zero buffer of the largest lazily zeroed level's layout: a fresh coarse guess (cpu.lua:138)
     // costs no memset, the first red half-sweep reads its black neighbours from here
     char* zbuf = nullptr;
     int64_t zbuf_reals = 0;
-    char* stage = nullptr;    // lexicographic staging buffer for set/get (level-0 size)
+    char* stage = nullptr;    // lexicographic staging buffer for host set/get (bounded: whole planes in chunks)
+    size_t stage_bytes = 0;
+    uint64_t* d_stats_h = nullptr;  // mgp_field_stats scratch: kSumBlocks + 1 hashes, then 3 kSumBlocks + 3 doubles
     double* d_part = nullptr;
     int64_t part_cap = 0;
     double* d_errs = nullptr;
@@ -410,6 +414,8 @@ int64_t level_count(const Level& L) { return L.p.nx * L.p.ny * (L.g.nz); }
 
 // ---- cycle pieces ----
 
+int materialize_zero(mgp_ctx* c, Level& L);
+
 // One half-sweep (colour `color`) reading `other`, writing `dst`; level-0 launches are timed.
 int half(mgp_ctx* c, int l, int color, char* other, char* dst, const char* old, double h, double cl, int part_off)
 {
@@ -477,6 +483,7 @@ int residual_restrict(mgp_ctx* c, int l, double h)
 {
     Level& L = c->lev[l];
     Level& C = c->lev[l + 1];
+    TRY(materialize_zero(c, L));
     TRY(exchange(c, L));
     int64_t zc = 0;
     const Geo gc = coarse_view(L, C, &zc);
@@ -500,6 +507,8 @@ int prolong_correct(mgp_ctx* c, int l)
     Level& L = c->lev[l];
     Level& C = c->lev[l + 1];
     const int linear = c->o.prolong == MGP_PROLONG_LINEAR;
+    TRY(materialize_zero(c, L));
+    TRY(materialize_zero(c, C));
     if (linear && C.p.dist) TRY(exchange(c, C));
     int64_t zc = 0;
     const Geo gc = coarse_view(L, C, &zc);
@@ -519,12 +528,15 @@ int coarse_solve_at(mgp_ctx* c, int l, double h)
 
 // RB-GS levels outside the tail / hand-off / fused levels only need u = 0 as the black input of their
 // first red half-sweep (a Gauss-Seidel update never reads the value it replaces, and the black
-// half-sweep then reads the new red cells), so their zeroing is deferred to that sweep.
+// half-sweep then reads the new red cells), so their zeroing is deferred to that sweep.  That sweep
+// is the first thing the next cycle_rec does on the level only when nu1 >= 1 (the coarsest level's
+// solve always sweeps); with nu1 == 0 the residual would read the stale u, so the zero is real then.
 bool lazy_zero_ok(const mgp_ctx* c, const Level& L)
 {
     const int l = (int)(&L - c->lev.data());
-    return c->zbuf && c->o.smoother == MGP_RBGS && !L.fused && l != c->tail_level && l != c->handoff_level &&
-           L.alloc <= c->zbuf_reals;
+    const bool sweeps_first = c->o.nu1 >= 1 || l == (int)c->lev.size() - 1;
+    return c->zbuf && sweeps_first && c->o.smoother == MGP_RBGS && !L.fused && l != c->tail_level &&
+           l != c->handoff_level && L.alloc <= c->zbuf_reals;
 }
 
 int zero_level(mgp_ctx* c, Level& L)
@@ -535,7 +547,19 @@ int zero_level(mgp_ctx* c, Level& L)
         return MGP_OK;
     }
     HIP_TRY(c, hipMemsetAsync(L.u, 0, (size_t)L.alloc * c->rb, c->s));
+    L.zero_pending = false;
     L.ghost_ok = true;  // every rank's V is zero, so the ghost planes are current
+    return MGP_OK;
+}
+
+// Any reader of u other than the first red half-sweep (the residual, the prolongation of the level
+// above, field I/O, a piece called through the ABI) sees a pending lazy zero as a real one.
+int materialize_zero(mgp_ctx* c, Level& L)
+{
+    if (!L.zero_pending) return MGP_OK;
+    HIP_TRY(c, hipMemsetAsync(L.u, 0, (size_t)L.alloc * c->rb, c->s));
+    L.zero_pending = false;
+    L.ghost_ok = true;
     return MGP_OK;
 }
 
@@ -965,6 +989,7 @@ static void destroy_impl(mgp_ctx* c)
     if (c->zbuf) (void)hipFree(c->zbuf);
     if (c->psi_old) (void)hipFree(c->psi_old);
     if (c->stage) (void)hipFree(c->stage);
+    if (c->d_stats_h) (void)hipFree(c->d_stats_h);
     if (c->d_part) (void)hipFree(c->d_part);
     if (c->d_errs) (void)hipFree(c->d_errs);
     if (c->d_err_cur) (void)hipFree(c->d_err_cur);
@@ -980,6 +1005,7 @@ static void destroy_impl(mgp_ctx* c)
     if (c->lb_ev2) (void)hipEventDestroy(c->lb_ev2);
     if (c->lb_red) (void)hipFree(c->lb_red);
     if (c->d_metrics) (void)hipFree(c->d_metrics);
+    if (c->d_rn) (void)hipFree(c->d_rn);
     if (c->s) (void)hipStreamDestroy(c->s);
     delete c;
 }
@@ -1102,9 +1128,16 @@ static int create_impl(mgp_ctx** out, const mgp_opts* o, mgp_loopback* lb)
         c->err = "hipMalloc failed for psiOld";
         return bail(MGP_ERR_OOM);
     }
-    if (hipMalloc(&c->stage, interior) != hipSuccess) {
-        c->err = "hipMalloc failed for the staging buffer";
-        return bail(MGP_ERR_OOM);
+    {
+        // staging for host I/O: at least one level-0 plane, at most ~256 MiB (or the whole interior)
+        const size_t plane = (size_t)(L0.p.nx * L0.p.ny) * rb;
+        c->stage_bytes = std::min(interior, std::max(plane, (size_t)256 << 20));
+        if (hipMalloc(&c->stage, c->stage_bytes) != hipSuccess ||
+            hipMalloc(&c->d_stats_h, sizeof(uint64_t) * (mgp::kSumBlocks + 1) + sizeof(double) * (3 * mgp::kSumBlocks + 3)) !=
+                hipSuccess) {
+            c->err = "hipMalloc failed for the staging buffer";
+            return bail(MGP_ERR_OOM);
+        }
     }
     {
         const char* v = std::getenv("MGP_GS");
@@ -1211,37 +1244,107 @@ int mgp_init_point_charge(mgp_ctx* c)
 }
 
 
+// Host <-> packed level I/O in plane chunks through the bounded staging buffer (a 4096 x 4096 x 512
+// slab is 34 GB per field; no full-size staging copy is ever allocated).
+static int planes_io(mgp_ctx* c, int level, int which, int64_t z_begin, int64_t nz, void* buf, int mem, bool to_device)
+{
+    if (check_level(c, level) != MGP_OK || (which != MGP_FIELD_U && which != MGP_FIELD_F) || !buf)
+        return c->fail(MGP_ERR_ARG, "field I/O: bad level / field / buffer");
+    Level& L = c->lev[level];
+    if (z_begin < 0 || nz < 0 || z_begin + nz > L.g.nz)
+        return c->fail(MGP_ERR_ARG, "field I/O: planes [%lld, %lld) outside the local slab of %lld planes",
+                       (long long)z_begin, (long long)(z_begin + nz), (long long)L.g.nz);
+    if (which == MGP_FIELD_U) TRY(materialize_zero(c, L));
+    char* base = c->ui(L, which == MGP_FIELD_U ? L.u : L.f);
+    const size_t rb = (size_t)c->rb;
+    const int64_t lex_plane = L.p.nx * L.p.ny;  // reals per plane, lexicographic
+    const int64_t per_chunk =
+        mem == MGP_MEM_DEVICE ? nz : std::max<int64_t>(1, (int64_t)(c->stage_bytes / (lex_plane * rb)));
+    for (int64_t z = z_begin; z < z_begin + nz; z += per_chunk) {
+        const int64_t cn = std::min(per_chunk, z_begin + nz - z);
+        Geo gs = L.g;
+        gs.nz = cn;
+        gs.z0 = L.g.z0 + z;
+        char* packed = base + (size_t)(z * L.g.P) * rb;
+        char* hb = (char*)buf + (size_t)((z - z_begin) * lex_plane) * rb;
+        const size_t bytes = (size_t)(cn * lex_plane) * rb;
+        if (to_device) {
+            const void* lex = hb;
+            if (mem != MGP_MEM_DEVICE) {
+                HIP_TRY(c, hipMemcpyAsync(c->stage, hb, bytes, hipMemcpyHostToDevice, c->s));
+                lex = c->stage;
+            }
+            HIP_TRY(c, mgp::launch_pack(c->rb, lex, packed, gs, c->s));
+        } else {
+            void* lex = mem == MGP_MEM_DEVICE ? (void*)hb : (void*)c->stage;
+            HIP_TRY(c, mgp::launch_unpack(c->rb, packed, lex, gs, c->s));
+            if (mem != MGP_MEM_DEVICE) {
+                HIP_TRY(c, hipMemcpyAsync(hb, c->stage, bytes, hipMemcpyDeviceToHost, c->s));
+                HIP_TRY(c, hipStreamSynchronize(c->s));  // the next chunk reuses the staging buffer
+            }
+        }
+    }
+    if (to_device) {
+        if (which == MGP_FIELD_U) L.ghost_ok = !L.p.dist;
+        else L.fghost_ok = !L.p.dist;
+    }
+    return sync_and_check(c);
+}
+
 int mgp_set_field(mgp_ctx* c, int level, int which, const void* src, int64_t count, int mem)
 {
-    if (!c || !src || check_level(c, level) != MGP_OK || (which != MGP_FIELD_U && which != MGP_FIELD_F))
-        return c ? c->fail(MGP_ERR_ARG, "mgp_set_field: bad argument") : MGP_ERR_ARG;
+    if (!c) return MGP_ERR_ARG;
+    if (check_level(c, level) != MGP_OK) return c->fail(MGP_ERR_ARG, "mgp_set_field: bad level %d", level);
     Level& L = c->lev[level];
     if (count != level_count(L))
         return c->fail(MGP_ERR_ARG, "mgp_set_field: count %lld != %lld", (long long)count, (long long)level_count(L));
-    const void* lex = src;
-    if (mem != MGP_MEM_DEVICE) {
-        HIP_TRY(c, hipMemcpyAsync(c->stage, src, (size_t)count * c->rb, hipMemcpyHostToDevice, c->s));
-        lex = c->stage;
-    }
-    HIP_TRY(c, mgp::launch_pack(c->rb, lex, c->ui(L, which == MGP_FIELD_U ? L.u : L.f), L.g, c->s));
-    if (which == MGP_FIELD_U) L.ghost_ok = !L.p.dist;
-    else L.fghost_ok = !L.p.dist;
-    return sync_and_check(c);
+    return planes_io(c, level, which, 0, L.g.nz, const_cast<void*>(src), mem, true);
 }
 
 int mgp_get_field(const mgp_ctx* cc, int level, int which, void* dst, int64_t count, int mem)
 {
     mgp_ctx* c = const_cast<mgp_ctx*>(cc);
-    if (!c || !dst || check_level(c, level) != MGP_OK || (which != MGP_FIELD_U && which != MGP_FIELD_F))
-        return c ? c->fail(MGP_ERR_ARG, "mgp_get_field: bad argument") : MGP_ERR_ARG;
+    if (!c) return MGP_ERR_ARG;
+    if (check_level(c, level) != MGP_OK) return c->fail(MGP_ERR_ARG, "mgp_get_field: bad level %d", level);
     Level& L = c->lev[level];
     if (count != level_count(L))
         return c->fail(MGP_ERR_ARG, "mgp_get_field: count %lld != %lld", (long long)count, (long long)level_count(L));
-    void* lex = mem == MGP_MEM_DEVICE ? dst : c->stage;
-    HIP_TRY(c, mgp::launch_unpack(c->rb, c->ui(L, which == MGP_FIELD_U ? L.u : L.f), lex, L.g, c->s));
-    if (mem != MGP_MEM_DEVICE)
-        HIP_TRY(c, hipMemcpyAsync(dst, c->stage, (size_t)count * c->rb, hipMemcpyDeviceToHost, c->s));
-    return sync_and_check(c);
+    return planes_io(c, level, which, 0, L.g.nz, dst, mem, false);
+}
+
+int mgp_set_planes(mgp_ctx* c, int level, int which, int64_t z_begin, int64_t nz, const void* src, int mem)
+{
+    if (!c) return MGP_ERR_ARG;
+    return planes_io(c, level, which, z_begin, nz, const_cast<void*>(src), mem, true);
+}
+
+int mgp_get_planes(const mgp_ctx* cc, int level, int which, int64_t z_begin, int64_t nz, void* dst, int mem)
+{
+    mgp_ctx* c = const_cast<mgp_ctx*>(cc);
+    if (!c) return MGP_ERR_ARG;
+    return planes_io(c, level, which, z_begin, nz, dst, mem, false);
+}
+
+int mgp_field_stats(const mgp_ctx* cc, int level, int which, uint64_t* hash, double stats[3])
+{
+    mgp_ctx* c = const_cast<mgp_ctx*>(cc);
+    if (!c) return MGP_ERR_ARG;
+    if (check_level(c, level) != MGP_OK || (which != MGP_FIELD_U && which != MGP_FIELD_F))
+        return c->fail(MGP_ERR_ARG, "mgp_field_stats: bad level / field");
+    Level& L = c->lev[level];
+    if (which == MGP_FIELD_U) TRY(materialize_zero(c, L));
+    uint64_t* hp = c->d_stats_h;
+    double* dp = (double*)(hp + mgp::kSumBlocks + 1);
+    HIP_TRY(c, mgp::launch_field_stats(c->rb, c->ui(L, which == MGP_FIELD_U ? L.u : L.f), L.g, hp, dp,
+                                       hp + mgp::kSumBlocks, dp + 3 * mgp::kSumBlocks, c->s));
+    uint64_t h = 0;
+    double d[3];
+    HIP_TRY(c, hipMemcpyAsync(&h, hp + mgp::kSumBlocks, sizeof h, hipMemcpyDeviceToHost, c->s));
+    HIP_TRY(c, hipMemcpyAsync(d, dp + 3 * mgp::kSumBlocks, sizeof d, hipMemcpyDeviceToHost, c->s));
+    TRY(sync_and_check(c));
+    if (hash) *hash = h;
+    if (stats) std::memcpy(stats, d, sizeof d);
+    return MGP_OK;
 }
 
 int mgp_cycles(mgp_ctx* c, int32_t k, double* errs)
@@ -1279,11 +1382,35 @@ int mgp_two_grid(mgp_ctx* c, double h, void* u, const void* f, int64_t L, int me
     for (int l = 0; l < (int)c->lev.size(); ++l) {
         Level& Lv = c->lev[l];
         if (Lv.p.nx != L) continue;
+        // twoGrid(h, u, f, L) works on the caller's buffers (cpu-raw.lua:186, gpu.lua:296): the level's
+        // own u / f (on level 0 the solver's psi and RHS) are saved and put back afterwards.  The
+        // levels below are the cycle's scratch (rs, Rs, vs, Vs of cpu-raw.lua:155-171), as in the reference.
         const int64_t n = level_count(Lv);
-        TRY(mgp_set_field(c, l, MGP_FIELD_U, u, n, mem));
-        TRY(mgp_set_field(c, l, MGP_FIELD_F, f, n, mem));
-        TRY(cycle_rec(c, l, h, c->o.cycle == MGP_CYCLE_F));
-        return mgp_get_field(c, l, MGP_FIELD_U, u, n, mem);
+        const size_t bytes = (size_t)Lv.alloc * c->rb;
+        TRY(materialize_zero(c, Lv));
+        char *su = nullptr, *sf = nullptr;
+        if (hipMalloc(&su, bytes) != hipSuccess || hipMalloc(&sf, bytes) != hipSuccess) {
+            if (su) (void)hipFree(su);
+            return c->fail(MGP_ERR_OOM, "mgp_two_grid: no room to save level %d", l);
+        }
+        int rc = MGP_OK;
+        auto step = [&](int r) { if (rc == MGP_OK) rc = r; };
+        step(hipMemcpyAsync(su, Lv.u, bytes, hipMemcpyDeviceToDevice, c->s) == hipSuccess ? MGP_OK : MGP_ERR_HIP);
+        step(hipMemcpyAsync(sf, Lv.f, bytes, hipMemcpyDeviceToDevice, c->s) == hipSuccess ? MGP_OK : MGP_ERR_HIP);
+        step(mgp_set_field(c, l, MGP_FIELD_U, u, n, mem));
+        step(mgp_set_field(c, l, MGP_FIELD_F, f, n, mem));
+        if (rc == MGP_OK) step(cycle_rec(c, l, h, c->o.cycle == MGP_CYCLE_F));
+        step(mgp_get_field(c, l, MGP_FIELD_U, u, n, mem));
+        TRY(materialize_zero(c, Lv));
+        const bool r1 = hipMemcpyAsync(Lv.u, su, bytes, hipMemcpyDeviceToDevice, c->s) == hipSuccess;
+        const bool r2 = hipMemcpyAsync(Lv.f, sf, bytes, hipMemcpyDeviceToDevice, c->s) == hipSuccess;
+        const bool r3 = hipStreamSynchronize(c->s) == hipSuccess;
+        (void)hipFree(su);
+        (void)hipFree(sf);
+        Lv.ghost_ok = Lv.fghost_ok = true;
+        if (rc != MGP_OK) return rc;
+        if (!(r1 && r2 && r3)) return c->fail(MGP_ERR_HIP, "mgp_two_grid: restoring level %d failed", l);
+        return MGP_OK;
     }
     return c->fail(MGP_ERR_ARG, "mgp_two_grid: no level of size %lld", (long long)L);
 }
@@ -1392,6 +1519,39 @@ int mgp_metrics(mgp_ctx* c, double* rel_err, int64_t* count, double* frob)
     if (rel_err) *rel_err = n > 0 ? h[0] / (double)n : NAN;    // test-gpu-obj.lua:240-243
     if (count) *count = n;
     if (frob) *frob = std::sqrt(h[2] / (double)c->ncells_global());  // gpu.lua:361-366
+    return MGP_OK;
+}
+
+int mgp_residual_norm(mgp_ctx* c, int level, double* rnorm, double* fnorm)
+{
+    if (!c) return MGP_ERR_ARG;
+    if (check_level(c, level) != MGP_OK) return c->fail(MGP_ERR_ARG, "mgp_residual_norm: bad level %d", level);
+    Level& L = c->lev[level];
+    TRY(materialize_zero(c, L));
+    TRY(exchange(c, L));
+    const int nb = mgp::resnorm_blocks(c->rb, L.g);
+    const int64_t need = 2 * (int64_t)(nb + mgp::sum_scratch(nb)) + 2;
+    if (need > c->d_rn_cap) {
+        if (c->d_rn) HIP_TRY(c, hipFree(c->d_rn));
+        c->d_rn = nullptr;
+        c->d_rn_cap = 0;
+        HIP_TRY(c, hipMalloc(&c->d_rn, sizeof(double) * need));
+        c->d_rn_cap = need;
+    }
+    double* out = c->d_rn + need - 2;
+    HIP_TRY(c, mgp::launch_residual_norm(c->rb, c->o.dim, c->ui(L, L.u), c->ui(L, L.f), L.g, level_h(c, level),
+                                         coarse_coef(c->o.coarse_bc, level), c->d_rn, out, c->s));
+    if (L.p.dist) {
+        if (c->lb)
+            TRY(lb_allreduce(c, out, 2));
+        else
+            NCCL_TRY(c, ncclAllReduce(out, out, 2, ncclDouble, ncclSum, c->comm, c->s));
+    }
+    double h[2];
+    HIP_TRY(c, hipMemcpyAsync(h, out, sizeof h, hipMemcpyDeviceToHost, c->s));
+    TRY(sync_and_check(c));
+    if (rnorm) *rnorm = std::sqrt(h[0]);
+    if (fnorm) *fnorm = std::sqrt(h[1]);
     return MGP_OK;
 }
 

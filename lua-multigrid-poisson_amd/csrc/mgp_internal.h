@@ -41,6 +41,11 @@ hipError_t launch_init_point_charge(int rb, int dim, void* u, void* f, Geo g, in
 // lexicographic (x fastest, this rank's planes) <-> packed
 hipError_t launch_pack(int rb, const void* lex, void* packed, Geo g, hipStream_t s);
 hipError_t launch_unpack(int rb, const void* packed, void* lex, Geo g, hipStream_t s);
+// Fingerprint of a packed field (this rank's planes): out_h = sum mod 2^64 of a per-cell mix of the
+// bits and the global lexicographic index; out_d = {sum, sum of squares, max |x|} in fp64.
+// hpart / dpart: kSumBlocks / 3 * kSumBlocks scratch.
+hipError_t launch_field_stats(int rb, const void* packed, Geo g, uint64_t* hpart, double* dpart, uint64_t* out_h,
+                              double* out_d, hipStream_t s);
 
 // One colour of a red/black sweep: dst(colour c) = relax(other(1-c), f) (cpu.lua:40-54 update).
 // other and dst may be the same buffer (in place) or different (out of place: Jacobi, the first
@@ -65,6 +70,11 @@ hipError_t launch_sqdiff_sum(int rb, const void* a, const void* b, int64_t n, do
 // over n elements; partials needs 3 * kSumBlocks doubles.
 hipError_t launch_metrics(int rb, const void* psi, const void* old, int64_t n, double* partials, double* out,
                           hipStream_t s);
+// out[0] = sum (f - A u)^2, out[1] = sum f^2 over the level's cells (fp64, wave-level then fixed-order
+// reductions).  partials: 2 * (resnorm_blocks() + sum_scratch(resnorm_blocks())) doubles.
+int resnorm_blocks(int rb, Geo g);
+hipError_t launch_residual_norm(int rb, int dim, const void* u, const void* f, Geo g, double h, double cl,
+                                double* partials, double* out, hipStream_t s);
 // Fixed-order fp64 sum of n partials into *out.  Needs sum_scratch(n) doubles of scratch right
 // after partials[n - 1].
 int sum_scratch(int n);

@@ -193,40 +193,157 @@ __device__ __forceinline__ bool slot_cell(int64_t s, const Geo& g, int& i, int& 
     return i < g.nx;
 }
 
+// Element-wise kernels over every packed slot of a level run grid-stride over at most kMaxBlocks
+// workgroups: a 4096 x 4096 x 512 slab has 8.6e9 slots, past the 2^32 work-items one launch allows.
+constexpr unsigned kMaxBlocks = 1u << 20;
+inline unsigned nblk_gs(int64_t n)
+{
+    const int64_t b = (n + kBlock - 1) / kBlock;
+    return (unsigned)(b < (int64_t)kMaxBlocks ? (b > 0 ? b : 1) : kMaxBlocks);
+}
+
 template <typename T>
 __global__ __launch_bounds__(kBlock) void k_init(T* __restrict__ u, T* __restrict__ f, Geo g, int64_t cx, int64_t cy,
                                                  int64_t cz, int dim3)
 {
-    const int64_t s = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (s >= g.P * g.nz) return;
-    int i, j;
-    int64_t k;
-    const bool cell = slot_cell(s, g, i, j, k);
-    const double charge = 1e+6, epsilon0 = 1;
-    const bool hit = cell && i == cx && j == cy && (!dim3 || g.z0 + k == cz);
-    const T v = hit ? (T)(-charge / epsilon0) : (T)0;
-    f[s] = v;
-    u[s] = -v;  // psi = -f (cpu.lua:193): -0.0 off the charge, as in the oracle
+    const int64_t n = g.P * g.nz;
+    for (int64_t s = (int64_t)blockIdx.x * kBlock + threadIdx.x; s < n; s += (int64_t)gridDim.x * kBlock) {
+        int i, j;
+        int64_t k;
+        const bool cell = slot_cell(s, g, i, j, k);
+        const double charge = 1e+6, epsilon0 = 1;
+        const bool hit = cell && i == cx && j == cy && (!dim3 || g.z0 + k == cz);
+        const T v = hit ? (T)(-charge / epsilon0) : (T)0;
+        f[s] = v;
+        u[s] = -v;  // psi = -f (cpu.lua:193): -0.0 off the charge, as in the oracle
+    }
 }
 
+// lex: planes 0 .. g.nz-1 of the (sub)slab described by g (g.z0 = global index of its plane 0)
 template <typename T>
 __global__ __launch_bounds__(kBlock) void k_pack(const T* __restrict__ lex, T* __restrict__ out, Geo g)
 {
-    const int64_t s = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (s >= g.P * g.nz) return;
-    int i, j;
-    int64_t k;
-    out[s] = slot_cell(s, g, i, j, k) ? lex[(k * g.ny + j) * (int64_t)g.nx + i] : (T)0;
+    const int64_t n = g.P * g.nz;
+    for (int64_t s = (int64_t)blockIdx.x * kBlock + threadIdx.x; s < n; s += (int64_t)gridDim.x * kBlock) {
+        int i, j;
+        int64_t k;
+        out[s] = slot_cell(s, g, i, j, k) ? lex[(k * g.ny + j) * (int64_t)g.nx + i] : (T)0;
+    }
 }
 
 template <typename T>
 __global__ __launch_bounds__(kBlock) void k_unpack(const T* __restrict__ in, T* __restrict__ lex, Geo g)
 {
-    const int64_t s = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (s >= g.P * g.nz) return;
-    int i, j;
-    int64_t k;
-    if (slot_cell(s, g, i, j, k)) lex[(k * g.ny + j) * (int64_t)g.nx + i] = in[s];
+    const int64_t n = g.P * g.nz;
+    for (int64_t s = (int64_t)blockIdx.x * kBlock + threadIdx.x; s < n; s += (int64_t)gridDim.x * kBlock) {
+        int i, j;
+        int64_t k;
+        if (slot_cell(s, g, i, j, k)) lex[(k * g.ny + j) * (int64_t)g.nx + i] = in[s];
+    }
+}
+
+// Order-independent fingerprint of a field (mgp_field_stats): per cell a 64-bit mix of its bit
+// pattern and its global lexicographic index, summed modulo 2^64, so two fields have the same
+// hash exactly when (with overwhelming probability) every cell is bit-identical, whatever the
+// slab decomposition or reduction order.  Alongside: fp64 sum, sum of squares and max |x|.
+__device__ __forceinline__ uint64_t mix64(uint64_t z)
+{
+    z += 0x9e3779b97f4a7c15ull;
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+    return z ^ (z >> 31);
+}
+
+template <typename T>
+__device__ __forceinline__ uint64_t real_bits(T v)
+{
+    if constexpr (sizeof(T) == 8) {
+        uint64_t b;
+        __builtin_memcpy(&b, &v, 8);
+        return b;
+    } else {
+        uint32_t b;
+        __builtin_memcpy(&b, &v, 4);
+        return b;
+    }
+}
+
+template <typename T>
+__global__ __launch_bounds__(kBlock) void k_field_stats(const T* __restrict__ in, Geo g, uint64_t* __restrict__ hpart,
+                                                        double* __restrict__ dpart)
+{
+    const int64_t n = g.P * g.nz;
+    uint64_t h = 0;
+    double s = 0.0, q = 0.0, mx = 0.0;
+    for (int64_t x = (int64_t)blockIdx.x * kBlock + threadIdx.x; x < n; x += (int64_t)gridDim.x * kBlock) {
+        int i, j;
+        int64_t k;
+        if (!slot_cell(x, g, i, j, k)) continue;
+        const T v = in[x];
+        const uint64_t gi = ((uint64_t)(g.z0 + k) * (uint64_t)g.ny + (uint64_t)j) * (uint64_t)g.nx + (uint64_t)i;
+        h += mix64(real_bits(v) ^ mix64(gi));
+        const double d = (double)v;
+        s += d;
+        q += d * d;
+        mx = fmax(mx, fabs(d));
+    }
+    __shared__ uint64_t sh[kBlock];
+    __shared__ double sd[3][kBlock];
+    sh[threadIdx.x] = h;
+    sd[0][threadIdx.x] = s;
+    sd[1][threadIdx.x] = q;
+    sd[2][threadIdx.x] = mx;
+    __syncthreads();
+    for (int w = kBlock / 2; w > 0; w >>= 1) {
+        if ((int)threadIdx.x < w) {
+            sh[threadIdx.x] += sh[threadIdx.x + w];
+            sd[0][threadIdx.x] += sd[0][threadIdx.x + w];
+            sd[1][threadIdx.x] += sd[1][threadIdx.x + w];
+            sd[2][threadIdx.x] = fmax(sd[2][threadIdx.x], sd[2][threadIdx.x + w]);
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        hpart[blockIdx.x] = sh[0];
+        for (int c = 0; c < 3; ++c) dpart[c * gridDim.x + blockIdx.x] = sd[c][0];
+    }
+}
+
+// one workgroup: the nb partials of k_field_stats -> out_h[0], out_d[0..2]
+__global__ __launch_bounds__(kBlock) void k_field_stats_final(const uint64_t* __restrict__ hpart,
+                                                              const double* __restrict__ dpart, int nb,
+                                                              uint64_t* __restrict__ out_h, double* __restrict__ out_d)
+{
+    uint64_t h = 0;
+    double s = 0.0, q = 0.0, mx = 0.0;
+    for (int b = threadIdx.x; b < nb; b += kBlock) {
+        h += hpart[b];
+        s += dpart[b];
+        q += dpart[nb + b];
+        mx = fmax(mx, dpart[2 * nb + b]);
+    }
+    __shared__ uint64_t sh[kBlock];
+    __shared__ double sd[3][kBlock];
+    sh[threadIdx.x] = h;
+    sd[0][threadIdx.x] = s;
+    sd[1][threadIdx.x] = q;
+    sd[2][threadIdx.x] = mx;
+    __syncthreads();
+    for (int w = kBlock / 2; w > 0; w >>= 1) {
+        if ((int)threadIdx.x < w) {
+            sh[threadIdx.x] += sh[threadIdx.x + w];
+            sd[0][threadIdx.x] += sd[0][threadIdx.x + w];
+            sd[1][threadIdx.x] += sd[1][threadIdx.x + w];
+            sd[2][threadIdx.x] = fmax(sd[2][threadIdx.x], sd[2][threadIdx.x + w]);
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        out_h[0] = sh[0];
+        out_d[0] = sd[0][0];
+        out_d[1] = sd[1][0];
+        out_d[2] = sd[2][0];
+    }
 }
 
 // ---- red/black half-sweep -------------------------------------------------------------------
@@ -433,6 +550,110 @@ __device__ __forceinline__ T residual_at(const T* __restrict__ u, const T* __res
     }
     const int nb = (i == 0) + (i == g.nx - 1) + (j == 0) + (j == g.ny - 1) + (DIM == 3 ? (gk == 0) + (gk == g.gnz - 1) : 0);
     return op.residual(s, f[c], u[c], nb);
+}
+
+// ---- residual norm (north star: wavefront-level reductions for the residual norm) -------------
+
+// Fixed-order fp64 sum across the 64 lanes of a wave (butterfly over lane distances 32 .. 1; every
+// lane ends with the same value, the same on every run).
+__device__ __forceinline__ double wave_sum(double v)
+{
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) v += __shfl_xor(v, d, 64);
+    return v;
+}
+
+// sum (f - A u)^2 and sum f^2 over both colours of a level (calcResidual, cpu.lua:108-123, squared
+// and reduced on the device instead of materialising r).  Vector form: a thread owns N cells of one
+// colour in one row (k_half's item; colour = the item's half of the grid), loads the other colour's
+// neighbours with half_load and its own cells with one vector load.  Per wave a butterfly sum, per
+// workgroup the 4 wave sums in fixed order, one fp64 pair per workgroup into partials[b] and
+// partials[fofs + b] (fofs leaves room for the first row's sum_partials scratch).
+template <typename T, int DIM>
+__global__ __launch_bounds__(kBlock) void k_resnorm(const T* __restrict__ u, const T* __restrict__ f, Geo g,
+                                                    Op<T, DIM> op, int64_t items, double* __restrict__ partials,
+                                                    int fofs)
+{
+    constexpr int N = VN<T>::n;
+    const int64_t it = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    double rr = 0.0, ff = 0.0;
+    if (it < 2 * items) {
+        const int color = it >= items;
+        HalfIn<T, N> in;
+        half_load<T, DIM>(in, u, f, g, color, it - color * items);
+        const Vec<T, N> uc = vload<T, N>(u + in.own);
+#pragma unroll
+        for (int e = 0; e < N; ++e) {
+            const int o = in.o;
+            const int i = 2 * (in.m0 + e) + o;
+            const T xl = o == 0 ? (e == 0 ? in.edge : in.cen.v[e - 1]) : in.cen.v[e];
+            const T xr = o == 0 ? in.cen.v[e] : (e == N - 1 ? in.edge : in.cen.v[e + 1]);
+            T sm = xl + xr;
+            sm = sm + in.yl.v[e];
+            sm = sm + in.yr.v[e];
+            if (DIM == 3) {
+                sm = sm + in.zl.v[e];
+                sm = sm + in.zr.v[e];
+            }
+            const T r = op.residual(sm, in.fv.v[e], uc.v[e], in.nbyz + (i == 0) + (i == g.nx - 1));
+            rr = __builtin_fma((double)r, (double)r, rr);
+            ff = __builtin_fma((double)in.fv.v[e], (double)in.fv.v[e], ff);
+        }
+    }
+    rr = wave_sum(rr);
+    ff = wave_sum(ff);
+    __shared__ double ws[2][kBlock / 64];
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) {
+        ws[0][w] = rr;
+        ws[1][w] = ff;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double a = 0.0, b = 0.0;
+        for (int k = 0; k < kBlock / 64; ++k) {
+            a += ws[0][k];
+            b += ws[1][k];
+        }
+        partials[blockIdx.x] = a;
+        partials[fofs + blockIdx.x] = b;
+    }
+}
+
+// Scalar form for small levels (hw < N, nx = 1 included): a thread per packed slot.
+template <typename T, int DIM>
+__global__ __launch_bounds__(kBlock) void k_resnorm_s(const T* __restrict__ u, const T* __restrict__ f, Geo g,
+                                                      Op<T, DIM> op, double* __restrict__ partials, int fofs)
+{
+    const int64_t s = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    double rr = 0.0, ff = 0.0;
+    if (s < g.P * g.nz) {
+        int i, j;
+        int64_t k;
+        if (slot_cell(s, g, i, j, k)) {
+            const T r = residual_at<T, DIM>(u, f, g, op, i, j, k);
+            rr = (double)r * (double)r;
+            ff = (double)f[s] * (double)f[s];
+        }
+    }
+    rr = wave_sum(rr);
+    ff = wave_sum(ff);
+    __shared__ double ws[2][kBlock / 64];
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) {
+        ws[0][w] = rr;
+        ws[1][w] = ff;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double a = 0.0, b = 0.0;
+        for (int k = 0; k < kBlock / 64; ++k) {
+            a += ws[0][k];
+            b += ws[1][k];
+        }
+        partials[blockIdx.x] = a;
+        partials[fofs + blockIdx.x] = b;
+    }
 }
 
 // One coarse cell of the fused residual + restriction (scalar; any sizes).
@@ -849,6 +1070,9 @@ __device__ __forceinline__ void lds_barrier()
 #ifndef ZS_TYPRE_F32
 #define ZS_TYPRE_F32 32
 #endif
+#ifndef ZS_TYPOST_F32
+#define ZS_TYPOST_F32 32
+#endif
 // Prefetch distance in steps: the loads of plane p + D are issued while plane p is computed.
 // D = 2 costs 3 register buffers and measured slower than D = 1 at 512^3 (601 / 878 us against
 // 579 / 787 us for PRE / POST).
@@ -859,7 +1083,7 @@ template <typename T>
 struct ZsTile;
 template <>
 struct ZsTile<float> {
-    static constexpr int TX = 64, TYPRE = ZS_TYPRE_F32, TYPOST = 32, NPRE = ZS_NPRE_F32, NPOST = ZS_NPOST_F32;
+    static constexpr int TX = 64, TYPRE = ZS_TYPRE_F32, TYPOST = ZS_TYPOST_F32, NPRE = ZS_NPRE_F32, NPOST = ZS_NPOST_F32;
 };
 template <>
 struct ZsTile<double> {
@@ -1629,21 +1853,68 @@ hipError_t launch_init_point_charge(int rb, int dim, void* u, void* f, Geo g, in
                                     hipStream_t s)
 {
     const int64_t n = g.P * g.nz;
-    MGP_REAL(rb, (k_init<T><<<nblk(n), kBlock, 0, s>>>((T*)u, (T*)f, g, cx, cy, cz, dim == 3)));
+    MGP_REAL(rb, (k_init<T><<<nblk_gs(n), kBlock, 0, s>>>((T*)u, (T*)f, g, cx, cy, cz, dim == 3)));
     return hipGetLastError();
 }
 
 hipError_t launch_pack(int rb, const void* lex, void* packed, Geo g, hipStream_t s)
 {
     const int64_t n = g.P * g.nz;
-    MGP_REAL(rb, (k_pack<T><<<nblk(n), kBlock, 0, s>>>((const T*)lex, (T*)packed, g)));
+    MGP_REAL(rb, (k_pack<T><<<nblk_gs(n), kBlock, 0, s>>>((const T*)lex, (T*)packed, g)));
     return hipGetLastError();
 }
 
 hipError_t launch_unpack(int rb, const void* packed, void* lex, Geo g, hipStream_t s)
 {
     const int64_t n = g.P * g.nz;
-    MGP_REAL(rb, (k_unpack<T><<<nblk(n), kBlock, 0, s>>>((const T*)packed, (T*)lex, g)));
+    MGP_REAL(rb, (k_unpack<T><<<nblk_gs(n), kBlock, 0, s>>>((const T*)packed, (T*)lex, g)));
+    return hipGetLastError();
+}
+
+int resnorm_blocks(int rb, Geo g)
+{
+    const int n = 16 / rb;
+    return (g.hw >= n && g.nx >= 2) ? (int)nblk(2 * (g.H / n) * g.nz) : (int)nblk(g.P * g.nz);
+}
+
+template <typename T, int D>
+static void resnorm_t(const void* u, const void* f, Geo g, double h, double cl, double* partials, double* out,
+                      hipStream_t s)
+{
+    const Op<T, D> op = make_op<T, D>(h, cl);
+    constexpr int n = VN<T>::n;
+    const unsigned nb = (unsigned)resnorm_blocks(sizeof(T), g);
+    const int fofs = (int)nb + sum_scratch((int)nb);
+    if (g.hw >= n && g.nx >= 2) {
+        const int64_t items = (g.H / n) * g.nz;
+        k_resnorm<T, D><<<nb, kBlock, 0, s>>>((const T*)u, (const T*)f, g, op, items, partials, fofs);
+    } else {
+        k_resnorm_s<T, D><<<nb, kBlock, 0, s>>>((const T*)u, (const T*)f, g, op, partials, fofs);
+    }
+    // the two rows of partials (sum r^2, sum f^2), each to one value in fixed order
+    (void)launch_sum_partials(partials, (int)nb, out, s);
+    (void)launch_sum_partials(partials + fofs, (int)nb, out + 1, s);
+}
+
+hipError_t launch_residual_norm(int rb, int dim, const void* u, const void* f, Geo g, double h, double cl,
+                                double* partials, double* out, hipStream_t s)
+{
+    if (rb == 8) {
+        if (dim == 3) resnorm_t<double, 3>(u, f, g, h, cl, partials, out, s);
+        else resnorm_t<double, 2>(u, f, g, h, cl, partials, out, s);
+    } else {
+        if (dim == 3) resnorm_t<float, 3>(u, f, g, h, cl, partials, out, s);
+        else resnorm_t<float, 2>(u, f, g, h, cl, partials, out, s);
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_field_stats(int rb, const void* packed, Geo g, uint64_t* hpart, double* dpart, uint64_t* out_h,
+                              double* out_d, hipStream_t s)
+{
+    const int nb = kSumBlocks;
+    MGP_REAL(rb, (k_field_stats<T><<<nb, kBlock, 0, s>>>((const T*)packed, g, hpart, dpart)));
+    k_field_stats_final<<<1, kBlock, 0, s>>>(hpart, dpart, nb, out_h, out_d);
     return hipGetLastError();
 }
 

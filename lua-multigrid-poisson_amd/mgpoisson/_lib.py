@@ -93,6 +93,9 @@ SIGNATURES = {
     "mgp_cycle": (ctypes.c_int, [_vp, _P(_dbl)]),
     "mgp_cycles": (ctypes.c_int, [_vp, _i32, _P(_dbl)]),
     "mgp_two_grid": (ctypes.c_int, [_vp, _dbl, _vp, _vp, _i64, ctypes.c_int]),
+    "mgp_set_planes": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, _i64, _i64, _vp, ctypes.c_int]),
+    "mgp_get_planes": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, _i64, _i64, _vp, ctypes.c_int]),
+    "mgp_field_stats": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, _P(ctypes.c_uint64), _P(_dbl)]),
     "mgp_smooth": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int]),
     "mgp_residual_restrict": (ctypes.c_int, [_vp, ctypes.c_int]),
     "mgp_prolong_correct": (ctypes.c_int, [_vp, ctypes.c_int]),
@@ -100,6 +103,7 @@ SIGNATURES = {
     "mgp_sync": (ctypes.c_int, [_vp]),
     "mgp_metrics": (ctypes.c_int, [_vp, _P(_dbl), _P(_i64), _P(_dbl)]),
     "mgp_set_coarse_level": (ctypes.c_int, [_vp, _i64]),
+    "mgp_residual_norm": (ctypes.c_int, [_vp, ctypes.c_int, _P(_dbl), _P(_dbl)]),
     "mgp_set_coarse_handoff": (ctypes.c_int, [_vp, _i64, COARSE_FN, _vp]),
     "mgp_timing": (ctypes.c_int, [_vp, ctypes.c_int]),
     "mgp_timing_read": (ctypes.c_int, [_vp, ctypes.c_int, _P(_dbl), _P(_i64), _P(_dbl)]),

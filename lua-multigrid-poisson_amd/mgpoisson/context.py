@@ -129,6 +129,28 @@ class Context:
         self._chk(L.lib.mgp_get_field(self._h, level, which, out.ctypes.data, out.size, L.MEM_HOST))
         return out
 
+    def get_planes(self, which, z_begin, nz, level=0):
+        """Local planes [z_begin, z_begin + nz) of a field as an (nz, ny, nx) host array."""
+        lv = self.levels[level]
+        out = np.empty((nz, lv["ny"], lv["nx"]), dtype=self.dtype)
+        self._chk(L.lib.mgp_get_planes(self._h, level, which, int(z_begin), int(nz), out.ctypes.data, L.MEM_HOST))
+        return out
+
+    def set_planes(self, which, z_begin, arr, level=0):
+        lv = self.levels[level]
+        a = np.ascontiguousarray(arr, dtype=self.dtype)
+        if a.size % (lv["ny"] * lv["nx"]) != 0:
+            raise ValueError("set_planes: the array must hold whole planes")
+        nz = a.size // (lv["ny"] * lv["nx"])
+        self._chk(L.lib.mgp_set_planes(self._h, level, which, int(z_begin), int(nz), a.ctypes.data, L.MEM_HOST))
+
+    def field_stats(self, which=L.FIELD_U, level=0):
+        """(hash, sum, sum of squares, max |x|) of this rank's part of a field, computed on the device."""
+        h = ctypes.c_uint64()
+        d = (ctypes.c_double * 3)()
+        self._chk(L.lib.mgp_field_stats(self._h, level, which, ctypes.byref(h), d))
+        return h.value, d[0], d[1], d[2]
+
     def set_psi(self, arr, level=0):
         self.set_field(L.FIELD_U, arr, level)
 
@@ -157,6 +179,10 @@ class Context:
         if not (u.flags.c_contiguous and u.dtype == self.dtype):
             raise ValueError("u must be a C-contiguous array of the context's real type")
         fc = np.ascontiguousarray(f, dtype=self.dtype)
+        lv = next((x for x in self.levels if x["nx"] == int(size)), None)
+        need = None if lv is None else lv["nx"] * lv["ny"] * (lv["nz_local"] if self.opts.dim == 3 else 1)
+        if need is not None and (u.size != need or fc.size != need):
+            raise ValueError(f"two_grid: u and f must hold {need} reals each (got {u.size}, {fc.size})")
         self._chk(L.lib.mgp_two_grid(self._h, float(h), u.ctypes.data, fc.ctypes.data, int(size), L.MEM_HOST))
 
     def two_grid_ptr(self, h: float, u_ptr: int, f_ptr: int, size: int, mem=L.MEM_DEVICE):
@@ -209,6 +235,12 @@ class Context:
         rel, n, frob = ctypes.c_double(), ctypes.c_int64(), ctypes.c_double()
         self._chk(L.lib.mgp_metrics(self._h, ctypes.byref(rel), ctypes.byref(n), ctypes.byref(frob)))
         return rel.value, n.value, frob.value
+
+    def residual_norm(self, level=0):
+        """(||f - A u||_2, ||f||_2) of a level, reduced on the device (fp64)."""
+        r, f = ctypes.c_double(), ctypes.c_double()
+        self._chk(L.lib.mgp_residual_norm(self._h, level, ctypes.byref(r), ctypes.byref(f)))
+        return r.value, f.value
 
     def sync(self):
         self._chk(L.lib.mgp_sync(self._h))
