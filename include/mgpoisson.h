@@ -43,7 +43,20 @@ enum { MGP_CYCLE_V = 0, MGP_CYCLE_F = 1 };             /* twoGrid recursion (gam
 enum { MGP_PROLONG_PC = 0, MGP_PROLONG_LINEAR = 1 };   /* cpu.lua:142-150 injection / (tri)linear */
 enum { MGP_COARSE_FRESH = 0, MGP_COARSE_WARM = 1 };    /* cpu.lua:138 zeros / cpu-raw.lua:221 Vs */
 enum { MGP_BC_ZERO = 0, MGP_BC_CONSISTENT = 1 };       /* coarse ghost: 0 (ref) / extrapolated */
-enum { MGP_FIELD_U = 0, MGP_FIELD_F = 1 };             /* psi (V on coarse levels) / f (R) */
+/* Fields of a level, by cpu-raw.lua's names (cpu-raw.lua:148-171).  U and F are the stored, writable
+ * state; the others are read-only views computed on request from it:
+ *   MGP_FIELD_U          psi on level 0, Vs[L] below (the coarse correction)
+ *   MGP_FIELD_F          f on level 0, Rs[L] below (the restricted residual)
+ *   MGP_FIELD_RESIDUAL   rs[L] = f - A u (calcResidual, cpu.lua:108-123)
+ *   MGP_FIELD_CORRECTION vs[L] = P Vs[L/2] (expandResidual, cpu.lua:142-150), the prolonged correction
+ *   MGP_FIELD_PSI_OLD    psiOld (level 0): the iterate before the last outer iteration (cpu.lua:200)
+ *   MGP_FIELD_ERROR      errorBuf (level 0) = (psi - psiOld)^2 per cell (calcFrobErr, gpu.lua:189-200)
+ *   MGP_FIELD_TMP        tmpU: the Jacobi target buffer (cpu-raw.lua:153, 176-184)
+ * PSI_OLD / ERROR need err_mode 1 and a psiOld that the cycle kept (not after a temporally blocked
+ * finest level, which overwrites it in place): MGP_ERR_STATE otherwise.  TMP: MGP_ERR_STATE when the
+ * level has no second buffer (red/black Gauss-Seidel works in place). */
+enum { MGP_FIELD_U = 0, MGP_FIELD_F = 1, MGP_FIELD_RESIDUAL = 2, MGP_FIELD_CORRECTION = 3, MGP_FIELD_PSI_OLD = 4,
+       MGP_FIELD_ERROR = 5, MGP_FIELD_TMP = 6, MGP_FIELD_KINDS = 7 };
 enum { MGP_MEM_HOST = 0, MGP_MEM_DEVICE = 1 };         /* where a caller buffer lives */
 
 typedef struct mgp_opts {
@@ -166,6 +179,27 @@ typedef struct mgp_loopback mgp_loopback;
 int         mgp_loopback_create(mgp_loopback** out, int world);
 void        mgp_loopback_destroy(mgp_loopback* lb);
 int         mgp_create_loopback(mgp_ctx** out, const mgp_opts* o, mgp_loopback* lb);
+/* Single-process multi-GPU group (the form of cpu-gpu.lua:55-72's one host object
+ * owning several engines): ONE host process drives `ngpu` GPUs of the node.  The library creates
+ * the RCCL communicators with ncclCommInitAll over devices[0..ngpu) (NULL = 0..ngpu-1) and one
+ * context per rank (rank r = z-slab r of the box, opts->rank / opts->world / opts->device are set
+ * by the group); every group call runs the ranks' work in one host thread per device inside the
+ * library and returns when all are done.  When all devices[] are equal the ranks share that GPU
+ * through the loopback transport (tests).  Field I/O is in the global x-fastest layout. */
+typedef struct mgp_group mgp_group;
+int         mgp_group_create(mgp_group** out, const mgp_opts* o, int ngpu, const int* devices);
+void        mgp_group_destroy(mgp_group* g);
+const char* mgp_group_last_error(const mgp_group* g);
+int         mgp_group_size(const mgp_group* g);
+mgp_ctx*    mgp_group_rank(mgp_group* g, int rank);   /* per-rank context (its slab, its stream) */
+int         mgp_group_init_point_charge(mgp_group* g);
+int         mgp_group_cycle(mgp_group* g, double* err_out);
+int         mgp_group_cycles(mgp_group* g, int32_t k, double* errs);
+int         mgp_group_set_field(mgp_group* g, int level, int which, const void* src, int64_t count, int mem);
+int         mgp_group_get_field(mgp_group* g, int level, int which, void* dst, int64_t count, int mem);
+int         mgp_group_residual_norm(mgp_group* g, int level, double* rnorm, double* fnorm);
+int         mgp_group_field_stats(mgp_group* g, int level, int which, uint64_t* hash, double stats[3]);
+
 /* Finest-level kernel timing with HIP events on the context's stream.  mgp_timing(c, 1) resets and
  * enables (cycles then run eagerly, without hipGraph replay, so each launch can be bracketed).
  * Timed kinds, level 0 only:

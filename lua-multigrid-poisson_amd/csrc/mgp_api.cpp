@@ -15,6 +15,8 @@
 #include <chrono>
 #include <condition_variable>
 #include <mutex>
+#include <functional>
+#include <thread>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -1010,7 +1012,7 @@ static void destroy_impl(mgp_ctx* c)
     delete c;
 }
 
-static int create_impl(mgp_ctx** out, const mgp_opts* o, mgp_loopback* lb);
+static int create_impl(mgp_ctx** out, const mgp_opts* o, mgp_loopback* lb, ncclComm_t comm = nullptr);
 
 int mgp_create(mgp_ctx** out, const mgp_opts* o) { return create_impl(out, o, nullptr); }
 
@@ -1035,7 +1037,7 @@ int mgp_create_loopback(mgp_ctx** out, const mgp_opts* o, mgp_loopback* lb)
     return create_impl(out, o, lb);
 }
 
-static int create_impl(mgp_ctx** out, const mgp_opts* o, mgp_loopback* lb)
+static int create_impl(mgp_ctx** out, const mgp_opts* o, mgp_loopback* lb, ncclComm_t ext_comm)
 {
     if (!out || !o) {
         g_create_error = "mgp_create: null argument";
@@ -1048,6 +1050,7 @@ static int create_impl(mgp_ctx** out, const mgp_opts* o, mgp_loopback* lb)
 
     mgp_ctx* c = new mgp_ctx();
     c->o = *o;
+    if (ext_comm && o->world > 1) c->comm = ext_comm;  // from ncclCommInitAll (mgp_group_create); owned from here
     if (c->o.dim == 2) c->o.n[2] = 1;
     c->rb = o->real_bytes;
     c->G = o->dim == 3 ? mgp::kGhost3D : 0;  // widened below when a distributed level is fused
@@ -1192,6 +1195,8 @@ static int create_impl(mgp_ctx** out, const mgp_opts* o, mgp_loopback* lb)
             return bail(MGP_ERR_ARG);
         }
         lb->ranks[c->o.rank] = c;
+    } else if (c->o.world > 1 && c->comm) {
+        // communicator handed in by mgp_group_create
     } else if (c->o.world > 1) {
         ncclUniqueId id;
         std::memcpy(&id, o->comm_id, sizeof(id));
@@ -1246,16 +1251,88 @@ int mgp_init_point_charge(mgp_ctx* c)
 
 // Host <-> packed level I/O in plane chunks through the bounded staging buffer (a 4096 x 4096 x 512
 // slab is 34 GB per field; no full-size staging copy is ever allocated).
+// The packed buffer a read of `which` comes from: stored fields directly, computed views into a
+// temporary level-sized buffer (*scratch, freed by the caller).
+static int field_source(mgp_ctx* c, int level, int which, char** src, char** scratch)
+{
+    Level& L = c->lev[(size_t)level];
+    *scratch = nullptr;
+    switch (which) {
+    case MGP_FIELD_U: *src = L.u; return MGP_OK;
+    case MGP_FIELD_F: *src = L.f; return MGP_OK;
+    case MGP_FIELD_TMP:
+        if (!L.t) return c->fail(MGP_ERR_STATE, "tmpU: level %d has no second buffer (in-place red/black GS)", level);
+        *src = L.t;
+        return MGP_OK;
+    case MGP_FIELD_PSI_OLD:
+    case MGP_FIELD_ERROR:
+        if (level != 0 || !c->metrics_old)
+            return c->fail(MGP_ERR_STATE, "psiOld / errorBuf: level 0 only, after an outer iteration with err_mode 1 "
+                                          "that kept psiOld (not with the temporally blocked finest level)");
+        break;
+    case MGP_FIELD_CORRECTION:
+        if (level + 1 >= (int)c->lev.size()) return c->fail(MGP_ERR_ARG, "vs: the coarsest level has none");
+        break;
+    case MGP_FIELD_RESIDUAL: break;
+    default: return c->fail(MGP_ERR_ARG, "unknown field %d", which);
+    }
+    const size_t bytes = (size_t)L.alloc * c->rb;
+    if (hipMalloc(scratch, bytes) != hipSuccess) return c->fail(MGP_ERR_OOM, "no room for a computed field view");
+    HIP_TRY(c, hipMemsetAsync(*scratch, 0, bytes, c->s));
+    char* sc = c->ui(L, *scratch);
+    const int64_t n = L.g.P * L.g.nz;
+    if (which == MGP_FIELD_PSI_OLD) {
+        HIP_TRY(c, hipMemcpyAsync(sc, c->metrics_old, (size_t)n * c->rb, hipMemcpyDeviceToDevice, c->s));
+    } else if (which == MGP_FIELD_ERROR) {
+        HIP_TRY(c, mgp::launch_sqdiff_field(c->rb, c->ui(L, L.u), c->metrics_old, sc, n, c->s));
+    } else if (which == MGP_FIELD_RESIDUAL) {
+        TRY(exchange(c, L));
+        HIP_TRY(c, mgp::launch_residual_field(c->rb, c->o.dim, c->ui(L, L.u), c->ui(L, L.f), sc, L.g, level_h(c, level),
+                                              coarse_coef(c->o.coarse_bc, level), c->s));
+    } else {  // MGP_FIELD_CORRECTION: P V onto zeros
+        Level& C = c->lev[(size_t)level + 1];
+        TRY(materialize_zero(c, C));
+        const int linear = c->o.prolong == MGP_PROLONG_LINEAR;
+        if (linear && C.p.dist) TRY(exchange(c, C));
+        int64_t zc = 0;
+        const Geo gc = coarse_view(L, C, &zc);
+        char* V = c->ui(C, C.u) + (size_t)(zc * C.g.P) * c->rb;
+        HIP_TRY(c, mgp::launch_prolong_correct(c->rb, c->o.dim, linear, sc, V, L.g, gc,
+                                               coarse_coef(c->o.coarse_bc, level + 1), c->s));
+    }
+    *src = *scratch;
+    return MGP_OK;
+}
+
+// Host <-> packed level I/O in plane chunks through the bounded staging buffer (a 4096 x 4096 x 512
+// slab is 34 GB per field; no full-size staging copy is ever allocated).
 static int planes_io(mgp_ctx* c, int level, int which, int64_t z_begin, int64_t nz, void* buf, int mem, bool to_device)
 {
-    if (check_level(c, level) != MGP_OK || (which != MGP_FIELD_U && which != MGP_FIELD_F) || !buf)
+    if (check_level(c, level) != MGP_OK || which < 0 || which >= MGP_FIELD_KINDS || !buf)
         return c->fail(MGP_ERR_ARG, "field I/O: bad level / field / buffer");
+    if (to_device && which != MGP_FIELD_U && which != MGP_FIELD_F)
+        return c->fail(MGP_ERR_ARG, "field %d is a read-only view", which);
     Level& L = c->lev[level];
     if (z_begin < 0 || nz < 0 || z_begin + nz > L.g.nz)
         return c->fail(MGP_ERR_ARG, "field I/O: planes [%lld, %lld) outside the local slab of %lld planes",
                        (long long)z_begin, (long long)(z_begin + nz), (long long)L.g.nz);
-    if (which == MGP_FIELD_U) TRY(materialize_zero(c, L));
-    char* base = c->ui(L, which == MGP_FIELD_U ? L.u : L.f);
+    if (which == MGP_FIELD_U || which == MGP_FIELD_RESIDUAL) TRY(materialize_zero(c, L));
+    char* src = nullptr;
+    char* scratch = nullptr;
+    if (to_device) {
+        src = which == MGP_FIELD_U ? L.u : L.f;
+    } else {
+        const int rc = field_source(c, level, which, &src, &scratch);
+        if (rc != MGP_OK) {
+            if (scratch) (void)hipFree(scratch);
+            return rc;
+        }
+    }
+    struct Free {
+        char* p;
+        ~Free() { if (p) (void)hipFree(p); }
+    } free_scratch{scratch};
+    char* base = c->ui(L, src);
     const size_t rb = (size_t)c->rb;
     const int64_t lex_plane = L.p.nx * L.p.ny;  // reals per plane, lexicographic
     const int64_t per_chunk =
@@ -1582,6 +1659,205 @@ int mgp_timing_read(mgp_ctx* c, int kind, double* ms_total, int64_t* launches, d
     if (ms_total) *ms_total = c->t_ms[kind];
     if (launches) *launches = c->t_launch[kind];
     if (bytes) *bytes = c->t_bytes[kind];
+    return MGP_OK;
+}
+
+// =====================================================================================
+// Single-process multi-GPU group (one Lua host driving the node's GPUs)
+// =====================================================================================
+
+struct mgp_group {
+    std::vector<mgp_ctx*> ranks;
+    std::vector<int> dev;
+    mgp_loopback* lb = nullptr;  // all ranks on one device: loopback transport
+    std::string err;
+};
+
+static thread_local std::string g_group_error;
+
+// Run fn(rank context, r) on every rank, each in its own host thread with its device current (the
+// ranks' halo exchanges and collectives must be issued concurrently).  First failure wins.
+static int group_run(mgp_group* g, const std::function<int(mgp_ctx*, int)>& fn)
+{
+    const int n = (int)g->ranks.size();
+    std::vector<int> rc((size_t)n, MGP_OK);
+    std::vector<std::thread> th;
+    th.reserve((size_t)n);
+    for (int r = 0; r < n; ++r)
+        th.emplace_back([&, r] {
+            if (hipSetDevice(g->dev[(size_t)r]) != hipSuccess) {
+                rc[(size_t)r] = MGP_ERR_HIP;
+                return;
+            }
+            rc[(size_t)r] = fn(g->ranks[(size_t)r], r);
+        });
+    for (auto& t : th) t.join();
+    for (int r = 0; r < n; ++r)
+        if (rc[(size_t)r] != MGP_OK) {
+            g->err = "rank " + std::to_string(r) + ": " + g->ranks[(size_t)r]->err;
+            return rc[(size_t)r];
+        }
+    return MGP_OK;
+}
+
+void mgp_group_destroy(mgp_group* g)
+{
+    if (!g) return;
+    for (auto* c : g->ranks)
+        if (c) {
+            (void)hipSetDevice(c->device);
+            destroy_impl(c);
+        }
+    delete g->lb;
+    delete g;
+}
+
+int mgp_group_create(mgp_group** out, const mgp_opts* o, int ngpu, const int* devices)
+{
+    if (!out || !o || ngpu < 1) {
+        g_create_error = "mgp_group_create: bad argument";
+        return MGP_ERR_ARG;
+    }
+    *out = nullptr;
+    mgp_group* g = new mgp_group();
+    for (int r = 0; r < ngpu; ++r) g->dev.push_back(devices ? devices[r] : r);
+    bool same = true;
+    for (int d : g->dev) same = same && d == g->dev[0];
+    mgp_opts ro = *o;
+    ro.world = ngpu;
+    ro.rank = 0;
+    {
+        std::vector<LevelPlan> plan;
+        const int rc = plan_levels(ro, plan, g_create_error);
+        if (rc != MGP_OK) {
+            delete g;
+            return rc;
+        }
+    }
+    std::vector<ncclComm_t> comms((size_t)ngpu, nullptr);
+    if (ngpu > 1 && same) {
+        mgp_loopback_create(&g->lb, ngpu);
+    } else if (ngpu > 1) {
+        const ncclResult_t r = ncclCommInitAll(comms.data(), ngpu, g->dev.data());
+        if (r != ncclSuccess) {
+            g_create_error = std::string("ncclCommInitAll: ") + ncclGetErrorString(r);
+            delete g;
+            return MGP_ERR_RCCL;
+        }
+    }
+    g->ranks.assign((size_t)ngpu, nullptr);
+    for (int r = 0; r < ngpu; ++r) {
+        ro.rank = r;
+        ro.device = g->dev[(size_t)r];
+        const int rc = create_impl(&g->ranks[(size_t)r], &ro, g->lb, comms[(size_t)r]);
+        if (rc != MGP_OK) {
+            for (int q = r + 1; q < ngpu; ++q)
+                if (comms[(size_t)q]) (void)ncclCommDestroy(comms[(size_t)q]);
+            const std::string e = g_create_error;
+            mgp_group_destroy(g);
+            g_create_error = "rank " + std::to_string(r) + ": " + e;
+            return rc;
+        }
+    }
+    *out = g;
+    return MGP_OK;
+}
+
+int mgp_group_size(const mgp_group* g) { return g ? (int)g->ranks.size() : MGP_ERR_ARG; }
+
+mgp_ctx* mgp_group_rank(mgp_group* g, int rank)
+{
+    return (g && rank >= 0 && rank < (int)g->ranks.size()) ? g->ranks[(size_t)rank] : nullptr;
+}
+
+const char* mgp_group_last_error(const mgp_group* g) { return g ? g->err.c_str() : g_create_error.c_str(); }
+
+int mgp_group_init_point_charge(mgp_group* g)
+{
+    if (!g) return MGP_ERR_ARG;
+    return group_run(g, [](mgp_ctx* c, int) { return mgp_init_point_charge(c); });
+}
+
+int mgp_group_cycles(mgp_group* g, int32_t k, double* errs)
+{
+    if (!g || k < 0) return MGP_ERR_ARG;
+    return group_run(g, [&](mgp_ctx* c, int r) { return mgp_cycles(c, k, r == 0 && errs ? errs : nullptr); });
+}
+
+int mgp_group_cycle(mgp_group* g, double* err_out)
+{
+    double e = NAN;
+    const int rc = mgp_group_cycles(g, 1, &e);
+    if (err_out) *err_out = e;
+    return rc;
+}
+
+// Global field of a level (x fastest, the whole box): each rank moves its own slab planes of a
+// distributed level; a replicated level is read from rank 0 and written to every rank.
+static int group_field_io(mgp_group* g, int level, int which, void* buf, int64_t count, int mem, bool to_device)
+{
+    if (!g || !buf) return MGP_ERR_ARG;
+    mgp_ctx* c0 = g->ranks[0];
+    if (check_level(c0, level) != MGP_OK) {
+        g->err = "bad level";
+        return MGP_ERR_ARG;
+    }
+    const LevelPlan& p = c0->lev[(size_t)level].p;
+    const int64_t plane = p.nx * p.ny;
+    if (count != plane * p.gnz) {
+        g->err = "count " + std::to_string(count) + " != " + std::to_string(plane * p.gnz);
+        return MGP_ERR_ARG;
+    }
+    return group_run(g, [&](mgp_ctx* c, int r) -> int {
+        const Level& L = c->lev[(size_t)level];
+        if (!L.p.dist && r > 0 && !to_device) return MGP_OK;
+        char* at = (char*)buf + (size_t)(L.p.z0 * plane) * c->rb;
+        return planes_io(c, level, which, 0, L.g.nz, at, mem, to_device);
+    });
+}
+
+int mgp_group_get_field(mgp_group* g, int level, int which, void* dst, int64_t count, int mem)
+{
+    return group_field_io(g, level, which, dst, count, mem, false);
+}
+
+int mgp_group_set_field(mgp_group* g, int level, int which, const void* src, int64_t count, int mem)
+{
+    return group_field_io(g, level, which, const_cast<void*>(src), count, mem, true);
+}
+
+int mgp_group_residual_norm(mgp_group* g, int level, double* rnorm, double* fnorm)
+{
+    if (!g) return MGP_ERR_ARG;
+    std::vector<double> rn(g->ranks.size()), fn(g->ranks.size());
+    TRY(group_run(g, [&](mgp_ctx* c, int r) { return mgp_residual_norm(c, level, &rn[(size_t)r], &fn[(size_t)r]); }));
+    if (rnorm) *rnorm = rn[0];  // all-reduced: every rank holds the global norms
+    if (fnorm) *fnorm = fn[0];
+    return MGP_OK;
+}
+
+int mgp_group_field_stats(mgp_group* g, int level, int which, uint64_t* hash, double stats[3])
+{
+    if (!g) return MGP_ERR_ARG;
+    const size_t n = g->ranks.size();
+    std::vector<uint64_t> h(n);
+    std::vector<double> d(3 * n);
+    TRY(group_run(g, [&](mgp_ctx* c, int r) { return mgp_field_stats(c, level, which, &h[(size_t)r], &d[3 * (size_t)r]); }));
+    const bool dist = g->ranks[0]->lev[(size_t)level].p.dist;
+    uint64_t hh = 0;
+    double s = 0, q = 0, mx = 0;
+    for (size_t r = 0; r < (dist ? n : 1); ++r) {
+        hh += h[r];
+        s += d[3 * r];
+        q += d[3 * r + 1];
+        mx = std::max(mx, d[3 * r + 2]);
+    }
+    if (hash) *hash = hh;
+    if (stats) {
+        stats[0] = s;
+        stats[1] = q;
+        stats[2] = mx;
+    }
     return MGP_OK;
 }
 

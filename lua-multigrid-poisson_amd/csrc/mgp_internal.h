@@ -47,6 +47,12 @@ hipError_t launch_unpack(int rb, const void* packed, void* lex, Geo g, hipStream
 hipError_t launch_field_stats(int rb, const void* packed, Geo g, uint64_t* hpart, double* dpart, uint64_t* out_h,
                               double* out_d, hipStream_t s);
 
+// Computed views for mgp_get_field (cpu-raw.lua's rs / errorBuf): r = f - A u at every packed slot, and
+// out = (a - b)^2 elementwise over n packed reals.
+hipError_t launch_residual_field(int rb, int dim, const void* u, const void* f, void* r, Geo g, double h, double cl,
+                                 hipStream_t s);
+hipError_t launch_sqdiff_field(int rb, const void* a, const void* b, void* out, int64_t n, hipStream_t s);
+
 // One colour of a red/black sweep: dst(colour c) = relax(other(1-c), f) (cpu.lua:40-54 update).
 // other and dst may be the same buffer (in place) or different (out of place: Jacobi, the first
 // sweep of a cycle).  With old != nullptr, sum (dst - old)^2 over colour c goes to one fp64

@@ -656,6 +656,31 @@ __global__ __launch_bounds__(kBlock) void k_resnorm_s(const T* __restrict__ u, c
     }
 }
 
+// rs[L] of cpu-raw.lua:155-171 (calcResidual, cpu.lua:108-123) materialised on request (mgp_get_field
+// MGP_FIELD_RESIDUAL): r at every packed slot, grid-stride.
+template <typename T, int DIM>
+__global__ __launch_bounds__(kBlock) void k_residual_field(const T* __restrict__ u, const T* __restrict__ f,
+                                                           T* __restrict__ r, Geo g, Op<T, DIM> op)
+{
+    const int64_t n = g.P * g.nz;
+    for (int64_t s = (int64_t)blockIdx.x * kBlock + threadIdx.x; s < n; s += (int64_t)gridDim.x * kBlock) {
+        int i, j;
+        int64_t k;
+        r[s] = slot_cell(s, g, i, j, k) ? residual_at<T, DIM>(u, f, g, op, i, j, k) : (T)0;
+    }
+}
+
+// errorBuf of cpu-raw.lua:96-100 / gpu.lua:189-200 (calcFrobErr): (psi - psiOld)^2 per cell, in real.
+template <typename T>
+__global__ __launch_bounds__(kBlock) void k_sqdiff_field(const T* __restrict__ a, const T* __restrict__ b,
+                                                         T* __restrict__ out, int64_t n)
+{
+    for (int64_t s = (int64_t)blockIdx.x * kBlock + threadIdx.x; s < n; s += (int64_t)gridDim.x * kBlock) {
+        const T d = a[s] - b[s];
+        out[s] = d * d;
+    }
+}
+
 // One coarse cell of the fused residual + restriction (scalar; any sizes).
 template <typename T, int DIM>
 __device__ __forceinline__ void resrestrict_item(const T* u, const T* f, T* R, const Geo& g, const Geo& gc,
@@ -1906,6 +1931,26 @@ hipError_t launch_residual_norm(int rb, int dim, const void* u, const void* f, G
         if (dim == 3) resnorm_t<float, 3>(u, f, g, h, cl, partials, out, s);
         else resnorm_t<float, 2>(u, f, g, h, cl, partials, out, s);
     }
+    return hipGetLastError();
+}
+
+hipError_t launch_residual_field(int rb, int dim, const void* u, const void* f, void* r, Geo g, double h, double cl,
+                                 hipStream_t s)
+{
+    const unsigned nb = nblk_gs(g.P * g.nz);
+    if (rb == 8) {
+        if (dim == 3) k_residual_field<double, 3><<<nb, kBlock, 0, s>>>((const double*)u, (const double*)f, (double*)r, g, make_op<double, 3>(h, cl));
+        else k_residual_field<double, 2><<<nb, kBlock, 0, s>>>((const double*)u, (const double*)f, (double*)r, g, make_op<double, 2>(h, cl));
+    } else {
+        if (dim == 3) k_residual_field<float, 3><<<nb, kBlock, 0, s>>>((const float*)u, (const float*)f, (float*)r, g, make_op<float, 3>(h, cl));
+        else k_residual_field<float, 2><<<nb, kBlock, 0, s>>>((const float*)u, (const float*)f, (float*)r, g, make_op<float, 2>(h, cl));
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_sqdiff_field(int rb, const void* a, const void* b, void* out, int64_t n, hipStream_t s)
+{
+    MGP_REAL(rb, (k_sqdiff_field<T><<<nblk_gs(n), kBlock, 0, s>>>((const T*)a, (const T*)b, (T*)out, n)));
     return hipGetLastError();
 }
 

@@ -2,37 +2,48 @@
 multigrid-poisson/hip.lua — drop-in GPU solver class for thenumbernine/lua-multigrid-poisson,
 backed by libmgpoisson.so (include/mgpoisson.h) through LuaJIT FFI.
 
-It accepts both constructor protocols of the reference:
+It accepts the constructor protocols of the reference:
   * cpu.lua table protocol (cpu.lua:173-216):
         local MG = require 'multigrid-poisson.hip'
         local mg = MG{size=n, maxiter=?, epsilon=?, errorCallback=function(iter, err) ... end, debug=?}
         mg:solve()            -- or mg:step() -> err
+        mg:twoGrid(h, u, f)   -- u, f: lua-matrix-style 1-based tables u[i][j] (x = i), u updated in place
+    mg.size is {n, n} (cpu.lua:178 matrix{size,size}); mg.smooth and mg.inPlaceIterativeSolver
+    (MG.Jacobi | MG.GaussSeidel, cpu.lua:56-57) are writable: a change rebuilds the device context
+    with psi and f kept.
   * cpu-raw.lua / gpu.lua positional protocol (cpu-raw.lua:142, 239; gpu.lua:26, 348):
         local mg = MG(size, real)    -- real = 'double' (default) or 'float'
         mg:run()              -- two outer iterations, prints '#iter err'
         mg:twoGrid(h, uPtr, fPtr, L) -- raw real* host buffers of an L x L grid (cpu-raw.lua:186)
+    Fields as cpu-raw.lua:148-171 names them, each an image-like {buffer=real*, width, height}
+    downloaded on access: mg.psi, mg.f, mg.psiOld, mg.errorBuf, mg.tmpU, and per level size L
+    mg.rs[L], mg.Rs[L], mg.vs[L], mg.Vs[L] (rs / vs computed on the device on request).
   * cpu-gpu.lua protocol (cpu-gpu.lua:55-72): MG(size, real, cpuDepth[, engine]) switches to the
     GPU's one-launch coarse engine at size 2^cpuDepth, or, given an engine with
     engine:twoGrid(h, uPtr, fPtr, L) (e.g. require'multigrid-poisson.cpu-raw'(2^cpuDepth)), hands
     that level's u and f to it and back, exactly as MultigridGPUSubset:twoGrid does.
-mg:metrics() returns relErr, count, frobErr of the last outer iteration (gpu.lua:173-200).
+  * Multi-GPU from this one Lua process (north_star: the V-cycle domain-decomposed across the
+    node's GPUs): MG{size=n, dim=3, ngpu=8[, devices={...}], ...}.  The library builds the RCCL
+    communicators (ncclCommInitAll) and runs every rank in its own host thread per call
+    (mgp_group_*); fields are the global box.
+mg:metrics() returns relErr, count, frobErr of the last outer iteration (gpu.lua:173-200);
+mg:residualNorm() returns ||f - A psi||, ||f|| (device reduction).
 Extra table fields select the build's configurations: dim (2|3), real, smoother ('jacobi'|'rbgs'),
 cycle ('V'|'F'), prolong ('pc'|'linear'), coarse_init ('fresh'|'warm'), coarse_bc
 ('zero'|'consistent'), device.  Defaults reproduce cpu.lua (2D, double, Jacobi 7+7, V-cycle,
 injection, fresh zero coarse guess, ghost value 0).
-
-Fields: mg.psi / mg.f return lua-matrix-style 1-based tables psi[i][j] (x = i) downloaded from
-the GPU; mg.psiBuffer / mg.fBuffer return raw real* copies (cpu-raw.lua's .psi.buffer).
 Errors from the library raise Lua errors (error()), as the reference's own failures do.
 
-Not executable in this repository's CI (no Lua runtime in the image); the Python mirror in
-../mgpoisson/solver.py is the tested twin of this file.
+Not executable in this repository's CI (no Lua runtime in the image): tests/test_lua_binding.py
+compiles the cdef below against include/mgpoisson.h, and ../mgpoisson/solver.py is the tested
+Python twin of this file.
 --]]
 local ffi = require 'ffi'
 local bit = require 'bit'
 
 ffi.cdef[[
 typedef struct mgp_ctx mgp_ctx;
+typedef struct mgp_group mgp_group;
 typedef struct mgp_opts {
     int32_t struct_size;
     int32_t dim;
@@ -56,15 +67,29 @@ void        mgp_opts_default(mgp_opts* o);
 int         mgp_create(mgp_ctx** out, const mgp_opts* o);
 void        mgp_destroy(mgp_ctx* c);
 const char* mgp_last_error(const mgp_ctx* c);
+int         mgp_num_levels(const mgp_ctx* c);
+int         mgp_level_info(const mgp_ctx* c, int level, int64_t info[8]);
 int         mgp_init_point_charge(mgp_ctx* c);
 int         mgp_set_field(mgp_ctx* c, int level, int which, const void* src, int64_t count, int mem);
 int         mgp_get_field(const mgp_ctx* c, int level, int which, void* dst, int64_t count, int mem);
+int         mgp_set_planes(mgp_ctx* c, int level, int which, int64_t z_begin, int64_t nz, const void* src, int mem);
+int         mgp_get_planes(const mgp_ctx* c, int level, int which, int64_t z_begin, int64_t nz, void* dst, int mem);
 int         mgp_cycle(mgp_ctx* c, double* err_out);
 int         mgp_two_grid(mgp_ctx* c, double h, void* u, const void* f, int64_t L, int mem);
 int         mgp_set_coarse_level(mgp_ctx* c, int64_t size);
 typedef int (*mgp_coarse_fn)(void* user, double h, void* u, const void* f, int64_t size);
 int         mgp_set_coarse_handoff(mgp_ctx* c, int64_t size, mgp_coarse_fn fn, void* user);
 int         mgp_metrics(mgp_ctx* c, double* rel_err, int64_t* count, double* frob);
+int         mgp_residual_norm(mgp_ctx* c, int level, double* rnorm, double* fnorm);
+int         mgp_group_create(mgp_group** out, const mgp_opts* o, int ngpu, const int* devices);
+void        mgp_group_destroy(mgp_group* g);
+const char* mgp_group_last_error(const mgp_group* g);
+int         mgp_group_init_point_charge(mgp_group* g);
+int         mgp_group_cycle(mgp_group* g, double* err_out);
+int         mgp_group_cycles(mgp_group* g, int32_t k, double* errs);
+int         mgp_group_set_field(mgp_group* g, int level, int which, const void* src, int64_t count, int mem);
+int         mgp_group_get_field(mgp_group* g, int level, int which, void* dst, int64_t count, int mem);
+int         mgp_group_residual_norm(mgp_group* g, int level, double* rnorm, double* fnorm);
 ]]
 
 local lib = ffi.load(os.getenv('MGP_LIBRARY') or 'mgpoisson')
@@ -76,19 +101,53 @@ local CODES = {
 	coarse_init = {fresh = 0, warm = 1},
 	coarse_bc = {zero = 0, consistent = 1},
 }
+-- include/mgpoisson.h MGP_FIELD_*; names of cpu-raw.lua:148-171
+local FIELD = {psi = 0, f = 1, rs = 2, vs = 3, psiOld = 4, errorBuf = 5, tmpU = 6, Vs = 0, Rs = 1}
 
 local function check(rc, ctx)
 	if rc < 0 then error('libmgpoisson: ' .. ffi.string(lib.mgp_last_error(ctx)), 3) end
 	return rc
 end
 
+local function checkGroup(rc, g)
+	if rc < 0 then error('libmgpoisson: ' .. ffi.string(lib.mgp_group_last_error(g)), 3) end
+	return rc
+end
+
 local MultigridHIP = {}
+-- cpu.lua:56-57 inPlaceIterativeSolver values (functions there, markers here)
+MultigridHIP.Jacobi = 'jacobi'
+MultigridHIP.GaussSeidel = 'rbgs'  -- the deterministic red/black form of cpu.lua:24-37 / gpu.lua:61-81
+
+local LEVEL_FIELDS = {rs = true, Rs = true, vs = true, Vs = true}
+local IMAGE_FIELDS = {psiOld = true, errorBuf = true, tmpU = true}
+
 MultigridHIP.__index = function(self, k)
-	if k == 'psi' then return self:getMatrix(0) end
-	if k == 'f' then return self:getMatrix(1) end
+	if k == 'psi' or k == 'f' then
+		if rawget(self, 'tableProtocol') then return self:getMatrix(FIELD[k]) end
+		return self:getImage(FIELD[k], 0)
+	end
 	if k == 'psiBuffer' then return self:getBuffer(0) end
 	if k == 'fBuffer' then return self:getBuffer(1) end
+	if IMAGE_FIELDS[k] then return self:getImage(FIELD[k], 0) end
+	if LEVEL_FIELDS[k] then
+		local mg = self
+		return setmetatable({}, {__index = function(_, L) return mg:getImage(FIELD[k], mg:levelOf(L)) end})
+	end
+	if k == 'inPlaceIterativeSolver' then return rawget(self, 'build').smoother end
 	return rawget(MultigridHIP, k)
+end
+
+MultigridHIP.__newindex = function(self, k, v)
+	if k == 'smooth' then
+		rawset(self, 'pendingSmooth', v)
+	elseif k == 'inPlaceIterativeSolver' then
+		local name = (v == MultigridHIP.GaussSeidel or v == 'GaussSeidel') and 'rbgs' or
+			((v == MultigridHIP.Jacobi or v == 'Jacobi') and 'jacobi' or error('inPlaceIterativeSolver: Jacobi | GaussSeidel'))
+		rawset(self, 'pendingSmoother', name)
+	else
+		rawset(self, k, v)
+	end
 end
 
 -- class defaults (cpu.lua:18-22, cpu-raw.lua:121-124)
@@ -106,11 +165,44 @@ setmetatable(MultigridHIP, {
 	end,
 })
 
+function MultigridHIP:makeOpts()
+	local b = rawget(self, 'build')
+	local n, dim = rawget(self, 'n'), rawget(self, 'dim')
+	local o = ffi.new('mgp_opts')
+	lib.mgp_opts_default(o)
+	o.dim = dim
+	o.n[0], o.n[1], o.n[2] = n, n, (dim == 3 and n or 1)
+	o.real_bytes = (b.real == 'float') and 4 or 8
+	o.nu1, o.nu2 = b.smooth, b.smooth
+	for field, map in pairs(CODES) do
+		if b[field] ~= nil then o[field] = assert(map[b[field]], 'unknown ' .. field) end
+	end
+	if b.device then o.device = b.device end
+	return o
+end
+
+function MultigridHIP:createContext()
+	local o = self:makeOpts()
+	local ngpu = rawget(self, 'ngpu')
+	if ngpu and ngpu > 1 then
+		local devs = rawget(self, 'devices')
+		local darr = devs and ffi.new('int[?]', ngpu, devs) or nil
+		local pp = ffi.new('mgp_group*[1]')
+		checkGroup(lib.mgp_group_create(pp, o, ngpu, darr), nil)
+		rawset(self, 'group', ffi.gc(pp[0], lib.mgp_group_destroy))
+	else
+		local pp = ffi.new('mgp_ctx*[1]')
+		check(lib.mgp_create(pp, o), nil)
+		rawset(self, 'ctx', ffi.gc(pp[0], lib.mgp_destroy))
+	end
+end
+
 function MultigridHIP:init(a, real, cpuDepth, engine)
 	local args
 	if type(a) == 'table' then
 		args = a
 		-- like cpu.lua:174-177: nil fields fall back to the class defaults
+		rawset(self, 'tableProtocol', true)
 		rawset(self, 'maxiter', args.maxiter)
 		rawset(self, 'epsilon', args.epsilon)
 		rawset(self, 'errorCallback', args.errorCallback)
@@ -124,29 +216,30 @@ function MultigridHIP:init(a, real, cpuDepth, engine)
 	local dim = args.dim or 2
 	rawset(self, 'real', args.real or 'double')
 	rawset(self, 'dim', dim)
-	rawset(self, 'size', n)
-	local o = ffi.new('mgp_opts')
-	lib.mgp_opts_default(o)
-	o.dim = dim
-	o.n[0], o.n[1], o.n[2] = n, n, (dim == 3 and n or 1)
-	o.real_bytes = (self.real == 'float') and 4 or 8
-	o.nu1, o.nu2 = args.smooth or self.smooth, args.smooth or self.smooth
-	for field, map in pairs(CODES) do
-		if args[field] ~= nil then o[field] = assert(map[args[field]], 'unknown ' .. field) end
+	rawset(self, 'n', n)
+	-- cpu.lua:178 self.size = matrix{size, size}; cpu-raw.lua:146 self.size = size
+	rawset(self, 'size', rawget(self, 'tableProtocol') and {n, n} or n)
+	rawset(self, 'ngpu', args.ngpu)
+	rawset(self, 'devices', args.devices)
+	local smoother = args.smoother
+	if args.inPlaceIterativeSolver then
+		smoother = (args.inPlaceIterativeSolver == MultigridHIP.GaussSeidel) and 'rbgs' or 'jacobi'
 	end
-	if args.device then o.device = args.device end
-	local pp = ffi.new('mgp_ctx*[1]')
-	check(lib.mgp_create(pp, o), nil)
-	rawset(self, 'ctx', ffi.gc(pp[0], lib.mgp_destroy))
-	rawset(self, 'count', n * n * (dim == 3 and n or 1))
-	rawset(self, 'ctype', (self.real == 'float') and 'float[?]' or 'double[?]')
-	if cpuDepth then
+	rawset(self, 'build', {real = rawget(self, 'real'), smooth = args.smooth or MultigridHIP.smooth,
+		smoother = smoother or 'jacobi', cycle = args.cycle, prolong = args.prolong,
+		coarse_init = args.coarse_init, coarse_bc = args.coarse_bc, device = args.device})
+	self:createContext()
+	local cells = n * n * (dim == 3 and n or 1)
+	rawset(self, 'count', cells)
+	rawset(self, 'ctype', (rawget(self, 'real') == 'float') and 'float[?]' or 'double[?]')
+	rawset(self, 'ptype', (rawget(self, 'real') == 'float') and 'float*' or 'double*')
+	if cpuDepth and not rawget(self, 'group') then
 		local L = bit.lshift(1, cpuDepth)
 		if engine then
 			-- cpu-gpu.lua:17-52: the callback runs engine:twoGrid on the level's host copies
+			local pt = rawget(self, 'ptype')
 			local cb = ffi.cast('mgp_coarse_fn', function(user, h, u, f, size)
-				local ok = pcall(engine.twoGrid, engine, h, ffi.cast(self.ctype:gsub('%[%?%]', '*'), u),
-					ffi.cast(self.ctype:gsub('%[%?%]', '*'), f), tonumber(size))
+				local ok = pcall(engine.twoGrid, engine, h, ffi.cast(pt, u), ffi.cast(pt, f), tonumber(size))
 				return ok and 0 or 1
 			end)
 			rawset(self, 'handoff', cb)  -- keep the callback alive
@@ -155,7 +248,42 @@ function MultigridHIP:init(a, real, cpuDepth, engine)
 			lib.mgp_set_coarse_level(self.ctx, L)  -- keeps the default switch when it does not fit
 		end
 	end
-	check(lib.mgp_init_point_charge(self.ctx), self.ctx)  -- cpu.lua:180-193
+	self:initPointCharge()
+end
+
+function MultigridHIP:initPointCharge()
+	local g = rawget(self, 'group')
+	if g then checkGroup(lib.mgp_group_init_point_charge(g), g)
+	else check(lib.mgp_init_point_charge(self.ctx), self.ctx) end  -- cpu.lua:180-193
+end
+
+-- a changed smooth / inPlaceIterativeSolver takes effect here (the reference reads them inside
+-- every twoGrid call, cpu.lua:96, 161): the context is rebuilt around the current psi and f
+function MultigridHIP:applyKnobs()
+	local ns, nm = rawget(self, 'pendingSmooth'), rawget(self, 'pendingSmoother')
+	if ns == nil and nm == nil then return end
+	local psi, f = self:getBuffer(0), self:getBuffer(1)
+	local b = rawget(self, 'build')
+	if ns ~= nil then b.smooth = ns end
+	if nm ~= nil then b.smoother = nm end
+	rawset(self, 'pendingSmooth', nil)
+	rawset(self, 'pendingSmoother', nil)
+	rawset(self, 'ctx', nil)
+	rawset(self, 'group', nil)
+	collectgarbage()
+	self:createContext()
+	self:setBuffer(0, psi)
+	self:setBuffer(1, f)
+end
+
+function MultigridHIP:levelOf(size)
+	local info = ffi.new('int64_t[8]')
+	local n = check(lib.mgp_num_levels(self.ctx), self.ctx)
+	for l = 0, n - 1 do
+		check(lib.mgp_level_info(self.ctx, l, info), self.ctx)
+		if tonumber(info[0]) == size then return l end
+	end
+	error('no level of size ' .. tostring(size))
 end
 
 function MultigridHIP:metrics()
@@ -164,16 +292,47 @@ function MultigridHIP:metrics()
 	return rel[0], tonumber(n[0]), frob[0]
 end
 
-function MultigridHIP:getBuffer(which)
-	local buf = ffi.new(self.ctype, self.count)
-	check(lib.mgp_get_field(self.ctx, 0, which, buf, self.count, 0), self.ctx)
-	return buf
+function MultigridHIP:residualNorm(level)
+	local r, f = ffi.new('double[1]'), ffi.new('double[1]')
+	local g = rawget(self, 'group')
+	if g then checkGroup(lib.mgp_group_residual_norm(g, level or 0, r, f), g)
+	else check(lib.mgp_residual_norm(self.ctx, level or 0, r, f), self.ctx) end
+	return r[0], f[0]
+end
+
+function MultigridHIP:getBuffer(which, level)
+	level = level or 0
+	local count = self.count
+	if level ~= 0 then
+		local info = ffi.new('int64_t[8]')
+		check(lib.mgp_level_info(self.ctx, level, info), self.ctx)
+		count = tonumber(info[0] * info[1] * info[3])
+	end
+	local buf = ffi.new(self.ctype, count)
+	local g = rawget(self, 'group')
+	if g then checkGroup(lib.mgp_group_get_field(g, level, which, buf, count, 0), g)
+	else check(lib.mgp_get_field(self.ctx, level, which, buf, count, 0), self.ctx) end
+	return buf, count
+end
+
+function MultigridHIP:setBuffer(which, buf)
+	local g = rawget(self, 'group')
+	if g then checkGroup(lib.mgp_group_set_field(g, 0, which, buf, self.count, 0), g)
+	else check(lib.mgp_set_field(self.ctx, 0, which, buf, self.count, 0), self.ctx) end
+end
+
+-- image-like view (cpu-raw.lua's image(w,h,1,real) with .buffer), a host copy
+function MultigridHIP:getImage(which, level)
+	local buf, count = self:getBuffer(which, level)
+	local w = math.floor(math.sqrt(count) + 0.5)
+	if self.dim == 3 then w = math.floor(count ^ (1 / 3) + 0.5) end
+	return {buffer = buf, width = w, height = w, count = count}
 end
 
 -- 1-based nested table m[i][j] with i = x (cpu.lua's matrix indexing), 2D only
 function MultigridHIP:getMatrix(which)
 	local buf = self:getBuffer(which)
-	local n = self.size
+	local n = self.n
 	if self.dim ~= 2 then return buf end
 	local m = {}
 	for i = 1, n do
@@ -186,11 +345,16 @@ end
 
 -- cpu.lua:196-206
 function MultigridHIP:step()
+	self:applyKnobs()
 	local err = ffi.new('double[1]')
-	check(lib.mgp_cycle(self.ctx, err), self.ctx)
+	local g = rawget(self, 'group')
+	if g then checkGroup(lib.mgp_group_cycle(g, err), g)
+	else check(lib.mgp_cycle(self.ctx, err), self.ctx) end
 	if self.debug then print('err', err[0]) end
 	return err[0]
 end
+
+local function finite(x) return x == x and x ~= math.huge and x ~= -math.huge end
 
 -- cpu.lua:208-216, break rules included
 function MultigridHIP:solve()
@@ -198,7 +362,7 @@ function MultigridHIP:solve()
 	for iter = 1, self.maxiter do
 		local err = self:step()
 		if self.errorCallback and self.errorCallback(iter, err) then break end
-		if err < self.epsilon or err ~= err or err == math.huge or err == -math.huge then break end
+		if err < self.epsilon or not finite(err) then break end
 	end
 end
 
@@ -208,12 +372,29 @@ function MultigridHIP:run()
 	for iter = 1, 2 do
 		local err = self:step()
 		print(iter, err)
-		if err < self.accuracy or err ~= err then break end
+		if err < self.accuracy or not finite(err) then break end  -- gpu.lua:371 math.isfinite
 	end
 end
 
--- cpu-raw.lua:186 twoGrid(h, u, f, L) on raw host real* buffers (u updated in place)
+-- cpu-raw.lua:186 twoGrid(h, u, f, L) on raw host real* buffers (u updated in place), or
+-- cpu.lua:70 twoGrid(h, u, f) on lua-matrix-style tables u[i][j] (x = i; u updated in place)
 function MultigridHIP:twoGrid(h, u, f, L)
+	self:applyKnobs()
+	if type(u) == 'table' then
+		local n = #u
+		local ub, fb = ffi.new(self.ctype, n * n), ffi.new(self.ctype, n * n)
+		for i = 1, n do
+			for j = 1, n do
+				ub[(i - 1) + n * (j - 1)] = u[i][j]
+				fb[(i - 1) + n * (j - 1)] = f[i][j]
+			end
+		end
+		check(lib.mgp_two_grid(self.ctx, h, ub, fb, n, 0), self.ctx)
+		for i = 1, n do
+			for j = 1, n do u[i][j] = tonumber(ub[(i - 1) + n * (j - 1)]) end
+		end
+		return u
+	end
 	check(lib.mgp_two_grid(self.ctx, h, u, f, L, 0), self.ctx)
 end
 

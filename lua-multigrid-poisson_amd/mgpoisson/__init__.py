@@ -3,8 +3,8 @@
 Importing this package loads the HIP library and fails loudly if it is missing.
 """
 from ._lib import MGPError, comm_unique_id, default_opts, plan  # noqa: F401
-from .context import Context, Loopback, make_opts  # noqa: F401
+from .context import Context, Group, Loopback, make_opts  # noqa: F401
 from .solver import MultigridHIP, MultigridHIPHybrid, MultigridHIPRaw  # noqa: F401
 
-__all__ = ["Context", "Loopback", "MGPError", "MultigridHIP", "MultigridHIPHybrid", "MultigridHIPRaw", "comm_unique_id", "default_opts",
+__all__ = ["Context", "Group", "Loopback", "MGPError", "MultigridHIP", "MultigridHIPHybrid", "MultigridHIPRaw", "comm_unique_id", "default_opts",
            "make_opts", "plan"]

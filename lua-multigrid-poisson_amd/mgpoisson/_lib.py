@@ -39,6 +39,10 @@ PROLONG_PC, PROLONG_LINEAR = 0, 1
 COARSE_FRESH, COARSE_WARM = 0, 1
 BC_ZERO, BC_CONSISTENT = 0, 1
 FIELD_U, FIELD_F = 0, 1
+FIELD_RESIDUAL, FIELD_CORRECTION, FIELD_PSI_OLD, FIELD_ERROR, FIELD_TMP = 2, 3, 4, 5, 6
+# cpu-raw.lua:148-171 names of the level fields (Vs/Rs are U/F below the finest level)
+FIELDS = {"psi": FIELD_U, "f": FIELD_F, "Vs": FIELD_U, "Rs": FIELD_F, "rs": FIELD_RESIDUAL, "vs": FIELD_CORRECTION,
+          "psiOld": FIELD_PSI_OLD, "errorBuf": FIELD_ERROR, "tmpU": FIELD_TMP}
 MEM_HOST, MEM_DEVICE = 0, 1
 # int fn(void* user, double h, void* u, const void* f, int64_t size)
 COARSE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_double, ctypes.c_void_p, ctypes.c_void_p,
@@ -107,6 +111,18 @@ SIGNATURES = {
     "mgp_set_coarse_handoff": (ctypes.c_int, [_vp, _i64, COARSE_FN, _vp]),
     "mgp_timing": (ctypes.c_int, [_vp, ctypes.c_int]),
     "mgp_timing_read": (ctypes.c_int, [_vp, ctypes.c_int, _P(_dbl), _P(_i64), _P(_dbl)]),
+    "mgp_group_create": (ctypes.c_int, [_P(_vp), _P(MGPOpts), ctypes.c_int, _P(ctypes.c_int)]),
+    "mgp_group_destroy": (None, [_vp]),
+    "mgp_group_last_error": (ctypes.c_char_p, [_vp]),
+    "mgp_group_size": (ctypes.c_int, [_vp]),
+    "mgp_group_rank": (_vp, [_vp, ctypes.c_int]),
+    "mgp_group_init_point_charge": (ctypes.c_int, [_vp]),
+    "mgp_group_cycle": (ctypes.c_int, [_vp, _P(_dbl)]),
+    "mgp_group_cycles": (ctypes.c_int, [_vp, _i32, _P(_dbl)]),
+    "mgp_group_set_field": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, _vp, _i64, ctypes.c_int]),
+    "mgp_group_get_field": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, _vp, _i64, ctypes.c_int]),
+    "mgp_group_residual_norm": (ctypes.c_int, [_vp, ctypes.c_int, _P(_dbl), _P(_dbl)]),
+    "mgp_group_field_stats": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, _P(ctypes.c_uint64), _P(_dbl)]),
 }
 
 for _name, (_res, _args) in SIGNATURES.items():
@@ -126,6 +142,13 @@ class MGPError(RuntimeError):
 def check(code: int, ctx=None) -> int:
     if code < 0:
         msg = lib.mgp_last_error(ctx)
+        raise MGPError(code, msg.decode() if msg else "")
+    return code
+
+
+def check_group(code: int, group=None) -> int:
+    if code < 0:
+        msg = lib.mgp_group_last_error(group)
         raise MGPError(code, msg.decode() if msg else "")
     return code
 

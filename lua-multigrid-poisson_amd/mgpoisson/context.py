@@ -257,3 +257,88 @@ class Context:
             self._chk(L.lib.mgp_timing_read(self._h, kind, ctypes.byref(ms), ctypes.byref(n), ctypes.byref(by)))
             out[name] = (ms.value, n.value, by.value)
         return out
+
+
+class Group:
+    """One host process driving `ngpu` GPUs (mgp_group_create): one z-slab context per rank, RCCL
+    communicators from ncclCommInitAll, every call run by one host thread per device inside the
+    library.  devices all equal (e.g. [0] * 8) = the ranks share that GPU through the loopback
+    transport (tests).  Field I/O is global (the whole box, x fastest)."""
+
+    def __init__(self, opts: L.MGPOpts, ngpu: int, devices=None):
+        self.opts = opts
+        self.dtype = np.dtype(np.float64 if opts.real_bytes == 8 else np.float32)
+        h = ctypes.c_void_p()
+        devs = None if devices is None else (ctypes.c_int * ngpu)(*devices)
+        L.check_group(L.lib.mgp_group_create(ctypes.byref(h), ctypes.byref(opts), ngpu, devs))
+        self._h = h
+        self.ngpu = ngpu
+        self.ranks = [_RankView(L.lib.mgp_group_rank(h, r), opts) for r in range(ngpu)]
+        self.levels = self.ranks[0].levels
+
+    def close(self):
+        if getattr(self, "_h", None):
+            L.lib.mgp_group_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _chk(self, rc):
+        return L.check_group(rc, self._h)
+
+    def shape(self, level=0):
+        lv = self.levels[level]
+        return (lv["nz_global"], lv["ny"], lv["nx"])
+
+    def init_point_charge(self):
+        self._chk(L.lib.mgp_group_init_point_charge(self._h))
+
+    def cycle(self) -> float:
+        e = ctypes.c_double()
+        self._chk(L.lib.mgp_group_cycle(self._h, ctypes.byref(e)))
+        return e.value
+
+    def cycles(self, k: int) -> np.ndarray:
+        errs = np.zeros(k, dtype=np.float64)
+        self._chk(L.lib.mgp_group_cycles(self._h, k, errs.ctypes.data_as(ctypes.POINTER(ctypes.c_double))))
+        return errs
+
+    def get_field(self, which, level=0):
+        out = np.empty(self.shape(level), dtype=self.dtype)
+        self._chk(L.lib.mgp_group_get_field(self._h, level, which, out.ctypes.data, out.size, L.MEM_HOST))
+        return out
+
+    def set_field(self, which, arr, level=0):
+        a = np.ascontiguousarray(arr, dtype=self.dtype)
+        self._chk(L.lib.mgp_group_set_field(self._h, level, which, a.ctypes.data, a.size, L.MEM_HOST))
+
+    def get_psi(self, level=0):
+        return self.get_field(L.FIELD_U, level)
+
+    def residual_norm(self, level=0):
+        r, f = ctypes.c_double(), ctypes.c_double()
+        self._chk(L.lib.mgp_group_residual_norm(self._h, level, ctypes.byref(r), ctypes.byref(f)))
+        return r.value, f.value
+
+    def field_stats(self, which=L.FIELD_U, level=0):
+        h = ctypes.c_uint64()
+        d = (ctypes.c_double * 3)()
+        self._chk(L.lib.mgp_group_field_stats(self._h, level, which, ctypes.byref(h), d))
+        return h.value, d[0], d[1], d[2]
+
+
+class _RankView(Context):
+    """A rank's context owned by a Group (not destroyed on its own)."""
+
+    def __init__(self, handle, opts):  # noqa: D401 - no super().__init__: the group created it
+        self.opts = opts
+        self.dtype = np.dtype(np.float64 if opts.real_bytes == 8 else np.float32)
+        self._h = ctypes.c_void_p(handle)
+        self._read_levels()
+
+    def close(self):
+        self._h = None

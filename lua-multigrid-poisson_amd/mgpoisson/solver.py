@@ -21,7 +21,74 @@ from . import _lib as L
 from .context import Context, make_opts
 
 
-class MultigridHIP:
+class _Smoother(str):
+    """The values of ``inPlaceIterativeSolver`` (cpu.lua:56-57): ``MultigridHIP.Jacobi`` (the
+    reference's active choice) or ``MultigridHIP.GaussSeidel`` (in the reference a lexicographic
+    in-place sweep that is racy on a GPU, gpu.lua:61-62; here its deterministic red/black form)."""
+
+
+class LevelFields:
+    """``mg.rs[L]`` / ``mg.Rs[L]`` / ``mg.vs[L]`` / ``mg.Vs[L]`` of cpu-raw.lua:155-171: the field of the
+    level of size L (a power of two, as the reference's table keys), downloaded from HBM."""
+
+    def __init__(self, ctx_fn, which):
+        self._ctx_fn = ctx_fn
+        self._which = which
+
+    def _level(self, size):
+        ctx = self._ctx_fn()
+        for l, lv in enumerate(ctx.levels):
+            if lv["nx"] == int(size):
+                return ctx, l
+        raise KeyError(size)
+
+    def __getitem__(self, size):
+        ctx, l = self._level(size)
+        return ctx.get_field(self._which, l)
+
+    def __setitem__(self, size, value):
+        ctx, l = self._level(size)
+        if self._which not in (L.FIELD_U, L.FIELD_F):
+            raise TypeError("rs / vs are computed views (read-only)")
+        ctx.set_field(self._which, value, l)
+
+    def keys(self):
+        return [lv["nx"] for lv in self._ctx_fn().levels]
+
+
+class _RawFields:
+    """cpu-raw.lua's buffer fields on a context: psiOld, errorBuf, tmpU and the per-level rs/Rs/vs/Vs."""
+
+    @property
+    def psiOld(self):
+        return self.ctx.get_field(L.FIELD_PSI_OLD, 0)
+
+    @property
+    def errorBuf(self):
+        return self.ctx.get_field(L.FIELD_ERROR, 0)
+
+    @property
+    def tmpU(self):
+        return self.ctx.get_field(L.FIELD_TMP, 0)
+
+    @property
+    def rs(self):
+        return LevelFields(lambda: self.ctx, L.FIELD_RESIDUAL)
+
+    @property
+    def Rs(self):
+        return LevelFields(lambda: self.ctx, L.FIELD_F)
+
+    @property
+    def vs(self):
+        return LevelFields(lambda: self.ctx, L.FIELD_CORRECTION)
+
+    @property
+    def Vs(self):
+        return LevelFields(lambda: self.ctx, L.FIELD_U)
+
+
+class MultigridHIP(_RawFields):
     """Drop-in for ``MultigridCPU`` (cpu.lua:15-218), solving on the GPU.
 
     ``MultigridHIP({'size': n, 'maxiter': ..., 'epsilon': ..., 'errorCallback': fn,
@@ -36,6 +103,8 @@ class MultigridHIP:
     smooth = 7  # cpu.lua:20
     epsilon = 1e-10  # cpu.lua:21
     maxiter = 1000  # cpu.lua:22
+    Jacobi = _Smoother("jacobi")  # cpu.lua:40-54
+    GaussSeidel = _Smoother("rbgs")  # cpu.lua:24-37, red/black on the GPU
 
     def __init__(self, args=None, **kw):
         a = dict(args or {})
@@ -53,7 +122,8 @@ class MultigridHIP:
             self.smooth = int(a["smooth"])
         self.dim = int(a.get("dim", 2))
         self.size = (n,) * self.dim  # matrix{size, size} (cpu.lua:178)
-        self._build = dict(dim=self.dim, real=a.get("real", "double"), smoother=a.get("smoother", "jacobi"),
+        sm = a.get("inPlaceIterativeSolver", a.get("smoother", "jacobi"))
+        self._build = dict(dim=self.dim, real=a.get("real", "double"), smoother=_smoother_name(sm),
                            cycle=a.get("cycle", "V"), prolong=a.get("prolong", "pc"),
                            coarse_init=a.get("coarse_init", "fresh"), coarse_bc=a.get("coarse_bc", "zero"),
                            device=a.get("device", -1))
@@ -64,6 +134,23 @@ class MultigridHIP:
 
     # The reference reads self.smooth inside every twoGrid call (cpu.lua:96, 161); the
     # sweep counts are baked into the device context, so a change rebuilds it, keeping psi/f.
+    @property
+    def inPlaceIterativeSolver(self):
+        """cpu.lua:56-57's knob: MultigridHIP.Jacobi or MultigridHIP.GaussSeidel (writable)."""
+        return self.Jacobi if self._build["smoother"] == "jacobi" else self.GaussSeidel
+
+    @inPlaceIterativeSolver.setter
+    def inPlaceIterativeSolver(self, value):
+        name = _smoother_name(value)
+        if name != self._build["smoother"]:
+            self._build["smoother"] = name
+            self._ctx_smooth = None  # rebuild on next use, keeping psi / f
+
+    @property
+    def ctx(self):
+        self._ensure_ctx()
+        return self._ctx
+
     def _ensure_ctx(self):
         if self._ctx is not None and self._ctx_smooth == self.smooth:
             return
@@ -116,12 +203,32 @@ class MultigridHIP:
                 break
 
     def twoGrid(self, h, u, f):
-        """cpu.lua:70 twoGrid(h, u, f) on an (L, L[, L]) host array u (updated in place)."""
+        """cpu.lua:70 twoGrid(h, u, f): u updated in place.  u / f are (L, L[, L]) host arrays, or
+        cpu.lua-style 1-based-indexed nested lists u[i][j] (x = i), whose rows are updated in place."""
         self._ensure_ctx()
-        self._ctx.two_grid(h, u, f, u.shape[-1])
+        if isinstance(u, np.ndarray):
+            self._ctx.two_grid(h, u, f, u.shape[-1])
+            return u
+        # lua-matrix form: nested lists indexed [i][j] with x = i (cpu.lua:43-53)
+        ua = np.ascontiguousarray(np.array(u, dtype=self._ctx.dtype).T)
+        fa = np.ascontiguousarray(np.array(f, dtype=self._ctx.dtype).T)
+        self._ctx.two_grid(h, ua, fa, ua.shape[-1])
+        for i, row in enumerate(u):
+            row[:] = ua[:, i].tolist()
+        return u
 
 
-class MultigridHIPRaw:
+def _smoother_name(v):
+    if callable(v) and getattr(v, "__name__", "") in ("Jacobi", "GaussSeidel"):
+        v = v.__name__
+    v = str(v)
+    names = {"jacobi": "jacobi", "Jacobi": "jacobi", "rbgs": "rbgs", "GaussSeidel": "rbgs", "gaussseidel": "rbgs"}
+    if v not in names:
+        raise ValueError(f"inPlaceIterativeSolver: {v!r} (Jacobi | GaussSeidel)")
+    return names[v]
+
+
+class MultigridHIPRaw(_RawFields):
     """Drop-in for ``MultigridCPURaw`` / ``MultigridGPU`` (cpu-raw.lua:118-260, gpu.lua:18-375).
 
     ``MultigridHIPRaw(size, real='double')``; ``run()`` does the reference's two hard-coded

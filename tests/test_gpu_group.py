@@ -1,0 +1,58 @@
+"""The single-process multi-GPU group (mgp_group_create): one host process, one context per rank,
+the ranks' work run by one host thread per device inside the library (the Lua
+host of north_star drives the node's GPUs this way).  On the one-GPU test box every rank sits on
+device 0 and the group uses the loopback transport; with distinct devices it builds its RCCL
+communicators with ncclCommInitAll.  Bar: the group's global psi and err == the single-domain run,
+bit for bit (err to summation order)."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _mg():
+    import mgpoisson
+
+    return mgpoisson
+
+
+CASES = [
+    ((64, 64, 128), 2, dict(real="float", smoother="rbgs", nu1=2, nu2=2, prolong="linear", coarse_bc="consistent"), None),
+    ((64, 64, 256), 8, dict(real="double", smoother="rbgs", nu1=2, nu2=2, prolong="linear", coarse_bc="consistent",
+                            cycle="F", gather_cells=4096), None),
+    ((128, 128, 128), 8, dict(real="float", smoother="rbgs", nu1=2, nu2=2, prolong="linear", coarse_bc="consistent"),
+     "65536"),
+    ((32, 32, 64), 2, dict(real="double", smoother="jacobi", nu1=3, nu2=3, prolong="pc", coarse_init="warm"), None),
+]
+
+
+@pytest.mark.parametrize("box,world,cfg,fused", CASES, ids=["w2-f32", "w8-F-f64", "w8-fused-f32", "w2-jacobi-warm"])
+def test_group_equals_single_domain(box, world, cfg, fused, monkeypatch):
+    mg = _mg()
+    if fused:
+        monkeypatch.setenv("MGP_FUSED", "1")
+        monkeypatch.setenv("MGP_FUSED_MIN_CELLS", fused)
+    g = mg.Group(mg.make_opts(dim=3, n=box, **cfg), world, devices=[0] * world)
+    assert len(g.ranks) == world
+    assert all(r.levels[0]["distributed"] for r in g.ranks)
+    assert [r.levels[0]["z0"] for r in g.ranks] == [k * box[2] // world for k in range(world)]
+    g.init_point_charge()
+    ref = mg.Context(mg.make_opts(dim=3, n=box, **cfg))
+    ref.init_point_charge()
+    eg = np.concatenate([g.cycles(2), [g.cycle()]])
+    er = ref.cycles(3)
+    assert np.array_equal(g.get_psi(), ref.get_psi())
+    np.testing.assert_allclose(eg, er, rtol=1e-12, atol=0)
+    assert g.field_stats()[0] == ref.field_stats()[0]
+    np.testing.assert_allclose(g.residual_norm(), ref.residual_norm(), rtol=1e-12, atol=0)
+    # global field I/O round trip through the ranks' slabs
+    u = np.random.default_rng(1).uniform(-1, 1, g.shape(0)).astype(g.dtype)
+    g.set_field(0, u)
+    assert np.array_equal(g.get_psi(), u)
+    g.close()
+
+
+def test_group_rejects_bad_split():
+    mg = _mg()
+    with pytest.raises(mg.MGPError):
+        mg.Group(mg.make_opts(dim=3, n=(16, 16, 16)), 16, devices=[0] * 16)

@@ -239,3 +239,60 @@ def test_loopback_w8_fused_config4_aspect(monkeypatch):
     for r in range(world):
         np.testing.assert_allclose(res[r][1], e_ref, rtol=1e-12, atol=0)
         np.testing.assert_allclose(res[r][2], ref.residual_norm(), rtol=1e-12, atol=0)
+
+
+@pytest.mark.parametrize("real", ["double", "float"])
+def test_cpu_raw_fields(real):
+    """cpu-raw.lua:148-171 state by name: rs/Rs/vs/Vs per level size, psiOld, errorBuf, tmpU."""
+    from oracle_lib import prolong_correct_arr
+
+    mg = _mg()
+    r = mg.MultigridHIPRaw(32, real, nu1=2, nu2=2, coarse_init="fresh")
+    r.quiet = True
+    r.run(1)
+    old = r.psi
+    r.run(1)
+    psi = r.psi
+    ctx = r.ctx
+    assert np.array_equal(r.psiOld, old)
+    d = psi - old
+    assert np.array_equal(r.errorBuf, d * d)
+    assert r.tmpU.shape == psi.shape  # Jacobi target buffer
+    assert sorted(r.rs.keys(), reverse=True) == [32, 16, 8, 4, 2, 1]
+    for size in (32, 16, 8):
+        lvl = [lv["nx"] for lv in ctx.levels].index(size)
+        u, f = r.Vs[size], r.Rs[size]
+        ref = residual_arr(2, u, f, (2.0 ** lvl) / 32, 0.0)
+        assert np.array_equal(r.rs[size], ref)
+        V = r.Vs[size // 2]
+        assert np.array_equal(r.vs[size], prolong_correct_arr(2, np.zeros_like(u), V, "pc", 0.0))
+    with pytest.raises(TypeError):
+        r.rs[8] = np.zeros((8, 8))
+
+
+def test_cpu_lua_knobs_and_matrix_two_grid():
+    """cpu.lua protocol: size is {n, n}, inPlaceIterativeSolver is writable (Jacobi <-> GaussSeidel,
+    rebuilding the device context with psi / f kept), twoGrid(h, u, f) takes lua-matrix-style lists."""
+    mg = _mg()
+    s = mg.MultigridHIP(size=16)
+    assert s.size == (16, 16)
+    assert s.inPlaceIterativeSolver == mg.MultigridHIP.Jacobi
+    s.step()
+    psi = s.psi
+    s.inPlaceIterativeSolver = mg.MultigridHIP.GaussSeidel
+    assert s.inPlaceIterativeSolver == mg.MultigridHIP.GaussSeidel
+    assert np.array_equal(s.psi, psi)
+    o = Oracle(dim=2, n=(16, 16, 1), smoother="rbgs")
+    o.set(0, psi)
+    o.set(1, s.f)
+    s.step()
+    o.step()
+    assert np.array_equal(s.psi, o.get(0))
+    u = _rand((8, 8), np.float64, 1)
+    f = _rand((8, 8), np.float64, 2)
+    ua = u.copy()
+    s.twoGrid(2.0 / 16, ua, f)
+    ul = [list(map(float, u[:, i])) for i in range(8)]  # ul[i][j], x = i
+    fl = [list(map(float, f[:, i])) for i in range(8)]
+    s.twoGrid(2.0 / 16, ul, fl)
+    assert np.array_equal(np.array(ul).T, ua)
