@@ -170,6 +170,16 @@ int         mgp_metrics(mgp_ctx* c, double* rel_err, int64_t* count, double* fro
  * converged relative residual ||r|| / ||f||. */
 int         mgp_residual_norm(mgp_ctx* c, int level, double* rnorm, double* fnorm);
 
+/* The reference's Krylov cross-check (test/converge-multigrid-vs-krylov.lua:38-69, solver.conjgrad) on
+ * the device, as an independent second oracle for the converged multigrid answer: matrix-free
+ * conjugate gradients on the finest level's operator (same 5-/7-point stencil, ghost 0) from
+ * x0 = -f with b = f, fp64 dot products, stopping when rSq / bSq < epsilon or after maxiter
+ * iterations.  The solution goes to x_out (level-0 cells, x fastest; may be NULL); linf_hist (maxiter
+ * doubles, may be NULL) gets |x|_inf after every iteration, the quantity the reference plots.  The
+ * solver's own psi / f are not changed.  Single-GPU contexts only. */
+int         mgp_cg_solve(mgp_ctx* c, double epsilon, int32_t maxiter, void* x_out, int mem, int32_t* iters,
+                         double* err, double* linf_hist);
+
 /* Loopback transport (tests only): the `world` ranks of a slab decomposition as contexts of ONE
  * process on one GPU, each driven by its own host thread.  Halo exchanges, the all-gather and the
  * err all-reduce become device copies ordered by events and a host barrier instead of RCCL calls;

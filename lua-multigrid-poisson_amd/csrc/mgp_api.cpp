@@ -1632,6 +1632,62 @@ int mgp_residual_norm(mgp_ctx* c, int level, double* rnorm, double* fnorm)
     return MGP_OK;
 }
 
+int mgp_cg_solve(mgp_ctx* c, double epsilon, int32_t maxiter, void* x_out, int mem, int32_t* iters, double* err,
+                 double* linf_hist)
+{
+    if (!c || maxiter < 0) return MGP_ERR_ARG;
+    if (c->o.world > 1) return c->fail(MGP_ERR_STATE, "mgp_cg_solve: single-GPU contexts only");
+    Level& L = c->lev[0];
+    const size_t bytes = (size_t)L.alloc * c->rb;
+    std::vector<char*> buf(4, nullptr);
+    double* scratch = nullptr;
+    void* lex = nullptr;
+    const int64_t count = level_count(L);
+    auto release = [&] {
+        for (char* b : buf)
+            if (b) (void)hipFree(b);
+        if (scratch) (void)hipFree(scratch);
+        if (lex && lex != x_out) (void)hipFree(lex);
+    };
+    for (auto& b : buf)
+        if (hipMalloc(&b, bytes) != hipSuccess || hipMemsetAsync(b, 0, bytes, c->s) != hipSuccess) {
+            release();
+            return c->fail(MGP_ERR_OOM, "mgp_cg_solve: no room for the CG vectors");
+        }
+    if (hipMalloc(&scratch, sizeof(double) * mgp::cg_scratch_doubles()) != hipSuccess) {
+        release();
+        return c->fail(MGP_ERR_OOM, "mgp_cg_solve: no room for the CG scratch");
+    }
+    mgp::CgArgs a{};
+    a.g = L.g;
+    a.h = level_h(c, 0);
+    a.cl = 0.0;
+    a.x = c->ui(L, buf[0]);
+    a.r = c->ui(L, buf[1]);
+    a.p = c->ui(L, buf[2]);
+    a.q = c->ui(L, buf[3]);
+    a.b = c->ui(L, L.f);
+    a.scratch = scratch;
+    a.x0_neg_b = true;  // converge-multigrid-vs-krylov.lua:45-46: x = -f, b = f
+    a.maxiter = maxiter;
+    a.epsilon = epsilon;
+    a.linf = linf_hist;
+    hipError_t e = mgp::launch_cg(c->rb, c->o.dim, a, c->s);
+    if (e == hipSuccess && x_out) {
+        if (mem == MGP_MEM_DEVICE) lex = x_out;
+        else e = hipMalloc(&lex, (size_t)count * c->rb);
+        if (e == hipSuccess) e = mgp::launch_unpack(c->rb, a.x, lex, L.g, c->s);
+        if (e == hipSuccess && mem != MGP_MEM_DEVICE)
+            e = hipMemcpyAsync(x_out, lex, (size_t)count * c->rb, hipMemcpyDeviceToHost, c->s);
+        if (e == hipSuccess) e = hipStreamSynchronize(c->s);
+    }
+    release();
+    if (e != hipSuccess) return c->fail(MGP_ERR_HIP, "mgp_cg_solve: %s", hipGetErrorString(e));
+    if (iters) *iters = a.iters;
+    if (err) *err = a.err;
+    return MGP_OK;
+}
+
 int mgp_timing(mgp_ctx* c, int enable)
 {
     if (!c) return MGP_ERR_ARG;

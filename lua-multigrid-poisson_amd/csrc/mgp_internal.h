@@ -129,6 +129,24 @@ struct TailSpec {
 size_t tail_lds_bytes(int rb, int dim, int jacobi, const Geo* g, int nlev);
 hipError_t launch_tail(int rb, int dim, const TailSpec& t, hipStream_t s);
 
+// Conjugate gradients on a level's operator (mgp_krylov.hip; converge-multigrid-vs-krylov.lua:38-69).
+// Packed level vectors x (in/out), b, and scratch r, p, q; scratch holds cg_scratch_doubles() doubles.
+struct CgArgs {
+    Geo g;
+    double h, cl;
+    void *x, *r, *p, *q;
+    const void* b;
+    double* scratch;
+    bool x0_neg_b;    // x0 = -b (the reference's start) instead of x's content
+    int maxiter;
+    double epsilon;   // stop when rSq / bSq < epsilon
+    double* linf;     // optional: |x|_inf after each iteration (maxiter entries)
+    int iters;        // out
+    double err;       // out: final rSq / bSq
+};
+int cg_scratch_doubles();
+hipError_t launch_cg(int rb, int dim, CgArgs& a, hipStream_t s);
+
 constexpr int kSumBlocks = 1024;
 
 }  // namespace mgp

@@ -108,6 +108,7 @@ SIGNATURES = {
     "mgp_metrics": (ctypes.c_int, [_vp, _P(_dbl), _P(_i64), _P(_dbl)]),
     "mgp_set_coarse_level": (ctypes.c_int, [_vp, _i64]),
     "mgp_residual_norm": (ctypes.c_int, [_vp, ctypes.c_int, _P(_dbl), _P(_dbl)]),
+    "mgp_cg_solve": (ctypes.c_int, [_vp, _dbl, _i32, _vp, ctypes.c_int, _P(_i32), _P(_dbl), _P(_dbl)]),
     "mgp_set_coarse_handoff": (ctypes.c_int, [_vp, _i64, COARSE_FN, _vp]),
     "mgp_timing": (ctypes.c_int, [_vp, ctypes.c_int]),
     "mgp_timing_read": (ctypes.c_int, [_vp, ctypes.c_int, _P(_dbl), _P(_i64), _P(_dbl)]),

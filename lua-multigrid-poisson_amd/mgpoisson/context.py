@@ -242,6 +242,19 @@ class Context:
         self._chk(L.lib.mgp_residual_norm(self._h, level, ctypes.byref(r), ctypes.byref(f)))
         return r.value, f.value
 
+    def cg_solve(self, epsilon=1e-20, maxiter=10000, history=False):
+        """Device CG on the finest level (converge-multigrid-vs-krylov.lua:38-69): x0 = -f, b = f, stop at
+        rSq / bSq < epsilon.  Returns (x, iterations, rSq / bSq[, |x|_inf per iteration])."""
+        x = np.empty(self.shape(0), dtype=self.dtype)
+        it, err = ctypes.c_int32(), ctypes.c_double()
+        hist = np.zeros(maxiter, dtype=np.float64) if history else None
+        self._chk(L.lib.mgp_cg_solve(self._h, float(epsilon), int(maxiter), x.ctypes.data, L.MEM_HOST, ctypes.byref(it),
+                                     ctypes.byref(err),
+                                     hist.ctypes.data_as(ctypes.POINTER(ctypes.c_double)) if history else None))
+        if history:
+            return x, it.value, err.value, hist[:it.value]
+        return x, it.value, err.value
+
     def sync(self):
         self._chk(L.lib.mgp_sync(self._h))
 

@@ -69,30 +69,9 @@ def bench(lo=5, hi=10, tries=1, cols=("hip",), cpudepth=3, out="cpu-vs-gpu.txt",
     return rows
 
 
-def _cg_linf_history(f: np.ndarray, h: float, epsilon: float, maxiter: int = 100000):
-    """|x|_inf per CG iteration on A x = f (5-point, zero ghosts), x0 = -f (converge...lua:37-58)."""
-    import scipy.sparse as sp
-    import scipy.sparse.linalg as spla
-
-    n = f.shape[0]
-    one = sp.diags([np.ones(n - 1), -2 * np.ones(n), np.ones(n - 1)], [-1, 0, 1])
-    eye = sp.identity(n)
-    A = (sp.kron(eye, one) + sp.kron(one, eye)) / (h * h)
-    hist = []
-    b = f.reshape(-1)
-    bsq = float(b @ b)
-
-    def cb(xk):
-        hist.append(float(np.max(np.abs(xk))))
-
-    # the reference stops when err = rSq / bSq < epsilon; scipy's rtol is on |r| / |b|
-    spla.cg(A, b, x0=-b.copy(), rtol=max(np.sqrt(epsilon), 1e-15), atol=0.0, maxiter=maxiter, callback=cb)
-    del bsq
-    return hist
-
-
-def converge(sizes=(4, 8, 16, 32, 64, 128), epsilon=1e-20, outdir="converge", maxiter=1000, quiet=False):
-    """converge-multigrid-vs-krylov.lua: |psi|_inf per multigrid iteration next to CG's."""
+def converge(sizes=(4, 8, 16, 32, 64, 128), epsilon=1e-20, outdir="converge", maxiter=1000, quiet=False,
+             cg_maxiter=20000):
+    """converge-multigrid-vs-krylov.lua: |psi|_inf per multigrid iteration next to CG's (both on the GPU)."""
     from .solver import MultigridHIP
 
     os.makedirs(outdir, exist_ok=True)
@@ -109,8 +88,9 @@ def converge(sizes=(4, 8, 16, 32, 64, 128), epsilon=1e-20, outdir="converge", ma
 
         mg = MultigridHIP(size=size, epsilon=epsilon, errorCallback=cb, maxiter=maxiter)
         mg.solve()
-        f = np.asarray(mg.f, dtype=np.float64)
-        cg = _cg_linf_history(f, 1.0 / size, epsilon)
+        # the conjugate-gradient column on the device (mgp_cg_solve: x0 = -f, b = f, converge...lua:38-69)
+        _, _, _, hist = mg.ctx.cg_solve(epsilon=epsilon, maxiter=cg_maxiter, history=True)
+        cg = [float(v) for v in hist]
         n = max(len(data), len(cg))
         cols = [data + [float("nan")] * (n - len(data)), cg + [float("nan")] * (n - len(cg))]
         finite = [v for c in cols for v in c if np.isfinite(v)]

@@ -296,3 +296,35 @@ def test_cpu_lua_knobs_and_matrix_two_grid():
     fl = [list(map(float, f[:, i])) for i in range(8)]
     s.twoGrid(2.0 / 16, ul, fl)
     assert np.array_equal(np.array(ul).T, ua)
+
+
+@pytest.mark.parametrize("dim,n,real", [(2, 64, "double"), (3, 32, "double"), (2, 32, "float")])
+def test_device_cg_second_oracle(dim, n, real):
+    """SURVEY §8(f) row 3 (converge-multigrid-vs-krylov.lua:38-69): conjugate gradients on the device
+    (x0 = -f, b = f, stop at rSq / bSq < eps) and the converged multigrid psi (north-star RB-GS 2+2
+    F-cycles) solve the same discrete system: they agree to 1e-8 relative (fp64; 1e-4 in fp32)."""
+    box = (n, n, n if dim == 3 else 1)
+    ctx = _ctx(dim=dim, n=box, real=real, smoother="rbgs", nu1=2, nu2=2, cycle="F", prolong="linear",
+               coarse_bc="consistent")
+    ctx.init_point_charge()
+    ctx.cycles(40)
+    mg = ctx.get_psi().astype(np.float64)
+    x, iters, err, hist = ctx.cg_solve(epsilon=1e-26 if real == "double" else 1e-12, maxiter=5000, history=True)
+    assert 0 < iters < 5000 and len(hist) == iters
+    assert hist[-1] == np.abs(x).max()
+    rel = np.linalg.norm(x.astype(np.float64) - mg) / np.linalg.norm(mg)
+    assert rel <= (1e-8 if real == "double" else 1e-4), rel
+    # the solver's own state is untouched
+    assert np.array_equal(ctx.get_psi(), mg.astype(ctx.dtype))
+
+
+def test_device_cg_matches_reference_operator_on_cpu_lua_path():
+    """The cpu.lua configuration (2D Jacobi 7+7 V, injection) converges to the same A^-1 f as CG."""
+    ctx = _ctx(dim=2, n=(16, 16, 1), real="double")
+    ctx.init_point_charge()
+    for _ in range(400):
+        if ctx.cycle() < 1e-12:
+            break
+    x, iters, err = ctx.cg_solve(epsilon=1e-28, maxiter=2000)
+    mg = ctx.get_psi()
+    assert np.abs(x - mg).max() <= 1e-8 * np.abs(mg).max()
