@@ -25,7 +25,6 @@
 #include "mgp_internal.h"
 
 #include <cstdlib>
-#include <type_traits>
 
 namespace mgp {
 namespace {
@@ -1352,6 +1351,7 @@ __global__ __launch_bounds__((ZsShape<T, PRE>::NTL)) void k_zs(const T* __restri
     constexpr int N = S::N, H = S::H, HWE = S::HWE, G = S::G, YE = S::YE, SLOT = S::SLOT, TX = S::TX,
                   TY = S::TY, NS3 = S::NS3, NTL = S::NTL;
     using VT = Vec<T, N>;
+    using PF = ZsPrefetch<T, N>;
     extern __shared__ __align__(16) unsigned char zs_smem[];
     T* const lds = reinterpret_cast<T*>(zs_smem);
     const int tid = threadIdx.x;
@@ -1392,10 +1392,16 @@ __global__ __launch_bounds__((ZsShape<T, PRE>::NTL)) void k_zs(const T* __restri
     const int p_end = Z0 + zc + (PRE ? 5 : 3);
     auto inz = [&](int q) { return z0 + q >= 0 && z0 + q < gnz; };  // inside the global box
     auto pcl = [&](int q) { return q < qlo ? qlo : (q > qhi ? qhi : q); };
+    // ring slot of plane q (q may be negative; ns = 3 as q mod 3)
+    auto slot = [&](int off, int ns, int q) {
+        const int r = ns == 3 ? ((q % 3) + 3) % 3 : (q & (ns - 1));
+        return lds + off + r * SLOT;
+    };
     auto nbyz = [&](int q) {
         return CLZ ? 0 : (gy == 0) + (gy == g.ny - 1) + (z0 + q == 0) + (z0 + q == gnz - 1);
     };
     const int rowpar = (gy + z0) & 1;
+    auto par = [&](int q) { return rowpar ^ (q & 1); };
     const T* const src_black = src + Hh;
 
     for (int i = tid; i < (int)(S::lds_bytes / sizeof(T)); i += NTL) lds[i] = (T)0;
@@ -1405,6 +1411,30 @@ __global__ __launch_bounds__((ZsShape<T, PRE>::NTL)) void k_zs(const T* __restri
     const int Ia = X0 / 2 - 8, Ja = Y0 / 2 - 3;
     auto ckl = [&](int K) { return K < 0 ? 0 : (K >= gc.gnz ? gc.gnz - 1 : K); };
     auto cslot = [&](int K) { return lds + S::OFFC + (K & 3) * S::CSLOT; };
+    auto cload = [&](PF& r, int K) {
+        K = ckl(K);
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int t = tid + i * NTL;
+            const int J = Ja + t / (S::CI / 2), I = Ia + 2 * (t % (S::CI / 2));
+            r.cv[i].v[0] = r.cv[i].v[1] = (T)0;
+            if (t < S::CPAIRS && J >= 0 && J < gc.ny && I >= 0 && I < gc.nx) {
+                // I even: cells I and I + 1 sit at m = I / 2 of the two colour halves
+                const T* row = V + (int64_t)(K - cz0) * gc.P + (int64_t)J * gc.hw + (I >> 1);
+                const int ce = (I + J + K) & 1;
+                r.cv[i].v[0] = row[ce * gc.H];
+                r.cv[i].v[1] = row[(ce ^ 1) * gc.H];
+            }
+        }
+    };
+    auto cstore = [&](const PF& r, int K) {
+        T* const sl = cslot(ckl(K));
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int t = tid + i * NTL;
+            if (t < S::CPAIRS) vstore<T, 2>(sl + 2 * t, r.cv[i]);  // pair t: cells 2t, 2t + 1 of the region
+        }
+    };
     auto crow = [&](int K, int J, T (&c)[N + 2]) {  // cells cgm - 1 .. cgm + N of coarse row J, plane K
         const T* const sl = cslot(ckl(K)) + (J - Ja) * S::CI + (cgm - Ia);
         const Vec<T, N> mid = vload<T, N>(sl);
@@ -1414,50 +1444,16 @@ __global__ __launch_bounds__((ZsShape<T, PRE>::NTL)) void k_zs(const T* __restri
         c[N + 1] = vload_lds_whole<T, N>(sl + N).v[0];
     };
 
-    // ---- register rings with static indices: plane x of a ring lives in slot (x - zlo) & 3, and the
-    // step loop is unrolled by 4 with the phase (p - zlo) & 3 a template constant, so no value is
-    // ever moved between registers (zlo = Z0 - H with Z0 a multiple of 4, so plane parities and
-    // the LDS ring slots are compile-time constants of the phase as well) ----
-    const VT vz = vzero<T, N>();
-    VT W0[4], W1[4], W2[4], W3[4], W4[4];  // stage outputs: A0 black, A1 red, A2 black, A3 red, A4 black
-    VT FR[4], FB[4];                        // f of the red / black cells of a plane
-    VT FR5[2], FB5;                         // PRE: f of plane p - 5, saved before the prefetch reuses its slot
-    VT UB[2];                               // prefetched black u (by step parity)
-    Vec<T, 2> CV[2][2];                     // POST: prefetched coarse pairs (by step parity)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) W0[i] = W1[i] = W2[i] = W3[i] = W4[i] = FR[i] = FB[i] = vz;
-    FR5[0] = FR5[1] = FB5 = UB[0] = UB[1] = vz;
-#pragma unroll
-    for (int i = 0; i < 2; ++i) CV[i][0] = CV[i][1] = vzero<T, 2>();
-
-    // POST: the coarse pairs of plane K (clamped to the box) into CV[b] / from CV[b] to its LDS slot
-    auto cload = [&](int bsel, int K) {
-        K = ckl(K);
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            const int t = tid + i * NTL;
-            const int J = Ja + t / (S::CI / 2), I = Ia + 2 * (t % (S::CI / 2));
-            Vec<T, 2> v = vzero<T, 2>();
-            if (t < S::CPAIRS && J >= 0 && J < gc.ny && I >= 0 && I < gc.nx) {
-                // I even: cells I and I + 1 sit at m = I / 2 of the two colour halves
-                const T* row = V + (int64_t)(K - cz0) * gc.P + (int64_t)J * gc.hw + (I >> 1);
-                const int ce = (I + J + K) & 1;
-                v.v[0] = row[ce * gc.H];
-                v.v[1] = row[(ce ^ 1) * gc.H];
-            }
-            CV[bsel][i] = v;
-        }
-    };
-    auto cstore = [&](int bsel, int K) {
-        T* const sl = cslot(ckl(K));
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            const int t = tid + i * NTL;
-            if (t < S::CPAIRS) vstore<T, 2>(sl + 2 * t, CV[bsel][i]);  // pair t: cells 2t, 2t + 1 of the region
-        }
+    auto prefetch = [&](PF& r, int p) {
+        // POST: fine plane 2m + 1 is the first to need coarse plane m + 1; it is loaded with the
+        // prefetch of plane 2m (issued first, so waiting for it leaves the rest in flight)
+        if (!PRE && ((z0 + p) & 1) == 0) cload(r, ((z0 + p) >> 1) + 1);
+        r.u = vload<T, N>(src_black + (int64_t)ZS_PLANE(pcl(p)) * P + goff);
+        r.f1 = vload<T, N>(f + (int64_t)ZS_PLANE(pcl(p - 1)) * P + goff);
+        r.f2 = vload<T, N>(f + (int64_t)ZS_PLANE(pcl(p - 2)) * P + Hh + goff);
     };
     // POST + ERR: psiOld of plane q (red, black), for the tile's own columns only
-    VT old0 = vz, old1 = vz;
+    VT old0, old1;
     auto load_old = [&](int q) {
         if (!PRE && ERR && tile_xy) {
             const T* dp = dst + (int64_t)pcl(q) * P;
@@ -1466,56 +1462,35 @@ __global__ __launch_bounds__((ZsShape<T, PRE>::NTL)) void k_zs(const T* __restri
         }
     };
 
+    const VT vz = vzero<T, N>();
+    VT w0a = vz, w0b = vz, w0c = vz;             // A0 black at p-2, p-1, p
+    VT w1a = vz, w1b = vz, w1c = vz;             // A1 red   at p-3, p-2, p-1
+    VT w2a = vz, w2b = vz, w2c = vz;             // A2 black at p-4, p-3, p-2
+    VT w3a = vz, w3b = vz, w3c = vz, w3d = vz;   // A3 red   at p-6, p-5, p-4, p-3
+    VT w4a = vz, w4b = vz, w4c = vz;             // A4 black at p-6, p-5, p-4
+    VT fr1 = vz, fr2 = vz, fr3 = vz, fr4 = vz;   // f1 of 1..4 steps back (red f at p-2 .. p-5)
+    VT fb1 = vz, fb2 = vz, fb3 = vz;             // f2 of 1..3 steps back (black f at p-3 .. p-5)
     T acc[N];
 #pragma unroll
     for (int e = 0; e < N; ++e) acc[e] = (T)0;
     double err = 0.0, err1 = 0.0;
     const bool even_row = (gy & 1) == 0;
     T* const xbase = lds + S::OFFX + (((ye + (H & 1)) >> 1) * G + gx) * 2 * N;
-    // LDS ring slots of plane x: 2-rings by (x - zlo) & 1, stage 3's by (x - zlo) & (NS3 - 1)
-    auto sl2 = [&](int off, int r) { return lds + off + (r & 1) * SLOT; };
-    auto sl3 = [&](int r) { return lds + S::OFF3 + (r & (NS3 - 1)) * SLOT; };
-    auto xsl = [&](int r) { return xbase + (r & 1) * (S::XPAIRS * G * 2 * N); };
-    static_assert(NS3 == 2 || NS3 == 4, "stage-3 LDS ring must divide the unroll");
-    constexpr int ZLO4 = (4 - (H & 3)) & 3;  // (zlo & 3) as Z0 % 4 == 0: zlo = Z0 - H
+    auto xs = [&](int q) { return xbase + (q & 1) * (S::XPAIRS * G * 2 * N); };
 
-    // prefetch issued at step p for step p + 1: black u of p + 1, red f of p, black f of p - 1; POST: the
-    // coarse plane fine plane 2m + 1 first needs, with the prefetch of plane 2m (issued first, so
-    // waiting for it leaves the rest in flight)
-    auto prefetch = [&](auto PHc, int p, bool clamp) {
-        constexpr int PH = decltype(PHc)::value;
-        const int pn = p + 1;
-        if (!PRE && ((z0 + pn) & 1) == 0) cload((PH + 1) & 1, ((z0 + pn) >> 1) + 1);
-        const int a0 = clamp ? pcl(pn) : pn, a1 = clamp ? pcl(pn - 1) : pn - 1, a2 = clamp ? pcl(pn - 2) : pn - 2;
-        UB[(PH + 1) & 1] = vload<T, N>(src_black + (int64_t)ZS_PLANE(a0) * P + goff);
-        FR[PH & 3] = vload<T, N>(f + (int64_t)ZS_PLANE(a1) * P + goff);
-        FB[(PH + 3) & 3] = vload<T, N>(f + (int64_t)ZS_PLANE(a2) * P + Hh + goff);
-    };
+    constexpr int D = ZS_DEPTH;
+    static_assert(D == 1 || D == 2, "prefetch distance");
+    // cur: plane p (loaded); nxt: plane p + 1 (in flight); nxd: the buffer plane p + D goes to
+    auto step = [&](const PF& cur, PF& nxt, PF& nxd, int p) {
+        if (p + D <= p_end) prefetch(nxd, p + D);
 
-    // One z-step.  PH = (p - zlo) & 3; EDGE: the step touches planes outside the chunk's steady range
-    // (clamped loads, planes outside the box forced to 0, conditional stores / residual).
-    auto step = [&](auto PHc, auto EDc, int p) {
-        constexpr int PH = decltype(PHc)::value;
-        constexpr bool EDGE = decltype(EDc)::value;
-        constexpr int RP = (PH + ZLO4) & 3;  // p & 3
-        // The plane index passes through an empty asm, so no global load of this step (the inputs are
-        // __restrict__, which the memory clobber of the previous step's barrier does not cover) is
-        // hoisted into an earlier step: that would hold four steps of prefetch in registers.
-        asm volatile("" : "+s"(p));
-        auto rs = [&](int k) { return (PH - k + 8) & 3; };  // ring slot of plane p - k
-        // plane parity and LDS slots of plane p - k (compile-time)
-        auto parq = [&](int k) { return rowpar ^ ((RP - k + 8) & 1); };
-        (void)RP;
-        if (PRE) {  // f of plane p - 4 (red) / p - 5 (black) leave their slots to this step's prefetch
-            FR5[PH & 1] = FR[rs(4)];
-            FB5 = FB[rs(5)];
-        }
-        if (!EDGE || p + 1 <= p_end) prefetch(PHc, p, EDGE);
+        // Every LDS read of a step hits a slot filled in the previous step (the writes come after
+        // the stages), so the compiler may schedule them as early as registers allow.
         ZsNb<T, N> n1, n2, n3, n4, nr, nk;
 
         // ---- stage 0: black cells of plane p ----
-        VT a0 = UB[PH & 1];
-        if (!PRE && (!EDGE || inz(p))) {
+        VT a0 = cur.u;
+        if (!PRE && inz(p)) {
             const int J = cgy >> 1, K = (z0 + p) >> 1;
             int Jn = (cgy & 1) ? J + 1 : J - 1;
             int Kn = ((z0 + p) & 1) ? K + 1 : K - 1;
@@ -1531,56 +1506,67 @@ __global__ __launch_bounds__((ZsShape<T, PRE>::NTL)) void k_zs(const T* __restri
             }
             zs_correct<T, N, LINEAR>(a0, cc, 1 ^ ((cgy + z0 + p) & 1), cgm, gc.nx, oy, oz, clc);
         }
-        if (EDGE && !inz(p)) a0 = vz;
-        W0[rs(0)] = a0;
+        if (!inz(p)) a0 = vz;
+        w0a = w0b;
+        w0b = w0c;
+        w0c = a0;
 
         // ---- stages 1..4: half-sweep k on plane p - k (red, black, red, black) ----
-        zs_nb_load<T, N>(n1, sl2(0, PH - 1), col);
-        VT o1 = zs_relax<T, N, CLZ>(W0[rs(2)], W0[rs(1)], W0[rs(0)], n1, FR[rs(1)], col, parq(1), nbyz(p - 1), g.nx, op);
-        if (EDGE && !inz(p - 1)) o1 = vz;
-        W1[rs(1)] = o1;
-        zs_nb_load<T, N>(n2, sl2(S::OFF1, PH - 2), col);
-        VT o2 = zs_relax<T, N, CLZ>(W1[rs(3)], W1[rs(2)], W1[rs(1)], n2, FB[rs(2)], col, 1 ^ parq(2), nbyz(p - 2), g.nx, op);
-        if (EDGE && !inz(p - 2)) o2 = vz;
-        W2[rs(2)] = o2;
-        zs_nb_load<T, N>(n3, sl2(S::OFF2, PH - 3), col);
-        VT o3 = zs_relax<T, N, CLZ>(W2[rs(4)], W2[rs(3)], W2[rs(2)], n3, FR[rs(3)], col, parq(3), nbyz(p - 3), g.nx, op);
-        if (EDGE && !inz(p - 3)) o3 = vz;
-        W3[rs(3)] = o3;
-        zs_nb_load<T, N>(n4, sl3(PH - 4 + 8), col);
-        VT o4 = zs_relax<T, N, CLZ>(W3[rs(5)], W3[rs(4)], W3[rs(3)], n4, FB[rs(4)], col, 1 ^ parq(4), nbyz(p - 4), g.nx, op);
-        if (EDGE && !inz(p - 4)) o4 = vz;
-        W4[rs(4)] = o4;
+        zs_nb_load<T, N>(n1, slot(0, 2, p - 1), col);
+        VT o1 = zs_relax<T, N, CLZ>(w0a, w0b, w0c, n1, cur.f1, col, par(p - 1), nbyz(p - 1), g.nx, op);
+        if (!inz(p - 1)) o1 = vz;
+        w1a = w1b;
+        w1b = w1c;
+        w1c = o1;
+        zs_nb_load<T, N>(n2, slot(S::OFF1, 2, p - 2), col);
+        VT o2 = zs_relax<T, N, CLZ>(w1a, w1b, w1c, n2, cur.f2, col, 1 ^ par(p - 2), nbyz(p - 2), g.nx, op);
+        if (!inz(p - 2)) o2 = vz;
+        w2a = w2b;
+        w2b = w2c;
+        w2c = o2;
+        zs_nb_load<T, N>(n3, slot(S::OFF2, 2, p - 3), col);
+        VT o3 = zs_relax<T, N, CLZ>(w2a, w2b, w2c, n3, fr2, col, par(p - 3), nbyz(p - 3), g.nx, op);
+        if (!inz(p - 3)) o3 = vz;
+        w3a = w3b;
+        w3b = w3c;
+        w3c = w3d;
+        w3d = o3;
+        zs_nb_load<T, N>(n4, slot(S::OFF3, NS3, p - 4), col);
+        VT o4 = zs_relax<T, N, CLZ>(w3b, w3c, w3d, n4, fb2, col, 1 ^ par(p - 4), nbyz(p - 4), g.nx, op);
+        if (!inz(p - 4)) o4 = vz;
+        w4a = w4b;
+        w4b = w4c;
+        w4c = o4;
 
         // ---- LDS writes (slots no stage of this step reads); columns outside the box stay 0 ----
         if (in_xy) {
-            vstore<T, N>(sl2(0, PH) + col.lrow, a0);
-            vstore<T, N>(sl2(S::OFF1, PH - 1) + col.lrow, o1);
-            vstore<T, N>(sl2(S::OFF2, PH - 2) + col.lrow, o2);
-            vstore<T, N>(sl3(PH - 3 + 8) + col.lrow, o3);
-            if (PRE) vstore<T, N>(sl2(S::OFF4, PH - 4) + col.lrow, o4);
+            vstore<T, N>(slot(0, 2, p) + col.lrow, a0);
+            vstore<T, N>(slot(S::OFF1, 2, p - 1) + col.lrow, o1);
+            vstore<T, N>(slot(S::OFF2, 2, p - 2) + col.lrow, o2);
+            vstore<T, N>(slot(S::OFF3, NS3, p - 3) + col.lrow, o3);
+            if (PRE) vstore<T, N>(slot(S::OFF4, 2, p - 4) + col.lrow, o4);
         }
         // POST: the coarse plane this step's prefetch loaded (first read two steps on; the slot it
         // replaces was last read three steps back)
-        if (!PRE && (!EDGE || p < p_end) && ((z0 + p + 1) & 1) == 0) cstore((PH + 1) & 1, ((z0 + p + 1) >> 1) + 1);
+        if (!PRE && p < p_end && ((z0 + p + 1) & 1) == 0) cstore(nxt, ((z0 + p + 1) >> 1) + 1);
 
         // ---- the smoothed plane p - 4: red final after stage 3, black after stage 4 ----
         {
             const int q = p - 4;
-            if ((!EDGE || (q >= Z0 && q < Z0 + zc)) && tile_xy) {
+            if (q >= Z0 && q < Z0 + zc && tile_xy) {
                 if (!PRE && ERR) {
 #pragma unroll
                     for (int e = 0; e < N; ++e) {
                         // (psi - psiOld)^2 in fp64, fused multiply-add into two accumulators (err
                         // matches the oracle's sum to summation order, not bit for bit)
-                        const double d0 = (double)W3[rs(4)].v[e] - (double)old0.v[e];
+                        const double d0 = (double)w3c.v[e] - (double)old0.v[e];
                         const double d1 = (double)o4.v[e] - (double)old1.v[e];
                         err = __builtin_fma(d0, d0, err);
                         err1 = __builtin_fma(d1, d1, err1);
                     }
                 }
                 T* dp = dst + (int64_t)q * P;
-                vstore<T, N>(dp + goff, W3[rs(4)]);
+                vstore<T, N>(dp + goff, w3c);
                 vstore<T, N>(dp + Hh + goff, o4);
             }
         }
@@ -1588,32 +1574,29 @@ __global__ __launch_bounds__((ZsShape<T, PRE>::NTL)) void k_zs(const T* __restri
         // ---- PRE: residual + restriction of plane p - 5 ----
         if (PRE) {
             const int q = p - 5;
-            const int pq = parq(5);
-            zs_nb_load<T, N>(nr, sl3(PH - 5 + 8), col);    // red of A4 at q
-            zs_nb_load<T, N>(nk, sl2(S::OFF4, PH - 5), col);  // black of A4 at q
+            const int pq = par(q);
+            zs_nb_load<T, N>(nr, slot(S::OFF3, NS3, q), col);  // red of A4 at q
+            zs_nb_load<T, N>(nk, slot(S::OFF4, 2, q), col);    // black of A4 at q
             T xr[2 * N];
             {
-                const T* x = xsl(PH - 6 + 8);  // the odd row's residuals of plane q - 1 (even rows read them)
+                const T* x = xs(q - 1);  // the odd row's residuals of plane q - 1 (even rows read them)
 #pragma unroll
                 for (int e = 0; e < 2 * N; ++e) xr[e] = x[e];
             }
             // red cells (x parity pq) see black neighbours, black cells (x parity 1 - pq) red ones
             T rred[N], rblk[N], rr[2][N];  // rr: [x parity][e]
-            zs_residual<T, N, CLZ>(W4[rs(6)], W4[rs(5)], W4[rs(4)], nk, W3[rs(5)], FR5[(PH + 1) & 1], col, pq, nbyz(q),
-                                   g.nx, op, rred);
-            zs_residual<T, N, CLZ>(W3[rs(6)], W3[rs(5)], W3[rs(4)], nr, W4[rs(5)], FB5, col, 1 ^ pq, nbyz(q), g.nx, op,
-                                   rblk);
+            zs_residual<T, N, CLZ>(w4a, w4b, w4c, nk, w3b, fr4, col, pq, nbyz(q), g.nx, op, rred);
+            zs_residual<T, N, CLZ>(w3a, w3b, w3c, nr, w4b, fb3, col, 1 ^ pq, nbyz(q), g.nx, op, rblk);
 #pragma unroll
             for (int e = 0; e < N; ++e) {
                 rr[0][e] = pq == 0 ? rred[e] : rblk[e];
                 rr[1][e] = pq == 0 ? rblk[e] : rred[e];
             }
             const int dq = q - Z0;
-            constexpr int DQ1 = (PH - H - 5 + 16) & 1;  // dq & 1 (dq = p - zlo - H - 5)
-            if ((!EDGE || (dq >= 0 && dq <= zc)) && tile_xy) {
+            if (dq >= 0 && dq <= zc && tile_xy) {
                 if (!even_row) {
-                    if (!EDGE || dq < zc) {
-                        T* x = xsl(PH - 5 + 8);
+                    if (dq < zc) {
+                        T* x = xs(q);
 #pragma unroll
                         for (int e = 0; e < N; ++e) {
                             x[e] = rr[0][e];
@@ -1621,13 +1604,13 @@ __global__ __launch_bounds__((ZsShape<T, PRE>::NTL)) void k_zs(const T* __restri
                         }
                     }
                 } else {
-                    if (!EDGE || dq >= 1) {  // the odd row's children of plane q - 1
+                    if (dq >= 1) {  // the odd row's children of plane q - 1
 #pragma unroll
                         for (int e = 0; e < N; ++e) {
                             acc[e] = acc[e] + xr[e];
                             acc[e] = acc[e] + xr[N + e];
                         }
-                        if (DQ1 == 0) {  // coarse plane (q - 1) / 2 complete
+                        if ((dq & 1) == 0) {  // coarse plane (q - 1) / 2 complete
                             const int K = (z0 + q - 1) >> 1, J = gy >> 1;  // global
                             T* rowc = R + (int64_t)(K - cz0) * gc.P + (int64_t)J * gc.hw;
 #pragma unroll
@@ -1637,10 +1620,10 @@ __global__ __launch_bounds__((ZsShape<T, PRE>::NTL)) void k_zs(const T* __restri
                             }
                         }
                     }
-                    if (!EDGE || dq < zc) {
+                    if (dq < zc) {
 #pragma unroll
                         for (int e = 0; e < N; ++e) {
-                            if (DQ1 == 0) {
+                            if ((dq & 1) == 0) {
                                 acc[e] = rr[0][e] + rr[1][e];
                             } else {
                                 acc[e] = acc[e] + rr[0][e];
@@ -1651,58 +1634,40 @@ __global__ __launch_bounds__((ZsShape<T, PRE>::NTL)) void k_zs(const T* __restri
                 }
             }
         }
-        if (!EDGE || p < p_end) load_old(p - 3);  // used at the end of the next step
+        fr4 = fr3;
+        fr3 = fr2;
+        fr2 = fr1;
+        fr1 = cur.f1;
+        fb3 = fb2;
+        fb2 = fb1;
+        fb1 = cur.f2;
+        if (p < p_end) load_old(p - 3);  // used at the end of the next step
         lds_barrier();
     };
 
-    // a block of 4 steps from p (phase 0 at p = zlo + 4 i); steady when every step of it is
-    // steady steps: stores and residual in range, and a next step exists (prefetch, coarse store, psiOld)
-    const int p_lo_st = Z0 + 6, p_hi_st = (Z0 + zc + 3 < p_end - 1) ? Z0 + zc + 3 : p_end - 1;
-    auto steady_block = [&](int p) {
-        return p >= p_lo_st && p + 3 <= p_hi_st && z0 + p - 6 >= 0 && z0 + p + 4 < gnz && p - 6 >= qlo &&
-               p + 4 <= qhi;
-    };
-    using I0 = std::integral_constant<int, 0>;
-    using I1 = std::integral_constant<int, 1>;
-    using I2 = std::integral_constant<int, 2>;
-    using I3 = std::integral_constant<int, 3>;
-    using ST = std::integral_constant<bool, false>;
-    using ED = std::integral_constant<bool, true>;
-
+    // D + 1 prefetch buffers, rotating (no copy of the in-flight registers)
+    PF pa, pb, pc;
     if (!PRE) {  // the coarse planes the first fine plane needs
         const int K = (z0 + zlo) >> 1;
         for (int k = K - 1; k <= K + 1; ++k) {
-            cload(0, k);
-            cstore(0, k);
+            cload(pa, k);
+            cstore(pa, k);
         }
         __syncthreads();
     }
-    // the prefetch of step zlo (as step zlo - 1, phase 3, would have issued it)
-    {
-        if (!PRE && ((z0 + zlo) & 1) == 0) cload(0, ((z0 + zlo) >> 1) + 1);
-        UB[0] = vload<T, N>(src_black + (int64_t)ZS_PLANE(pcl(zlo)) * P + goff);
-        FR[3] = vload<T, N>(f + (int64_t)ZS_PLANE(pcl(zlo - 1)) * P + goff);
-        FB[2] = vload<T, N>(f + (int64_t)ZS_PLANE(pcl(zlo - 2)) * P + Hh + goff);
-    }
+    prefetch(pa, zlo);
     load_old(zlo - 4);
-    for (int p = zlo; p <= p_end; p += 4) {
-#ifndef ZS_STEADY_POST
-#define ZS_STEADY_POST 0
-#endif
-#ifdef ZS_NO_STEADY
-        if (false) {
-#else
-        if ((PRE || ZS_STEADY_POST) && steady_block(p)) {
-#endif
-            step(I0(), ST(), p);
-            step(I1(), ST(), p + 1);
-            step(I2(), ST(), p + 2);
-            step(I3(), ST(), p + 3);
-        } else {
-            step(I0(), ED(), p);
-            if (p + 1 <= p_end) step(I1(), ED(), p + 1);
-            if (p + 2 <= p_end) step(I2(), ED(), p + 2);
-            if (p + 3 <= p_end) step(I3(), ED(), p + 3);
+    if constexpr (D == 1) {
+        for (int p = zlo; p <= p_end; p += 2) {
+            step(pa, pb, pb, p);
+            if (p + 1 <= p_end) step(pb, pa, pa, p + 1);
+        }
+    } else {
+        prefetch(pb, zlo + 1);  // p_end - zlo >= 7
+        for (int p = zlo; p <= p_end; p += 3) {
+            step(pa, pb, pc, p);
+            if (p + 1 <= p_end) step(pb, pc, pa, p + 1);
+            if (p + 2 <= p_end) step(pc, pa, pb, p + 2);
         }
     }
     if (ERR) block_partial_t<NTL>(err + err1, partials);

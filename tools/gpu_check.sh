@@ -6,7 +6,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 if [ -z "${SKIP_TESTS:-}" ]; then
-  timeout -k 10 ${TEST_LIMIT:-600} python3 -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread ${PYTEST_ARGS:-} > gpurun_out/pytest_gpu.log 2>&1
+  timeout -k 10 ${TEST_LIMIT:-600} python3 -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread ${TESTK:+-k "$TESTK"} > gpurun_out/pytest_gpu.log 2>&1
   rc=$?; tail -n 15 gpurun_out/pytest_gpu.log; [ $rc -eq 0 ] || exit $rc
 fi
 i=0
