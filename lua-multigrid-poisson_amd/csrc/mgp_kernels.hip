@@ -25,6 +25,7 @@
 #include "mgp_internal.h"
 
 #include <cstdlib>
+#include <type_traits>
 
 namespace mgp {
 namespace {
@@ -1098,12 +1099,6 @@ __device__ __forceinline__ void lds_barrier()
 #ifndef ZS_TYPOST_F32
 #define ZS_TYPOST_F32 32
 #endif
-// Prefetch distance in steps: the loads of plane p + D are issued while plane p is computed.
-// D = 2 costs 3 register buffers and measured slower than D = 1 at 512^3 (601 / 878 us against
-// 579 / 787 us for PRE / POST).
-#ifndef ZS_DEPTH
-#define ZS_DEPTH 1
-#endif
 template <typename T>
 struct ZsTile;
 template <>
@@ -1153,7 +1148,19 @@ struct ZsPrefetch {
     Vec<T, 2> cv[2];                                   // POST: this thread's coarse pairs for the ring
     Vec<T, N> f1, f2;  // f of half-sweeps 1 (red, plane p - 1) and 2 (black, plane p - 2); sweeps 3
                        // and 4 reuse them two steps later
+    Vec<T, N> o0, o1;  // POST + ERR: psiOld (red, black) of plane p - 4, the plane step p finalizes
 };
+
+// Pin a prefetched vector: the compiler must have waited for its load before this point, and no
+// memory access is moved across it.  Used at the top of a step so that the wait for plane p's loads
+// (a vmcnt(0) once stores are pending: gfx9 counts loads and stores together) comes before plane
+// p + 1's prefetch is issued, not after it.
+template <typename T, int N>
+__device__ __forceinline__ void zs_hold(const Vec<T, N>& a)
+{
+#pragma unroll
+    for (int e = 0; e < N; ++e) asm volatile("" ::"v"(a.v[e]));
+}
 
 struct ZsCol {
     int lrow, lym, lyp, lxm, lxp, gm;
@@ -1341,8 +1348,15 @@ __device__ __forceinline__ void block_partial_t(double acc, double* partials)
 // coarse plane of local fine plane 0 (gc.z0 = g.z0 / 2).  zc: planes per z-chunk.  gz: readable
 // ghost planes per side of src / f / dst (on a distributed level they must hold the neighbours'
 // current H planes).  CLZ: the level operator has no boundary modification (cl == 0, level 0).
+#ifndef ZS_WPE_PRE
+#define ZS_WPE_PRE 2
+#endif
+#ifndef ZS_WPE_POST
+#define ZS_WPE_POST 4
+#endif
 template <typename T, bool PRE, int LINEAR, bool ERR, bool CLZ>
-__global__ __launch_bounds__((ZsShape<T, PRE>::NTL)) void k_zs(const T* __restrict__ src, const T* __restrict__ f,
+__global__ __launch_bounds__((ZsShape<T, PRE>::NTL))
+__attribute__((amdgpu_waves_per_eu(1, PRE ? ZS_WPE_PRE : ZS_WPE_POST))) void k_zs(const T* __restrict__ src, const T* __restrict__ f,
                                                                 T* __restrict__ dst, T* __restrict__ R,
                                                                 const T* __restrict__ V, double* __restrict__ partials,
                                                                 Geo g, Geo gc, Op<T, 3> op, T clc, int zc, int gz)
@@ -1444,21 +1458,22 @@ __global__ __launch_bounds__((ZsShape<T, PRE>::NTL)) void k_zs(const T* __restri
         c[N + 1] = vload_lds_whole<T, N>(sl + N).v[0];
     };
 
-    auto prefetch = [&](PF& r, int p) {
+    // ST (steady): every plane the step touches lies inside the box, the readable planes and the
+    // chunk, so the plane clamps and the box / chunk tests drop out and a step is one basic block
+    // the scheduler can interleave (LDS reads of all stages up front).
+    auto prefetch = [&](auto st, PF& r, int p) {
+        constexpr bool ST = decltype(st)::value;
+        auto pc = [&](int q) { return ST ? q : pcl(q); };
         // POST: fine plane 2m + 1 is the first to need coarse plane m + 1; it is loaded with the
-        // prefetch of plane 2m (issued first, so waiting for it leaves the rest in flight)
+        // prefetch of plane 2m and put in the ring at the top of step 2m
         if (!PRE && ((z0 + p) & 1) == 0) cload(r, ((z0 + p) >> 1) + 1);
-        r.u = vload<T, N>(src_black + (int64_t)ZS_PLANE(pcl(p)) * P + goff);
-        r.f1 = vload<T, N>(f + (int64_t)ZS_PLANE(pcl(p - 1)) * P + goff);
-        r.f2 = vload<T, N>(f + (int64_t)ZS_PLANE(pcl(p - 2)) * P + Hh + goff);
-    };
-    // POST + ERR: psiOld of plane q (red, black), for the tile's own columns only
-    VT old0, old1;
-    auto load_old = [&](int q) {
-        if (!PRE && ERR && tile_xy) {
-            const T* dp = dst + (int64_t)pcl(q) * P;
-            old0 = vload<T, N>(dp + goff);
-            old1 = vload<T, N>(dp + Hh + goff);
+        r.u = vload<T, N>(src_black + (int64_t)ZS_PLANE(pc(p)) * P + goff);
+        r.f1 = vload<T, N>(f + (int64_t)ZS_PLANE(pc(p - 1)) * P + goff);
+        r.f2 = vload<T, N>(f + (int64_t)ZS_PLANE(pc(p - 2)) * P + Hh + goff);
+        if (!PRE && ERR && tile_xy) {  // psiOld of plane p - 4, for the tile's own columns only
+            const T* dp = dst + (int64_t)pc(p - 4) * P;
+            r.o0 = vload<T, N>(dp + goff);
+            r.o1 = vload<T, N>(dp + Hh + goff);
         }
     };
 
@@ -1478,11 +1493,25 @@ __global__ __launch_bounds__((ZsShape<T, PRE>::NTL)) void k_zs(const T* __restri
     T* const xbase = lds + S::OFFX + (((ye + (H & 1)) >> 1) * G + gx) * 2 * N;
     auto xs = [&](int q) { return xbase + (q & 1) * (S::XPAIRS * G * 2 * N); };
 
-    constexpr int D = ZS_DEPTH;
-    static_assert(D == 1 || D == 2, "prefetch distance");
-    // cur: plane p (loaded); nxt: plane p + 1 (in flight); nxd: the buffer plane p + D goes to
-    auto step = [&](const PF& cur, PF& nxt, PF& nxd, int p) {
-        if (p + D <= p_end) prefetch(nxd, p + D);
+    // cur: plane p (loaded one step earlier); nxt: the buffer plane p + 1 is loaded into
+    auto step = [&](auto st, const PF& cur, PF& nxt, int p) {
+        constexpr bool ST = decltype(st)::value;
+        zs_hold<T, N>(cur.u);
+        zs_hold<T, N>(cur.f1);
+        zs_hold<T, N>(cur.f2);
+        if (!PRE && ERR) {
+            zs_hold<T, N>(cur.o0);
+            zs_hold<T, N>(cur.o1);
+        }
+        if (!PRE) {
+            zs_hold<T, 2>(cur.cv[0]);
+            zs_hold<T, 2>(cur.cv[1]);
+        }
+        asm volatile("" ::: "memory");
+        // POST: the coarse plane cur's prefetch loaded (first read one step on; the slot it replaces
+        // was last read three steps back)
+        if (!PRE && ((z0 + p) & 1) == 0) cstore(cur, ((z0 + p) >> 1) + 1);
+        if (ST || p + 1 <= p_end) prefetch(st, nxt, p + 1);
 
         // Every LDS read of a step hits a slot filled in the previous step (the writes come after
         // the stages), so the compiler may schedule them as early as registers allow.
@@ -1490,7 +1519,7 @@ __global__ __launch_bounds__((ZsShape<T, PRE>::NTL)) void k_zs(const T* __restri
 
         // ---- stage 0: black cells of plane p ----
         VT a0 = cur.u;
-        if (!PRE && inz(p)) {
+        if (!PRE && (ST || inz(p))) {
             const int J = cgy >> 1, K = (z0 + p) >> 1;
             int Jn = (cgy & 1) ? J + 1 : J - 1;
             int Kn = ((z0 + p) & 1) ? K + 1 : K - 1;
@@ -1506,7 +1535,7 @@ __global__ __launch_bounds__((ZsShape<T, PRE>::NTL)) void k_zs(const T* __restri
             }
             zs_correct<T, N, LINEAR>(a0, cc, 1 ^ ((cgy + z0 + p) & 1), cgm, gc.nx, oy, oz, clc);
         }
-        if (!inz(p)) a0 = vz;
+        if (!ST && !inz(p)) a0 = vz;
         w0a = w0b;
         w0b = w0c;
         w0c = a0;
@@ -1514,26 +1543,26 @@ __global__ __launch_bounds__((ZsShape<T, PRE>::NTL)) void k_zs(const T* __restri
         // ---- stages 1..4: half-sweep k on plane p - k (red, black, red, black) ----
         zs_nb_load<T, N>(n1, slot(0, 2, p - 1), col);
         VT o1 = zs_relax<T, N, CLZ>(w0a, w0b, w0c, n1, cur.f1, col, par(p - 1), nbyz(p - 1), g.nx, op);
-        if (!inz(p - 1)) o1 = vz;
+        if (!ST && !inz(p - 1)) o1 = vz;
         w1a = w1b;
         w1b = w1c;
         w1c = o1;
         zs_nb_load<T, N>(n2, slot(S::OFF1, 2, p - 2), col);
         VT o2 = zs_relax<T, N, CLZ>(w1a, w1b, w1c, n2, cur.f2, col, 1 ^ par(p - 2), nbyz(p - 2), g.nx, op);
-        if (!inz(p - 2)) o2 = vz;
+        if (!ST && !inz(p - 2)) o2 = vz;
         w2a = w2b;
         w2b = w2c;
         w2c = o2;
         zs_nb_load<T, N>(n3, slot(S::OFF2, 2, p - 3), col);
         VT o3 = zs_relax<T, N, CLZ>(w2a, w2b, w2c, n3, fr2, col, par(p - 3), nbyz(p - 3), g.nx, op);
-        if (!inz(p - 3)) o3 = vz;
+        if (!ST && !inz(p - 3)) o3 = vz;
         w3a = w3b;
         w3b = w3c;
         w3c = w3d;
         w3d = o3;
         zs_nb_load<T, N>(n4, slot(S::OFF3, NS3, p - 4), col);
         VT o4 = zs_relax<T, N, CLZ>(w3b, w3c, w3d, n4, fb2, col, 1 ^ par(p - 4), nbyz(p - 4), g.nx, op);
-        if (!inz(p - 4)) o4 = vz;
+        if (!ST && !inz(p - 4)) o4 = vz;
         w4a = w4b;
         w4b = w4c;
         w4c = o4;
@@ -1546,21 +1575,18 @@ __global__ __launch_bounds__((ZsShape<T, PRE>::NTL)) void k_zs(const T* __restri
             vstore<T, N>(slot(S::OFF3, NS3, p - 3) + col.lrow, o3);
             if (PRE) vstore<T, N>(slot(S::OFF4, 2, p - 4) + col.lrow, o4);
         }
-        // POST: the coarse plane this step's prefetch loaded (first read two steps on; the slot it
-        // replaces was last read three steps back)
-        if (!PRE && p < p_end && ((z0 + p + 1) & 1) == 0) cstore(nxt, ((z0 + p + 1) >> 1) + 1);
 
         // ---- the smoothed plane p - 4: red final after stage 3, black after stage 4 ----
         {
             const int q = p - 4;
-            if (q >= Z0 && q < Z0 + zc && tile_xy) {
+            if ((ST || (q >= Z0 && q < Z0 + zc)) && tile_xy) {
                 if (!PRE && ERR) {
 #pragma unroll
                     for (int e = 0; e < N; ++e) {
                         // (psi - psiOld)^2 in fp64, fused multiply-add into two accumulators (err
                         // matches the oracle's sum to summation order, not bit for bit)
-                        const double d0 = (double)w3c.v[e] - (double)old0.v[e];
-                        const double d1 = (double)o4.v[e] - (double)old1.v[e];
+                        const double d0 = (double)w3c.v[e] - (double)cur.o0.v[e];
+                        const double d1 = (double)o4.v[e] - (double)cur.o1.v[e];
                         err = __builtin_fma(d0, d0, err);
                         err1 = __builtin_fma(d1, d1, err1);
                     }
@@ -1593,9 +1619,9 @@ __global__ __launch_bounds__((ZsShape<T, PRE>::NTL)) void k_zs(const T* __restri
                 rr[1][e] = pq == 0 ? rblk[e] : rred[e];
             }
             const int dq = q - Z0;
-            if (dq >= 0 && dq <= zc && tile_xy) {
+            if ((ST || (dq >= 0 && dq <= zc)) && tile_xy) {
                 if (!even_row) {
-                    if (dq < zc) {
+                    if (ST || dq < zc) {
                         T* x = xs(q);
 #pragma unroll
                         for (int e = 0; e < N; ++e) {
@@ -1604,7 +1630,7 @@ __global__ __launch_bounds__((ZsShape<T, PRE>::NTL)) void k_zs(const T* __restri
                         }
                     }
                 } else {
-                    if (dq >= 1) {  // the odd row's children of plane q - 1
+                    if (ST || dq >= 1) {  // the odd row's children of plane q - 1
 #pragma unroll
                         for (int e = 0; e < N; ++e) {
                             acc[e] = acc[e] + xr[e];
@@ -1620,7 +1646,7 @@ __global__ __launch_bounds__((ZsShape<T, PRE>::NTL)) void k_zs(const T* __restri
                             }
                         }
                     }
-                    if (dq < zc) {
+                    if (ST || dq < zc) {
 #pragma unroll
                         for (int e = 0; e < N; ++e) {
                             if ((dq & 1) == 0) {
@@ -1641,12 +1667,12 @@ __global__ __launch_bounds__((ZsShape<T, PRE>::NTL)) void k_zs(const T* __restri
         fb3 = fb2;
         fb2 = fb1;
         fb1 = cur.f2;
-        if (p < p_end) load_old(p - 3);  // used at the end of the next step
         lds_barrier();
     };
 
-    // D + 1 prefetch buffers, rotating (no copy of the in-flight registers)
-    PF pa, pb, pc;
+    const std::false_type GEN;
+    const std::true_type STY;
+    PF pa, pb;
     if (!PRE) {  // the coarse planes the first fine plane needs
         const int K = (z0 + zlo) >> 1;
         for (int k = K - 1; k <= K + 1; ++k) {
@@ -1655,20 +1681,30 @@ __global__ __launch_bounds__((ZsShape<T, PRE>::NTL)) void k_zs(const T* __restri
         }
         __syncthreads();
     }
-    prefetch(pa, zlo);
-    load_old(zlo - 4);
-    if constexpr (D == 1) {
-        for (int p = zlo; p <= p_end; p += 2) {
-            step(pa, pb, pb, p);
-            if (p + 1 <= p_end) step(pb, pa, pa, p + 1);
-        }
-    } else {
-        prefetch(pb, zlo + 1);  // p_end - zlo >= 7
-        for (int p = zlo; p <= p_end; p += 3) {
-            step(pa, pb, pc, p);
-            if (p + 1 <= p_end) step(pb, pc, pa, p + 1);
-            if (p + 2 <= p_end) step(pc, pa, pb, p + 2);
-        }
+    prefetch(GEN, pa, zlo);
+    // steady steps [ps, pe]: stages inside the box (z0 + p - 5 >= 0, z0 + p < gnz), the stored plane
+    // and PRE's residual plane inside the chunk, the prefetched planes (p + 1 .. p - 3) readable
+    int ps = Z0 + 6, pe = Z0 + zc + 3;
+    ps = ps > 5 - z0 ? ps : 5 - z0;
+    ps = ps > qlo + 3 ? ps : qlo + 3;
+    pe = pe < gnz - 1 - z0 ? pe : gnz - 1 - z0;
+    pe = pe < qhi - 1 ? pe : qhi - 1;
+    pe = pe < p_end - 1 ? pe : p_end - 1;
+    if ((ps - zlo) & 1) ++ps;          // even prologue: the steady loop starts with pa
+    if ((pe - ps + 1) & 1) --pe;       // whole pairs
+    if (pe < ps) ps = pe = zlo - 1;    // no steady part (pe < ps: the epilogue takes all)
+    int p = zlo;
+    for (; p < ps; p += 2) {
+        step(GEN, pa, pb, p);
+        step(GEN, pb, pa, p + 1);
+    }
+    for (; p <= pe; p += 2) {
+        step(STY, pa, pb, p);
+        step(STY, pb, pa, p + 1);
+    }
+    for (; p <= p_end; p += 2) {
+        step(GEN, pa, pb, p);
+        if (p + 1 <= p_end) step(GEN, pb, pa, p + 1);
     }
     if (ERR) block_partial_t<NTL>(err + err1, partials);
 }

@@ -4,7 +4,7 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out/var
-for lib in lua-multigrid-poisson_amd/mgpoisson/libmgpoisson.so var/*/libmgpoisson.so; do
+for lib in lua-multigrid-poisson_amd/mgpoisson/libmgpoisson.so $(ls var/*/libmgpoisson.so 2>/dev/null); do
   name=$(basename $(dirname $lib)); [ "$name" = mgpoisson ] && name=base
   MGP_LIBRARY=$PWD/$lib timeout -k 10 120 python3 bench.py --steps ${STEPS:-30} --warmup 3 --cpu-cycles 0 ${BENCH_ARGS:-} > gpurun_out/var/$name.log 2>&1
   rc=$?
