@@ -1281,7 +1281,7 @@ struct ZsCoarse {
 
 template <typename T, int N, int LINEAR>
 __device__ __forceinline__ void zs_correct(Vec<T, N>& uv, const ZsCoarse<T, N>& cur, int o, int I0, int cx, bool oy,
-                                           bool oz, T cl)
+                                           bool oz, T cl, bool fast)
 {
     const T w0 = (T)0.75, w1 = (T)0.25;
     if (!LINEAR) {
@@ -1289,7 +1289,7 @@ __device__ __forceinline__ void zs_correct(Vec<T, N>& uv, const ZsCoarse<T, N>& 
         for (int e = 0; e < N; ++e) uv.v[e] = uv.v[e] + cur.c00[e + 1];
         return;
     }
-    if (__all(!oy && !oz && I0 > 0 && I0 + N < cx)) {
+    if (fast) {  // __all(!oy && !oz && I0 > 0 && I0 + N < cx), from the caller
 #pragma unroll
         for (int e = 0; e < N; ++e) {
             const int pe = e + 1;
@@ -1461,19 +1461,34 @@ __attribute__((amdgpu_waves_per_eu(1, PRE ? ZS_WPE_PRE : ZS_WPE_POST))) void k_z
     // ST (steady): every plane the step touches lies inside the box, the readable planes and the
     // chunk, so the plane clamps and the box / chunk tests drop out and a step is one basic block
     // the scheduler can interleave (LDS reads of all stages up front).
+    // In steady steps z0, Z0 and zc are even (checked before the steady loop), so the parity of p
+    // is static within a step pair: zz0 / the caller's p carry it as known low bits and the parity
+    // tests below fold away.
     auto prefetch = [&](auto st, PF& r, int p) {
         constexpr bool ST = decltype(st)::value;
-        auto pc = [&](int q) { return ST ? q : pcl(q); };
+        const int zz0 = ST ? (z0 & ~1) : z0;
         // POST: fine plane 2m + 1 is the first to need coarse plane m + 1; it is loaded with the
         // prefetch of plane 2m and put in the ring at the top of step 2m
-        if (!PRE && ((z0 + p) & 1) == 0) cload(r, ((z0 + p) >> 1) + 1);
-        r.u = vload<T, N>(src_black + (int64_t)ZS_PLANE(pc(p)) * P + goff);
-        r.f1 = vload<T, N>(f + (int64_t)ZS_PLANE(pc(p - 1)) * P + goff);
-        r.f2 = vload<T, N>(f + (int64_t)ZS_PLANE(pc(p - 2)) * P + Hh + goff);
-        if (!PRE && ERR && tile_xy) {  // psiOld of plane p - 4, for the tile's own columns only
-            const T* dp = dst + (int64_t)pc(p - 4) * P;
-            r.o0 = vload<T, N>(dp + goff);
-            r.o1 = vload<T, N>(dp + Hh + goff);
+        if (!PRE && ((zz0 + p) & 1) == 0) cload(r, ((zz0 + p) >> 1) + 1);
+        if (ST) {  // one 64-bit plane offset, the others by subtraction
+            const int64_t pP = (int64_t)ZS_PLANE(p) * P;
+            r.u = vload<T, N>(src_black + pP + goff);
+            r.f1 = vload<T, N>(f + (pP - P) + goff);
+            r.f2 = vload<T, N>(f + (pP - 2 * P) + Hh + goff);
+            if (!PRE && ERR && tile_xy) {  // psiOld of plane p - 4, for the tile's own columns only
+                const T* dp = dst + (pP - 4 * P);
+                r.o0 = vload<T, N>(dp + goff);
+                r.o1 = vload<T, N>(dp + Hh + goff);
+            }
+        } else {
+            r.u = vload<T, N>(src_black + (int64_t)ZS_PLANE(pcl(p)) * P + goff);
+            r.f1 = vload<T, N>(f + (int64_t)ZS_PLANE(pcl(p - 1)) * P + goff);
+            r.f2 = vload<T, N>(f + (int64_t)ZS_PLANE(pcl(p - 2)) * P + Hh + goff);
+            if (!PRE && ERR && tile_xy) {
+                const T* dp = dst + (int64_t)pcl(p - 4) * P;
+                r.o0 = vload<T, N>(dp + goff);
+                r.o1 = vload<T, N>(dp + Hh + goff);
+            }
         }
     };
 
@@ -1494,8 +1509,14 @@ __attribute__((amdgpu_waves_per_eu(1, PRE ? ZS_WPE_PRE : ZS_WPE_POST))) void k_z
     auto xs = [&](int q) { return xbase + (q & 1) * (S::XPAIRS * G * 2 * N); };
 
     // cur: plane p (loaded one step earlier); nxt: the buffer plane p + 1 is loaded into
-    auto step = [&](auto st, const PF& cur, PF& nxt, int p) {
+    // POST: the per-lane half of the interior test of the coarse correction (loop invariant)
+    const bool corr_lane = !PRE && (cgy >> 1) + ((cgy & 1) ? 1 : -1) >= 0 && (cgy >> 1) + ((cgy & 1) ? 1 : -1) < gc.ny &&
+                           cgm > 0 && cgm + N < gc.nx;
+    const bool corr_fast = __all(corr_lane);
+    auto step = [&](auto st, auto pp, const PF& cur, PF& nxt, int p) {
         constexpr bool ST = decltype(st)::value;
+        if (ST) p = (p & ~1) | decltype(pp)::value;  // p's parity, known to the compiler
+        const int zz0 = ST ? (z0 & ~1) : z0;
         zs_hold<T, N>(cur.u);
         zs_hold<T, N>(cur.f1);
         zs_hold<T, N>(cur.f2);
@@ -1510,7 +1531,7 @@ __attribute__((amdgpu_waves_per_eu(1, PRE ? ZS_WPE_PRE : ZS_WPE_POST))) void k_z
         asm volatile("" ::: "memory");
         // POST: the coarse plane cur's prefetch loaded (first read one step on; the slot it replaces
         // was last read three steps back)
-        if (!PRE && ((z0 + p) & 1) == 0) cstore(cur, ((z0 + p) >> 1) + 1);
+        if (!PRE && ((zz0 + p) & 1) == 0) cstore(cur, ((zz0 + p) >> 1) + 1);
         if (ST || p + 1 <= p_end) prefetch(st, nxt, p + 1);
 
         // Every LDS read of a step hits a slot filled in the previous step (the writes come after
@@ -1520,10 +1541,10 @@ __attribute__((amdgpu_waves_per_eu(1, PRE ? ZS_WPE_PRE : ZS_WPE_POST))) void k_z
         // ---- stage 0: black cells of plane p ----
         VT a0 = cur.u;
         if (!PRE && (ST || inz(p))) {
-            const int J = cgy >> 1, K = (z0 + p) >> 1;
+            const int J = cgy >> 1, K = (zz0 + p) >> 1;
             int Jn = (cgy & 1) ? J + 1 : J - 1;
-            int Kn = ((z0 + p) & 1) ? K + 1 : K - 1;
-            const bool oy = Jn < 0 || Jn >= gc.ny, oz = Kn < 0 || Kn >= gc.gnz;
+            int Kn = ((zz0 + p) & 1) ? K + 1 : K - 1;
+            const bool oy = Jn < 0 || Jn >= gc.ny, oz = !ST && (Kn < 0 || Kn >= gc.gnz);
             if (oy) Jn = J;
             if (oz) Kn = K;
             ZsCoarse<T, N> cc;
@@ -1533,7 +1554,8 @@ __attribute__((amdgpu_waves_per_eu(1, PRE ? ZS_WPE_PRE : ZS_WPE_POST))) void k_z
                 crow(Kn, J, cc.c01);
                 crow(Kn, Jn, cc.c11);
             }
-            zs_correct<T, N, LINEAR>(a0, cc, 1 ^ ((cgy + z0 + p) & 1), cgm, gc.nx, oy, oz, clc);
+            zs_correct<T, N, LINEAR>(a0, cc, 1 ^ ((cgy + zz0 + p) & 1), cgm, gc.nx, oy, oz, clc,
+                                     ST ? corr_fast : __all(!oy && !oz && cgm > 0 && cgm + N < gc.nx));
         }
         if (!ST && !inz(p)) a0 = vz;
         w0a = w0b;
@@ -1618,7 +1640,7 @@ __attribute__((amdgpu_waves_per_eu(1, PRE ? ZS_WPE_PRE : ZS_WPE_POST))) void k_z
                 rr[0][e] = pq == 0 ? rred[e] : rblk[e];
                 rr[1][e] = pq == 0 ? rblk[e] : rred[e];
             }
-            const int dq = q - Z0;
+            const int dq = q - (ST ? (Z0 & ~1) : Z0);
             if ((ST || (dq >= 0 && dq <= zc)) && tile_xy) {
                 if (!even_row) {
                     if (ST || dq < zc) {
@@ -1637,7 +1659,7 @@ __attribute__((amdgpu_waves_per_eu(1, PRE ? ZS_WPE_PRE : ZS_WPE_POST))) void k_z
                             acc[e] = acc[e] + xr[N + e];
                         }
                         if ((dq & 1) == 0) {  // coarse plane (q - 1) / 2 complete
-                            const int K = (z0 + q - 1) >> 1, J = gy >> 1;  // global
+                            const int K = (zz0 + q - 1) >> 1, J = gy >> 1;  // global
                             T* rowc = R + (int64_t)(K - cz0) * gc.P + (int64_t)J * gc.hw;
 #pragma unroll
                             for (int e = 0; e < N; ++e) {
@@ -1687,24 +1709,35 @@ __attribute__((amdgpu_waves_per_eu(1, PRE ? ZS_WPE_PRE : ZS_WPE_POST))) void k_z
     int ps = Z0 + 6, pe = Z0 + zc + 3;
     ps = ps > 5 - z0 ? ps : 5 - z0;
     ps = ps > qlo + 3 ? ps : qlo + 3;
-    pe = pe < gnz - 1 - z0 ? pe : gnz - 1 - z0;
+    pe = pe < gnz - (PRE ? 1 : 2) - z0 ? pe : gnz - (PRE ? 1 : 2) - z0;  // POST: Kn inside the coarse box
     pe = pe < qhi - 1 ? pe : qhi - 1;
     pe = pe < p_end - 1 ? pe : p_end - 1;
     if ((ps - zlo) & 1) ++ps;          // even prologue: the steady loop starts with pa
     if ((pe - ps + 1) & 1) --pe;       // whole pairs
-    if (pe < ps) ps = pe = zlo - 1;    // no steady part (pe < ps: the epilogue takes all)
+    // no steady part (the epilogue takes all) without whole pairs or with odd z0 / Z0 (static parity)
+    if (pe < ps || ((z0 | Z0) & 1)) ps = pe = zlo - 1;
     int p = zlo;
+    const std::integral_constant<int, 0> P0;
+    const std::integral_constant<int, 1> P1;
     for (; p < ps; p += 2) {
-        step(GEN, pa, pb, p);
-        step(GEN, pb, pa, p + 1);
+        step(GEN, P0, pa, pb, p);
+        step(GEN, P0, pb, pa, p + 1);
     }
-    for (; p <= pe; p += 2) {
-        step(STY, pa, pb, p);
-        step(STY, pb, pa, p + 1);
+    // steady pairs start at p = ps, whose parity is zlo's (even prologue): H & 1 when Z0 is even
+    if (H & 1) {
+        for (; p <= pe; p += 2) {
+            step(STY, P1, pa, pb, p);
+            step(STY, P0, pb, pa, p + 1);
+        }
+    } else {
+        for (; p <= pe; p += 2) {
+            step(STY, P0, pa, pb, p);
+            step(STY, P1, pb, pa, p + 1);
+        }
     }
     for (; p <= p_end; p += 2) {
-        step(GEN, pa, pb, p);
-        if (p + 1 <= p_end) step(GEN, pb, pa, p + 1);
+        step(GEN, P0, pa, pb, p);
+        if (p + 1 <= p_end) step(GEN, P0, pb, pa, p + 1);
     }
     if (ERR) block_partial_t<NTL>(err + err1, partials);
 }
