@@ -1776,6 +1776,7 @@ __global__ __launch_bounds__(tail_threads<T>()) void k_tail(const TailArgs<T, DI
     constexpr int G = DIM == 3 ? kGhost3D : 0;
     const int tid = threadIdx.x;
     // level l: u at off, f at off + region, Jacobi target at off + 2 region
+#ifndef TAIL_NOCOPYIN  // timing experiment only: results are wrong
     for (int l = 0; l < a.nlev; ++l) {
         const Geo& g = a.g[l];
         T* U = lds + a.off[l];
@@ -1789,11 +1790,27 @@ __global__ __launch_bounds__(tail_threads<T>()) void k_tail(const TailArgs<T, DI
             if (a.jacobi) U[e + 2 * a.region[l]] = (T)0;
         }
     }
+#endif
     __syncthreads();
+#ifdef TAIL_PROF  // timing experiment: shader cycles per op into f of the first level (tools/tail_prof.py)
+    __shared__ float tprof[128];
+    __shared__ long long tlast;
+#endif
     unsigned alt = 0;  // Jacobi: bit l = level l's iterate currently lives in its second array
     auto cur = [&](int l) { return lds + a.off[l] + G * a.g[l].P + (((alt >> l) & 1) ? 2 * a.region[l] : 0); };
     auto rhs = [&](int l) { return lds + a.off[l] + a.region[l] + G * a.g[l].P; };
+#ifdef TAIL_NOOPS  // timing experiment only: results are wrong
+    for (int pc = 0; pc < 0; ++pc) {
+#else
     for (int pc = 0; pc < a.nops; ++pc) {
+#endif
+#ifdef TAIL_PROF
+        if (tid == 0) {
+            const long long now = (long long)__builtin_amdgcn_s_memtime();
+            if (pc > 0 && pc <= 128) tprof[pc - 1] = (float)(now - tlast);
+            tlast = now;
+        }
+#endif
         const uint32_t w = a.ops[pc];
         const int op = (int)(w & 15), l = (int)((w >> 4) & 15), arg = (int)(w >> 8);
         const Geo g = a.g[l];
@@ -1835,6 +1852,14 @@ __global__ __launch_bounds__(tail_threads<T>()) void k_tail(const TailArgs<T, DI
             __syncthreads();
         }
     }
+#ifdef TAIL_PROF
+    if (tid == 0) {
+        const long long now = (long long)__builtin_amdgcn_s_memtime();
+        if (a.nops <= 128) tprof[a.nops - 1] = (float)(now - tlast);
+        for (int i = 0; i < 128 && i < a.nops; ++i) rhs(0)[i] = (T)tprof[i];
+    }
+    __syncthreads();
+#endif
     for (int l = 0; l < a.nlev; ++l) {
         const T* U = cur(l);
         const T* F = rhs(l);
@@ -2244,14 +2269,19 @@ static hipError_t fused_attr()
     return e;
 }
 
+#ifdef TAIL_PROF
+constexpr int kTailStaticLds = 1024;
+#else
+constexpr int kTailStaticLds = 0;
+#endif
 template <typename T, int D>
 static hipError_t tail_attr()
 {
     hipError_t e = hipFuncSetAttribute((const void*)k_tail<T, D, 0>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       (int)kTailMaxLds);
+                                       (int)kTailMaxLds - kTailStaticLds);
     if (e == hipSuccess)
         e = hipFuncSetAttribute((const void*)k_tail<T, D, 1>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)kTailMaxLds);
+                                (int)kTailMaxLds - kTailStaticLds);
     return e;
 }
 
