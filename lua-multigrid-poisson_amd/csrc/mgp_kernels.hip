@@ -1493,13 +1493,15 @@ __attribute__((amdgpu_waves_per_eu(1, PRE ? ZS_WPE_PRE : ZS_WPE_POST))) void k_z
     };
 
     const VT vz = vzero<T, N>();
-    VT w0a = vz, w0b = vz, w0c = vz;             // A0 black at p-2, p-1, p
-    VT w1a = vz, w1b = vz, w1c = vz;             // A1 red   at p-3, p-2, p-1
-    VT w2a = vz, w2b = vz, w2c = vz;             // A2 black at p-4, p-3, p-2
-    VT w3a = vz, w3b = vz, w3c = vz, w3d = vz;   // A3 red   at p-6, p-5, p-4, p-3
-    VT w4a = vz, w4b = vz, w4c = vz;             // A4 black at p-6, p-5, p-4
-    VT fr1 = vz, fr2 = vz, fr3 = vz, fr4 = vz;   // f1 of 1..4 steps back (red f at p-2 .. p-5)
-    VT fb1 = vz, fb2 = vz, fb3 = vz;             // f2 of 1..3 steps back (black f at p-3 .. p-5)
+    // Register rings of four planes: plane q lives in slot (q - zlo) & 3.  Every loop runs whole
+    // groups of four steps, so each step knows its slot offset R = (p - zlo) & 3 at compile time and
+    // the rings never move (no register rotation).
+    VT W0[4], W1[4], W2[4], W3[4], W4[4], FR[4], FB[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) W0[i] = W1[i] = W2[i] = W3[i] = W4[i] = FR[i] = FB[i] = vz;
+    // W0: A0 black at p-2 .. p; W1: A1 red at p-3 .. p-1; W2: A2 black at p-4 .. p-2;
+    // W3: A3 red at p-6 .. p-3; W4: A4 black at p-6 .. p-4; FR: red f (cur.f1) of planes p-5 .. p-2;
+    // FB: black f (cur.f2) of planes p-5 .. p-3
     T acc[N];
 #pragma unroll
     for (int e = 0; e < N; ++e) acc[e] = (T)0;
@@ -1513,9 +1515,13 @@ __attribute__((amdgpu_waves_per_eu(1, PRE ? ZS_WPE_PRE : ZS_WPE_POST))) void k_z
     const bool corr_lane = !PRE && (cgy >> 1) + ((cgy & 1) ? 1 : -1) >= 0 && (cgy >> 1) + ((cgy & 1) ? 1 : -1) < gc.ny &&
                            cgm > 0 && cgm + N < gc.nx;
     const bool corr_fast = __all(corr_lane);
-    auto step = [&](auto st, auto pp, const PF& cur, PF& nxt, int p) {
+    auto step = [&](auto st, auto rt, const PF& cur, PF& nxt, int p) {
         constexpr bool ST = decltype(st)::value;
-        if (ST) p = (p & ~1) | decltype(pp)::value;  // p's parity, known to the compiler
+        constexpr int RS = decltype(rt)::value;  // (p - zlo) & 3
+        // ring slot of plane p - k
+        auto sl = [](int k) constexpr { return (RS - k) & 3; };
+        // steady: Z0 even, so p's parity is zlo's plus RS
+        if (ST) p = (p & ~1) | ((H + RS) & 1);
         const int zz0 = ST ? (z0 & ~1) : z0;
         zs_hold<T, N>(cur.u);
         zs_hold<T, N>(cur.f1);
@@ -1558,36 +1564,28 @@ __attribute__((amdgpu_waves_per_eu(1, PRE ? ZS_WPE_PRE : ZS_WPE_POST))) void k_z
                                      ST ? corr_fast : __all(!oy && !oz && cgm > 0 && cgm + N < gc.nx));
         }
         if (!ST && !inz(p)) a0 = vz;
-        w0a = w0b;
-        w0b = w0c;
-        w0c = a0;
+        W0[sl(0)] = a0;
 
         // ---- stages 1..4: half-sweep k on plane p - k (red, black, red, black) ----
         zs_nb_load<T, N>(n1, slot(0, 2, p - 1), col);
-        VT o1 = zs_relax<T, N, CLZ>(w0a, w0b, w0c, n1, cur.f1, col, par(p - 1), nbyz(p - 1), g.nx, op);
+        VT o1 = zs_relax<T, N, CLZ>(W0[sl(2)], W0[sl(1)], W0[sl(0)], n1, cur.f1, col, par(p - 1), nbyz(p - 1), g.nx, op);
         if (!ST && !inz(p - 1)) o1 = vz;
-        w1a = w1b;
-        w1b = w1c;
-        w1c = o1;
+        W1[sl(1)] = o1;
         zs_nb_load<T, N>(n2, slot(S::OFF1, 2, p - 2), col);
-        VT o2 = zs_relax<T, N, CLZ>(w1a, w1b, w1c, n2, cur.f2, col, 1 ^ par(p - 2), nbyz(p - 2), g.nx, op);
+        VT o2 = zs_relax<T, N, CLZ>(W1[sl(3)], W1[sl(2)], W1[sl(1)], n2, cur.f2, col, 1 ^ par(p - 2), nbyz(p - 2), g.nx,
+                                    op);
         if (!ST && !inz(p - 2)) o2 = vz;
-        w2a = w2b;
-        w2b = w2c;
-        w2c = o2;
+        W2[sl(2)] = o2;
         zs_nb_load<T, N>(n3, slot(S::OFF2, 2, p - 3), col);
-        VT o3 = zs_relax<T, N, CLZ>(w2a, w2b, w2c, n3, fr2, col, par(p - 3), nbyz(p - 3), g.nx, op);
+        VT o3 = zs_relax<T, N, CLZ>(W2[sl(4)], W2[sl(3)], W2[sl(2)], n3, FR[sl(3)], col, par(p - 3), nbyz(p - 3), g.nx,
+                                    op);
         if (!ST && !inz(p - 3)) o3 = vz;
-        w3a = w3b;
-        w3b = w3c;
-        w3c = w3d;
-        w3d = o3;
+        W3[sl(3)] = o3;
         zs_nb_load<T, N>(n4, slot(S::OFF3, NS3, p - 4), col);
-        VT o4 = zs_relax<T, N, CLZ>(w3b, w3c, w3d, n4, fb2, col, 1 ^ par(p - 4), nbyz(p - 4), g.nx, op);
+        VT o4 = zs_relax<T, N, CLZ>(W3[sl(5)], W3[sl(4)], W3[sl(3)], n4, FB[sl(4)], col, 1 ^ par(p - 4), nbyz(p - 4),
+                                    g.nx, op);
         if (!ST && !inz(p - 4)) o4 = vz;
-        w4a = w4b;
-        w4b = w4c;
-        w4c = o4;
+        W4[sl(4)] = o4;
 
         // ---- LDS writes (slots no stage of this step reads); columns outside the box stay 0 ----
         if (in_xy) {
@@ -1607,14 +1605,14 @@ __attribute__((amdgpu_waves_per_eu(1, PRE ? ZS_WPE_PRE : ZS_WPE_POST))) void k_z
                     for (int e = 0; e < N; ++e) {
                         // (psi - psiOld)^2 in fp64, fused multiply-add into two accumulators (err
                         // matches the oracle's sum to summation order, not bit for bit)
-                        const double d0 = (double)w3c.v[e] - (double)cur.o0.v[e];
+                        const double d0 = (double)W3[sl(4)].v[e] - (double)cur.o0.v[e];
                         const double d1 = (double)o4.v[e] - (double)cur.o1.v[e];
                         err = __builtin_fma(d0, d0, err);
                         err1 = __builtin_fma(d1, d1, err1);
                     }
                 }
                 T* dp = dst + (int64_t)q * P;
-                vstore<T, N>(dp + goff, w3c);
+                vstore<T, N>(dp + goff, W3[sl(4)]);
                 vstore<T, N>(dp + Hh + goff, o4);
             }
         }
@@ -1633,8 +1631,10 @@ __attribute__((amdgpu_waves_per_eu(1, PRE ? ZS_WPE_PRE : ZS_WPE_POST))) void k_z
             }
             // red cells (x parity pq) see black neighbours, black cells (x parity 1 - pq) red ones
             T rred[N], rblk[N], rr[2][N];  // rr: [x parity][e]
-            zs_residual<T, N, CLZ>(w4a, w4b, w4c, nk, w3b, fr4, col, pq, nbyz(q), g.nx, op, rred);
-            zs_residual<T, N, CLZ>(w3a, w3b, w3c, nr, w4b, fb3, col, 1 ^ pq, nbyz(q), g.nx, op, rblk);
+            zs_residual<T, N, CLZ>(W4[sl(6)], W4[sl(5)], W4[sl(4)], nk, W3[sl(5)], FR[sl(5)], col, pq, nbyz(q), g.nx, op,
+                                   rred);
+            zs_residual<T, N, CLZ>(W3[sl(6)], W3[sl(5)], W3[sl(4)], nr, W4[sl(5)], FB[sl(5)], col, 1 ^ pq, nbyz(q), g.nx,
+                                   op, rblk);
 #pragma unroll
             for (int e = 0; e < N; ++e) {
                 rr[0][e] = pq == 0 ? rred[e] : rblk[e];
@@ -1682,13 +1682,8 @@ __attribute__((amdgpu_waves_per_eu(1, PRE ? ZS_WPE_PRE : ZS_WPE_POST))) void k_z
                 }
             }
         }
-        fr4 = fr3;
-        fr3 = fr2;
-        fr2 = fr1;
-        fr1 = cur.f1;
-        fb3 = fb2;
-        fb2 = fb1;
-        fb1 = cur.f2;
+        FR[sl(1)] = cur.f1;  // red f of plane p - 1 (replaces p - 5, read above)
+        FB[sl(2)] = cur.f2;  // black f of plane p - 2
         lds_barrier();
     };
 
@@ -1712,32 +1707,32 @@ __attribute__((amdgpu_waves_per_eu(1, PRE ? ZS_WPE_PRE : ZS_WPE_POST))) void k_z
     pe = pe < gnz - (PRE ? 1 : 2) - z0 ? pe : gnz - (PRE ? 1 : 2) - z0;  // POST: Kn inside the coarse box
     pe = pe < qhi - 1 ? pe : qhi - 1;
     pe = pe < p_end - 1 ? pe : p_end - 1;
-    if ((ps - zlo) & 1) ++ps;          // even prologue: the steady loop starts with pa
-    if ((pe - ps + 1) & 1) --pe;       // whole pairs
-    // no steady part (the epilogue takes all) without whole pairs or with odd z0 / Z0 (static parity)
+    ps += (zlo - ps) & 3;              // whole groups of four steps in the prologue
+    pe -= (pe - ps + 1) & 3;           // and in the steady part
+    // no steady part (the epilogue takes all) without a whole group or with odd z0 / Z0 (static parity)
     if (pe < ps || ((z0 | Z0) & 1)) ps = pe = zlo - 1;
     int p = zlo;
-    const std::integral_constant<int, 0> P0;
-    const std::integral_constant<int, 1> P1;
-    for (; p < ps; p += 2) {
-        step(GEN, P0, pa, pb, p);
-        step(GEN, P0, pb, pa, p + 1);
+    const std::integral_constant<int, 0> R0;
+    const std::integral_constant<int, 1> R1;
+    const std::integral_constant<int, 2> R2;
+    const std::integral_constant<int, 3> R3;
+    for (; p < ps; p += 4) {
+        step(GEN, R0, pa, pb, p);
+        step(GEN, R1, pb, pa, p + 1);
+        step(GEN, R2, pa, pb, p + 2);
+        step(GEN, R3, pb, pa, p + 3);
     }
-    // steady pairs start at p = ps, whose parity is zlo's (even prologue): H & 1 when Z0 is even
-    if (H & 1) {
-        for (; p <= pe; p += 2) {
-            step(STY, P1, pa, pb, p);
-            step(STY, P0, pb, pa, p + 1);
-        }
-    } else {
-        for (; p <= pe; p += 2) {
-            step(STY, P0, pa, pb, p);
-            step(STY, P1, pb, pa, p + 1);
-        }
+    for (; p <= pe; p += 4) {
+        step(STY, R0, pa, pb, p);
+        step(STY, R1, pb, pa, p + 1);
+        step(STY, R2, pa, pb, p + 2);
+        step(STY, R3, pb, pa, p + 3);
     }
-    for (; p <= p_end; p += 2) {
-        step(GEN, P0, pa, pb, p);
-        if (p + 1 <= p_end) step(GEN, P0, pb, pa, p + 1);
+    for (; p <= p_end; p += 4) {
+        step(GEN, R0, pa, pb, p);
+        if (p + 1 <= p_end) step(GEN, R1, pb, pa, p + 1);
+        if (p + 2 <= p_end) step(GEN, R2, pa, pb, p + 2);
+        if (p + 3 <= p_end) step(GEN, R3, pb, pa, p + 3);
     }
     if (ERR) block_partial_t<NTL>(err + err1, partials);
 }
