@@ -46,7 +46,7 @@ def parse():
     p.add_argument("--cycle", default="V", choices=["V", "F"])
     p.add_argument("--nu", type=int, default=2)
     p.add_argument("--no-timing", action="store_true", help="skip the per-launch smoother events")
-    p.add_argument("--cpu-cycles", type=int, default=2, help="oracle cycles timed for cpu_baseline (0 = skip)")
+    p.add_argument("--cpu-cycles", type=int, default=4, help="oracle cycles timed for cpu_baseline (0 = skip)")
     p.add_argument("--cpu-threads", type=int, default=0,
                    help="threads of the OpenMP cpu_baseline (0 = OMP_NUM_THREADS or all host cores)")
     p.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "pmc_traffic_current.json"),
