@@ -115,6 +115,8 @@ struct Level {
     bool fghost_ok = true;  // f's ghost planes likewise
     bool fused = false;     // smoothing phases run temporally blocked (k_zs); needs t
     bool zero_pending = false;  // u is logically 0: the next red half-sweep reads c->zbuf instead
+    bool ghost_zero = false;    // u is 0 everywhere, so ghost planes of any depth are current
+    int64_t exchanges = 0;      // halo exchanges of this level so far (mgp_level_info info[7])
     int zc = 0, zc_pre = 0;  // k_zs z-chunks (planes per workgroup) of POST and PRE
 };
 
@@ -149,7 +151,8 @@ struct mgp_loopback {
 struct mgp_ctx {
     mgp_opts o{};
     int rb = 8;
-    int G = 0;  // ghost planes per side (kGhost3D in 3D, 0 in 2D)
+    int G = 0;  // ghost planes per side (kGhost3D in 3D, 0 in 2D; kGhostZs for distributed 3D)
+    bool deep_halo = true;  // smooth_deep on distributed levels below the finest
     std::vector<Level> lev;
     hipStream_t s = nullptr;
     int device = 0;
@@ -349,6 +352,7 @@ int exchange_buf(mgp_ctx* c, Level& L, char* buf, int depth = 1)
 {
     if (depth > c->G || depth > L.g.nz)
         return c->fail(MGP_ERR_STATE, "internal: exchange depth %d (ghost %d, slab %d)", depth, c->G, (int)L.g.nz);
+    ++L.exchanges;
     if (c->lb) return lb_exchange(c, (int)(&L - c->lev.data()), buf, depth);
     const size_t rb = (size_t)c->rb;
     const size_t cnt = (size_t)(depth * L.g.P);
@@ -419,17 +423,61 @@ int64_t level_count(const Level& L) { return L.p.nx * L.p.ny * (L.g.nz); }
 int materialize_zero(mgp_ctx* c, Level& L);
 
 // One half-sweep (colour `color`) reading `other`, writing `dst`; level-0 launches are timed.
-int half(mgp_ctx* c, int l, int color, char* other, char* dst, const char* old, double h, double cl, int part_off)
+// lo / hi > 0: the slab extended by that many ghost planes below / above (deep-halo smoothing).
+int half(mgp_ctx* c, int l, int color, char* other, char* dst, const char* old, double h, double cl, int part_off,
+         int lo = 0, int hi = 0)
 {
     Level& L = c->lev[l];
+    Geo g = L.g;
+    size_t back = 0;
+    if (lo || hi) {
+        g.nz += lo + hi;
+        g.z0 -= lo;
+        back = (size_t)(lo * L.g.P) * c->rb;
+    }
     // only the plain finest half-sweep (k_half<T, dim, 1, false>) is timed, so the event total
     // matches that kernel's rocprofv3 row; the err-fused variant reads psiOld as well
     hipEvent_t e;
     TRY(timed_begin(c, old ? -1 : l, &e));
-    HIP_TRY(c, mgp::launch_half_sweep(c->rb, c->o.dim, l == 0, color, c->ui(L, other), c->ui(L, L.f), c->ui(L, dst),
-                                      old ? c->ui(L, (char*)old) : nullptr, c->d_part + part_off, L.g, h, cl,
-                                      c->use_gs, c->s));
+    HIP_TRY(c, mgp::launch_half_sweep(c->rb, c->o.dim, l == 0, color, c->ui(L, other) - back, c->ui(L, L.f) - back,
+                                      c->ui(L, dst) - back, old ? c->ui(L, (char*)old) : nullptr, c->d_part + part_off,
+                                      g, h, cl, c->use_gs, c->s));
     TRY(timed_end(c, e, MGP_TIMING_HALF_SWEEP, 1.5 * c->rb * (double)level_cells(L)));
+    return MGP_OK;
+}
+
+// Deep-halo RB-GS on a distributed level below the finest: ONE exchange of D = 2 sweeps + 1 planes
+// of u (none when u is a fresh zero) and, once per change of f, of f replaces the exchange before
+// every half-sweep.  Half-sweep s computes the slab extended by D - 1 - s ghost planes on every side
+// that has a neighbour, redundantly with that neighbour and with the same arithmetic, so the slab's
+// own planes are bit-identical to the exchanging schedule and the first ghost plane is current at the
+// end (restriction and the level above's prolongation need it).
+bool deep_halo_ok(const mgp_ctx* c, const Level& L, int sweeps, bool want_err)
+{
+    const int l = (int)(&L - c->lev.data());
+    const int D = 2 * sweeps + 1;
+    return c->deep_halo && l > 0 && L.p.dist && c->o.smoother == MGP_RBGS && !want_err && sweeps >= 1 && D <= c->G &&
+           D <= L.g.nz;
+}
+
+int smooth_deep(mgp_ctx* c, int l, int sweeps, double h)
+{
+    Level& L = c->lev[l];
+    const double cl = coarse_coef(c->o.coarse_bc, l);
+    const int D = 2 * sweeps + 1;
+    if (!L.fghost_ok) {
+        TRY(exchange_buf(c, L, L.f, c->G));
+        L.fghost_ok = true;
+    }
+    if (!L.zero_pending && !L.ghost_zero) TRY(exchange_buf(c, L, L.u, D));
+    for (int s = 0; s < 2 * sweeps; ++s) {
+        const int ext = D - 1 - s;
+        const int lo = c->o.rank > 0 ? ext : 0, hi = c->o.rank < c->o.world - 1 ? ext : 0;
+        TRY(half(c, l, s & 1, s == 0 && L.zero_pending ? c->zbuf : L.u, L.u, nullptr, h, cl, 0, lo, hi));
+        if (s == 0) L.zero_pending = false;
+    }
+    L.ghost_ok = true;  // the first ghost plane was swept last at extension 1 (black) / 2 (red)
+    L.ghost_zero = false;
     return MGP_OK;
 }
 
@@ -437,6 +485,7 @@ int smooth(mgp_ctx* c, int l, int sweeps, double h, bool want_err = false)
 {
     Level& L = c->lev[l];
     const double cl = coarse_coef(c->o.coarse_bc, l);
+    if (deep_halo_ok(c, L, sweeps, want_err)) return smooth_deep(c, l, sweeps, h);
     for (int sw = 0; sw < sweeps; ++sw) {
         if (c->o.smoother == MGP_JACOBI) {
             // both colours from the old iterate into t, then swap (no copy back, cf. gpu.lua:292)
@@ -445,6 +494,7 @@ int smooth(mgp_ctx* c, int l, int sweeps, double h, bool want_err = false)
             TRY(half(c, l, 1, L.u, L.t, nullptr, h, cl, 0));
             std::swap(L.u, L.t);
             L.ghost_ok = !L.p.dist;
+            L.ghost_zero = false;
             continue;
         }
         const bool oop = l == 0 && c->in_cycle && c->err_fuse && !c->first_done;  // keep psiOld in t
@@ -464,6 +514,7 @@ int smooth(mgp_ctx* c, int l, int sweeps, double h, bool want_err = false)
             c->first_done = true;
         }
         L.ghost_ok = !L.p.dist;
+        L.ghost_zero = false;
         if (last_err) {
             HIP_TRY(c, mgp::launch_sum_partials(c->d_part, 2 * nb, c->err_dst, c->s));
             c->err_done = true;
@@ -518,6 +569,7 @@ int prolong_correct(mgp_ctx* c, int l)
     HIP_TRY(c, mgp::launch_prolong_correct(c->rb, c->o.dim, linear, c->ui(L, L.u), V, L.g, gc,
                                            coarse_coef(c->o.coarse_bc, l + 1), c->s));
     L.ghost_ok = !L.p.dist;
+    L.ghost_zero = false;
     return MGP_OK;
 }
 
@@ -546,11 +598,13 @@ int zero_level(mgp_ctx* c, Level& L)
     if (lazy_zero_ok(c, L)) {
         L.zero_pending = true;
         L.ghost_ok = true;
+        L.ghost_zero = true;
         return MGP_OK;
     }
     HIP_TRY(c, hipMemsetAsync(L.u, 0, (size_t)L.alloc * c->rb, c->s));
     L.zero_pending = false;
     L.ghost_ok = true;  // every rank's V is zero, so the ghost planes are current
+    L.ghost_zero = true;
     return MGP_OK;
 }
 
@@ -562,6 +616,7 @@ int materialize_zero(mgp_ctx* c, Level& L)
     HIP_TRY(c, hipMemsetAsync(L.u, 0, (size_t)L.alloc * c->rb, c->s));
     L.zero_pending = false;
     L.ghost_ok = true;
+    L.ghost_zero = true;
     return MGP_OK;
 }
 
@@ -598,6 +653,7 @@ int fused_pre(mgp_ctx* c, int l, double h)
     TRY(timed_end(c, e, MGP_TIMING_FUSED_PRE, (3.0 * c->o.nu1 + 2.125) * c->rb * (double)level_cells(L)));
     std::swap(L.u, L.t);  // u = smoothed; t = the previous iterate (psiOld on level 0)
     L.ghost_ok = !L.p.dist;
+    L.ghost_zero = false;
     C.fghost_ok = !C.p.dist;
     if (L.p.dist && !C.p.dist) {  // agglomerate the coarse right-hand side, as residual_restrict
         const size_t count = (size_t)((L.g.nz / 2) * C.g.P);
@@ -645,6 +701,7 @@ int fused_post(mgp_ctx* c, int l, double h, bool want_err)
                   (3.0 * c->o.nu2 + 2.125 + (want_err ? 2.0 : 0.0)) * c->rb * (double)level_cells(L)));
     std::swap(L.u, L.t);
     L.ghost_ok = !L.p.dist;
+    L.ghost_zero = false;
     if (want_err) {
         HIP_TRY(c, mgp::launch_sum_partials(c->d_part, mgp::fused_blocks(c->rb, L.g, L.zc), c->err_dst, c->s));
         c->err_done = true;
@@ -732,6 +789,7 @@ int run_handoff(mgp_ctx* c, int l, double h)
     TRY(mgp_set_field(c, l, MGP_FIELD_U, c->hbuf_u.data(), n, MGP_MEM_HOST));
     TRY(mgp_set_field(c, l, MGP_FIELD_F, c->hbuf_f.data(), n, MGP_MEM_HOST));
     L.ghost_ok = !L.p.dist;
+    L.ghost_zero = false;
     return MGP_OK;
 }
 
@@ -750,6 +808,7 @@ int run_tail(mgp_ctx* c, bool fcycle)
         t.h[i] = level_h(c, T + i);
         t.cl[i] = coarse_coef(c->o.coarse_bc, T + i);
         L.ghost_ok = true;
+        L.ghost_zero = false;
     }
     const std::vector<uint32_t>& p = fcycle ? c->tail_f : c->tail_v;
     t.nops = (int)p.size();
@@ -1054,6 +1113,12 @@ static int create_impl(mgp_ctx** out, const mgp_opts* o, mgp_loopback* lb, ncclC
     if (c->o.dim == 2) c->o.n[2] = 1;
     c->rb = o->real_bytes;
     c->G = o->dim == 3 ? mgp::kGhost3D : 0;  // widened below when a distributed level is fused
+    {
+        const char* v = std::getenv("MGP_DEEP_HALO");  // 0: exchange before every half-sweep instead
+        c->deep_halo = !(v && std::atoi(v) == 0);
+    }
+    // distributed 3D levels sweep with deep halos (smooth_deep): kGhostZs ghost planes per side
+    if (c->deep_halo && o->dim == 3 && o->world > 1) c->G = mgp::kGhostZs;
     auto bail = [&](int code) {
         g_create_error = c->err;
         destroy_impl(c);
@@ -1232,7 +1297,7 @@ int mgp_level_info(const mgp_ctx* c, int level, int64_t info[8])
     info[4] = p.z0;
     info[5] = p.dist;
     info[6] = c->tail_level >= 0 && level >= c->tail_level;  // run inside the one-launch coarse tail
-    info[7] = 0;
+    info[7] = c->lev[level].exchanges;
     return MGP_OK;
 }
 
@@ -1244,6 +1309,7 @@ int mgp_init_point_charge(mgp_ctx* c)
     HIP_TRY(c, mgp::launch_init_point_charge(c->rb, c->o.dim, c->ui(L, L.u), c->ui(L, L.f), L.g, L.p.nx / 2,
                                              L.p.ny / 2, cz, c->s));
     L.ghost_ok = !L.p.dist;
+    L.ghost_zero = false;
     L.fghost_ok = !L.p.dist;
     return sync_and_check(c);
 }
@@ -1362,8 +1428,12 @@ static int planes_io(mgp_ctx* c, int level, int which, int64_t z_begin, int64_t 
         }
     }
     if (to_device) {
-        if (which == MGP_FIELD_U) L.ghost_ok = !L.p.dist;
-        else L.fghost_ok = !L.p.dist;
+        if (which == MGP_FIELD_U) {
+            L.ghost_ok = !L.p.dist;
+            L.ghost_zero = false;
+        } else {
+            L.fghost_ok = !L.p.dist;
+        }
     }
     return sync_and_check(c);
 }
@@ -1485,6 +1555,7 @@ int mgp_two_grid(mgp_ctx* c, double h, void* u, const void* f, int64_t L, int me
         (void)hipFree(su);
         (void)hipFree(sf);
         Lv.ghost_ok = Lv.fghost_ok = true;
+        Lv.ghost_zero = false;
         if (rc != MGP_OK) return rc;
         if (!(r1 && r2 && r3)) return c->fail(MGP_ERR_HIP, "mgp_two_grid: restoring level %d failed", l);
         return MGP_OK;

@@ -394,6 +394,59 @@ def test_fused_slab_decomposition_loopback(box, world, gather, cfg, monkeypatch)
                         min_dist=1 if gather >= 65536 else 2)
 
 
+def _loopback_run(box, world, gather, cfg, cycles=2):
+    """Run `world` loopback ranks; returns (gathered psi, per-rank list of per-level exchange counts)."""
+    import threading
+
+    mg = _mg()
+    lb = mg.Loopback(world)
+    out, errors = [None] * world, []
+
+    def rank_main(r):
+        try:
+            ctx = mg.Context(mg.make_opts(dim=3, n=box, rank=r, world=world, gather_cells=gather, device=0,
+                                          comm_id=b"\0" * 128, **cfg), loopback=lb)
+            ctx.init_point_charge()
+            ctx.cycles(cycles)
+            ctx._read_levels()
+            out[r] = (ctx.get_psi(), [lv["exchanges"] for lv in ctx.levels], [lv["distributed"] for lv in ctx.levels])
+            ctx.close()
+        except Exception as e:  # noqa: BLE001 - surfaced below
+            errors.append((r, repr(e)))
+
+    threads = [threading.Thread(target=rank_main, args=(r,)) for r in range(world)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join(timeout=600)
+    lb.close()
+    assert not errors, errors
+    return np.concatenate([out[r][0] for r in range(world)], axis=0), [out[r][1] for r in range(world)], out[0][2]
+
+
+@pytest.mark.parametrize("world,real", [(2, "float"), (4, "double")])
+def test_deep_halo_smoothing_loopback(world, real, monkeypatch):
+    """Deep-halo RB-GS on distributed levels below the finest (smooth_deep): one exchange of 2 nu + 1
+    planes per smoothing phase instead of one per half-sweep.  psi is bit-identical to the exchanging
+    schedule (MGP_DEEP_HALO=0) and to the single domain, with fewer exchanges on every such level."""
+    box, gather = (64, 64, 128), 4096
+    cfg = dict(real=real, smoother="rbgs", nu1=2, nu2=2, prolong="linear", coarse_bc="consistent")
+    monkeypatch.setenv("MGP_DEEP_HALO", "1")
+    psi_d, ex_d, dist = _loopback_run(box, world, gather, cfg)
+    monkeypatch.setenv("MGP_DEEP_HALO", "0")
+    psi_s, ex_s, _ = _loopback_run(box, world, gather, cfg)
+    assert np.array_equal(psi_d, psi_s)
+    ref = _ctx(dim=3, n=box, gather_cells=gather, **cfg)
+    ref.init_point_charge()
+    ref.cycles(2)
+    assert np.array_equal(psi_d, ref.get_psi())
+    deep_levels = [l for l in range(1, len(dist)) if dist[l] and box[2] // world >> l >= 5]
+    assert deep_levels, dist
+    for l in deep_levels:
+        assert ex_d[0][l] < ex_s[0][l], (l, ex_d[0], ex_s[0])
+    assert sum(ex_d[0]) < sum(ex_s[0])
+
+
 def _loopback_vs_single(box, world, gather, cfg, expect_fused=False, min_dist=2):
     import threading
 
