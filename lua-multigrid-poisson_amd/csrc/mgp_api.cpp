@@ -276,13 +276,14 @@ Geo make_geo(const LevelPlan& p, int dim)
 
 int lb_fail(mgp_ctx* c) { return c->fail(MGP_ERR_STATE, "loopback group barrier timed out or broken"); }
 
-int lb_exchange(mgp_ctx* c, int l, char* buf, int depth)
+int lb_exchange(mgp_ctx* c, int l, char* buf, int depth, int colour)
 {
     mgp_loopback* g = c->lb;
     const size_t rb = (size_t)c->rb;
     const Level& L = c->lev[l];
     const size_t bytes = (size_t)(depth * L.g.P) * rb;
-    auto at = [&](char* b, int64_t k) { return b + (size_t)((k + c->G) * L.g.P) * rb; };
+    const size_t coff = colour < 0 ? 0 : (size_t)(colour * L.g.H) * rb;  // one colour half per plane
+    auto at = [&](char* b, int64_t k) { return b + (size_t)((k + c->G) * L.g.P) * rb + coff; };
     c->lb_buf = buf;
     HIP_TRY(c, hipEventRecord(c->lb_ev, c->s));  // my boundary planes are final here
     if (!g->barrier()) return lb_fail(c);
@@ -292,8 +293,12 @@ int lb_exchange(mgp_ctx* c, int l, char* buf, int depth)
         mgp_ctx* o = g->ranks[nb];
         HIP_TRY(c, hipStreamWaitEvent(c->s, o->lb_ev, 0));
         const char* src = nb < r ? at(o->lb_buf, L.g.nz - depth) : at(o->lb_buf, 0);
-        HIP_TRY(c, hipMemcpyAsync(nb < r ? at(buf, -depth) : at(buf, L.g.nz), src, bytes, hipMemcpyDeviceToDevice,
-                                  c->s));
+        char* dst = nb < r ? at(buf, -depth) : at(buf, L.g.nz);
+        if (colour < 0)
+            HIP_TRY(c, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, c->s));
+        else
+            HIP_TRY(c, hipMemcpy2DAsync(dst, (size_t)L.g.P * rb, src, (size_t)L.g.P * rb, (size_t)L.g.H * rb,
+                                        (size_t)depth, hipMemcpyDeviceToDevice, c->s));
     }
     HIP_TRY(c, hipEventRecord(c->lb_ev2, c->s));  // my pulls are done here
     if (!g->barrier()) return lb_fail(c);
@@ -348,25 +353,36 @@ int lb_allreduce(mgp_ctx* c, double* v, int n = 1)
 // Exchange `depth` boundary planes of `buf` with each z-neighbour: my first interior planes go to
 // rank-1's upper ghosts, my last to rank+1's lower ghosts.  Planes are contiguous in the packed
 // layout, so each direction is one ncclSend/ncclRecv pair on that neighbour's xGMI link.
-int exchange_buf(mgp_ctx* c, Level& L, char* buf, int depth = 1)
+// colour 0 / 1: only that colour's half of each plane (depth pairs of H reals), for readers that never
+// look at the other colour (a red/black sweep reads only black cells of its input: the red ones are
+// overwritten before they are read), halving the bytes.
+int exchange_buf(mgp_ctx* c, Level& L, char* buf, int depth = 1, int colour = -1)
 {
     if (depth > c->G || depth > L.g.nz)
         return c->fail(MGP_ERR_STATE, "internal: exchange depth %d (ghost %d, slab %d)", depth, c->G, (int)L.g.nz);
     ++L.exchanges;
-    if (c->lb) return lb_exchange(c, (int)(&L - c->lev.data()), buf, depth);
+    if (c->lb) return lb_exchange(c, (int)(&L - c->lev.data()), buf, depth, colour);
     const size_t rb = (size_t)c->rb;
-    const size_t cnt = (size_t)(depth * L.g.P);
-    auto at = [&](int64_t k) { return buf + (size_t)((k + c->G) * L.g.P) * rb; };
-    NCCL_TRY(c, ncclGroupStart());
-    if (c->o.rank > 0) {
-        NCCL_TRY(c, ncclSend(at(0), cnt, c->nccl_real(), c->o.rank - 1, c->comm, c->s));
-        NCCL_TRY(c, ncclRecv(at(-depth), cnt, c->nccl_real(), c->o.rank - 1, c->comm, c->s));
+    const size_t coff = colour < 0 ? 0 : (size_t)(colour * L.g.H) * rb;
+    auto at = [&](int64_t k) { return buf + (size_t)((k + c->G) * L.g.P) * rb + coff; };
+    // one message per direction (whole planes) or one per plane (a colour half of each)
+    const int msgs = colour < 0 ? 1 : depth;
+    const size_t cnt = colour < 0 ? (size_t)(depth * L.g.P) : (size_t)L.g.H;
+    ncclResult_t r = ncclGroupStart();
+    for (int i = 0; i < msgs && r == ncclSuccess; ++i) {
+        if (c->o.rank > 0) {
+            r = ncclSend(at(i), cnt, c->nccl_real(), c->o.rank - 1, c->comm, c->s);
+            if (r == ncclSuccess) r = ncclRecv(at(i - depth), cnt, c->nccl_real(), c->o.rank - 1, c->comm, c->s);
+        }
+        if (c->o.rank < c->o.world - 1 && r == ncclSuccess) {
+            r = ncclSend(at(L.g.nz - depth + i), cnt, c->nccl_real(), c->o.rank + 1, c->comm, c->s);
+            if (r == ncclSuccess) r = ncclRecv(at(L.g.nz + i), cnt, c->nccl_real(), c->o.rank + 1, c->comm, c->s);
+        }
     }
-    if (c->o.rank < c->o.world - 1) {
-        NCCL_TRY(c, ncclSend(at(L.g.nz - depth), cnt, c->nccl_real(), c->o.rank + 1, c->comm, c->s));
-        NCCL_TRY(c, ncclRecv(at(L.g.nz), cnt, c->nccl_real(), c->o.rank + 1, c->comm, c->s));
-    }
-    NCCL_TRY(c, ncclGroupEnd());
+    const ncclResult_t e = ncclGroupEnd();  // always closes the group, also after a failed call
+    if (r == ncclSuccess) r = e;
+    if (r != ncclSuccess) return c->fail(MGP_ERR_RCCL, "halo exchange (level %d): %s", (int)(&L - c->lev.data()),
+                                         ncclGetErrorString(r));
     return MGP_OK;
 }
 
@@ -469,7 +485,7 @@ int smooth_deep(mgp_ctx* c, int l, int sweeps, double h)
         TRY(exchange_buf(c, L, L.f, c->G));
         L.fghost_ok = true;
     }
-    if (!L.zero_pending && !L.ghost_zero) TRY(exchange_buf(c, L, L.u, D));
+    if (!L.zero_pending && !L.ghost_zero) TRY(exchange_buf(c, L, L.u, D, 1));  // black cells only
     for (int s = 0; s < 2 * sweeps; ++s) {
         const int ext = D - 1 - s;
         const int lo = c->o.rank > 0 ? ext : 0, hi = c->o.rank < c->o.world - 1 ? ext : 0;
@@ -628,7 +644,7 @@ int fused_pre(mgp_ctx* c, int l, double h)
     Level& L = c->lev[l];
     Level& C = c->lev[l + 1];
     if (L.p.dist) {  // the trapezoid reads kZsHaloPre planes of u and f beyond the slab
-        TRY(exchange_buf(c, L, L.u, mgp::kZsHaloPre));
+        TRY(exchange_buf(c, L, L.u, mgp::kZsHaloPre, 1));  // k_zs reads only black cells of its input
         if (!L.fghost_ok) TRY(exchange_buf(c, L, L.f, mgp::kZsHaloPre));
         L.fghost_ok = true;
     }
@@ -672,7 +688,7 @@ int fused_post(mgp_ctx* c, int l, double h, bool want_err)
     Level& L = c->lev[l];
     Level& C = c->lev[l + 1];
     if (L.p.dist) {  // kZsHaloPost planes of u and f, kZsHaloCoarse coarse planes of V
-        TRY(exchange_buf(c, L, L.u, mgp::kZsHaloPost));
+        TRY(exchange_buf(c, L, L.u, mgp::kZsHaloPost, 1));
         if (!L.fghost_ok) TRY(exchange_buf(c, L, L.f, mgp::kZsHaloPost));
         L.fghost_ok = true;
         if (C.p.dist) TRY(exchange_buf(c, C, C.u, mgp::kZsHaloCoarse));
