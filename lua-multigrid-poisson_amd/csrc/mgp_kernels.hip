@@ -1259,19 +1259,36 @@ __device__ __forceinline__ void zs_nbsum(const Vec<T, N>& zl, const Vec<T, N>& c
     }
 }
 
+// Steady-step diagonals of a level with a boundary-modified operator (cl != 0): inside the z-range
+// of the steady steps a cell's face count is nby (its row on a y face) plus 1 for the x-face cell,
+// which can only be the first cell of a group at the left edge (x parity 0) or the last at the right
+// edge (x parity 1).  db / yb = dg[nby] / RN(1/dg[nby]), de / ye = dg[nby + 1] / RN(1/dg[nby + 1]):
+// the table Markstein division of Op::relax without selects over the whole table.
+template <typename T>
+struct ZsDiag {
+    T db, yb, de, ye;
+    bool left, right;
+};
+
 // One half-sweep of my N cells of one colour (x parity o) from the other colour's window
 // (zl, cen, zr) and its in-plane operands: k_half's expressions.  Waves whose cells all have the
 // interior diagonal (every wave of a level with cl = 0) take the reciprocal form, which is what
 // Op::relax computes there.
-template <typename T, int N, bool CLZ>
+template <typename T, int N, bool CLZ, bool ST = false>
 __device__ __forceinline__ Vec<T, N> zs_relax(const Vec<T, N>& zl, const Vec<T, N>& cen, const Vec<T, N>& zr,
                                               const ZsNb<T, N>& nb, const Vec<T, N>& fv, const ZsCol& c, int o,
-                                              int nbyz, int nx, const Op<T, 3>& op)
+                                              int nbyz, int nx, const Op<T, 3>& op, const ZsDiag<T>& dz)
 {
     T t[N];
     zs_nbsum<T, N>(zl, cen, zr, nb, o, t);
     Vec<T, N> out;
-    if (CLZ || __all(nbyz == 0 && c.xin)) {
+    if (!CLZ && ST) {
+#pragma unroll
+        for (int e = 0; e < N; ++e) {
+            const bool edge = (e == 0 && o == 0 && dz.left) || (e == N - 1 && o == 1 && dz.right);
+            out.v[e] = div_rn(fv.v[e] - t[e] * op.inv_hSq, edge ? dz.de : dz.db, edge ? dz.ye : dz.yb);
+        }
+    } else if (CLZ || __all(nbyz == 0 && c.xin)) {
 #pragma unroll
         for (int e = 0; e < N; ++e) out.v[e] = div_rn(fv.v[e] - t[e] * op.inv_hSq, op.adiag, op.yadiag);
     } else {
@@ -1285,14 +1302,23 @@ __device__ __forceinline__ Vec<T, N> zs_relax(const Vec<T, N>& zl, const Vec<T, 
 }
 
 // Residual of my N cells of one colour (x parity o) at one plane: k_resrestrict's expressions.
-template <typename T, int N, bool CLZ>
+template <typename T, int N, bool CLZ, bool ST = false>
 __device__ __forceinline__ void zs_residual(const Vec<T, N>& zl, const Vec<T, N>& cen, const Vec<T, N>& zr,
                                             const ZsNb<T, N>& nb, const Vec<T, N>& uc, const Vec<T, N>& fv,
-                                            const ZsCol& c, int o, int nbyz, int nx, const Op<T, 3>& op, T (&rr)[N])
+                                            const ZsCol& c, int o, int nbyz, int nx, const Op<T, 3>& op,
+                                            const ZsDiag<T>& dz, T (&rr)[N])
 {
     T t[N];
     zs_nbsum<T, N>(zl, cen, zr, nb, o, t);
-    if (CLZ || __all(nbyz == 0 && c.xin)) {
+    if (!CLZ && ST) {
+#pragma unroll
+        for (int e = 0; e < N; ++e) {
+            const bool edge = (e == 0 && o == 0 && dz.left) || (e == N - 1 && o == 1 && dz.right);
+            const T askew = t[e] * op.inv_hSq;
+            const T a_u = askew + (edge ? dz.de : dz.db) * uc.v[e];
+            rr[e] = fv.v[e] - a_u;
+        }
+    } else if (CLZ || __all(nbyz == 0 && c.xin)) {
 #pragma unroll
         for (int e = 0; e < N; ++e) {
             const T askew = t[e] * op.inv_hSq;
@@ -1439,6 +1465,16 @@ __attribute__((amdgpu_waves_per_eu(1, PRE ? ZS_WPE_PRE : ZS_WPE_POST))) void k_z
     const int goff = cgy * hw + cgm;  // in-plane offset (nx * ny < 2^31)
     const bool tile_xy = on && ye >= H && ye < H + TY && gx >= S::HXG && gx < G - S::HXG;
     const int zlo = Z0 - H;
+    ZsDiag<T> dz;
+    {
+        const int nby = (gy == 0) + (gy == g.ny - 1);  // 0 .. 2 (ny >= 2)
+        dz.db = nby == 0 ? op.dg[0] : (nby == 1 ? op.dg[1] : op.dg[2]);
+        dz.yb = nby == 0 ? op.ydg[0] : (nby == 1 ? op.ydg[1] : op.ydg[2]);
+        dz.de = nby == 0 ? op.dg[1] : (nby == 1 ? op.dg[2] : op.dg[3]);
+        dz.ye = nby == 0 ? op.ydg[1] : (nby == 1 ? op.ydg[2] : op.ydg[3]);
+        dz.left = col.gm == 0;
+        dz.right = col.gm + N == hw;
+    }
     const int p_end = Z0 + zc + (PRE ? 5 : 3);
     auto inz = [&](int q) { return z0 + q >= 0 && z0 + q < gnz; };  // inside the global box
     auto pcl = [&](int q) { return q < qlo ? qlo : (q > qhi ? qhi : q); };
@@ -1604,22 +1640,22 @@ __attribute__((amdgpu_waves_per_eu(1, PRE ? ZS_WPE_PRE : ZS_WPE_POST))) void k_z
 
         // ---- stages 1..4: half-sweep k on plane p - k (red, black, red, black) ----
         zs_nb_load<T, N>(n1, slot(0, 2, p - 1), col);
-        VT o1 = zs_relax<T, N, CLZ>(W0[sl(2)], W0[sl(1)], W0[sl(0)], n1, cur.f1, col, par(p - 1), nbyz(p - 1), g.nx, op);
+        VT o1 = zs_relax<T, N, CLZ, ST>(W0[sl(2)], W0[sl(1)], W0[sl(0)], n1, cur.f1, col, par(p - 1), nbyz(p - 1), g.nx, op, dz);
         if (!ST && !inz(p - 1)) o1 = vz;
         W1[sl(1)] = o1;
         zs_nb_load<T, N>(n2, slot(S::OFF1, 2, p - 2), col);
-        VT o2 = zs_relax<T, N, CLZ>(W1[sl(3)], W1[sl(2)], W1[sl(1)], n2, cur.f2, col, 1 ^ par(p - 2), nbyz(p - 2), g.nx,
-                                    op);
+        VT o2 = zs_relax<T, N, CLZ, ST>(W1[sl(3)], W1[sl(2)], W1[sl(1)], n2, cur.f2, col, 1 ^ par(p - 2), nbyz(p - 2), g.nx,
+                                    op, dz);
         if (!ST && !inz(p - 2)) o2 = vz;
         W2[sl(2)] = o2;
         zs_nb_load<T, N>(n3, slot(S::OFF2, 2, p - 3), col);
-        VT o3 = zs_relax<T, N, CLZ>(W2[sl(4)], W2[sl(3)], W2[sl(2)], n3, FR[sl(3)], col, par(p - 3), nbyz(p - 3), g.nx,
-                                    op);
+        VT o3 = zs_relax<T, N, CLZ, ST>(W2[sl(4)], W2[sl(3)], W2[sl(2)], n3, FR[sl(3)], col, par(p - 3), nbyz(p - 3), g.nx,
+                                    op, dz);
         if (!ST && !inz(p - 3)) o3 = vz;
         W3[sl(3)] = o3;
         zs_nb_load<T, N>(n4, slot(S::OFF3, NS3, p - 4), col);
-        VT o4 = zs_relax<T, N, CLZ>(W3[sl(5)], W3[sl(4)], W3[sl(3)], n4, FB[sl(4)], col, 1 ^ par(p - 4), nbyz(p - 4),
-                                    g.nx, op);
+        VT o4 = zs_relax<T, N, CLZ, ST>(W3[sl(5)], W3[sl(4)], W3[sl(3)], n4, FB[sl(4)], col, 1 ^ par(p - 4), nbyz(p - 4),
+                                    g.nx, op, dz);
         if (!ST && !inz(p - 4)) o4 = vz;
         W4[sl(4)] = o4;
 
@@ -1667,10 +1703,10 @@ __attribute__((amdgpu_waves_per_eu(1, PRE ? ZS_WPE_PRE : ZS_WPE_POST))) void k_z
             }
             // red cells (x parity pq) see black neighbours, black cells (x parity 1 - pq) red ones
             T rred[N], rblk[N], rr[2][N];  // rr: [x parity][e]
-            zs_residual<T, N, CLZ>(W4[sl(6)], W4[sl(5)], W4[sl(4)], nk, W3[sl(5)], FR[sl(5)], col, pq, nbyz(q), g.nx, op,
-                                   rred);
-            zs_residual<T, N, CLZ>(W3[sl(6)], W3[sl(5)], W3[sl(4)], nr, W4[sl(5)], FB[sl(5)], col, 1 ^ pq, nbyz(q), g.nx,
-                                   op, rblk);
+            zs_residual<T, N, CLZ, ST>(W4[sl(6)], W4[sl(5)], W4[sl(4)], nk, W3[sl(5)], FR[sl(5)], col, pq, nbyz(q), g.nx, op,
+                                   dz, rred);
+            zs_residual<T, N, CLZ, ST>(W3[sl(6)], W3[sl(5)], W3[sl(4)], nr, W4[sl(5)], FB[sl(5)], col, 1 ^ pq, nbyz(q), g.nx,
+                                   op, dz, rblk);
 #pragma unroll
             for (int e = 0; e < N; ++e) {
                 rr[0][e] = pq == 0 ? rred[e] : rblk[e];
@@ -1784,7 +1820,10 @@ __attribute__((amdgpu_waves_per_eu(1, PRE ? ZS_WPE_PRE : ZS_WPE_POST))) void k_z
 
 // 1024 threads = 16 waves on the CU; fp64 gets 512 so the kernel keeps 256 VGPRs without spills
 template <typename T>
-constexpr int tail_threads() { return sizeof(T) == 4 ? 1024 : 512; }
+#ifndef TAIL_THREADS_F32
+#define TAIL_THREADS_F32 1024
+#endif
+constexpr int tail_threads() { return sizeof(T) == 4 ? TAIL_THREADS_F32 : 512; }
 
 template <typename T, int DIM>
 struct TailArgs {
