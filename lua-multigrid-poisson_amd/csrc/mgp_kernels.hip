@@ -1111,6 +1111,11 @@ __device__ __forceinline__ void lds_barrier()
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 #endif
 }
+#ifdef ZS_NOCHAIN  // timing experiment only: each stage's newest z-neighbour is an older ring entry,
+#define ZS_NC 1    // so the stages of a step do not depend on each other (results are wrong)
+#else
+#define ZS_NC 0
+#endif
 #ifdef ZS_NOLOAD  // timing experiment only: every plane reads plane 0 (cache-resident)
 #define ZS_PLANE(q) 0
 #else
@@ -1543,12 +1548,16 @@ __attribute__((amdgpu_waves_per_eu(1, PRE ? ZS_WPE_PRE : ZS_WPE_POST))) void k_z
         // prefetch of plane 2m and put in the ring at the top of step 2m
         if (!PRE && ((zz0 + p) & 1) == 0) cload(r, ((zz0 + p) >> 1) + 1);
         if (ST) {  // one 64-bit plane offset, the others by subtraction
-            const int64_t pP = (int64_t)ZS_PLANE(p) * P;
+#ifdef ZS_NOLOAD
+            const int64_t pP = 0, Pz = 0;  // every plane reads plane 0
+#else
+            const int64_t pP = (int64_t)p * P, Pz = P;
+#endif
             r.u = vload<T, N>(src_black + pP + goff);
-            r.f1 = vload<T, N>(f + (pP - P) + goff);
-            r.f2 = vload<T, N>(f + (pP - 2 * P) + Hh + goff);
+            r.f1 = vload<T, N>(f + (pP - Pz) + goff);
+            r.f2 = vload<T, N>(f + (pP - 2 * Pz) + Hh + goff);
             if (!PRE && ERR && tile_xy) {  // psiOld of plane p - 4, for the tile's own columns only
-                const T* dp = dst + (pP - 4 * P);
+                const T* dp = dst + (pP - 4 * Pz);
                 r.o0 = vload<T, N>(dp + goff);
                 r.o1 = vload<T, N>(dp + Hh + goff);
             }
@@ -1640,21 +1649,21 @@ __attribute__((amdgpu_waves_per_eu(1, PRE ? ZS_WPE_PRE : ZS_WPE_POST))) void k_z
 
         // ---- stages 1..4: half-sweep k on plane p - k (red, black, red, black) ----
         zs_nb_load<T, N>(n1, slot(0, 2, p - 1), col);
-        VT o1 = zs_relax<T, N, CLZ, ST>(W0[sl(2)], W0[sl(1)], W0[sl(0)], n1, cur.f1, col, par(p - 1), nbyz(p - 1), g.nx, op, dz);
+        VT o1 = zs_relax<T, N, CLZ, ST>(W0[sl(2)], W0[sl(1)], W0[sl(ZS_NC ? 3 : 0)], n1, cur.f1, col, par(p - 1), nbyz(p - 1), g.nx, op, dz);
         if (!ST && !inz(p - 1)) o1 = vz;
         W1[sl(1)] = o1;
         zs_nb_load<T, N>(n2, slot(S::OFF1, 2, p - 2), col);
-        VT o2 = zs_relax<T, N, CLZ, ST>(W1[sl(3)], W1[sl(2)], W1[sl(1)], n2, cur.f2, col, 1 ^ par(p - 2), nbyz(p - 2), g.nx,
+        VT o2 = zs_relax<T, N, CLZ, ST>(W1[sl(3)], W1[sl(2)], W1[sl(ZS_NC ? 0 : 1)], n2, cur.f2, col, 1 ^ par(p - 2), nbyz(p - 2), g.nx,
                                     op, dz);
         if (!ST && !inz(p - 2)) o2 = vz;
         W2[sl(2)] = o2;
         zs_nb_load<T, N>(n3, slot(S::OFF2, 2, p - 3), col);
-        VT o3 = zs_relax<T, N, CLZ, ST>(W2[sl(4)], W2[sl(3)], W2[sl(2)], n3, FR[sl(3)], col, par(p - 3), nbyz(p - 3), g.nx,
+        VT o3 = zs_relax<T, N, CLZ, ST>(W2[sl(4)], W2[sl(3)], W2[sl(ZS_NC ? 1 : 2)], n3, FR[sl(3)], col, par(p - 3), nbyz(p - 3), g.nx,
                                     op, dz);
         if (!ST && !inz(p - 3)) o3 = vz;
         W3[sl(3)] = o3;
         zs_nb_load<T, N>(n4, slot(S::OFF3, NS3, p - 4), col);
-        VT o4 = zs_relax<T, N, CLZ, ST>(W3[sl(5)], W3[sl(4)], W3[sl(3)], n4, FB[sl(4)], col, 1 ^ par(p - 4), nbyz(p - 4),
+        VT o4 = zs_relax<T, N, CLZ, ST>(W3[sl(5)], W3[sl(4)], W3[sl(ZS_NC ? 2 : 3)], n4, FB[sl(4)], col, 1 ^ par(p - 4), nbyz(p - 4),
                                     g.nx, op, dz);
         if (!ST && !inz(p - 4)) o4 = vz;
         W4[sl(4)] = o4;
@@ -1703,7 +1712,7 @@ __attribute__((amdgpu_waves_per_eu(1, PRE ? ZS_WPE_PRE : ZS_WPE_POST))) void k_z
             }
             // red cells (x parity pq) see black neighbours, black cells (x parity 1 - pq) red ones
             T rred[N], rblk[N], rr[2][N];  // rr: [x parity][e]
-            zs_residual<T, N, CLZ, ST>(W4[sl(6)], W4[sl(5)], W4[sl(4)], nk, W3[sl(5)], FR[sl(5)], col, pq, nbyz(q), g.nx, op,
+            zs_residual<T, N, CLZ, ST>(W4[sl(6)], W4[sl(5)], W4[sl(ZS_NC ? 3 : 4)], nk, W3[sl(5)], FR[sl(5)], col, pq, nbyz(q), g.nx, op,
                                    dz, rred);
             zs_residual<T, N, CLZ, ST>(W3[sl(6)], W3[sl(5)], W3[sl(4)], nr, W4[sl(5)], FB[sl(5)], col, 1 ^ pq, nbyz(q), g.nx,
                                    op, dz, rblk);
