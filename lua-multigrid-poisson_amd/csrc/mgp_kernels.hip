@@ -1133,7 +1133,9 @@ __device__ __forceinline__ void lds_barrier()
 #define ZS_NPOST_F32 2
 #endif
 // PRE tile height: 64 (less y halo, 12 waves) spills at the 168-VGPR cap and measured slower
-// (640 against 578 us)
+// (640 against 578 us).  fp64 PRE: 32 x 32 tiles (8 waves, 216 VGPRs) instead of 64 x 16 (9 waves,
+// spilling at the 168-VGPR cap): 1111 -> 800 us at 512^3; fp64 POST stays 64 x 16 (890 us against
+// 999 / 1536 us for 32 x 32 / 32 x 16).
 #ifndef ZS_TYPRE_F32
 #define ZS_TYPRE_F32 32
 #endif
@@ -1144,18 +1146,33 @@ template <typename T>
 struct ZsTile;
 template <>
 struct ZsTile<float> {
-    static constexpr int TX = 64, TYPRE = ZS_TYPRE_F32, TYPOST = ZS_TYPOST_F32, NPRE = ZS_NPRE_F32, NPOST = ZS_NPOST_F32;
+    static constexpr int TXPRE = 64, TXPOST = 64, TYPRE = ZS_TYPRE_F32, TYPOST = ZS_TYPOST_F32, NPRE = ZS_NPRE_F32,
+                         NPOST = ZS_NPOST_F32;
 };
+#ifndef ZS_TXPRE_F64
+#define ZS_TXPRE_F64 32
+#endif
+#ifndef ZS_TXPOST_F64
+#define ZS_TXPOST_F64 64
+#endif
+#ifndef ZS_TYPRE_F64
+#define ZS_TYPRE_F64 32
+#endif
+#ifndef ZS_TYPOST_F64
+#define ZS_TYPOST_F64 16
+#endif
 template <>
 struct ZsTile<double> {
-    static constexpr int TX = 64, TYPRE = 16, TYPOST = 16, NPRE = 2, NPOST = 2;
+    static constexpr int TXPRE = ZS_TXPRE_F64, TXPOST = ZS_TXPOST_F64, TYPRE = ZS_TYPRE_F64, TYPOST = ZS_TYPOST_F64,
+                         NPRE = 2, NPOST = 2;
 };
 constexpr int kZsHX = 8;  // x halo cells per side (>= the trapezoid depth, whole groups)
 
 template <typename T, bool PRE>
 struct ZsShape {
     static constexpr int N = PRE ? ZsTile<T>::NPRE : ZsTile<T>::NPOST;
-    static constexpr int TX = ZsTile<T>::TX, TY = PRE ? ZsTile<T>::TYPRE : ZsTile<T>::TYPOST;
+    static constexpr int TX = PRE ? ZsTile<T>::TXPRE : ZsTile<T>::TXPOST;
+    static constexpr int TY = PRE ? ZsTile<T>::TYPRE : ZsTile<T>::TYPOST;
     static constexpr int H = PRE ? 5 : 4;              // y/z halo = stages that read neighbours
     static constexpr int HWE = (TX + 2 * kZsHX) / 2;   // reals per LDS half-row
     static constexpr int G = HWE / N;                  // column groups per row
@@ -2296,9 +2313,11 @@ static hipError_t fused_dispatch(const FusedArgs& a, hipStream_t s)
 // tile of a phase (pre) or the tallest of both (pre < 0)
 static void zs_tile(int rb, int& tx, int& ty, int pre = -1)
 {
-    tx = rb == 4 ? ZsTile<float>::TX : ZsTile<double>::TX;
+    const int xa = rb == 4 ? ZsTile<float>::TXPRE : ZsTile<double>::TXPRE;
+    const int xb = rb == 4 ? ZsTile<float>::TXPOST : ZsTile<double>::TXPOST;
     const int a = rb == 4 ? ZsTile<float>::TYPRE : ZsTile<double>::TYPRE;
     const int b = rb == 4 ? ZsTile<float>::TYPOST : ZsTile<double>::TYPOST;
+    tx = pre < 0 ? (xa > xb ? xa : xb) : (pre ? xa : xb);
     ty = pre < 0 ? (a > b ? a : b) : (pre ? a : b);
 }
 
