@@ -1142,12 +1142,18 @@ __device__ __forceinline__ void lds_barrier()
 #ifndef ZS_TYPOST_F32
 #define ZS_TYPOST_F32 32
 #endif
+#ifndef ZS_TXPRE_F32
+#define ZS_TXPRE_F32 64
+#endif
+#ifndef ZS_TXPOST_F32
+#define ZS_TXPOST_F32 64
+#endif
 template <typename T>
 struct ZsTile;
 template <>
 struct ZsTile<float> {
-    static constexpr int TXPRE = 64, TXPOST = 64, TYPRE = ZS_TYPRE_F32, TYPOST = ZS_TYPOST_F32, NPRE = ZS_NPRE_F32,
-                         NPOST = ZS_NPOST_F32;
+    static constexpr int TXPRE = ZS_TXPRE_F32, TXPOST = ZS_TXPOST_F32, TYPRE = ZS_TYPRE_F32, TYPOST = ZS_TYPOST_F32,
+                         NPRE = ZS_NPRE_F32, NPOST = ZS_NPOST_F32;
 };
 #ifndef ZS_TXPRE_F64
 #define ZS_TXPRE_F64 32
