@@ -114,6 +114,7 @@ struct Level {
     bool ghost_ok = true;   // u's ghost planes hold the neighbours' current planes
     bool fghost_ok = true;  // f's ghost planes likewise
     bool fused = false;     // smoothing phases run temporally blocked (k_zs); needs t
+    bool blk = false;       // smoothing phases run as 3D-tiled one-launch phases (k_blk); needs t
     bool zero_pending = false;  // u is logically 0: the next red half-sweep reads c->zbuf instead
     bool ghost_zero = false;    // u is 0 everywhere, so ghost planes of any depth are current
     int64_t exchanges = 0;      // halo exchanges of this level so far (mgp_level_info info[7])
@@ -153,6 +154,8 @@ struct mgp_ctx {
     int rb = 8;
     int G = 0;  // ghost planes per side (kGhost3D in 3D, 0 in 2D; kGhostZs for distributed 3D)
     bool deep_halo = true;  // smooth_deep on distributed levels below the finest
+    int blk_tile = mgp::kBlkTile;  // k_blk owned tile edge
+    bool fresh_sweep = true;        // k_fresh for the first sweep of a lazily zeroed level (MGP_FRESH=0: off)
     std::vector<Level> lev;
     hipStream_t s = nullptr;
     int device = 0;
@@ -515,6 +518,15 @@ int smooth(mgp_ctx* c, int l, int sweeps, double h, bool want_err = false)
         }
         const bool oop = l == 0 && c->in_cycle && c->err_fuse && !c->first_done;  // keep psiOld in t
         const bool last_err = want_err && sw == sweeps - 1;
+        if (sw == 0 && L.zero_pending && c->fresh_sweep && !oop && !last_err && !L.p.dist &&
+            mgp::fresh_supported(c->rb, L.g)) {
+            // the first sweep of a fresh zero guess from f alone (k_fresh: both colours, one pass)
+            HIP_TRY(c, mgp::launch_fresh_sweep(c->rb, c->o.dim, c->ui(L, L.f), c->ui(L, L.u), L.g, h, cl, c->s));
+            L.zero_pending = false;
+            L.ghost_ok = true;
+            L.ghost_zero = false;
+            continue;
+        }
         const char* old = last_err ? L.t : nullptr;
         const int nb = mgp::half_blocks(c->rb, L.g, c->use_gs);
         char* dst = oop ? L.t : L.u;
@@ -725,6 +737,63 @@ int fused_post(mgp_ctx* c, int l, double h, bool want_err)
     return MGP_OK;
 }
 
+// smooth(l, nu1) + residual_restrict(l) of a small replicated level as one 3D-tiled launch:
+// u -> t, R -> f of l+1 (a pending fresh zero is read as such, no memset)
+int block_pre(mgp_ctx* c, int l, double h)
+{
+    Level& L = c->lev[l];
+    Level& C = c->lev[l + 1];
+    int64_t zc = 0;
+    mgp::BlockArgs a{};
+    a.pre = true;
+    a.ns = c->o.nu1;
+    a.tile = c->blk_tile;
+    a.src = L.zero_pending ? nullptr : c->ui(L, L.u);
+    a.f = c->ui(L, L.f);
+    a.dst = c->ui(L, L.t);
+    a.g = L.g;
+    a.gc = coarse_view(L, C, &zc);
+    a.R = c->ui(C, C.f) + (size_t)(zc * C.g.P) * c->rb;
+    a.h = h;
+    a.cl = coarse_coef(c->o.coarse_bc, l);
+    HIP_TRY(c, mgp::launch_block(c->rb, a, c->s));
+    L.zero_pending = false;
+    std::swap(L.u, L.t);
+    L.ghost_ok = true;
+    L.ghost_zero = false;
+    C.fghost_ok = true;
+    return MGP_OK;
+}
+
+// prolong_correct(l) + smooth(l, nu2) of a small replicated level as one 3D-tiled launch: u + P V -> t
+int block_post(mgp_ctx* c, int l, double h)
+{
+    Level& L = c->lev[l];
+    Level& C = c->lev[l + 1];
+    TRY(materialize_zero(c, L));
+    TRY(materialize_zero(c, C));
+    int64_t zc = 0;
+    mgp::BlockArgs a{};
+    a.pre = false;
+    a.linear = c->o.prolong == MGP_PROLONG_LINEAR;
+    a.ns = c->o.nu2;
+    a.tile = c->blk_tile;
+    a.src = c->ui(L, L.u);
+    a.f = c->ui(L, L.f);
+    a.dst = c->ui(L, L.t);
+    a.g = L.g;
+    a.gc = coarse_view(L, C, &zc);
+    a.V = c->ui(C, C.u) + (size_t)(zc * C.g.P) * c->rb;
+    a.h = h;
+    a.cl = coarse_coef(c->o.coarse_bc, l);
+    a.clc = coarse_coef(c->o.coarse_bc, l + 1);
+    HIP_TRY(c, mgp::launch_block(c->rb, a, c->s));
+    std::swap(L.u, L.t);
+    L.ghost_ok = true;
+    L.ghost_zero = false;
+    return MGP_OK;
+}
+
 // The ops of cycle_rec(l, fcycle) for levels >= T, recorded for k_tail (levels relative to T).
 void tail_gen(const mgp_ctx* c, int T, int l, bool fcycle, std::vector<uint32_t>& ops)
 {
@@ -840,8 +909,11 @@ int cycle_rec(mgp_ctx* c, int l, double h, bool fcycle)
     if (l == c->tail_level && h == level_h(c, l)) return run_tail(c, fcycle);
     if (l == last) return coarse_solve_at(c, l, h);
     const bool fused = c->lev[l].fused && h == level_h(c, l);
+    const bool blk = !fused && c->lev[l].blk && h == level_h(c, l);
     if (fused) {
         TRY(fused_pre(c, l, h));
+    } else if (blk) {
+        TRY(block_pre(c, l, h));
     } else {
         TRY(smooth(c, l, c->o.nu1, h));
         TRY(residual_restrict(c, l, h));
@@ -852,6 +924,8 @@ int cycle_rec(mgp_ctx* c, int l, double h, bool fcycle)
     const bool want_err = l == 0 && c->in_cycle && c->err_fuse;
     if (fused) {
         TRY(fused_post(c, l, h, want_err));
+    } else if (blk && !want_err) {
+        TRY(block_post(c, l, h));
     } else {
         TRY(prolong_correct(c, l));
         TRY(smooth(c, l, c->o.nu2, h, want_err));
@@ -1130,6 +1204,10 @@ static int create_impl(mgp_ctx** out, const mgp_opts* o, mgp_loopback* lb, ncclC
     c->rb = o->real_bytes;
     c->G = o->dim == 3 ? mgp::kGhost3D : 0;  // widened below when a distributed level is fused
     {
+        const char* v = std::getenv("MGP_FRESH");
+        c->fresh_sweep = !(v && std::atoi(v) == 0);
+    }
+    {
         const char* v = std::getenv("MGP_DEEP_HALO");  // 0: exchange before every half-sweep instead
         c->deep_halo = !(v && std::atoi(v) == 0);
     }
@@ -1189,11 +1267,25 @@ static int create_impl(mgp_ctx** out, const mgp_opts* o, mgp_loopback* lb, ncclC
             if (L.fused && L.p.dist) c->G = mgp::kGhostZs;
         }
     }
+    {
+        // 3D-tiled one-launch phases (k_blk) on replicated RB-GS levels 1 .. of <= MGP_BLK_CELLS cells
+        // (default 2^18 = 64^3) below the finest; MGP_BLK=0 turns them off (bit-identical results)
+        const char* v = std::getenv("MGP_BLK");
+        const char* vm = std::getenv("MGP_BLK_CELLS");
+        const int64_t max_cells = vm ? std::atoll(vm) : (int64_t(1) << 18);
+        const int ns = std::max(c->o.nu1, c->o.nu2);
+        const bool on = !(v && std::atoi(v) == 0) && c->o.smoother == MGP_RBGS && c->o.nu1 >= 1 && c->o.nu2 >= 1;
+        for (size_t l = 1; l + 1 < c->lev.size(); ++l) {
+            Level& L = c->lev[l];
+            L.blk = on && !L.fused && !L.p.dist && level_cells(L) <= max_cells &&
+                    mgp::block_supported(c->rb, c->o.dim, ns, L.g, c->blk_tile);
+        }
+    }
     for (auto& L : c->lev) L.alloc = L.g.P * (L.g.nz + 2 * c->G);
     for (size_t l = 0; l < c->lev.size(); ++l) {
         Level& L = c->lev[l];
         const size_t bytes = (size_t)L.alloc * rb;
-        const bool need_t = c->o.smoother == MGP_JACOBI || (l == 0 && c->err_fuse) || L.fused;
+        const bool need_t = c->o.smoother == MGP_JACOBI || (l == 0 && c->err_fuse) || L.fused || L.blk;
         if (hipMalloc(&L.u, bytes) != hipSuccess || hipMalloc(&L.f, bytes) != hipSuccess ||
             (need_t && hipMalloc(&L.t, bytes) != hipSuccess)) {
             c->err = "hipMalloc failed for level " + std::to_string(l) + " (" + std::to_string(bytes) + " bytes)";
@@ -1312,7 +1404,8 @@ int mgp_level_info(const mgp_ctx* c, int level, int64_t info[8])
     info[3] = p.nz;
     info[4] = p.z0;
     info[5] = p.dist;
-    info[6] = c->tail_level >= 0 && level >= c->tail_level;  // run inside the one-launch coarse tail
+    const Level& L = c->lev[level];
+    info[6] = c->tail_level >= 0 && level >= c->tail_level ? 1 : L.fused ? 2 : L.blk ? 3 : 0;  // phase engine
     info[7] = c->lev[level].exchanges;
     return MGP_OK;
 }

@@ -61,6 +61,10 @@ hipError_t launch_sqdiff_field(int rb, const void* a, const void* b, void* out, 
 int half_blocks(int rb, Geo g, bool gs);
 hipError_t launch_half_sweep(int rb, int dim, bool fine, int color, const void* other, const void* f, void* dst,
                              const void* old, double* partials, Geo g, double h, double cl, bool gs, hipStream_t s);
+// The first red/black sweep of a fresh zero guess (cpu.lua:138) in one pass: u (both colours) from f
+// alone, bit-identical to the red and black half-sweeps reading u = 0.  Levels with hw >= 16 / rb.
+bool fresh_supported(int rb, const Geo& g);
+hipError_t launch_fresh_sweep(int rb, int dim, const void* f, void* u, Geo g, double h, double cl, hipStream_t s);
 // Fused residual + restriction (calcResidual + reduceResidual): R (coarse packed, pointing at the
 // coarse plane of this rank's fine plane 0; its Geo is gc) from u, f of the fine level.
 hipError_t launch_residual_restrict(int rb, int dim, const void* u, const void* f, void* R, Geo g, Geo gc, double h,
@@ -110,6 +114,29 @@ hipError_t prepare_kernels(int rb);
 int fused_zc(int rb, const Geo& g, bool pre);
 int fused_blocks(int rb, const Geo& g, int zc);
 hipError_t launch_fused(int rb, const FusedArgs& a, hipStream_t s);
+
+// 3D-tiled smoothing phases of a small replicated 3D red/black level (k_blk: one launch per phase,
+// the tile and its halo in LDS):
+//   pre : dst = ns sweeps of src; R (coarse packed, Geo gc) = restrict(residual(dst))
+//   post: dst = ns sweeps of (src + P V)
+// src == nullptr reads u = 0 (a fresh coarse guess).  src != dst.
+constexpr int kBlkMaxSweeps = 2;
+constexpr int kBlkTile = 8;  // owned tile edge (every axis of a tiled level is a multiple)
+struct BlockArgs {
+    bool pre;
+    int linear;
+    int ns;
+    int tile;  // owned tile edge (kBlkTile)
+    const void* src;
+    const void* f;
+    void* dst;
+    void* R;
+    const void* V;
+    Geo g, gc;
+    double h, cl, clc;
+};
+bool block_supported(int rb, int dim, int ns, const Geo& g, int tile);
+hipError_t launch_block(int rb, const BlockArgs& a, hipStream_t s);
 
 // Coarse-level tail: the sub-cycle below one level as a single one-workgroup launch with every
 // level in LDS.  ops[] = (op | level << 4 | arg << 8), levels relative to the tail's first level.

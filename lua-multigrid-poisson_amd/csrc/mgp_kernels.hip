@@ -564,6 +564,83 @@ __global__ __launch_bounds__(kBlock) void k_half_s(const T* __restrict__ other, 
     if (ERR) block_partial<T>(acc, partials);
 }
 
+// First RB-GS sweep from a fresh zero guess (cpu.lua:138), both colours in one pass over f.
+// With u = 0 the red half-sweep's neighbour sum is +0, so red = relax(0, f_red, nb): a pointwise
+// function of f.  The black half-sweep then needs the red values of its six neighbours, which
+// this thread recomputes from f (red rows j-1, j, j+1 and planes k-1, k+1 of its N-cell segment,
+// plus one edge cell) with the same expression, so u after the sweep is bit-identical to the two
+// half-sweeps reading a zero black input.  A thread owns the N red and N black cells at half
+// positions m0 .. m0+N-1 of one row.  HBM: read f, write u (the per-piece pair also reads the
+// zero input and re-reads the red cells).
+template <typename T, int DIM>
+__global__ __launch_bounds__(kBlock) void k_fresh(const T* __restrict__ f, T* __restrict__ u, Geo g, Op<T, DIM> op)
+{
+    constexpr int N = VN<T>::n;
+    constexpr int LN = N == 4 ? 2 : 1;
+    const int lgpr = g.lhw - LN;
+    const int b = xcd_remap(blockIdx.x, gridDim.x);
+    const int64_t it = (int64_t)b * kBlock + threadIdx.x;
+    const int grp = (int)(it & ((1 << lgpr) - 1));
+    const int j = (int)((it >> lgpr) & (g.ny - 1));
+    const int64_t k = it >> (lgpr + g.ly);
+    if (k >= g.nz) return;
+    const int m0 = grp * N;
+    const int64_t gk = g.z0 + k;
+    const int ob = 1 ^ (int)((j + gk) & 1);  // x parity of this row's black cells (red: ob ^ 1)
+    // red values of row (jj, kk) at m0 .. m0+N-1 (0 outside the box)
+    auto red_row = [&](int jj, int64_t kk, Vec<T, N>& r) {
+        const int64_t gkk = g.z0 + kk;
+        if (jj < 0 || jj >= g.ny || (DIM == 3 && (gkk < 0 || gkk >= g.gnz))) {
+            r = vzero<T, N>();
+            return;
+        }
+        const int orr = (int)((jj + gkk) & 1);  // x parity of red cells in that row
+        const Vec<T, N> fv = vload<T, N>(f + kk * g.P + (int64_t)jj * g.hw + m0);
+        const int nbyz = (jj == 0) + (jj == g.ny - 1) + (DIM == 3 ? (gkk == 0) + (gkk == g.gnz - 1) : 0);
+#pragma unroll
+        for (int e = 0; e < N; ++e) {
+            const int i = 2 * (m0 + e) + orr;
+            r.v[e] = op.relax((T)0, fv.v[e], nbyz + (i == 0) + (i == g.nx - 1));
+        }
+    };
+    Vec<T, N> rc, ryl, ryr, rzl, rzr;
+    red_row(j, k, rc);
+    red_row(j - 1, k, ryl);
+    red_row(j + 1, k, ryr);
+    if (DIM == 3) {
+        red_row(j, k - 1, rzl);
+        red_row(j, k + 1, rzr);
+    }
+    // the red x-neighbour outside the segment: m0 - 1 (black cells at even x) or m0 + N (odd x)
+    const int me = ob == 0 ? m0 - 1 : m0 + N;
+    T edge = (T)0;
+    if (me >= 0 && me < g.hw) {
+        const int i = 2 * me + (ob ^ 1);
+        const int nbyz = (j == 0) + (j == g.ny - 1) + (DIM == 3 ? (gk == 0) + (gk == g.gnz - 1) : 0);
+        edge = op.relax((T)0, f[k * g.P + (int64_t)j * g.hw + me], nbyz + (i == 0) + (i == g.nx - 1));
+    }
+    const int64_t own = k * g.P + (int64_t)j * g.hw + m0;
+    const Vec<T, N> fb = vload<T, N>(f + own + g.H);
+    const int nbyz = (j == 0) + (j == g.ny - 1) + (DIM == 3 ? (gk == 0) + (gk == g.gnz - 1) : 0);
+    Vec<T, N> out;
+#pragma unroll
+    for (int e = 0; e < N; ++e) {
+        const int i = 2 * (m0 + e) + ob;
+        const T xl = ob == 0 ? (e == 0 ? edge : rc.v[e - 1]) : rc.v[e];
+        const T xr = ob == 0 ? rc.v[e] : (e == N - 1 ? edge : rc.v[e + 1]);
+        T s = xl + xr;
+        s = s + ryl.v[e];
+        s = s + ryr.v[e];
+        if (DIM == 3) {
+            s = s + rzl.v[e];
+            s = s + rzr.v[e];
+        }
+        out.v[e] = op.relax(s, fb.v[e], nbyz + (i == 0) + (i == g.nx - 1));
+    }
+    vstore<T, N>(u + own, rc);
+    vstore<T, N>(u + own + g.H, out);
+}
+
 // ---- fused residual + restriction -----------------------------------------------------------
 
 // Residual of one fine cell from packed u (generic, scalar loads).
@@ -890,18 +967,10 @@ __device__ __forceinline__ T cval(const T* __restrict__ V, const Geo& gc, int I,
     return s == (T)1 ? v : s * v;
 }
 
-// One fine slot of colour `color` of the prolongation + correction (scalar; any sizes).
+// (P V) at fine cell (i, j, local plane k): the oracle's per-cell prolongation value.
 template <typename T, int DIM, int LINEAR>
-__device__ __forceinline__ void prolong_item(T* u, const T* V, const Geo& g, const Geo& gc, T cl, int color,
-                                             int64_t it)
+__device__ __forceinline__ T prolong_value(const T* V, const Geo& g, const Geo& gc, T cl, int i, int j, int64_t k)
 {
-    const int m = (int)(it & (g.hw - 1));
-    const int j = (int)((it >> g.lhw) & (g.ny - 1));
-    const int64_t k = it >> (g.lhw + g.ly);
-    const int o = color ^ (int)((j + g.z0 + k) & 1);
-    const int i = 2 * m + o;
-    if (i >= g.nx) return;
-    const int64_t own = k * g.P + color * g.H + (int64_t)j * g.hw + m;
     const int I = i >> 1, J = j >> 1;
     const int64_t K = DIM == 3 ? (k >> 1) : 0;
     T v;
@@ -933,6 +1002,22 @@ __device__ __forceinline__ void prolong_item(T* u, const T* V, const Geo& g, con
             v = w0 * b0 + w1 * b1;
         }
     }
+    return v;
+}
+
+// One fine slot of colour `color` of the prolongation + correction (scalar; any sizes).
+template <typename T, int DIM, int LINEAR>
+__device__ __forceinline__ void prolong_item(T* u, const T* V, const Geo& g, const Geo& gc, T cl, int color,
+                                             int64_t it)
+{
+    const int m = (int)(it & (g.hw - 1));
+    const int j = (int)((it >> g.lhw) & (g.ny - 1));
+    const int64_t k = it >> (g.lhw + g.ly);
+    const int o = color ^ (int)((j + g.z0 + k) & 1);
+    const int i = 2 * m + o;
+    if (i >= g.nx) return;
+    const int64_t own = k * g.P + color * g.H + (int64_t)j * g.hw + m;
+    const T v = prolong_value<T, DIM, LINEAR>(V, g, gc, cl, i, j, k);
     u[own] = u[own] + v;
 }
 
@@ -1973,6 +2058,173 @@ __global__ __launch_bounds__(tail_threads<T>()) void k_tail(const TailArgs<T, DI
     }
 }
 
+// ---- 3D-tiled smoothing phases of small levels (k_blk) ----------------------------------------
+//
+// Below ~128^3 a launch costs more than its work (≈5 us per kernel, most of it the kernel
+// boundary), so a smoothing phase of nu RB-GS sweeps runs as ONE launch instead of 2 nu + 1:
+//   PRE : nu sweeps of src, then residual + restriction   (smooth(l, nu1) + residual_restrict(l))
+//   POST: src + P V, then nu sweeps                        (prolong_correct(l) + smooth(l, nu2))
+// A workgroup owns a tx x ty x tz tile, loads it with a halo of E = 2 nu + 1 (PRE) / 2 nu (POST)
+// cells (x halo rounded up to even so the LDS rows keep the global red/black packing) into LDS,
+// and runs the half-sweeps there on a region that shrinks by one cell per half-sweep (the halo is
+// recomputed redundantly by the neighbouring tiles with the same arithmetic), one barrier each.
+// Only black cells of the input are read (Gauss-Seidel never reads the value it replaces: the red
+// half-sweep overwrites the red ones); cells outside the box are 0 in LDS and never written.
+// Every expression is half_item's / resrestrict_item's / prolong_value's, so the result is
+// bit-identical to the launch-per-piece path and to the oracle.  src == nullptr: u = 0 (a fresh
+// coarse guess, cpu.lua:138, without the memset).  src and dst are different buffers.
+
+constexpr int kBlkThreads = 1024;  // 16 waves: the levels are small, so a workgroup is most of a CU
+
+// Compile-time shape of a phase: owned B^3 tile, halo E (y, z) and HX (x, even), NS sweeps.
+template <bool PRE, int B, int NS>
+struct BlkShape {
+    static constexpr int E = PRE ? 2 * NS + 1 : 2 * NS;
+    static constexpr int HX = (E + 1) & ~1;
+    static constexpr int EX = B + 2 * HX, EY = B + 2 * E, EZ = B + 2 * E, EH = EX / 2;
+    static constexpr int cells = EX * EY * EZ;
+    static constexpr int lidx(int lz, int ly, int c, int mm) { return ((lz * EY + ly) * 2 + c) * EH + mm; }
+};
+
+template <typename T, bool PRE, int LINEAR, int B, int NS>
+__global__ __launch_bounds__(kBlkThreads) void k_blk(const T* __restrict__ src, const T* __restrict__ f,
+                                                     T* __restrict__ dst, T* __restrict__ R, const T* __restrict__ V,
+                                                     Geo g, Geo gc, Op<T, 3> op, T clc)
+{
+    using S = BlkShape<PRE, B, NS>;
+    constexpr int E = S::E, HX = S::HX, EY = S::EY, EZ = S::EZ, EH = S::EH;
+    constexpr int NT = kBlkThreads;
+    extern __shared__ __align__(16) unsigned char blk_smem[];
+    T* const U = reinterpret_cast<T*>(blk_smem);
+    T* const F = U + S::cells;
+    T* const RS = F + S::cells;  // PRE: residuals of the owned cells (x fastest)
+    const int tid = threadIdx.x;
+    const int ntx = g.nx / B, nty = g.ny / B;
+    const int b = blockIdx.x;
+    const int X0 = (b % ntx) * B, Y0 = ((b / ntx) % nty) * B, Z0 = (b / (ntx * nty)) * B;
+    const int xs = X0 - HX, ys = Y0 - E, zs = Z0 - E;  // global (local-plane) origin of the LDS box
+    const int mxs = xs >> 1;                           // xs is even
+    const int nzl = (int)g.nz, gnz = (int)g.gnz, gz0 = (int)g.z0;
+    const int p0 = (ys + zs + gz0) & 1;                // parity of LDS row (0, 0)
+
+    // load: every LDS slot of both colours (u: black cells in the box, 0 elsewhere; f: cells in the
+    // box), all of a thread's global loads in flight at once
+    {
+        constexpr int n = EZ * EY * 2 * EH;
+        constexpr int NB = (n + NT - 1) / NT;
+        T uv[NB], fv[NB];
+#pragma unroll
+        for (int q = 0; q < NB; ++q) {
+            const int it = tid + q * NT;
+            const int row = it / (2 * EH), rest = it % (2 * EH);
+            const int lz = row / EY, ly = row % EY;
+            const int c = rest >= EH, mm = rest - c * EH;
+            const int gm = mxs + mm, gj = ys + ly, gk = zs + lz;
+            const bool in = it < n && gm >= 0 && gm < g.hw && gj >= 0 && gj < g.ny && gk >= 0 && gk < nzl;
+            const int64_t gi = (int64_t)gk * g.P + c * g.H + (int64_t)gj * g.hw + gm;
+            fv[q] = in ? f[gi] : (T)0;
+            uv[q] = in && c == 1 && src ? src[gi] : (T)0;
+            if (!PRE && in && c == 1) {
+                const int i = 2 * gm + (1 ^ ((ly + lz + p0) & 1));
+                uv[q] = uv[q] + prolong_value<T, 3, LINEAR>(V, g, gc, clc, i, gj, (int64_t)gk);
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < NB; ++q) {
+            const int it = tid + q * NT;
+            if (it < n) {
+                U[it] = uv[q];
+                F[it] = fv[q];
+            }
+        }
+    }
+    __syncthreads();
+
+    // half-sweeps: colour s & 1 (red first) on the tile extended by e = E - 1 - s cells (cells
+    // outside the box are skipped: they stay 0); half_item's expressions
+#pragma unroll
+    for (int s = 0; s < 2 * NS; ++s) {
+        const int c = s & 1, e = E - 1 - s;
+        const int xlo = HX - e, xhi = HX + B - 1 + e;
+        const int mlo = xlo >> 1, nm = (xhi >> 1) - mlo + 1;
+        const int ny = B + 2 * e, n = ny * ny * nm;
+#pragma unroll
+        for (int q = 0; q < (n + NT - 1) / NT; ++q) {
+            const int it = tid + q * NT;
+            const int row = it / nm, mm = mlo + it % nm;
+            const int ly = E - e + row % ny, lz = E - e + row / ny;
+            const int o = c ^ ((ly + lz + p0) & 1);
+            const int lx = 2 * mm + o;
+            const int gi = xs + lx, gj = ys + ly, gkl = zs + lz;
+            if (it < n && lx >= xlo && lx <= xhi && gi >= 0 && gi < g.nx && gj >= 0 && gj < g.ny && gkl >= 0 &&
+                gkl < nzl) {
+                const int oth = S::lidx(lz, ly, c ^ 1, mm);
+                T sum = U[oth - 1 + o] + U[oth + o];
+                sum = sum + U[oth - 2 * EH];
+                sum = sum + U[oth + 2 * EH];
+                sum = sum + U[oth - 2 * EH * EY];
+                sum = sum + U[oth + 2 * EH * EY];
+                const int gk = gz0 + gkl;
+                const int nb = (gi == 0) + (gi == g.nx - 1) + (gj == 0) + (gj == g.ny - 1) + (gk == 0) + (gk == gnz - 1);
+                const int own = S::lidx(lz, ly, c, mm);
+                U[own] = op.relax(sum, F[own], nb);
+            }
+        }
+        __syncthreads();
+    }
+
+    if (PRE) {
+        // residual of every owned cell into RS (residual_at's expressions) ...
+#pragma unroll
+        for (int q = 0; q < (B * B * B + NT - 1) / NT; ++q) {
+            const int it = tid + q * NT;
+            if (it < B * B * B) {
+                const int x = it % B, y = (it / B) % B, z = it / (B * B);
+                const int lx = HX + x, ly = E + y, lz = E + z;
+                const int c = (lx & 1) ^ ((ly + lz + p0) & 1);
+                const int mm = lx >> 1, o = lx & 1;
+                const int own = S::lidx(lz, ly, c, mm), oth = S::lidx(lz, ly, c ^ 1, mm);
+                T sum = U[oth - 1 + o] + U[oth + o];
+                sum = sum + U[oth - 2 * EH];
+                sum = sum + U[oth + 2 * EH];
+                sum = sum + U[oth - 2 * EH * EY];
+                sum = sum + U[oth + 2 * EH * EY];
+                const int gi = X0 + x, gj = Y0 + y, gk = gz0 + Z0 + z;
+                const int nb = (gi == 0) + (gi == g.nx - 1) + (gj == 0) + (gj == g.ny - 1) + (gk == 0) + (gk == gnz - 1);
+                RS[it] = op.residual(sum, F[own], U[own], nb);
+            }
+        }
+        __syncthreads();
+        // ... then one coarse cell per thread, children summed in resrestrict_item's order
+        constexpr int C = B / 2;
+        if (tid < C * C * C) {
+            const int I = tid % C, J = (tid / C) % C, K = tid / (C * C);
+            const int r0 = (2 * K * B + 2 * J) * B + 2 * I;
+            T sm = RS[r0] + RS[r0 + 1];
+            sm = sm + RS[r0 + B];
+            sm = sm + RS[r0 + B + 1];
+            sm = sm + RS[r0 + B * B];
+            sm = sm + RS[r0 + B * B + 1];
+            sm = sm + RS[r0 + B * B + B];
+            sm = sm + RS[r0 + B * B + B + 1];
+            R[pidx(gc, (X0 >> 1) + I, (Y0 >> 1) + J, (int64_t)((Z0 >> 1) + K))] = (T)0.125 * sm;
+        }
+    }
+    // the owned cells (both colours) to dst
+    {
+        constexpr int H2 = B / 2, n = B * B * 2 * H2;
+#pragma unroll
+        for (int q = 0; q < (n + NT - 1) / NT; ++q) {
+            const int it = tid + q * NT;
+            if (it < n) {
+                const int mm = it % H2, c = (it / H2) & 1, ly = (it / (2 * H2)) % B, lz = it / (2 * H2 * B);
+                dst[(int64_t)(Z0 + lz) * g.P + c * g.H + (int64_t)(Y0 + ly) * g.hw + (X0 >> 1) + mm] =
+                    U[S::lidx(lz + E, ly + E, c, (HX >> 1) + mm)];
+            }
+        }
+    }
+}
+
 // ---- reductions -----------------------------------------------------------------------------
 
 template <typename T>
@@ -2232,6 +2484,23 @@ hipError_t launch_half_sweep(int rb, int dim, bool fine, int color, const void* 
 }
 
 template <typename T, int D>
+static hipError_t fresh_t(const void* f, void* u, Geo g, double h, double cl, hipStream_t s)
+{
+    const int64_t items = half_items(sizeof(T), g);
+    k_fresh<T, D><<<nblk(items), kBlock, 0, s>>>((const T*)f, (T*)u, g, make_op<T, D>(h, cl));
+    return hipGetLastError();
+}
+
+bool fresh_supported(int rb, const Geo& g) { return half_vector(rb, g); }
+
+hipError_t launch_fresh_sweep(int rb, int dim, const void* f, void* u, Geo g, double h, double cl, hipStream_t s)
+{
+    if (!fresh_supported(rb, g)) return hipErrorInvalidValue;
+    if (rb == 8) return dim == 3 ? fresh_t<double, 3>(f, u, g, h, cl, s) : fresh_t<double, 2>(f, u, g, h, cl, s);
+    return dim == 3 ? fresh_t<float, 3>(f, u, g, h, cl, s) : fresh_t<float, 2>(f, u, g, h, cl, s);
+}
+
+template <typename T, int D>
 static void rr_t(const void* u, const void* f, void* R, Geo g, Geo gc, double h, double cl, hipStream_t s)
 {
     const Op<T, D> op = make_op<T, D>(h, cl);
@@ -2389,6 +2658,9 @@ static hipError_t tail_attr()
     return e;
 }
 
+template <typename T>
+static hipError_t blk_attr();
+
 hipError_t prepare_kernels(int rb)
 {
     hipError_t e = hipSuccess;
@@ -2399,11 +2671,13 @@ hipError_t prepare_kernels(int rb)
         MGP_CHAIN((fused_attr<float, false>()));
         MGP_CHAIN((tail_attr<float, 2>()));
         MGP_CHAIN((tail_attr<float, 3>()));
+        MGP_CHAIN((blk_attr<float>()));
     } else {
         MGP_CHAIN((fused_attr<double, true>()));
         MGP_CHAIN((fused_attr<double, false>()));
         MGP_CHAIN((tail_attr<double, 2>()));
         MGP_CHAIN((tail_attr<double, 3>()));
+        MGP_CHAIN((blk_attr<double>()));
     }
 #undef MGP_CHAIN
     return e;
@@ -2454,6 +2728,69 @@ hipError_t launch_tail(int rb, int dim, const TailSpec& t, hipStream_t s)
     if (t.nlev < 1 || t.nlev > kTailMaxLevels || t.nops > kTailMaxOps) return hipErrorInvalidValue;
     if (rb == 8) return dim == 3 ? tail_t<double, 3>(t, s) : tail_t<double, 2>(t, s);
     return dim == 3 ? tail_t<float, 3>(t, s) : tail_t<float, 2>(t, s);
+}
+
+// ---- 3D-tiled phases of small levels ----
+
+template <typename T, bool PRE, int B, int NS>
+constexpr size_t blk_lds()
+{
+    using S = BlkShape<PRE, B, NS>;
+    return (2 * (size_t)S::cells + (PRE ? (size_t)B * B * B : 0)) * sizeof(T);
+}
+
+// the owned tile edge B: a power of two dividing every axis of the level
+bool block_supported(int rb, int dim, int ns, const Geo& g, int tile)
+{
+    if (dim != 3 || ns < 1 || ns > kBlkMaxSweeps || tile != kBlkTile) return false;
+    if (g.nx < tile || g.ny < tile || g.nz < tile || g.z0 != 0 || g.gnz != g.nz) return false;
+    const size_t lds = rb == 8 ? blk_lds<double, true, kBlkTile, kBlkMaxSweeps>()
+                               : blk_lds<float, true, kBlkTile, kBlkMaxSweeps>();
+    return lds <= kTailMaxLds;
+}
+
+template <typename T, int NS>
+static hipError_t blk_attr_ns()
+{
+    constexpr int B = kBlkTile;
+    const auto A = hipFuncAttributeMaxDynamicSharedMemorySize;
+    hipError_t e = hipFuncSetAttribute((const void*)k_blk<T, true, 0, B, NS>, A, (int)blk_lds<T, true, B, NS>());
+    if (e == hipSuccess) e = hipFuncSetAttribute((const void*)k_blk<T, false, 0, B, NS>, A, (int)blk_lds<T, false, B, NS>());
+    if (e == hipSuccess) e = hipFuncSetAttribute((const void*)k_blk<T, false, 1, B, NS>, A, (int)blk_lds<T, false, B, NS>());
+    return e;
+}
+
+template <typename T>
+static hipError_t blk_attr()
+{
+    hipError_t e = blk_attr_ns<T, 1>();
+    return e == hipSuccess ? blk_attr_ns<T, 2>() : e;
+}
+
+template <typename T, int NS>
+static hipError_t blk_t(const BlockArgs& a, hipStream_t s)
+{
+    constexpr int B = kBlkTile;
+    const Op<T, 3> op = make_op<T, 3>(a.h, a.cl);
+    const unsigned nb = (unsigned)((a.g.nx / B) * (a.g.ny / B) * (a.g.nz / B));
+    const T* src = (const T*)a.src;
+    if (a.pre)
+        k_blk<T, true, 0, B, NS><<<nb, kBlkThreads, blk_lds<T, true, B, NS>(), s>>>(
+            src, (const T*)a.f, (T*)a.dst, (T*)a.R, (const T*)a.V, a.g, a.gc, op, (T)a.clc);
+    else if (a.linear)
+        k_blk<T, false, 1, B, NS><<<nb, kBlkThreads, blk_lds<T, false, B, NS>(), s>>>(
+            src, (const T*)a.f, (T*)a.dst, (T*)a.R, (const T*)a.V, a.g, a.gc, op, (T)a.clc);
+    else
+        k_blk<T, false, 0, B, NS><<<nb, kBlkThreads, blk_lds<T, false, B, NS>(), s>>>(
+            src, (const T*)a.f, (T*)a.dst, (T*)a.R, (const T*)a.V, a.g, a.gc, op, (T)a.clc);
+    return hipGetLastError();
+}
+
+hipError_t launch_block(int rb, const BlockArgs& a, hipStream_t s)
+{
+    if (!block_supported(rb, 3, a.ns, a.g, a.tile)) return hipErrorInvalidValue;
+    if (rb == 8) return a.ns == 1 ? blk_t<double, 1>(a, s) : blk_t<double, 2>(a, s);
+    return a.ns == 1 ? blk_t<float, 1>(a, s) : blk_t<float, 2>(a, s);
 }
 
 hipError_t launch_sqdiff_sum(int rb, const void* a, const void* b, int64_t n, double* partials, double* out,

@@ -81,7 +81,8 @@ class Context:
         for l in range(L.lib.mgp_num_levels(self._h)):
             L.check(L.lib.mgp_level_info(self._h, l, info), self._h)
             self.levels.append(dict(nx=info[0], ny=info[1], nz_global=info[2], nz_local=info[3],
-                                    z0=info[4], distributed=bool(info[5]), tail=bool(info[6]), exchanges=info[7]))
+                                    z0=info[4], distributed=bool(info[5]), tail=info[6] == 1,
+                                    engine=("piece", "tail", "zs", "blk")[info[6]], exchanges=info[7]))
 
     # -- lifecycle --
     def close(self):

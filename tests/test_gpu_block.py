@@ -1,0 +1,136 @@
+"""GPU tests of the 3D-tiled one-launch smoothing phases of small levels (k_blk).
+
+Below ~128^3 a cycle's pieces are launch-bound, so a level's PRE phase (nu1 RB-GS sweeps +
+calcResidual + reduceResidual, cpu.lua:108-135) and POST phase (expandResidual + addTo + nu2 sweeps,
+cpu.lua:142-158) each run as one launch with the tile and its halo in LDS.  The bar is the same as
+for every other engine: psi bit-identical to the C oracle and to one launch per piece (MGP_BLK=0) on
+every level, err to summation order.
+"""
+import numpy as np
+import pytest
+
+from oracle_lib import Oracle
+from test_gpu_parity import _check_err
+
+pytestmark = pytest.mark.gpu
+
+
+def _mg():
+    import mgpoisson
+
+    return mgpoisson
+
+
+def _ctx(**kw):
+    mg = _mg()
+    return mg.Context(mg.make_opts(**kw))
+
+
+BLK_CONFIGS = [
+    # the bench's family: levels 64^3 and 32^3 tiled, 16^3 and below in the coarse tail
+    dict(n=(64, 64, 64), real="float", nu1=2, nu2=2, prolong="linear", coarse_bc="consistent"),
+    dict(n=(128, 128, 128), real="float", nu1=2, nu2=2, prolong="linear", coarse_bc="consistent"),
+    dict(n=(64, 64, 64), real="double", nu1=2, nu2=2, prolong="linear", coarse_bc="consistent", cycle="F"),
+    # non-cubic boxes (tiles clipped per axis), injection, zero coarse boundary, warm coarse guesses
+    dict(n=(128, 64, 32), real="double", nu1=2, nu2=2, prolong="pc", coarse_bc="zero"),
+    dict(n=(32, 64, 128), real="float", nu1=2, nu2=2, prolong="linear", coarse_bc="consistent", coarse_init="warm"),
+    # one sweep per phase / unequal phases
+    dict(n=(64, 64, 64), real="float", nu1=1, nu2=2, prolong="linear", coarse_bc="consistent"),
+    dict(n=(64, 32, 64), real="double", nu1=2, nu2=1, prolong="linear", coarse_bc="consistent", cycle="F"),
+    # no coarse tail: tiled levels down to 4 x 4 x 4 (tiles smaller than the halo, every cell on the box)
+    dict(n=(32, 32, 32), real="float", nu1=2, nu2=2, prolong="linear", coarse_bc="consistent", tail=0),
+    dict(n=(64, 16, 32), real="double", nu1=1, nu2=1, prolong="pc", coarse_bc="consistent", tail=0),
+]
+
+
+def _id(c):
+    return "-".join(f"{k}{v}" for k, v in c.items()).replace(" ", "").replace("(", "").replace(")", "").replace(",", "x")
+
+
+@pytest.mark.parametrize("cfg", BLK_CONFIGS, ids=_id)
+def test_block_phases_match_oracle(cfg, monkeypatch):
+    cfg = dict(cfg)
+    tail = cfg.pop("tail", 1)
+    kw = dict(dim=3, smoother="rbgs", **cfg)
+    if not tail:
+        monkeypatch.setenv("MGP_TAIL", "0")
+    monkeypatch.setenv("MGP_BLK", "1")
+    a = _ctx(**kw)
+    monkeypatch.setenv("MGP_BLK", "0")
+    b = _ctx(**kw)
+    assert any(lv["engine"] == "blk" for lv in a.levels), a.levels
+    assert not any(lv["engine"] == "blk" for lv in b.levels)
+    assert a.levels[0]["engine"] != "blk"
+    o = Oracle(threads=8, **kw)
+    for x in (a, b, o):
+        x.init_point_charge()
+    for it in range(3):
+        old = o.get(0)
+        ea, eb, eo = a.cycle(), b.cycle(), o.step()
+        new = o.get(0)
+        assert np.array_equal(a.get_psi(), new), f"tiled psi differs from the oracle after cycle {it + 1}"
+        assert np.array_equal(b.get_psi(), new), f"per-piece psi differs from the oracle after cycle {it + 1}"
+        _check_err(ea, eo, new, old)
+        assert abs(ea - eb) <= 1e-12 * abs(eb)
+    for level in range(len(a.levels)):
+        assert np.array_equal(a.get_psi(level), b.get_psi(level)), f"psi level {level}"
+        assert np.array_equal(a.get_f(level), b.get_f(level)), f"f level {level}"
+
+
+def test_block_graph_replay_equals_eager(monkeypatch):
+    """The tiled phases swap u / t per phase: graph replay (cached per pointer state) == eager."""
+    kw = dict(dim=3, n=(128, 128, 128), real="float", smoother="rbgs", nu1=2, nu2=2, prolong="linear",
+              coarse_bc="consistent", cycle="F")
+    g = _ctx(**kw)
+    monkeypatch.setenv("MGP_GRAPH", "0")
+    e = _ctx(**kw)
+    assert [lv["engine"] for lv in g.levels][1:3] == ["blk", "blk"]
+    g.init_point_charge()
+    e.init_point_charge()
+    eg = np.concatenate([g.cycles(3), g.cycles(4)])
+    ee = np.concatenate([e.cycles(3), e.cycles(4)])
+    assert np.array_equal(g.get_psi(), e.get_psi())
+    assert np.array_equal(eg, ee)
+
+
+def test_block_levels_of_the_bench_config():
+    """512^3 fp32 RB-GS 2+2: level 0 temporally blocked, 256^3 and 128^3 per piece, 64^3 and 32^3 tiled, then
+    the tail."""
+    ctx = _ctx(dim=3, n=(512, 512, 512), real="float", smoother="rbgs", nu1=2, nu2=2, prolong="linear",
+               coarse_bc="consistent")
+    eng = [lv["engine"] for lv in ctx.levels]
+    assert eng[:5] == ["zs", "piece", "piece", "blk", "blk"] and eng[5] == "tail", eng
+
+
+FRESH_CONFIGS = [
+    dict(dim=3, n=(64, 64, 64), real="double", nu1=2, nu2=2, prolong="linear", coarse_bc="consistent"),
+    dict(dim=3, n=(128, 64, 32), real="float", nu1=2, nu2=2, prolong="pc", coarse_bc="zero", cycle="F"),
+    dict(dim=3, n=(32, 64, 128), real="float", nu1=1, nu2=2, prolong="linear", coarse_bc="consistent"),
+    dict(dim=2, n=(256, 256, 1), real="double", nu1=2, nu2=2, prolong="linear", coarse_bc="consistent", cycle="F"),
+    dict(dim=2, n=(128, 128, 1), real="float", nu1=1, nu2=1, prolong="pc", coarse_bc="zero"),
+]
+
+
+@pytest.mark.parametrize("cfg", FRESH_CONFIGS, ids=_id)
+def test_fresh_first_sweep_matches_oracle(cfg, monkeypatch):
+    """k_fresh (the first RB-GS sweep of a fresh coarse guess from f alone, cpu.lua:138) == the two
+    half-sweeps reading a zero black input == the oracle, on every level (tiled phases off, so every
+    level above the tail sweeps per piece)."""
+    kw = dict(smoother="rbgs", **cfg)
+    monkeypatch.setenv("MGP_BLK", "0")
+    monkeypatch.setenv("MGP_FRESH", "1")
+    a = _ctx(**kw)
+    monkeypatch.setenv("MGP_FRESH", "0")
+    b = _ctx(**kw)
+    o = Oracle(threads=8, **kw)
+    for x in (a, b, o):
+        x.init_point_charge()
+    for it in range(3):
+        old = o.get(0)
+        ea, eb, eo = a.cycle(), b.cycle(), o.step()
+        new = o.get(0)
+        assert np.array_equal(a.get_psi(), new), f"psi differs from the oracle after cycle {it + 1}"
+        assert np.array_equal(b.get_psi(), new)
+        _check_err(ea, eo, new, old)
+    for level in range(len(a.levels)):
+        assert np.array_equal(a.get_psi(level), b.get_psi(level)), f"psi level {level}"
