@@ -156,6 +156,7 @@ struct mgp_ctx {
     bool deep_halo = true;  // smooth_deep on distributed levels below the finest
     int blk_tile = mgp::kBlkTile;  // k_blk owned tile edge
     bool fresh_sweep = true;        // k_fresh for the first sweep of a lazily zeroed level (MGP_FRESH=0: off)
+    bool lazy_zero = true;          // fresh coarse guesses without a memset where a reader can take it (MGP_LAZY_ZERO=0: off)
     std::vector<Level> lev;
     hipStream_t s = nullptr;
     int device = 0;
@@ -189,7 +190,7 @@ struct mgp_ctx {
     bool first_done = false;
     bool err_done = false;
     // hipGraph replay of whole cycles (single GPU): one instantiated graph per pointer state of
-    // the level buffers (the finest level alternates u/t every cycle), err written to d_err_cur
+    // the level buffers (the finest level alternates u/t every cycle), err written to d_errs[*d_slot]
     struct GraphEntry {
         std::vector<char*> pre, post;
         hipGraphExec_t exec = nullptr;
@@ -207,6 +208,8 @@ struct mgp_ctx {
     std::vector<char> hbuf_u, hbuf_f;
     double* d_err_cur = nullptr;
     double* err_dst = nullptr;  // where this cycle's sum of squares goes
+    int* err_ctr = nullptr;     // when set: err_dst[*err_ctr], advanced on the device (mgp_cycles on one GPU)
+    int* d_slot = nullptr;      // that device counter
     std::string err;
     // finest-level kernel timing: event pairs around level-0 launches of each timed kind
     bool timing = false;
@@ -505,6 +508,9 @@ int smooth(mgp_ctx* c, int l, int sweeps, double h, bool want_err = false)
     Level& L = c->lev[l];
     const double cl = coarse_coef(c->o.coarse_bc, l);
     if (deep_halo_ok(c, L, sweeps, want_err)) return smooth_deep(c, l, sweeps, h);
+    // a pending zero that no zero-aware path below can read (the tail level swept outside the tail)
+    if (L.zero_pending && (c->o.smoother != MGP_RBGS || !c->zbuf || L.alloc > c->zbuf_reals))
+        TRY(materialize_zero(c, L));
     for (int sw = 0; sw < sweeps; ++sw) {
         if (c->o.smoother == MGP_JACOBI) {
             // both colours from the old iterate into t, then swap (no copy back, cf. gpu.lua:292)
@@ -544,7 +550,7 @@ int smooth(mgp_ctx* c, int l, int sweeps, double h, bool want_err = false)
         L.ghost_ok = !L.p.dist;
         L.ghost_zero = false;
         if (last_err) {
-            HIP_TRY(c, mgp::launch_sum_partials(c->d_part, 2 * nb, c->err_dst, c->s));
+            HIP_TRY(c, mgp::launch_sum_partials(c->d_part, 2 * nb, c->err_dst, c->s, c->err_ctr));
             c->err_done = true;
         }
     }
@@ -616,9 +622,10 @@ int coarse_solve_at(mgp_ctx* c, int l, double h)
 bool lazy_zero_ok(const mgp_ctx* c, const Level& L)
 {
     const int l = (int)(&L - c->lev.data());
+    if (l == c->handoff_level || !c->lazy_zero) return false;
+    if (l == c->tail_level) return true;  // run_tail loads it as zeros (any smoother)
     const bool sweeps_first = c->o.nu1 >= 1 || l == (int)c->lev.size() - 1;
-    return c->zbuf && sweeps_first && c->o.smoother == MGP_RBGS && !L.fused && l != c->tail_level &&
-           l != c->handoff_level && L.alloc <= c->zbuf_reals;
+    return c->zbuf && sweeps_first && c->o.smoother == MGP_RBGS && !L.fused && L.alloc <= c->zbuf_reals;
 }
 
 int zero_level(mgp_ctx* c, Level& L)
@@ -731,7 +738,8 @@ int fused_post(mgp_ctx* c, int l, double h, bool want_err)
     L.ghost_ok = !L.p.dist;
     L.ghost_zero = false;
     if (want_err) {
-        HIP_TRY(c, mgp::launch_sum_partials(c->d_part, mgp::fused_blocks(c->rb, L.g, L.zc), c->err_dst, c->s));
+        HIP_TRY(c, mgp::launch_sum_partials(c->d_part, mgp::fused_blocks(c->rb, L.g, L.zc), c->err_dst, c->s,
+                                            c->err_ctr));
         c->err_done = true;
     }
     return MGP_OK;
@@ -895,6 +903,8 @@ int run_tail(mgp_ctx* c, bool fcycle)
         L.ghost_ok = true;
         L.ghost_zero = false;
     }
+    t.zero_first = c->lev[T].zero_pending;
+    c->lev[T].zero_pending = false;
     const std::vector<uint32_t>& p = fcycle ? c->tail_f : c->tail_v;
     t.nops = (int)p.size();
     std::copy(p.begin(), p.end(), t.ops);
@@ -966,8 +976,8 @@ int one_cycle(mgp_ctx* c, double* dst)
     if (fuse && !c->err_done) return c->fail(MGP_ERR_STATE, "internal: fused err launch did not run");
     if (c->o.err_mode && !fuse) {
         Level& L0 = c->lev[0];
-        HIP_TRY(c, mgp::launch_sqdiff_sum(c->rb, c->ui(L0, L0.u), c->psi_old, L0.g.P * L0.g.nz, c->d_part, dst,
-                                          c->s));
+        HIP_TRY(c, mgp::launch_sqdiff_sum(c->rb, c->ui(L0, L0.u), c->psi_old, L0.g.P * L0.g.nz, c->d_part, dst, c->s,
+                                          c->err_ctr));
     }
     if (c->o.err_mode && c->o.world > 1) {
         if (c->lb)
@@ -1005,9 +1015,9 @@ int graph_cycle(mgp_ctx* c, int slot)
     for (auto& e : c->graphs)
         if (e.pre == pre) hit = &e;
     if (!hit) {
-        if (c->graphs.size() >= 8) return one_cycle(c, c->d_errs + slot);  // unusual state churn: eager
+        if (c->graphs.size() >= 8) return one_cycle(c, c->d_errs);  // unusual state churn: eager
         HIP_TRY(c, hipStreamBeginCapture(c->s, hipStreamCaptureModeThreadLocal));
-        const int rc = one_cycle(c, c->d_err_cur);
+        const int rc = one_cycle(c, c->d_errs);  // err into d_errs[*d_slot] (mgp_cycles set err_ctr)
         hipGraph_t graph = nullptr;
         const hipError_t ec = hipStreamEndCapture(c->s, &graph);
         if (rc != MGP_OK) {
@@ -1028,14 +1038,14 @@ int graph_cycle(mgp_ctx* c, int slot)
     set_level_state(c, hit->post);
     update_metrics_old(c);
     HIP_TRY(c, hipGraphLaunch(hit->exec, c->s));
-    if (c->o.err_mode)
-        HIP_TRY(c, hipMemcpyAsync(c->d_errs + slot, c->d_err_cur, sizeof(double), hipMemcpyDeviceToDevice, c->s));
+    (void)slot;
     return MGP_OK;
 }
 
 int ensure_errs(mgp_ctx* c, int k)
 {
     if (k <= c->errs_cap) return MGP_OK;
+    drop_graphs(c);  // captured graphs write into d_errs
     if (c->d_errs) HIP_TRY(c, hipFree(c->d_errs));
     c->d_errs = nullptr;
     int cap = std::max(k, 64);
@@ -1144,6 +1154,7 @@ static void destroy_impl(mgp_ctx* c)
     if (c->d_part) (void)hipFree(c->d_part);
     if (c->d_errs) (void)hipFree(c->d_errs);
     if (c->d_err_cur) (void)hipFree(c->d_err_cur);
+    if (c->d_slot) (void)hipFree(c->d_slot);
     for (auto& g : c->graphs) (void)hipGraphExecDestroy(g.exec);
     for (auto e : c->ev) (void)hipEventDestroy(e);
     if (c->comm) (void)ncclCommDestroy(c->comm);
@@ -1326,7 +1337,8 @@ static int create_impl(mgp_ctx** out, const mgp_opts* o, mgp_loopback* lb, ncclC
         c->err = "hipMalloc failed for reduction partials";
         return bail(MGP_ERR_OOM);
     }
-    if (ensure_errs(c, 64) != MGP_OK || hipMalloc(&c->d_err_cur, sizeof(double)) != hipSuccess) {
+    if (ensure_errs(c, 64) != MGP_OK || hipMalloc(&c->d_err_cur, sizeof(double)) != hipSuccess ||
+        hipMalloc(&c->d_slot, sizeof(int)) != hipSuccess) {
         c->err = "hipMalloc failed for err slots";
         return bail(MGP_ERR_OOM);
     }
@@ -1345,7 +1357,7 @@ static int create_impl(mgp_ctx** out, const mgp_opts* o, mgp_loopback* lb, ncclC
             return bail(MGP_ERR_OOM);
         }
         const char* v = std::getenv("MGP_LAZY_ZERO");  // 0: memset every fresh coarse guess instead
-        if (v && std::atoi(v) == 0) c->zbuf_reals = 0;
+        if (v && std::atoi(v) == 0) c->lazy_zero = false;
     }
     he = mgp::prepare_kernels(c->rb);
     if (he != hipSuccess) {
@@ -1608,7 +1620,16 @@ int mgp_cycles(mgp_ctx* c, int32_t k, double* errs)
     if (!c || k < 0) return MGP_ERR_ARG;
     TRY(ensure_errs(c, k));
     const bool graph = c->use_graph && !c->timing && !c->handoff_fn;
-    for (int i = 0; i < k; ++i) TRY(graph ? graph_cycle(c, i) : one_cycle(c, c->d_errs + i));
+    // one GPU: every cycle's err goes to d_errs[*d_slot] and advances the device counter (graph replays
+    // need no per-cycle copy); with ranks the all-reduce needs the slot's address, so it is explicit
+    const bool ctr = c->o.world == 1 && c->o.err_mode && k > 0;
+    if (ctr) HIP_TRY(c, hipMemsetAsync(c->d_slot, 0, sizeof(int), c->s));
+    c->err_ctr = ctr ? c->d_slot : nullptr;
+    int rc = MGP_OK;
+    for (int i = 0; i < k && rc == MGP_OK; ++i)
+        rc = graph ? graph_cycle(c, i) : one_cycle(c, ctr ? c->d_errs : c->d_errs + i);
+    c->err_ctr = nullptr;
+    TRY(rc);
     TRY(sync_and_check(c));
     if (errs) {
         if (!c->o.err_mode) {

@@ -73,9 +73,10 @@ hipError_t launch_residual_restrict(int rb, int dim, const void* u, const void* 
 // this rank's fine plane 0; planes -1 and gc.nz of V must be readable for the linear kind.
 hipError_t launch_prolong_correct(int rb, int dim, int linear, void* u, const void* V, Geo g, Geo gc, double clc,
                                   hipStream_t s);
-// Deterministic two-pass fp64 sum of (a - b)^2 over n elements into *out.
+// Deterministic two-pass fp64 sum of (a - b)^2 over n elements into *out (ctr != nullptr: into
+// out[*ctr], then ++*ctr on the device).
 hipError_t launch_sqdiff_sum(int rb, const void* a, const void* b, int64_t n, double* partials, double* out,
-                             hipStream_t s);
+                             hipStream_t s, int* ctr = nullptr);
 // out[0..2] = {sum |1 - psi/psiOld| over nonzero entries, their count, sum (psi - psiOld)^2}
 // over n elements; partials needs 3 * kSumBlocks doubles.
 hipError_t launch_metrics(int rb, const void* psi, const void* old, int64_t n, double* partials, double* out,
@@ -88,7 +89,7 @@ hipError_t launch_residual_norm(int rb, int dim, const void* u, const void* f, G
 // Fixed-order fp64 sum of n partials into *out.  Needs sum_scratch(n) doubles of scratch right
 // after partials[n - 1].
 int sum_scratch(int n);
-hipError_t launch_sum_partials(const double* partials, int n, double* out, hipStream_t s);
+hipError_t launch_sum_partials(const double* partials, int n, double* out, hipStream_t s, int* ctr = nullptr);
 
 // Temporally blocked smoothing phases of a replicated 3D red/black level (ns = 2 sweeps):
 //   pre : dst = nu1 sweeps of src; R (coarse packed, Geo gc) = restrict(residual(dst))
@@ -146,6 +147,7 @@ constexpr size_t kTailMaxLds = 160 * 1024;  // gfx950 LDS per workgroup
 enum TailOp { TAIL_SMOOTH = 1, TAIL_RR = 2, TAIL_ZERO = 3, TAIL_PROLONG = 4 };
 struct TailSpec {
     int nlev, nops, jacobi, linear;
+    int zero_first;  // the first level's u is logically 0 (a fresh guess): loaded as zeros
     void* u[kTailMaxLevels];  // interior plane 0 of each level's u / f (global)
     void* f[kTailMaxLevels];
     Geo g[kTailMaxLevels];

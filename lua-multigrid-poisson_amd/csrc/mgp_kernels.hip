@@ -1944,7 +1944,7 @@ constexpr int tail_threads() { return sizeof(T) == 4 ? TAIL_THREADS_F32 : 512; }
 
 template <typename T, int DIM>
 struct TailArgs {
-    int nlev, nops, jacobi, pad;
+    int nlev, nops, jacobi, zero0;  // zero0: level 0's u is a fresh zero guess (not read)
     int64_t off[kTailMaxLevels];     // element offset of the level's LDS region
     int64_t region[kTailMaxLevels];  // elements of one LDS array of the level (ghost planes included)
     T* u[kTailMaxLevels];            // global interior plane 0 of u / f
@@ -1972,7 +1972,7 @@ __global__ __launch_bounds__(tail_threads<T>()) void k_tail(const TailArgs<T, DI
         for (int64_t e = tid; e < a.region[l]; e += kTailThreads) {
             const int64_t ie = e - lo;
             const bool in = ie >= 0 && ie < n;
-            U[e] = in ? a.u[l][ie] : (T)0;
+            U[e] = in && !(l == 0 && a.zero0) ? a.u[l][ie] : (T)0;
             F[e] = in ? a.f[l][ie] : (T)0;
             if (a.jacobi) U[e + 2 * a.region[l]] = (T)0;
         }
@@ -2288,7 +2288,10 @@ __global__ __launch_bounds__(1024) void k_sum_chunks(const double* __restrict__ 
     if (threadIdx.x == 0) out[blockIdx.x] = sh[0];
 }
 
-__global__ __launch_bounds__(1024) void k_sum_n(const double* __restrict__ partials, int n, double* __restrict__ out)
+// ctr != nullptr: the result goes to out[*ctr] and *ctr advances (a replayed graph fills consecutive
+// err slots without a per-cycle copy)
+__global__ __launch_bounds__(1024) void k_sum_n(const double* __restrict__ partials, int n, double* __restrict__ out,
+                                                int* __restrict__ ctr = nullptr)
 {
     __shared__ double sh[1024];
     double a = 0.0;
@@ -2299,7 +2302,15 @@ __global__ __launch_bounds__(1024) void k_sum_n(const double* __restrict__ parti
         if ((int)threadIdx.x < w) sh[threadIdx.x] += sh[threadIdx.x + w];
         __syncthreads();
     }
-    if (threadIdx.x == 0) *out = sh[0];
+    if (threadIdx.x == 0) {
+        if (ctr) {
+            const int k = *ctr;
+            out[k] = sh[0];
+            *ctr = k + 1;
+        } else {
+            *out = sh[0];
+        }
+    }
 }
 
 template <typename T>
@@ -2705,6 +2716,7 @@ static hipError_t tail_t(const TailSpec& t, hipStream_t s)
     a.nlev = t.nlev;
     a.nops = t.nops;
     a.jacobi = t.jacobi;
+    a.zero0 = t.zero_first;
     const int G = D == 3 ? kGhost3D : 0;
     int64_t off = 0;
     for (int l = 0; l < t.nlev; ++l) {
@@ -2794,10 +2806,10 @@ hipError_t launch_block(int rb, const BlockArgs& a, hipStream_t s)
 }
 
 hipError_t launch_sqdiff_sum(int rb, const void* a, const void* b, int64_t n, double* partials, double* out,
-                             hipStream_t s)
+                             hipStream_t s, int* ctr)
 {
     MGP_REAL(rb, (k_sqdiff_partial<T><<<kSumBlocks, kBlock, 0, s>>>((const T*)a, (const T*)b, n, partials)));
-    k_sum_n<<<1, 1024, 0, s>>>(partials, kSumBlocks, out);
+    k_sum_n<<<1, 1024, 0, s>>>(partials, kSumBlocks, out, ctr);
     return hipGetLastError();
 }
 
@@ -2811,16 +2823,16 @@ hipError_t launch_metrics(int rb, const void* psi, const void* old, int64_t n, d
 
 int sum_scratch(int n) { return n <= 8192 ? 0 : (n + 8191) / 8192; }
 
-hipError_t launch_sum_partials(const double* partials, int n, double* out, hipStream_t s)
+hipError_t launch_sum_partials(const double* partials, int n, double* out, hipStream_t s, int* ctr)
 {
     const int nb = sum_scratch(n);
     if (nb == 0) {
-        k_sum_n<<<1, 1024, 0, s>>>(partials, n, out);
+        k_sum_n<<<1, 1024, 0, s>>>(partials, n, out, ctr);
     } else {
         // two fixed-order levels; the first level's sums go right after the partials
         double* mid = const_cast<double*>(partials) + n;
         k_sum_chunks<<<nb, 1024, 0, s>>>(partials, n, 8192, mid);
-        k_sum_n<<<1, 1024, 0, s>>>(mid, nb, out);
+        k_sum_n<<<1, 1024, 0, s>>>(mid, nb, out, ctr);
     }
     return hipGetLastError();
 }
