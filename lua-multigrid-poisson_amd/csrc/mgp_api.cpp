@@ -154,7 +154,6 @@ struct mgp_ctx {
     int rb = 8;
     int G = 0;  // ghost planes per side (kGhost3D in 3D, 0 in 2D; kGhostZs for distributed 3D)
     bool deep_halo = true;  // smooth_deep on distributed levels below the finest
-    int blk_tile = mgp::kBlkTile;  // k_blk owned tile edge
     bool fresh_sweep = true;        // k_fresh for the first sweep of a lazily zeroed level (MGP_FRESH=0: off)
     bool lazy_zero = true;          // fresh coarse guesses without a memset where a reader can take it (MGP_LAZY_ZERO=0: off)
     std::vector<Level> lev;
@@ -755,7 +754,6 @@ int block_pre(mgp_ctx* c, int l, double h)
     mgp::BlockArgs a{};
     a.pre = true;
     a.ns = c->o.nu1;
-    a.tile = c->blk_tile;
     a.src = L.zero_pending ? nullptr : c->ui(L, L.u);
     a.f = c->ui(L, L.f);
     a.dst = c->ui(L, L.t);
@@ -764,7 +762,7 @@ int block_pre(mgp_ctx* c, int l, double h)
     a.R = c->ui(C, C.f) + (size_t)(zc * C.g.P) * c->rb;
     a.h = h;
     a.cl = coarse_coef(c->o.coarse_bc, l);
-    HIP_TRY(c, mgp::launch_block(c->rb, a, c->s));
+    HIP_TRY(c, mgp::launch_block(c->rb, c->o.dim, a, c->s));
     L.zero_pending = false;
     std::swap(L.u, L.t);
     L.ghost_ok = true;
@@ -785,7 +783,6 @@ int block_post(mgp_ctx* c, int l, double h)
     a.pre = false;
     a.linear = c->o.prolong == MGP_PROLONG_LINEAR;
     a.ns = c->o.nu2;
-    a.tile = c->blk_tile;
     a.src = c->ui(L, L.u);
     a.f = c->ui(L, L.f);
     a.dst = c->ui(L, L.t);
@@ -795,7 +792,7 @@ int block_post(mgp_ctx* c, int l, double h)
     a.h = h;
     a.cl = coarse_coef(c->o.coarse_bc, l);
     a.clc = coarse_coef(c->o.coarse_bc, l + 1);
-    HIP_TRY(c, mgp::launch_block(c->rb, a, c->s));
+    HIP_TRY(c, mgp::launch_block(c->rb, c->o.dim, a, c->s));
     std::swap(L.u, L.t);
     L.ghost_ok = true;
     L.ghost_zero = false;
@@ -1289,7 +1286,7 @@ static int create_impl(mgp_ctx** out, const mgp_opts* o, mgp_loopback* lb, ncclC
         for (size_t l = 1; l + 1 < c->lev.size(); ++l) {
             Level& L = c->lev[l];
             L.blk = on && !L.fused && !L.p.dist && level_cells(L) <= max_cells &&
-                    mgp::block_supported(c->rb, c->o.dim, ns, L.g, c->blk_tile);
+                    mgp::block_supported(c->rb, c->o.dim, ns, L.g);
         }
     }
     for (auto& L : c->lev) L.alloc = L.g.P * (L.g.nz + 2 * c->G);

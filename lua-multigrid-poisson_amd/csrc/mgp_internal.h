@@ -116,18 +116,18 @@ int fused_zc(int rb, const Geo& g, bool pre);
 int fused_blocks(int rb, const Geo& g, int zc);
 hipError_t launch_fused(int rb, const FusedArgs& a, hipStream_t s);
 
-// 3D-tiled smoothing phases of a small replicated 3D red/black level (k_blk: one launch per phase,
-// the tile and its halo in LDS):
+// Tiled smoothing phases of a small replicated red/black level (k_blk: one launch per phase, the 3D
+// or 2D tile and its halo in LDS):
 //   pre : dst = ns sweeps of src; R (coarse packed, Geo gc) = restrict(residual(dst))
 //   post: dst = ns sweeps of (src + P V)
 // src == nullptr reads u = 0 (a fresh coarse guess).  src != dst.
 constexpr int kBlkMaxSweeps = 2;
-constexpr int kBlkTile = 8;  // owned tile edge (every axis of a tiled level is a multiple)
+constexpr int kBlkTile = 8;     // 3D owned tile edge (every axis of a tiled level is a multiple)
+constexpr int kBlkTile2D = 32;  // 2D owned tile edge
 struct BlockArgs {
     bool pre;
     int linear;
     int ns;
-    int tile;  // owned tile edge (kBlkTile)
     const void* src;
     const void* f;
     void* dst;
@@ -136,8 +136,8 @@ struct BlockArgs {
     Geo g, gc;
     double h, cl, clc;
 };
-bool block_supported(int rb, int dim, int ns, const Geo& g, int tile);
-hipError_t launch_block(int rb, const BlockArgs& a, hipStream_t s);
+bool block_supported(int rb, int dim, int ns, const Geo& g);
+hipError_t launch_block(int rb, int dim, const BlockArgs& a, hipStream_t s);
 
 // Coarse-level tail: the sub-cycle below one level as a single one-workgroup launch with every
 // level in LDS.  ops[] = (op | level << 4 | arg << 8), levels relative to the tail's first level.

@@ -2074,26 +2074,32 @@ __global__ __launch_bounds__(tail_threads<T>()) void k_tail(const TailArgs<T, DI
 // bit-identical to the launch-per-piece path and to the oracle.  src == nullptr: u = 0 (a fresh
 // coarse guess, cpu.lua:138, without the memset).  src and dst are different buffers.
 
-constexpr int kBlkThreads = 1024;  // 16 waves: the levels are small, so a workgroup is most of a CU
+// 3D: 16 waves (the levels are small, so a workgroup is most of a CU); 2D tiles are 32 x 32
+template <int DIM>
+constexpr int blk_threads() { return DIM == 3 ? 1024 : 256; }
 
-// Compile-time shape of a phase: owned B^3 tile, halo E (y, z) and HX (x, even), NS sweeps.
-template <bool PRE, int B, int NS>
+// Compile-time shape of a phase: owned B^DIM tile, halo E (y, z) and HX (x, even), NS sweeps.
+template <int DIM, bool PRE, int B, int NS>
 struct BlkShape {
     static constexpr int E = PRE ? 2 * NS + 1 : 2 * NS;
     static constexpr int HX = (E + 1) & ~1;
-    static constexpr int EX = B + 2 * HX, EY = B + 2 * E, EZ = B + 2 * E, EH = EX / 2;
+    static constexpr int EX = B + 2 * HX, EY = B + 2 * E, EZ = DIM == 3 ? B + 2 * E : 1, EH = EX / 2;
+    static constexpr int BZ = DIM == 3 ? B : 1;  // owned planes
     static constexpr int cells = EX * EY * EZ;
+    static constexpr int owned = B * B * BZ;
     static constexpr int lidx(int lz, int ly, int c, int mm) { return ((lz * EY + ly) * 2 + c) * EH + mm; }
 };
 
-template <typename T, bool PRE, int LINEAR, int B, int NS>
-__global__ __launch_bounds__(kBlkThreads) void k_blk(const T* __restrict__ src, const T* __restrict__ f,
-                                                     T* __restrict__ dst, T* __restrict__ R, const T* __restrict__ V,
-                                                     Geo g, Geo gc, Op<T, 3> op, T clc)
+template <typename T, int DIM, bool PRE, int LINEAR, int B, int NS>
+__global__ __launch_bounds__(blk_threads<DIM>()) void k_blk(const T* __restrict__ src, const T* __restrict__ f,
+                                                            T* __restrict__ dst, T* __restrict__ R,
+                                                            const T* __restrict__ V, Geo g, Geo gc, Op<T, DIM> op,
+                                                            T clc)
 {
-    using S = BlkShape<PRE, B, NS>;
-    constexpr int E = S::E, HX = S::HX, EY = S::EY, EZ = S::EZ, EH = S::EH;
-    constexpr int NT = kBlkThreads;
+    using S = BlkShape<DIM, PRE, B, NS>;
+    constexpr int E = S::E, HX = S::HX, EY = S::EY, EZ = S::EZ, EH = S::EH, BZ = S::BZ;
+    constexpr int EZH = DIM == 3 ? E : 0;  // z halo
+    constexpr int NT = blk_threads<DIM>();
     extern __shared__ __align__(16) unsigned char blk_smem[];
     T* const U = reinterpret_cast<T*>(blk_smem);
     T* const F = U + S::cells;
@@ -2101,11 +2107,14 @@ __global__ __launch_bounds__(kBlkThreads) void k_blk(const T* __restrict__ src, 
     const int tid = threadIdx.x;
     const int ntx = g.nx / B, nty = g.ny / B;
     const int b = blockIdx.x;
-    const int X0 = (b % ntx) * B, Y0 = ((b / ntx) % nty) * B, Z0 = (b / (ntx * nty)) * B;
-    const int xs = X0 - HX, ys = Y0 - E, zs = Z0 - E;  // global (local-plane) origin of the LDS box
-    const int mxs = xs >> 1;                           // xs is even
+    const int X0 = (b % ntx) * B, Y0 = ((b / ntx) % nty) * B, Z0 = (b / (ntx * nty)) * BZ;
+    const int xs = X0 - HX, ys = Y0 - E, zs = Z0 - EZH;  // global (local-plane) origin of the LDS box
+    const int mxs = xs >> 1;                            // xs is even
     const int nzl = (int)g.nz, gnz = (int)g.gnz, gz0 = (int)g.z0;
-    const int p0 = (ys + zs + gz0) & 1;                // parity of LDS row (0, 0)
+    const int p0 = (ys + zs + gz0) & 1;                 // parity of LDS row (0, 0)
+    auto faces = [&](int gi, int gj, int gk) {          // box faces of a cell (gk global)
+        return (gi == 0) + (gi == g.nx - 1) + (gj == 0) + (gj == g.ny - 1) + (DIM == 3 ? (gk == 0) + (gk == gnz - 1) : 0);
+    };
 
     // load: every LDS slot of both colours (u: black cells in the box, 0 elsewhere; f: cells in the
     // box), all of a thread's global loads in flight at once
@@ -2126,7 +2135,7 @@ __global__ __launch_bounds__(kBlkThreads) void k_blk(const T* __restrict__ src, 
             uv[q] = in && c == 1 && src ? src[gi] : (T)0;
             if (!PRE && in && c == 1) {
                 const int i = 2 * gm + (1 ^ ((ly + lz + p0) & 1));
-                uv[q] = uv[q] + prolong_value<T, 3, LINEAR>(V, g, gc, clc, i, gj, (int64_t)gk);
+                uv[q] = uv[q] + prolong_value<T, DIM, LINEAR>(V, g, gc, clc, i, gj, (int64_t)gk);
             }
         }
 #pragma unroll
@@ -2140,34 +2149,42 @@ __global__ __launch_bounds__(kBlkThreads) void k_blk(const T* __restrict__ src, 
     }
     __syncthreads();
 
+    // in-plane and z neighbour sum of LDS cell (lx, ly, lz) of colour c: half_item's order
+    auto nbsum = [&](int lx, int ly, int lz, int c) {
+        const int mm = lx >> 1, o = lx & 1;
+        const int oth = S::lidx(lz, ly, c ^ 1, mm);
+        T sum = U[oth - 1 + o] + U[oth + o];
+        sum = sum + U[oth - 2 * EH];
+        sum = sum + U[oth + 2 * EH];
+        if (DIM == 3) {
+            sum = sum + U[oth - 2 * EH * EY];
+            sum = sum + U[oth + 2 * EH * EY];
+        }
+        return sum;
+    };
+
     // half-sweeps: colour s & 1 (red first) on the tile extended by e = E - 1 - s cells (cells
-    // outside the box are skipped: they stay 0); half_item's expressions
+    // outside the box are skipped: they stay 0)
 #pragma unroll
     for (int s = 0; s < 2 * NS; ++s) {
         const int c = s & 1, e = E - 1 - s;
         const int xlo = HX - e, xhi = HX + B - 1 + e;
         const int mlo = xlo >> 1, nm = (xhi >> 1) - mlo + 1;
-        const int ny = B + 2 * e, n = ny * ny * nm;
+        const int ny = B + 2 * e, nz = DIM == 3 ? B + 2 * e : 1, n = nz * ny * nm;
+        const int lz0 = DIM == 3 ? E - e : 0;
 #pragma unroll
         for (int q = 0; q < (n + NT - 1) / NT; ++q) {
             const int it = tid + q * NT;
             const int row = it / nm, mm = mlo + it % nm;
-            const int ly = E - e + row % ny, lz = E - e + row / ny;
+            const int ly = E - e + row % ny, lz = lz0 + row / ny;
             const int o = c ^ ((ly + lz + p0) & 1);
             const int lx = 2 * mm + o;
             const int gi = xs + lx, gj = ys + ly, gkl = zs + lz;
             if (it < n && lx >= xlo && lx <= xhi && gi >= 0 && gi < g.nx && gj >= 0 && gj < g.ny && gkl >= 0 &&
                 gkl < nzl) {
-                const int oth = S::lidx(lz, ly, c ^ 1, mm);
-                T sum = U[oth - 1 + o] + U[oth + o];
-                sum = sum + U[oth - 2 * EH];
-                sum = sum + U[oth + 2 * EH];
-                sum = sum + U[oth - 2 * EH * EY];
-                sum = sum + U[oth + 2 * EH * EY];
-                const int gk = gz0 + gkl;
-                const int nb = (gi == 0) + (gi == g.nx - 1) + (gj == 0) + (gj == g.ny - 1) + (gk == 0) + (gk == gnz - 1);
+                const T sum = nbsum(lx, ly, lz, c);
                 const int own = S::lidx(lz, ly, c, mm);
-                U[own] = op.relax(sum, F[own], nb);
+                U[own] = op.relax(sum, F[own], faces(gi, gj, gz0 + gkl));
             }
         }
         __syncthreads();
@@ -2176,50 +2193,45 @@ __global__ __launch_bounds__(kBlkThreads) void k_blk(const T* __restrict__ src, 
     if (PRE) {
         // residual of every owned cell into RS (residual_at's expressions) ...
 #pragma unroll
-        for (int q = 0; q < (B * B * B + NT - 1) / NT; ++q) {
+        for (int q = 0; q < (S::owned + NT - 1) / NT; ++q) {
             const int it = tid + q * NT;
-            if (it < B * B * B) {
+            if (it < S::owned) {
                 const int x = it % B, y = (it / B) % B, z = it / (B * B);
-                const int lx = HX + x, ly = E + y, lz = E + z;
+                const int lx = HX + x, ly = E + y, lz = EZH + z;
                 const int c = (lx & 1) ^ ((ly + lz + p0) & 1);
-                const int mm = lx >> 1, o = lx & 1;
-                const int own = S::lidx(lz, ly, c, mm), oth = S::lidx(lz, ly, c ^ 1, mm);
-                T sum = U[oth - 1 + o] + U[oth + o];
-                sum = sum + U[oth - 2 * EH];
-                sum = sum + U[oth + 2 * EH];
-                sum = sum + U[oth - 2 * EH * EY];
-                sum = sum + U[oth + 2 * EH * EY];
-                const int gi = X0 + x, gj = Y0 + y, gk = gz0 + Z0 + z;
-                const int nb = (gi == 0) + (gi == g.nx - 1) + (gj == 0) + (gj == g.ny - 1) + (gk == 0) + (gk == gnz - 1);
-                RS[it] = op.residual(sum, F[own], U[own], nb);
+                const int own = S::lidx(lz, ly, c, lx >> 1);
+                const T sum = nbsum(lx, ly, lz, c);
+                RS[it] = op.residual(sum, F[own], U[own], faces(X0 + x, Y0 + y, gz0 + Z0 + z));
             }
         }
         __syncthreads();
         // ... then one coarse cell per thread, children summed in resrestrict_item's order
-        constexpr int C = B / 2;
-        if (tid < C * C * C) {
-            const int I = tid % C, J = (tid / C) % C, K = tid / (C * C);
+        constexpr int C = B / 2, CZ = DIM == 3 ? C : 1;
+        for (int it = tid; it < C * C * CZ; it += NT) {
+            const int I = it % C, J = (it / C) % C, K = it / (C * C);
             const int r0 = (2 * K * B + 2 * J) * B + 2 * I;
             T sm = RS[r0] + RS[r0 + 1];
             sm = sm + RS[r0 + B];
             sm = sm + RS[r0 + B + 1];
-            sm = sm + RS[r0 + B * B];
-            sm = sm + RS[r0 + B * B + 1];
-            sm = sm + RS[r0 + B * B + B];
-            sm = sm + RS[r0 + B * B + B + 1];
-            R[pidx(gc, (X0 >> 1) + I, (Y0 >> 1) + J, (int64_t)((Z0 >> 1) + K))] = (T)0.125 * sm;
+            if (DIM == 3) {
+                sm = sm + RS[r0 + B * B];
+                sm = sm + RS[r0 + B * B + 1];
+                sm = sm + RS[r0 + B * B + B];
+                sm = sm + RS[r0 + B * B + B + 1];
+            }
+            R[pidx(gc, (X0 >> 1) + I, (Y0 >> 1) + J, (int64_t)((Z0 >> 1) + K))] = (DIM == 3 ? (T)0.125 : (T)0.25) * sm;
         }
     }
     // the owned cells (both colours) to dst
     {
-        constexpr int H2 = B / 2, n = B * B * 2 * H2;
+        constexpr int H2 = B / 2, n = BZ * B * 2 * H2;
 #pragma unroll
         for (int q = 0; q < (n + NT - 1) / NT; ++q) {
             const int it = tid + q * NT;
             if (it < n) {
                 const int mm = it % H2, c = (it / H2) & 1, ly = (it / (2 * H2)) % B, lz = it / (2 * H2 * B);
                 dst[(int64_t)(Z0 + lz) * g.P + c * g.H + (int64_t)(Y0 + ly) * g.hw + (X0 >> 1) + mm] =
-                    U[S::lidx(lz + E, ly + E, c, (HX >> 1) + mm)];
+                    U[S::lidx(lz + EZH, ly + E, c, (HX >> 1) + mm)];
             }
         }
     }
@@ -2744,65 +2756,78 @@ hipError_t launch_tail(int rb, int dim, const TailSpec& t, hipStream_t s)
 
 // ---- 3D-tiled phases of small levels ----
 
-template <typename T, bool PRE, int B, int NS>
+template <int DIM>
+constexpr int blk_tile() { return DIM == 3 ? kBlkTile : kBlkTile2D; }
+
+template <typename T, int DIM, bool PRE, int NS>
 constexpr size_t blk_lds()
 {
-    using S = BlkShape<PRE, B, NS>;
-    return (2 * (size_t)S::cells + (PRE ? (size_t)B * B * B : 0)) * sizeof(T);
+    using S = BlkShape<DIM, PRE, blk_tile<DIM>(), NS>;
+    return (2 * (size_t)S::cells + (PRE ? (size_t)S::owned : 0)) * sizeof(T);
 }
 
-// the owned tile edge B: a power of two dividing every axis of the level
-bool block_supported(int rb, int dim, int ns, const Geo& g, int tile)
+// the owned tile edge B divides every axis of the level (3D: B^3 tiles, 2D: B^2)
+bool block_supported(int rb, int dim, int ns, const Geo& g)
 {
-    if (dim != 3 || ns < 1 || ns > kBlkMaxSweeps || tile != kBlkTile) return false;
-    if (g.nx < tile || g.ny < tile || g.nz < tile || g.z0 != 0 || g.gnz != g.nz) return false;
-    const size_t lds = rb == 8 ? blk_lds<double, true, kBlkTile, kBlkMaxSweeps>()
-                               : blk_lds<float, true, kBlkTile, kBlkMaxSweeps>();
+    if ((dim != 2 && dim != 3) || ns < 1 || ns > kBlkMaxSweeps) return false;
+    const int B = dim == 3 ? kBlkTile : kBlkTile2D;
+    if (g.nx < B || g.ny < B || (dim == 3 && g.nz < B) || g.z0 != 0 || g.gnz != g.nz) return false;
+    const size_t lds = rb == 8 ? (dim == 3 ? blk_lds<double, 3, true, kBlkMaxSweeps>() : blk_lds<double, 2, true, kBlkMaxSweeps>())
+                               : (dim == 3 ? blk_lds<float, 3, true, kBlkMaxSweeps>() : blk_lds<float, 2, true, kBlkMaxSweeps>());
     return lds <= kTailMaxLds;
 }
 
-template <typename T, int NS>
+template <typename T, int D, int NS>
 static hipError_t blk_attr_ns()
 {
-    constexpr int B = kBlkTile;
+    constexpr int B = blk_tile<D>();
     const auto A = hipFuncAttributeMaxDynamicSharedMemorySize;
-    hipError_t e = hipFuncSetAttribute((const void*)k_blk<T, true, 0, B, NS>, A, (int)blk_lds<T, true, B, NS>());
-    if (e == hipSuccess) e = hipFuncSetAttribute((const void*)k_blk<T, false, 0, B, NS>, A, (int)blk_lds<T, false, B, NS>());
-    if (e == hipSuccess) e = hipFuncSetAttribute((const void*)k_blk<T, false, 1, B, NS>, A, (int)blk_lds<T, false, B, NS>());
+    const int pre = (int)blk_lds<T, D, true, NS>(), post = (int)blk_lds<T, D, false, NS>();
+    hipError_t e = hipFuncSetAttribute((const void*)k_blk<T, D, true, 0, B, NS>, A, pre);
+    if (e == hipSuccess) e = hipFuncSetAttribute((const void*)k_blk<T, D, false, 0, B, NS>, A, post);
+    if (e == hipSuccess) e = hipFuncSetAttribute((const void*)k_blk<T, D, false, 1, B, NS>, A, post);
     return e;
 }
 
 template <typename T>
 static hipError_t blk_attr()
 {
-    hipError_t e = blk_attr_ns<T, 1>();
-    return e == hipSuccess ? blk_attr_ns<T, 2>() : e;
+    hipError_t e = blk_attr_ns<T, 3, 1>();
+    if (e == hipSuccess) e = blk_attr_ns<T, 3, 2>();
+    if (e == hipSuccess) e = blk_attr_ns<T, 2, 1>();
+    if (e == hipSuccess) e = blk_attr_ns<T, 2, 2>();
+    return e;
 }
 
-template <typename T, int NS>
+template <typename T, int D, int NS>
 static hipError_t blk_t(const BlockArgs& a, hipStream_t s)
 {
-    constexpr int B = kBlkTile;
-    const Op<T, 3> op = make_op<T, 3>(a.h, a.cl);
-    const unsigned nb = (unsigned)((a.g.nx / B) * (a.g.ny / B) * (a.g.nz / B));
+    constexpr int B = blk_tile<D>();
+    constexpr int NT = blk_threads<D>();
+    const Op<T, D> op = make_op<T, D>(a.h, a.cl);
+    const unsigned nb = (unsigned)((a.g.nx / B) * (a.g.ny / B) * (D == 3 ? a.g.nz / B : 1));
     const T* src = (const T*)a.src;
     if (a.pre)
-        k_blk<T, true, 0, B, NS><<<nb, kBlkThreads, blk_lds<T, true, B, NS>(), s>>>(
+        k_blk<T, D, true, 0, B, NS><<<nb, NT, blk_lds<T, D, true, NS>(), s>>>(
             src, (const T*)a.f, (T*)a.dst, (T*)a.R, (const T*)a.V, a.g, a.gc, op, (T)a.clc);
     else if (a.linear)
-        k_blk<T, false, 1, B, NS><<<nb, kBlkThreads, blk_lds<T, false, B, NS>(), s>>>(
+        k_blk<T, D, false, 1, B, NS><<<nb, NT, blk_lds<T, D, false, NS>(), s>>>(
             src, (const T*)a.f, (T*)a.dst, (T*)a.R, (const T*)a.V, a.g, a.gc, op, (T)a.clc);
     else
-        k_blk<T, false, 0, B, NS><<<nb, kBlkThreads, blk_lds<T, false, B, NS>(), s>>>(
+        k_blk<T, D, false, 0, B, NS><<<nb, NT, blk_lds<T, D, false, NS>(), s>>>(
             src, (const T*)a.f, (T*)a.dst, (T*)a.R, (const T*)a.V, a.g, a.gc, op, (T)a.clc);
     return hipGetLastError();
 }
 
-hipError_t launch_block(int rb, const BlockArgs& a, hipStream_t s)
+hipError_t launch_block(int rb, int dim, const BlockArgs& a, hipStream_t s)
 {
-    if (!block_supported(rb, 3, a.ns, a.g, a.tile)) return hipErrorInvalidValue;
-    if (rb == 8) return a.ns == 1 ? blk_t<double, 1>(a, s) : blk_t<double, 2>(a, s);
-    return a.ns == 1 ? blk_t<float, 1>(a, s) : blk_t<float, 2>(a, s);
+    if (!block_supported(rb, dim, a.ns, a.g)) return hipErrorInvalidValue;
+    if (rb == 8) {
+        if (dim == 3) return a.ns == 1 ? blk_t<double, 3, 1>(a, s) : blk_t<double, 3, 2>(a, s);
+        return a.ns == 1 ? blk_t<double, 2, 1>(a, s) : blk_t<double, 2, 2>(a, s);
+    }
+    if (dim == 3) return a.ns == 1 ? blk_t<float, 3, 1>(a, s) : blk_t<float, 3, 2>(a, s);
+    return a.ns == 1 ? blk_t<float, 2, 1>(a, s) : blk_t<float, 2, 2>(a, s);
 }
 
 hipError_t launch_sqdiff_sum(int rb, const void* a, const void* b, int64_t n, double* partials, double* out,

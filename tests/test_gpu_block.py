@@ -40,6 +40,11 @@ BLK_CONFIGS = [
     # no coarse tail: tiled levels down to 4 x 4 x 4 (tiles smaller than the halo, every cell on the box)
     dict(n=(32, 32, 32), real="float", nu1=2, nu2=2, prolong="linear", coarse_bc="consistent", tail=0),
     dict(n=(64, 16, 32), real="double", nu1=1, nu2=1, prolong="pc", coarse_bc="consistent", tail=0),
+    # 2D: 32 x 32 tiles (configs[1] family: RB-GS 2+2, linear, consistent coarse boundary)
+    dict(dim=2, n=(512, 512, 1), real="float", nu1=2, nu2=2, prolong="linear", coarse_bc="consistent"),
+    dict(dim=2, n=(256, 256, 1), real="double", nu1=2, nu2=2, prolong="linear", coarse_bc="consistent", cycle="F"),
+    dict(dim=2, n=(256, 128, 1), real="float", nu1=1, nu2=2, prolong="pc", coarse_bc="zero", coarse_init="warm"),
+    dict(dim=2, n=(128, 128, 1), real="double", nu1=2, nu2=1, prolong="linear", coarse_bc="consistent", tail=0),
 ]
 
 
@@ -51,7 +56,8 @@ def _id(c):
 def test_block_phases_match_oracle(cfg, monkeypatch):
     cfg = dict(cfg)
     tail = cfg.pop("tail", 1)
-    kw = dict(dim=3, smoother="rbgs", **cfg)
+    kw = dict(smoother="rbgs", **cfg)
+    kw.setdefault("dim", 3)
     if not tail:
         monkeypatch.setenv("MGP_TAIL", "0")
     monkeypatch.setenv("MGP_BLK", "1")
@@ -91,6 +97,14 @@ def test_block_graph_replay_equals_eager(monkeypatch):
     ee = np.concatenate([e.cycles(3), e.cycles(4)])
     assert np.array_equal(g.get_psi(), e.get_psi())
     assert np.array_equal(eg, ee)
+
+
+def test_block_levels_of_the_2d_config():
+    """4096^2 RB-GS 2+2 (configs[1]): 512^2 .. 128^2 tiled, 64^2 and below in the tail."""
+    ctx = _ctx(dim=2, n=(4096, 4096, 1), real="float", smoother="rbgs", nu1=2, nu2=2, prolong="linear",
+               coarse_bc="consistent")
+    eng = [lv["engine"] for lv in ctx.levels]
+    assert eng[:6] == ["piece", "piece", "piece", "blk", "blk", "blk"] and eng[6] == "tail", eng
 
 
 def test_block_levels_of_the_bench_config():
