@@ -2058,6 +2058,226 @@ __global__ __launch_bounds__(tail_threads<T>()) void k_tail(const TailArgs<T, DI
     }
 }
 
+// ---- cubic coarse tail with compile-time level shapes (k_tail_c) ------------------------------
+//
+// The same op program as k_tail for the common case of a cubic 3D red/black tail whose first level
+// is TN^3 (TN = 16: levels 16, 8, 4, 2, 1).  Each level lives in LDS as an unpacked (n+2)^3 array
+// with a zero halo (the Dirichlet ghost), so a cell's neighbours are fixed offsets, every loop
+// bound and index is a compile-time constant and no box test is needed.  The per-cell arithmetic
+// is half_item's / residual_at + resrestrict_item's / prolong_value's, so results are
+// bit-identical to k_tail and to the launch-per-piece path.
+template <int N>
+struct TcLev {
+    static constexpr int W = N + 2, P = W * W * W;
+    static __device__ __forceinline__ int idx(int i, int j, int k) { return ((k + 1) * W + (j + 1)) * W + (i + 1); }
+};
+template <int TN>
+constexpr int tc_off(int l)  // element offset of level l's (u, f) pair
+{
+    int o = 0;
+    for (int q = 0; q < l; ++q) o += 2 * ((TN >> q) + 2) * ((TN >> q) + 2) * ((TN >> q) + 2);
+    return o;
+}
+template <int TN>
+constexpr int tc_cells()
+{
+    int o = 0;
+    for (int n = TN; n >= 1; n >>= 1) o += 2 * (n + 2) * (n + 2) * (n + 2);
+    return o;
+}
+constexpr int kTcThreads = 1024;
+
+template <typename T, int N>
+__device__ __forceinline__ void tc_half(T* U, const T* F, const Op<T, 3>& op, int c, int tid)
+{
+    using L = TcLev<N>;
+    constexpr int HN = N >= 2 ? N / 2 : 1;
+    constexpr int CNT = N >= 2 ? N * N * N / 2 : 1;
+    if (N == 1 && c == 1) return;  // the single cell is red
+#pragma unroll 1
+    for (int q0 = 0; q0 < CNT; q0 += kTcThreads) {
+        const int q = q0 + tid;
+        if (q < CNT) {
+            const int i2 = q % HN, j = (q / HN) % N, k = q / (HN * N);
+            const int i = N >= 2 ? 2 * i2 + ((j + k + c) & 1) : 0;
+            const int x = L::idx(i, j, k);
+            T sm = U[x - 1] + U[x + 1];
+            sm = sm + U[x - L::W];
+            sm = sm + U[x + L::W];
+            sm = sm + U[x - L::W * L::W];
+            sm = sm + U[x + L::W * L::W];
+            const int nb = (i == 0) + (i == N - 1) + (j == 0) + (j == N - 1) + (k == 0) + (k == N - 1);
+            U[x] = op.relax(sm, F[x], nb);
+        }
+    }
+}
+
+template <typename T, int N>
+__device__ __forceinline__ void tc_rr(const T* U, const T* F, T* Fc, const Op<T, 3>& op, int tid)
+{
+    using L = TcLev<N>;
+    using C = TcLev<N / 2>;
+    constexpr int M = N / 2, CNT = M * M * M;
+    auto res = [&](int i, int j, int k) {
+        const int x = L::idx(i, j, k);
+        T sm = U[x - 1] + U[x + 1];
+        sm = sm + U[x - L::W];
+        sm = sm + U[x + L::W];
+        sm = sm + U[x - L::W * L::W];
+        sm = sm + U[x + L::W * L::W];
+        const int nb = (i == 0) + (i == N - 1) + (j == 0) + (j == N - 1) + (k == 0) + (k == N - 1);
+        return op.residual(sm, F[x], U[x], nb);
+    };
+    for (int q = tid; q < CNT; q += kTcThreads) {
+        const int I = q % M, J = (q / M) % M, K = q / (M * M);
+        const int i = 2 * I, j = 2 * J, k = 2 * K;
+        T sm = res(i, j, k) + res(i + 1, j, k);
+        sm = sm + res(i, j + 1, k);
+        sm = sm + res(i + 1, j + 1, k);
+        sm = sm + res(i, j, k + 1);
+        sm = sm + res(i + 1, j, k + 1);
+        sm = sm + res(i, j + 1, k + 1);
+        sm = sm + res(i + 1, j + 1, k + 1);
+        Fc[C::idx(I, J, K)] = (T)0.125 * sm;
+    }
+}
+
+template <typename T, int N, int LINEAR>
+__device__ __forceinline__ void tc_prolong(T* U, const T* V, T cl, int tid)
+{
+    using L = TcLev<N>;
+    using C = TcLev<N / 2>;
+    constexpr int M = N / 2, CNT = N * N * N;
+#pragma unroll 1
+    for (int q0 = 0; q0 < CNT; q0 += kTcThreads) {
+        const int q = q0 + tid;
+        if (q < CNT) {
+            const int i = q % N, j = (q / N) % N, k = q / (N * N);
+            const int I = i >> 1, J = j >> 1, K = k >> 1;
+            T v;
+            if (!LINEAR) {
+                v = V[C::idx(I, J, K)];
+            } else {
+                const T w0 = (T)0.75, w1 = (T)0.25;
+                int In = (i & 1) ? I + 1 : I - 1, Jn = (j & 1) ? J + 1 : J - 1, Kn = (k & 1) ? K + 1 : K - 1;
+                const bool ox = In < 0 || In >= M, oy = Jn < 0 || Jn >= M, oz = Kn < 0 || Kn >= M;
+                if (ox) In = I;
+                if (oy) Jn = J;
+                if (oz) Kn = K;
+                auto cv = [&](int a, int b, int d, bool fx, bool fy, bool fz) {  // cval()
+                    T s = (T)1;
+                    if (fx) s = -cl * s;
+                    if (fy) s = -cl * s;
+                    if (fz) s = -cl * s;
+                    const T val = V[C::idx(a, b, d)];
+                    return s == (T)1 ? val : s * val;
+                };
+                const T a00 = w0 * cv(I, J, K, false, false, false) + w1 * cv(In, J, K, ox, false, false);
+                const T a10 = w0 * cv(I, Jn, K, false, oy, false) + w1 * cv(In, Jn, K, ox, oy, false);
+                const T a01 = w0 * cv(I, J, Kn, false, false, oz) + w1 * cv(In, J, Kn, ox, false, oz);
+                const T a11 = w0 * cv(I, Jn, Kn, false, oy, oz) + w1 * cv(In, Jn, Kn, ox, oy, oz);
+                const T b0 = w0 * a00 + w1 * a10;
+                const T b1 = w0 * a01 + w1 * a11;
+                v = w0 * b0 + w1 * b1;
+            }
+            const int x = L::idx(i, j, k);
+            U[x] = U[x] + v;
+        }
+    }
+}
+
+// level l of a TN^3 tail: copy in (zero halo), copy out
+template <typename T, int N>
+__device__ __forceinline__ void tc_copy(T* U, T* F, T* gu, T* gf, bool in, bool zero_u, int tid)
+{
+    using L = TcLev<N>;
+    constexpr int HW = N >= 2 ? N / 2 : 1;
+    constexpr int64_t H = (int64_t)HW * N, P = 2 * H;
+    for (int q = tid; q < L::P; q += kTcThreads) {
+        const int i = q % L::W - 1, j = (q / L::W) % L::W - 1, k = q / (L::W * L::W) - 1;
+        const bool inside = i >= 0 && i < N && j >= 0 && j < N && k >= 0 && k < N;
+        const int64_t gi = (int64_t)k * P + ((i + j + k) & 1) * H + (int64_t)j * HW + (i >> 1);
+        if (in) {
+            U[q] = inside && !zero_u ? gu[gi] : (T)0;
+            F[q] = inside ? gf[gi] : (T)0;
+        } else if (inside) {
+            gu[gi] = U[q];
+            gf[gi] = F[q];
+        }
+    }
+}
+
+template <typename T, int TN, int LINEAR>
+__global__ __launch_bounds__(kTcThreads) void k_tail_c(const TailArgs<T, 3> a)
+{
+    extern __shared__ __align__(16) unsigned char tc_smem[];
+    T* const lds = reinterpret_cast<T*>(tc_smem);
+    const int tid = threadIdx.x;
+    // the level operators in LDS, read per op (held in registers for all levels they spill)
+    __shared__ Op<T, 3> sop[5];
+    if (tid < 5 && tid < a.nlev) sop[tid] = a.op[tid];
+    // level l (n = TN >> l): u at tc_off(l), f right after it
+#define TC_LEVELS(X) X(0) X(1) X(2) X(3) X(4)
+#define TC_U(l) (lds + tc_off<TN>(l))
+#define TC_F(l) (lds + tc_off<TN>(l) + TcLev<(TN >> (l))>::P)
+#define TC_IN(l) if (l < a.nlev) tc_copy<T, (TN >> (l))>(TC_U(l), TC_F(l), a.u[l], a.f[l], true, l == 0 && a.zero0, tid);
+    TC_LEVELS(TC_IN)
+    __syncthreads();
+    for (int pc = 0; pc < a.nops; ++pc) {
+        const uint32_t w = a.ops[pc];
+        const int op = (int)(w & 15), l = (int)((w >> 4) & 15), arg = (int)(w >> 8);
+        // an opaque copy of the thread index per op: the index arithmetic of every (level, op) would
+        // otherwise be hoisted out of this loop and held in registers for the whole program
+        int tid = threadIdx.x;
+        asm volatile("" : "+v"(tid));
+#define TC_CASE(L)                                                                              \
+    case L:                                                                                     \
+        if constexpr ((TN >> (L)) >= 1) {                                                       \
+            constexpr int N = TN >> (L);                                                        \
+            if (op == TAIL_SMOOTH) {                                                            \
+                for (int sw = 0; sw < arg; ++sw) {                                              \
+                    tc_half<T, N>(TC_U(L), TC_F(L), sop[L], 0, tid);                            \
+                    __syncthreads();                                                            \
+                    if (N >= 2) {                                                               \
+                        tc_half<T, N>(TC_U(L), TC_F(L), sop[L], 1, tid);                        \
+                        __syncthreads();                                                        \
+                    }                                                                           \
+                }                                                                               \
+            } else if (op == TAIL_ZERO) {                                                       \
+                T* u = TC_U(L);                                                                 \
+                for (int q = tid; q < N * N * N; q += kTcThreads)                               \
+                    u[TcLev<N>::idx(q % N, (q / N) % N, q / (N * N))] = (T)0;                   \
+                __syncthreads();                                                                \
+            } else if constexpr (N >= 2 && (L) + 1 < 5) {                                       \
+                if (op == TAIL_RR) {                                                            \
+                    tc_rr<T, N>(TC_U(L), TC_F(L), TC_F((L) + 1), sop[L], tid);                  \
+                    __syncthreads();                                                            \
+                } else if (op == TAIL_PROLONG) {                                                \
+                    tc_prolong<T, N, LINEAR>(TC_U(L), TC_U((L) + 1), sop[(L) + 1].cl, tid);     \
+                    __syncthreads();                                                            \
+                }                                                                               \
+            }                                                                                   \
+        }                                                                                       \
+        break;
+        switch (l) {
+            TC_CASE(0)
+            TC_CASE(1)
+            TC_CASE(2)
+            TC_CASE(3)
+            TC_CASE(4)
+            default: break;
+        }
+#undef TC_CASE
+    }
+#define TC_OUT(l) if (l < a.nlev) tc_copy<T, (TN >> (l))>(TC_U(l), TC_F(l), a.u[l], a.f[l], false, false, tid);
+    TC_LEVELS(TC_OUT)
+#undef TC_OUT
+#undef TC_IN
+#undef TC_F
+#undef TC_U
+#undef TC_LEVELS
+}
+
 // ---- 3D-tiled smoothing phases of small levels (k_blk) ----------------------------------------
 //
 // Below ~128^3 a launch costs more than its work (≈5 us per kernel, most of it the kernel
@@ -2670,6 +2890,9 @@ constexpr int kTailStaticLds = 1024;
 #else
 constexpr int kTailStaticLds = 0;
 #endif
+template <typename T>
+static hipError_t tail_c_attr();
+
 template <typename T, int D>
 static hipError_t tail_attr()
 {
@@ -2694,12 +2917,14 @@ hipError_t prepare_kernels(int rb)
         MGP_CHAIN((fused_attr<float, false>()));
         MGP_CHAIN((tail_attr<float, 2>()));
         MGP_CHAIN((tail_attr<float, 3>()));
+        MGP_CHAIN((tail_c_attr<float>()));
         MGP_CHAIN((blk_attr<float>()));
     } else {
         MGP_CHAIN((fused_attr<double, true>()));
         MGP_CHAIN((fused_attr<double, false>()));
         MGP_CHAIN((tail_attr<double, 2>()));
         MGP_CHAIN((tail_attr<double, 3>()));
+        MGP_CHAIN((tail_c_attr<double>()));
         MGP_CHAIN((blk_attr<double>()));
     }
 #undef MGP_CHAIN
@@ -2719,6 +2944,20 @@ size_t tail_lds_bytes(int rb, int dim, int jacobi, const Geo* g, int nlev)
     size_t n = 0;
     for (int l = 0; l < nlev; ++l) n += (size_t)((g[l].nz + 2 * G) * g[l].P) * (jacobi ? 3 : 2);
     return n * (size_t)rb;
+}
+
+// k_tail_c applies: 3D red/black, levels TN^3, (TN/2)^3, ... 1 (TN = kTailCubicTop), one rank's box
+constexpr int kTailCubicTop = 16;
+static bool tail_cubic(const TailSpec& t)
+{
+    const char* v = std::getenv("MGP_TAIL_CUBIC");  // 0: the generic k_tail
+    if ((v && std::atoi(v) == 0) || t.jacobi || t.nlev != 5) return false;
+    for (int l = 0; l < t.nlev; ++l) {
+        const Geo& g = t.g[l];
+        const int n = kTailCubicTop >> l;
+        if (g.nx != n || g.ny != n || g.nz != n || g.gnz != n || g.z0 != 0) return false;
+    }
+    return true;
 }
 
 template <typename T, int D>
@@ -2741,10 +2980,28 @@ static hipError_t tail_t(const TailSpec& t, hipStream_t s)
         off += a.region[l] * (t.jacobi ? 3 : 2);
     }
     for (int i = 0; i < t.nops; ++i) a.ops[i] = t.ops[i];
+    if (D == 3 && tail_cubic(t)) {
+        if constexpr (D == 3) {
+            constexpr size_t cb = (size_t)tc_cells<kTailCubicTop>() * sizeof(T);
+            auto kc = t.linear ? k_tail_c<T, kTailCubicTop, 1> : k_tail_c<T, kTailCubicTop, 0>;
+            kc<<<1, kTcThreads, cb, s>>>(a);
+            return hipGetLastError();
+        }
+    }
     const size_t bytes = (size_t)off * sizeof(T);
     auto kern = t.linear ? k_tail<T, D, 1> : k_tail<T, D, 0>;
     kern<<<1, tail_threads<T>(), bytes, s>>>(a);
     return hipGetLastError();
+}
+
+template <typename T>
+static hipError_t tail_c_attr()
+{
+    const int b = (int)(tc_cells<kTailCubicTop>() * sizeof(T));
+    const auto A = hipFuncAttributeMaxDynamicSharedMemorySize;
+    hipError_t e = hipFuncSetAttribute((const void*)k_tail_c<T, kTailCubicTop, 0>, A, b);
+    if (e == hipSuccess) e = hipFuncSetAttribute((const void*)k_tail_c<T, kTailCubicTop, 1>, A, b);
+    return e;
 }
 
 hipError_t launch_tail(int rb, int dim, const TailSpec& t, hipStream_t s)

@@ -148,3 +148,40 @@ def test_fresh_first_sweep_matches_oracle(cfg, monkeypatch):
         _check_err(ea, eo, new, old)
     for level in range(len(a.levels)):
         assert np.array_equal(a.get_psi(level), b.get_psi(level)), f"psi level {level}"
+
+
+CUBIC_TAIL_CONFIGS = [
+    dict(n=(64, 64, 64), real="float", nu1=2, nu2=2, prolong="linear", coarse_bc="consistent"),
+    dict(n=(32, 32, 32), real="double", nu1=2, nu2=2, prolong="pc", coarse_bc="zero", cycle="F", coarse_init="warm"),
+    dict(n=(128, 128, 128), real="float", nu1=1, nu2=3, prolong="linear", coarse_bc="consistent", cycle="F"),
+    dict(n=(32, 32, 32), real="double", nu1=2, nu2=1, prolong="linear", coarse_bc="consistent", coarse_sweeps=3),
+]
+
+
+@pytest.mark.parametrize("cfg", CUBIC_TAIL_CONFIGS, ids=_id)
+def test_cubic_tail_equals_generic_tail_and_oracle(cfg, monkeypatch):
+    """k_tail_c (compile-time 16^3 .. 1 cubic tail, zero-halo LDS levels) == the generic k_tail == the
+    oracle: psi and f bit-identical on every level."""
+    kw = dict(dim=3, smoother="rbgs", **cfg)
+    monkeypatch.setenv("MGP_TAIL_CUBIC", "1")
+    a = _ctx(**kw)
+    monkeypatch.setenv("MGP_TAIL_CUBIC", "0")
+    b = _ctx(**kw)
+    assert [lv["nx"] for lv in a.levels if lv["tail"]] == [16, 8, 4, 2, 1]
+    o = Oracle(threads=8, **kw)
+    for x in (a, b, o):
+        x.init_point_charge()
+    for it in range(3):
+        old = o.get(0)
+        monkeypatch.setenv("MGP_TAIL_CUBIC", "1")
+        ea = a.cycle()
+        monkeypatch.setenv("MGP_TAIL_CUBIC", "0")
+        eb = b.cycle()
+        eo = o.step()
+        new = o.get(0)
+        assert np.array_equal(a.get_psi(), new), f"psi differs from the oracle after cycle {it + 1}"
+        assert np.array_equal(b.get_psi(), new)
+        _check_err(ea, eo, new, old)
+    for level in range(len(a.levels)):
+        assert np.array_equal(a.get_psi(level), b.get_psi(level)), f"psi level {level}"
+        assert np.array_equal(a.get_f(level), b.get_f(level)), f"f level {level}"
