@@ -2060,99 +2060,114 @@ __global__ __launch_bounds__(tail_threads<T>()) void k_tail(const TailArgs<T, DI
 
 // ---- cubic coarse tail with compile-time level shapes (k_tail_c) ------------------------------
 //
-// The same op program as k_tail for the common case of a cubic 3D red/black tail whose first level
-// is TN^3 (TN = 16: levels 16, 8, 4, 2, 1).  Each level lives in LDS as an unpacked (n+2)^3 array
-// with a zero halo (the Dirichlet ghost), so a cell's neighbours are fixed offsets, every loop
-// bound and index is a compile-time constant and no box test is needed.  The per-cell arithmetic
-// is half_item's / residual_at + resrestrict_item's / prolong_value's, so results are
-// bit-identical to k_tail and to the launch-per-piece path.
-template <int N>
+// The same op program as k_tail for the common case of a cubic (square) red/black tail whose first
+// level is TN^DIM (3D: TN = 16, levels 16 .. 1; 2D: TN = 64, levels 64 .. 1).  Each level lives in
+// LDS as an unpacked (n+2)^DIM array with a zero halo (the Dirichlet ghost), so a cell's neighbours
+// are fixed offsets, every loop bound and index is a compile-time constant and no box test is
+// needed.  The per-cell arithmetic is half_item's / residual_at + resrestrict_item's /
+// prolong_value's, so results are bit-identical to k_tail and to the launch-per-piece path.
+template <int DIM, int N>
 struct TcLev {
-    static constexpr int W = N + 2, P = W * W * W;
-    static __device__ __forceinline__ int idx(int i, int j, int k) { return ((k + 1) * W + (j + 1)) * W + (i + 1); }
+    static constexpr int W = N + 2, P = DIM == 3 ? W * W * W : W * W;
+    static constexpr int CELLS = DIM == 3 ? N * N * N : N * N;
+    static __device__ __forceinline__ int idx(int i, int j, int k)
+    {
+        return DIM == 3 ? ((k + 1) * W + (j + 1)) * W + (i + 1) : (j + 1) * W + (i + 1);
+    }
 };
-template <int TN>
+template <int DIM, int TN>
 constexpr int tc_off(int l)  // element offset of level l's (u, f) pair
 {
     int o = 0;
-    for (int q = 0; q < l; ++q) o += 2 * ((TN >> q) + 2) * ((TN >> q) + 2) * ((TN >> q) + 2);
+    for (int q = 0; q < l; ++q) {
+        const int w = (TN >> q) + 2;
+        o += 2 * (DIM == 3 ? w * w * w : w * w);
+    }
     return o;
 }
-template <int TN>
-constexpr int tc_cells()
+template <int DIM, int TN>
+constexpr int tc_levels()
 {
-    int o = 0;
-    for (int n = TN; n >= 1; n >>= 1) o += 2 * (n + 2) * (n + 2) * (n + 2);
-    return o;
+    int n = 0;
+    for (int t = TN; t >= 1; t >>= 1) ++n;
+    return n;
 }
+template <int DIM>
+constexpr int tc_top() { return DIM == 3 ? 16 : 64; }
 constexpr int kTcThreads = 1024;
 
-template <typename T, int N>
-__device__ __forceinline__ void tc_half(T* U, const T* F, const Op<T, 3>& op, int c, int tid)
+template <typename T, int DIM, int N>
+__device__ __forceinline__ void tc_half(T* U, const T* F, const Op<T, DIM>& op, int c, int tid)
 {
-    using L = TcLev<N>;
+    using L = TcLev<DIM, N>;
     constexpr int HN = N >= 2 ? N / 2 : 1;
-    constexpr int CNT = N >= 2 ? N * N * N / 2 : 1;
+    constexpr int CNT = N >= 2 ? L::CELLS / 2 : 1;
     if (N == 1 && c == 1) return;  // the single cell is red
 #pragma unroll 1
     for (int q0 = 0; q0 < CNT; q0 += kTcThreads) {
         const int q = q0 + tid;
         if (q < CNT) {
-            const int i2 = q % HN, j = (q / HN) % N, k = q / (HN * N);
+            const int i2 = q % HN, j = (q / HN) % N, k = DIM == 3 ? q / (HN * N) : 0;
             const int i = N >= 2 ? 2 * i2 + ((j + k + c) & 1) : 0;
             const int x = L::idx(i, j, k);
             T sm = U[x - 1] + U[x + 1];
             sm = sm + U[x - L::W];
             sm = sm + U[x + L::W];
-            sm = sm + U[x - L::W * L::W];
-            sm = sm + U[x + L::W * L::W];
-            const int nb = (i == 0) + (i == N - 1) + (j == 0) + (j == N - 1) + (k == 0) + (k == N - 1);
+            if (DIM == 3) {
+                sm = sm + U[x - L::W * L::W];
+                sm = sm + U[x + L::W * L::W];
+            }
+            const int nb = (i == 0) + (i == N - 1) + (j == 0) + (j == N - 1) + (DIM == 3 ? (k == 0) + (k == N - 1) : 0);
             U[x] = op.relax(sm, F[x], nb);
         }
     }
 }
 
-template <typename T, int N>
-__device__ __forceinline__ void tc_rr(const T* U, const T* F, T* Fc, const Op<T, 3>& op, int tid)
+template <typename T, int DIM, int N>
+__device__ __forceinline__ void tc_rr(const T* U, const T* F, T* Fc, const Op<T, DIM>& op, int tid)
 {
-    using L = TcLev<N>;
-    using C = TcLev<N / 2>;
-    constexpr int M = N / 2, CNT = M * M * M;
+    using L = TcLev<DIM, N>;
+    using C = TcLev<DIM, N / 2>;
+    constexpr int M = N / 2, CNT = C::CELLS;
     auto res = [&](int i, int j, int k) {
         const int x = L::idx(i, j, k);
         T sm = U[x - 1] + U[x + 1];
         sm = sm + U[x - L::W];
         sm = sm + U[x + L::W];
-        sm = sm + U[x - L::W * L::W];
-        sm = sm + U[x + L::W * L::W];
-        const int nb = (i == 0) + (i == N - 1) + (j == 0) + (j == N - 1) + (k == 0) + (k == N - 1);
+        if (DIM == 3) {
+            sm = sm + U[x - L::W * L::W];
+            sm = sm + U[x + L::W * L::W];
+        }
+        const int nb = (i == 0) + (i == N - 1) + (j == 0) + (j == N - 1) + (DIM == 3 ? (k == 0) + (k == N - 1) : 0);
         return op.residual(sm, F[x], U[x], nb);
     };
     for (int q = tid; q < CNT; q += kTcThreads) {
-        const int I = q % M, J = (q / M) % M, K = q / (M * M);
+        const int I = q % M, J = (q / M) % M, K = DIM == 3 ? q / (M * M) : 0;
         const int i = 2 * I, j = 2 * J, k = 2 * K;
         T sm = res(i, j, k) + res(i + 1, j, k);
         sm = sm + res(i, j + 1, k);
         sm = sm + res(i + 1, j + 1, k);
-        sm = sm + res(i, j, k + 1);
-        sm = sm + res(i + 1, j, k + 1);
-        sm = sm + res(i, j + 1, k + 1);
-        sm = sm + res(i + 1, j + 1, k + 1);
-        Fc[C::idx(I, J, K)] = (T)0.125 * sm;
+        if (DIM == 3) {
+            sm = sm + res(i, j, k + 1);
+            sm = sm + res(i + 1, j, k + 1);
+            sm = sm + res(i, j + 1, k + 1);
+            sm = sm + res(i + 1, j + 1, k + 1);
+        }
+        Fc[C::idx(I, J, K)] = (DIM == 3 ? (T)0.125 : (T)0.25) * sm;
     }
 }
 
-template <typename T, int N, int LINEAR>
+template <typename T, int DIM, int N, int LINEAR>
 __device__ __forceinline__ void tc_prolong(T* U, const T* V, T cl, int tid)
 {
-    using L = TcLev<N>;
-    using C = TcLev<N / 2>;
-    constexpr int M = N / 2, CNT = N * N * N;
+    using L = TcLev<DIM, N>;
+    using C = TcLev<DIM, N / 2>;
+    constexpr int M = N / 2, CNT = L::CELLS;
 #pragma unroll 1
     for (int q0 = 0; q0 < CNT; q0 += kTcThreads) {
         const int q = q0 + tid;
         if (q < CNT) {
-            const int i = q % N, j = (q / N) % N, k = q / (N * N);
+            const int i = q % N, j = (q / N) % N, k = DIM == 3 ? q / (N * N) : 0;
             const int I = i >> 1, J = j >> 1, K = k >> 1;
             T v;
             if (!LINEAR) {
@@ -2160,10 +2175,10 @@ __device__ __forceinline__ void tc_prolong(T* U, const T* V, T cl, int tid)
             } else {
                 const T w0 = (T)0.75, w1 = (T)0.25;
                 int In = (i & 1) ? I + 1 : I - 1, Jn = (j & 1) ? J + 1 : J - 1, Kn = (k & 1) ? K + 1 : K - 1;
-                const bool ox = In < 0 || In >= M, oy = Jn < 0 || Jn >= M, oz = Kn < 0 || Kn >= M;
+                const bool ox = In < 0 || In >= M, oy = Jn < 0 || Jn >= M, oz = DIM == 3 && (Kn < 0 || Kn >= M);
                 if (ox) In = I;
                 if (oy) Jn = J;
-                if (oz) Kn = K;
+                if (oz || DIM == 2) Kn = K;
                 auto cv = [&](int a, int b, int d, bool fx, bool fy, bool fz) {  // cval()
                     T s = (T)1;
                     if (fx) s = -cl * s;
@@ -2172,13 +2187,19 @@ __device__ __forceinline__ void tc_prolong(T* U, const T* V, T cl, int tid)
                     const T val = V[C::idx(a, b, d)];
                     return s == (T)1 ? val : s * val;
                 };
-                const T a00 = w0 * cv(I, J, K, false, false, false) + w1 * cv(In, J, K, ox, false, false);
-                const T a10 = w0 * cv(I, Jn, K, false, oy, false) + w1 * cv(In, Jn, K, ox, oy, false);
-                const T a01 = w0 * cv(I, J, Kn, false, false, oz) + w1 * cv(In, J, Kn, ox, false, oz);
-                const T a11 = w0 * cv(I, Jn, Kn, false, oy, oz) + w1 * cv(In, Jn, Kn, ox, oy, oz);
-                const T b0 = w0 * a00 + w1 * a10;
-                const T b1 = w0 * a01 + w1 * a11;
-                v = w0 * b0 + w1 * b1;
+                if (DIM == 2) {
+                    const T a0 = w0 * cv(I, J, 0, false, false, false) + w1 * cv(In, J, 0, ox, false, false);
+                    const T a1 = w0 * cv(I, Jn, 0, false, oy, false) + w1 * cv(In, Jn, 0, ox, oy, false);
+                    v = w0 * a0 + w1 * a1;
+                } else {
+                    const T a00 = w0 * cv(I, J, K, false, false, false) + w1 * cv(In, J, K, ox, false, false);
+                    const T a10 = w0 * cv(I, Jn, K, false, oy, false) + w1 * cv(In, Jn, K, ox, oy, false);
+                    const T a01 = w0 * cv(I, J, Kn, false, false, oz) + w1 * cv(In, J, Kn, ox, false, oz);
+                    const T a11 = w0 * cv(I, Jn, Kn, false, oy, oz) + w1 * cv(In, Jn, Kn, ox, oy, oz);
+                    const T b0 = w0 * a00 + w1 * a10;
+                    const T b1 = w0 * a01 + w1 * a11;
+                    v = w0 * b0 + w1 * b1;
+                }
             }
             const int x = L::idx(i, j, k);
             U[x] = U[x] + v;
@@ -2186,15 +2207,15 @@ __device__ __forceinline__ void tc_prolong(T* U, const T* V, T cl, int tid)
     }
 }
 
-// level l of a TN^3 tail: copy in (zero halo), copy out
-template <typename T, int N>
+// level l of the tail: copy in (zero halo; zero_u: a fresh guess) or out, packed global layout
+template <typename T, int DIM, int N>
 __device__ __forceinline__ void tc_copy(T* U, T* F, T* gu, T* gf, bool in, bool zero_u, int tid)
 {
-    using L = TcLev<N>;
+    using L = TcLev<DIM, N>;
     constexpr int HW = N >= 2 ? N / 2 : 1;
     constexpr int64_t H = (int64_t)HW * N, P = 2 * H;
     for (int q = tid; q < L::P; q += kTcThreads) {
-        const int i = q % L::W - 1, j = (q / L::W) % L::W - 1, k = q / (L::W * L::W) - 1;
+        const int i = q % L::W - 1, j = (q / L::W) % L::W - 1, k = DIM == 3 ? q / (L::W * L::W) - 1 : 0;
         const bool inside = i >= 0 && i < N && j >= 0 && j < N && k >= 0 && k < N;
         const int64_t gi = (int64_t)k * P + ((i + j + k) & 1) * H + (int64_t)j * HW + (i >> 1);
         if (in) {
@@ -2207,21 +2228,22 @@ __device__ __forceinline__ void tc_copy(T* U, T* F, T* gu, T* gf, bool in, bool 
     }
 }
 
-template <typename T, int TN, int LINEAR>
-__global__ __launch_bounds__(kTcThreads) void k_tail_c(const TailArgs<T, 3> a)
+template <typename T, int DIM, int LINEAR>
+__global__ __launch_bounds__(kTcThreads) void k_tail_c(const TailArgs<T, DIM> a)
 {
+    constexpr int TN = tc_top<DIM>(), NL = tc_levels<DIM, TN>();
     extern __shared__ __align__(16) unsigned char tc_smem[];
     T* const lds = reinterpret_cast<T*>(tc_smem);
-    const int tid = threadIdx.x;
     // the level operators in LDS, read per op (held in registers for all levels they spill)
-    __shared__ Op<T, 3> sop[5];
-    if (tid < 5 && tid < a.nlev) sop[tid] = a.op[tid];
-    // level l (n = TN >> l): u at tc_off(l), f right after it
-#define TC_LEVELS(X) X(0) X(1) X(2) X(3) X(4)
-#define TC_U(l) (lds + tc_off<TN>(l))
-#define TC_F(l) (lds + tc_off<TN>(l) + TcLev<(TN >> (l))>::P)
-#define TC_IN(l) if (l < a.nlev) tc_copy<T, (TN >> (l))>(TC_U(l), TC_F(l), a.u[l], a.f[l], true, l == 0 && a.zero0, tid);
-    TC_LEVELS(TC_IN)
+    __shared__ Op<T, DIM> sop[NL];
+    if ((int)threadIdx.x < NL) sop[threadIdx.x] = a.op[threadIdx.x];
+#define TC_U(l) (lds + tc_off<DIM, TN>(l))
+#define TC_F(l) (lds + tc_off<DIM, TN>(l) + TcLev<DIM, (TN >> (l))>::P)
+#define TC_COPY(l, IN)                                                                                    \
+    if constexpr ((l) < NL) tc_copy<T, DIM, (TN >> (l))>(TC_U(l), TC_F(l), a.u[l], a.f[l], IN, IN && (l) == 0 && a.zero0, \
+                                                         threadIdx.x);
+    TC_COPY(0, true) TC_COPY(1, true) TC_COPY(2, true) TC_COPY(3, true) TC_COPY(4, true) TC_COPY(5, true)
+    TC_COPY(6, true)
     __syncthreads();
     for (int pc = 0; pc < a.nops; ++pc) {
         const uint32_t w = a.ops[pc];
@@ -2230,34 +2252,34 @@ __global__ __launch_bounds__(kTcThreads) void k_tail_c(const TailArgs<T, 3> a)
         // otherwise be hoisted out of this loop and held in registers for the whole program
         int tid = threadIdx.x;
         asm volatile("" : "+v"(tid));
-#define TC_CASE(L)                                                                              \
-    case L:                                                                                     \
-        if constexpr ((TN >> (L)) >= 1) {                                                       \
-            constexpr int N = TN >> (L);                                                        \
-            if (op == TAIL_SMOOTH) {                                                            \
-                for (int sw = 0; sw < arg; ++sw) {                                              \
-                    tc_half<T, N>(TC_U(L), TC_F(L), sop[L], 0, tid);                            \
-                    __syncthreads();                                                            \
-                    if (N >= 2) {                                                               \
-                        tc_half<T, N>(TC_U(L), TC_F(L), sop[L], 1, tid);                        \
-                        __syncthreads();                                                        \
-                    }                                                                           \
-                }                                                                               \
-            } else if (op == TAIL_ZERO) {                                                       \
-                T* u = TC_U(L);                                                                 \
-                for (int q = tid; q < N * N * N; q += kTcThreads)                               \
-                    u[TcLev<N>::idx(q % N, (q / N) % N, q / (N * N))] = (T)0;                   \
-                __syncthreads();                                                                \
-            } else if constexpr (N >= 2 && (L) + 1 < 5) {                                       \
-                if (op == TAIL_RR) {                                                            \
-                    tc_rr<T, N>(TC_U(L), TC_F(L), TC_F((L) + 1), sop[L], tid);                  \
-                    __syncthreads();                                                            \
-                } else if (op == TAIL_PROLONG) {                                                \
-                    tc_prolong<T, N, LINEAR>(TC_U(L), TC_U((L) + 1), sop[(L) + 1].cl, tid);     \
-                    __syncthreads();                                                            \
-                }                                                                               \
-            }                                                                                   \
-        }                                                                                       \
+#define TC_CASE(L)                                                                                     \
+    case L:                                                                                            \
+        if constexpr ((L) < NL) {                                                                      \
+            constexpr int N = TN >> (L);                                                               \
+            if (op == TAIL_SMOOTH) {                                                                   \
+                for (int sw = 0; sw < arg; ++sw) {                                                     \
+                    tc_half<T, DIM, N>(TC_U(L), TC_F(L), sop[L], 0, tid);                              \
+                    __syncthreads();                                                                   \
+                    if (N >= 2) {                                                                      \
+                        tc_half<T, DIM, N>(TC_U(L), TC_F(L), sop[L], 1, tid);                          \
+                        __syncthreads();                                                               \
+                    }                                                                                  \
+                }                                                                                      \
+            } else if (op == TAIL_ZERO) {                                                              \
+                T* u = TC_U(L);                                                                        \
+                for (int q = tid; q < TcLev<DIM, N>::CELLS; q += kTcThreads)                           \
+                    u[TcLev<DIM, N>::idx(q % N, (q / N) % N, DIM == 3 ? q / (N * N) : 0)] = (T)0;      \
+                __syncthreads();                                                                       \
+            } else if constexpr (N >= 2 && (L) + 1 < NL) {                                             \
+                if (op == TAIL_RR) {                                                                   \
+                    tc_rr<T, DIM, N>(TC_U(L), TC_F(L), TC_F((L) + 1), sop[L], tid);                    \
+                    __syncthreads();                                                                   \
+                } else if (op == TAIL_PROLONG) {                                                       \
+                    tc_prolong<T, DIM, N, LINEAR>(TC_U(L), TC_U((L) + 1), sop[(L) + 1].cl, tid);       \
+                    __syncthreads();                                                                   \
+                }                                                                                      \
+            }                                                                                          \
+        }                                                                                              \
         break;
         switch (l) {
             TC_CASE(0)
@@ -2265,17 +2287,23 @@ __global__ __launch_bounds__(kTcThreads) void k_tail_c(const TailArgs<T, 3> a)
             TC_CASE(2)
             TC_CASE(3)
             TC_CASE(4)
+            TC_CASE(5)
+            TC_CASE(6)
             default: break;
         }
 #undef TC_CASE
     }
-#define TC_OUT(l) if (l < a.nlev) tc_copy<T, (TN >> (l))>(TC_U(l), TC_F(l), a.u[l], a.f[l], false, false, tid);
-    TC_LEVELS(TC_OUT)
-#undef TC_OUT
-#undef TC_IN
+    TC_COPY(0, false) TC_COPY(1, false) TC_COPY(2, false) TC_COPY(3, false) TC_COPY(4, false) TC_COPY(5, false)
+    TC_COPY(6, false)
+#undef TC_COPY
 #undef TC_F
 #undef TC_U
-#undef TC_LEVELS
+}
+
+template <int DIM>
+constexpr size_t tc_lds(int rb)
+{
+    return (size_t)tc_off<DIM, tc_top<DIM>()>(tc_levels<DIM, tc_top<DIM>()>()) * rb;
 }
 
 // ---- 3D-tiled smoothing phases of small levels (k_blk) ----------------------------------------
@@ -2946,16 +2974,17 @@ size_t tail_lds_bytes(int rb, int dim, int jacobi, const Geo* g, int nlev)
     return n * (size_t)rb;
 }
 
-// k_tail_c applies: 3D red/black, levels TN^3, (TN/2)^3, ... 1 (TN = kTailCubicTop), one rank's box
-constexpr int kTailCubicTop = 16;
-static bool tail_cubic(const TailSpec& t)
+// k_tail_c applies: red/black, levels TN^DIM, (TN/2)^DIM, ... 1 (TN = tc_top<DIM>()), one rank's box
+static bool tail_cubic(const TailSpec& t, int dim)
 {
     const char* v = std::getenv("MGP_TAIL_CUBIC");  // 0: the generic k_tail
-    if ((v && std::atoi(v) == 0) || t.jacobi || t.nlev != 5) return false;
+    const int top = dim == 3 ? tc_top<3>() : tc_top<2>();
+    const int nl = dim == 3 ? tc_levels<3, tc_top<3>()>() : tc_levels<2, tc_top<2>()>();
+    if ((v && std::atoi(v) == 0) || t.jacobi || t.nlev != nl) return false;
     for (int l = 0; l < t.nlev; ++l) {
         const Geo& g = t.g[l];
-        const int n = kTailCubicTop >> l;
-        if (g.nx != n || g.ny != n || g.nz != n || g.gnz != n || g.z0 != 0) return false;
+        const int n = top >> l;
+        if (g.nx != n || g.ny != n || (dim == 3 && (g.nz != n || g.gnz != n)) || g.z0 != 0) return false;
     }
     return true;
 }
@@ -2980,13 +3009,10 @@ static hipError_t tail_t(const TailSpec& t, hipStream_t s)
         off += a.region[l] * (t.jacobi ? 3 : 2);
     }
     for (int i = 0; i < t.nops; ++i) a.ops[i] = t.ops[i];
-    if (D == 3 && tail_cubic(t)) {
-        if constexpr (D == 3) {
-            constexpr size_t cb = (size_t)tc_cells<kTailCubicTop>() * sizeof(T);
-            auto kc = t.linear ? k_tail_c<T, kTailCubicTop, 1> : k_tail_c<T, kTailCubicTop, 0>;
-            kc<<<1, kTcThreads, cb, s>>>(a);
-            return hipGetLastError();
-        }
+    if (tail_cubic(t, D)) {
+        auto kc = t.linear ? k_tail_c<T, D, 1> : k_tail_c<T, D, 0>;
+        kc<<<1, kTcThreads, tc_lds<D>(sizeof(T)), s>>>(a);
+        return hipGetLastError();
     }
     const size_t bytes = (size_t)off * sizeof(T);
     auto kern = t.linear ? k_tail<T, D, 1> : k_tail<T, D, 0>;
@@ -2997,10 +3023,12 @@ static hipError_t tail_t(const TailSpec& t, hipStream_t s)
 template <typename T>
 static hipError_t tail_c_attr()
 {
-    const int b = (int)(tc_cells<kTailCubicTop>() * sizeof(T));
     const auto A = hipFuncAttributeMaxDynamicSharedMemorySize;
-    hipError_t e = hipFuncSetAttribute((const void*)k_tail_c<T, kTailCubicTop, 0>, A, b);
-    if (e == hipSuccess) e = hipFuncSetAttribute((const void*)k_tail_c<T, kTailCubicTop, 1>, A, b);
+    const int b3 = (int)tc_lds<3>(sizeof(T)), b2 = (int)tc_lds<2>(sizeof(T));
+    hipError_t e = hipFuncSetAttribute((const void*)k_tail_c<T, 3, 0>, A, b3);
+    if (e == hipSuccess) e = hipFuncSetAttribute((const void*)k_tail_c<T, 3, 1>, A, b3);
+    if (e == hipSuccess) e = hipFuncSetAttribute((const void*)k_tail_c<T, 2, 0>, A, b2);
+    if (e == hipSuccess) e = hipFuncSetAttribute((const void*)k_tail_c<T, 2, 1>, A, b2);
     return e;
 }
 

@@ -155,19 +155,24 @@ CUBIC_TAIL_CONFIGS = [
     dict(n=(32, 32, 32), real="double", nu1=2, nu2=2, prolong="pc", coarse_bc="zero", cycle="F", coarse_init="warm"),
     dict(n=(128, 128, 128), real="float", nu1=1, nu2=3, prolong="linear", coarse_bc="consistent", cycle="F"),
     dict(n=(32, 32, 32), real="double", nu1=2, nu2=1, prolong="linear", coarse_bc="consistent", coarse_sweeps=3),
+    # 2D: levels 64^2 .. 1
+    dict(dim=2, n=(256, 256, 1), real="float", nu1=2, nu2=2, prolong="linear", coarse_bc="consistent"),
+    dict(dim=2, n=(128, 128, 1), real="double", nu1=2, nu2=2, prolong="pc", coarse_bc="zero", cycle="F", coarse_init="warm"),
 ]
 
 
 @pytest.mark.parametrize("cfg", CUBIC_TAIL_CONFIGS, ids=_id)
 def test_cubic_tail_equals_generic_tail_and_oracle(cfg, monkeypatch):
-    """k_tail_c (compile-time 16^3 .. 1 cubic tail, zero-halo LDS levels) == the generic k_tail == the
-    oracle: psi and f bit-identical on every level."""
-    kw = dict(dim=3, smoother="rbgs", **cfg)
+    """k_tail_c (compile-time cubic tail: 16^3 .. 1 in 3D, 64^2 .. 1 in 2D, zero-halo LDS levels) == the
+    generic k_tail == the oracle: psi and f bit-identical on every level."""
+    kw = dict(smoother="rbgs", **cfg)
+    kw.setdefault("dim", 3)
     monkeypatch.setenv("MGP_TAIL_CUBIC", "1")
     a = _ctx(**kw)
     monkeypatch.setenv("MGP_TAIL_CUBIC", "0")
     b = _ctx(**kw)
-    assert [lv["nx"] for lv in a.levels if lv["tail"]] == [16, 8, 4, 2, 1]
+    top = 16 if kw["dim"] == 3 else 64
+    assert [lv["nx"] for lv in a.levels if lv["tail"]] == [top >> l for l in range(top.bit_length())]
     o = Oracle(threads=8, **kw)
     for x in (a, b, o):
         x.init_point_charge()
