@@ -156,6 +156,9 @@ struct mgp_ctx {
     bool deep_halo = true;  // smooth_deep on distributed levels below the finest
     bool fresh_sweep = true;        // k_fresh for the first sweep of a lazily zeroed level (MGP_FRESH=0: off)
     bool lazy_zero = true;          // fresh coarse guesses without a memset where a reader can take it (MGP_LAZY_ZERO=0: off)
+    bool post1 = false;             // k_post1: prolongation fused into the first post red half-sweep (MGP_POST1=1;
+                                    // measured slower: 5 rows of P V per thread cost more VALU and L2 loads
+                                    // than the prolongation pass it saves)
     std::vector<Level> lev;
     hipStream_t s = nullptr;
     int device = 0;
@@ -502,11 +505,12 @@ int smooth_deep(mgp_ctx* c, int l, int sweeps, double h)
     return MGP_OK;
 }
 
-int smooth(mgp_ctx* c, int l, int sweeps, double h, bool want_err = false)
+// red_done: the first sweep's red half-sweep already ran (k_post1), start at its black half
+int smooth(mgp_ctx* c, int l, int sweeps, double h, bool want_err = false, bool red_done = false)
 {
     Level& L = c->lev[l];
     const double cl = coarse_coef(c->o.coarse_bc, l);
-    if (deep_halo_ok(c, L, sweeps, want_err)) return smooth_deep(c, l, sweeps, h);
+    if (!red_done && deep_halo_ok(c, L, sweeps, want_err)) return smooth_deep(c, l, sweeps, h);
     // a pending zero that no zero-aware path below can read (the tail level swept outside the tail)
     if (L.zero_pending && (c->o.smoother != MGP_RBGS || !c->zbuf || L.alloc > c->zbuf_reals))
         TRY(materialize_zero(c, L));
@@ -535,8 +539,10 @@ int smooth(mgp_ctx* c, int l, int sweeps, double h, bool want_err = false)
         const char* old = last_err ? L.t : nullptr;
         const int nb = mgp::half_blocks(c->rb, L.g, c->use_gs);
         char* dst = oop ? L.t : L.u;
-        TRY(exchange(c, L));
-        TRY(half(c, l, 0, L.zero_pending ? c->zbuf : L.u, dst, old, h, cl, 0));  // red from black
+        if (!(red_done && sw == 0)) {
+            TRY(exchange(c, L));
+            TRY(half(c, l, 0, L.zero_pending ? c->zbuf : L.u, dst, old, h, cl, 0));  // red from black
+        }
         L.zero_pending = false;
         if (L.p.dist) {  // black reads the new red planes of dst
             TRY(exchange_buf(c, L, dst));
@@ -602,6 +608,33 @@ int prolong_correct(mgp_ctx* c, int l)
     HIP_TRY(c, mgp::launch_prolong_correct(c->rb, c->o.dim, linear, c->ui(L, L.u), V, L.g, gc,
                                            coarse_coef(c->o.coarse_bc, l + 1), c->s));
     L.ghost_ok = !L.p.dist;
+    L.ghost_zero = false;
+    return MGP_OK;
+}
+
+// prolong_correct(l) + the red half of smooth(l, nu2)'s first sweep as one pass (k_post1)
+bool post1_ok(const mgp_ctx* c, int l, bool want_err)
+{
+    const Level& L = c->lev[l];
+    const Level& C = c->lev[l + 1];
+    int64_t zc = 0;
+    return c->post1 && c->o.smoother == MGP_RBGS && c->o.nu2 >= 1 && !(want_err && c->o.nu2 == 1) && !L.p.dist &&
+           !C.p.dist && mgp::post1_supported(c->rb, L.g, coarse_view(L, C, &zc));
+}
+
+int post_first(mgp_ctx* c, int l, double h)
+{
+    Level& L = c->lev[l];
+    Level& C = c->lev[l + 1];
+    TRY(materialize_zero(c, L));
+    TRY(materialize_zero(c, C));
+    int64_t zc = 0;
+    const Geo gc = coarse_view(L, C, &zc);
+    char* V = c->ui(C, C.u) + (size_t)(zc * C.g.P) * c->rb;
+    HIP_TRY(c, mgp::launch_post_first(c->rb, c->o.dim, c->o.prolong == MGP_PROLONG_LINEAR, c->ui(L, L.u), V,
+                                      c->ui(L, L.f), L.g, gc, h, coarse_coef(c->o.coarse_bc, l),
+                                      coarse_coef(c->o.coarse_bc, l + 1), c->s));
+    L.ghost_ok = true;
     L.ghost_zero = false;
     return MGP_OK;
 }
@@ -933,6 +966,9 @@ int cycle_rec(mgp_ctx* c, int l, double h, bool fcycle)
         TRY(fused_post(c, l, h, want_err));
     } else if (blk && !want_err) {
         TRY(block_post(c, l, h));
+    } else if (post1_ok(c, l, want_err)) {
+        TRY(post_first(c, l, h));
+        TRY(smooth(c, l, c->o.nu2, h, want_err, true));
     } else {
         TRY(prolong_correct(c, l));
         TRY(smooth(c, l, c->o.nu2, h, want_err));
@@ -1214,6 +1250,8 @@ static int create_impl(mgp_ctx** out, const mgp_opts* o, mgp_loopback* lb, ncclC
     {
         const char* v = std::getenv("MGP_FRESH");
         c->fresh_sweep = !(v && std::atoi(v) == 0);
+        const char* vp = std::getenv("MGP_POST1");
+        c->post1 = vp && std::atoi(vp) != 0;
     }
     {
         const char* v = std::getenv("MGP_DEEP_HALO");  // 0: exchange before every half-sweep instead

@@ -65,6 +65,12 @@ hipError_t launch_half_sweep(int rb, int dim, bool fine, int color, const void* 
 // alone, bit-identical to the red and black half-sweeps reading u = 0.  Levels with hw >= 16 / rb.
 bool fresh_supported(int rb, const Geo& g);
 hipError_t launch_fresh_sweep(int rb, int dim, const void* f, void* u, Geo g, double h, double cl, hipStream_t s);
+// prolong_correct + the red half of the first post-smoothing sweep in one pass: red cells of u from black u
+// + P V (never stored: the black half-sweep that follows replaces the black cells without reading
+// them).  Vector levels of one rank's box with coarse nx >= 16 / rb.
+bool post1_supported(int rb, const Geo& g, const Geo& gc);
+hipError_t launch_post_first(int rb, int dim, int linear, void* u, const void* V, const void* f, Geo g, Geo gc,
+                             double h, double cl, double clc, hipStream_t s);
 // Fused residual + restriction (calcResidual + reduceResidual): R (coarse packed, pointing at the
 // coarse plane of this rank's fine plane 0; its Geo is gc) from u, f of the fine level.
 hipError_t launch_residual_restrict(int rb, int dim, const void* u, const void* f, void* R, Geo g, Geo gc, double h,

@@ -88,6 +88,33 @@ __device__ __forceinline__ void vstore_nt(T* p, const Vec<T, N>& a)
     __builtin_nontemporal_store(r, reinterpret_cast<V4*>(p));
 }
 
+// Non-temporal 8- or 16-byte access, or a plain one (NT = false)
+template <typename T, int N, bool NT>
+__device__ __forceinline__ Vec<T, N> gload(const T* p)
+{
+    if constexpr (!NT) {
+        return vload<T, N>(p);
+    } else {
+        typedef float vt __attribute__((ext_vector_type(sizeof(T) * N / 4)));
+        const vt r = __builtin_nontemporal_load(reinterpret_cast<const vt*>(p));
+        Vec<T, N> a;
+        __builtin_memcpy(&a, &r, sizeof(a));
+        return a;
+    }
+}
+template <typename T, int N, bool NT>
+__device__ __forceinline__ void gstore(T* p, const Vec<T, N>& a)
+{
+    if constexpr (!NT) {
+        vstore<T, N>(p, a);
+    } else {
+        typedef float vt __attribute__((ext_vector_type(sizeof(T) * N / 4)));
+        vt r;
+        __builtin_memcpy(&r, &a, sizeof(a));
+        __builtin_nontemporal_store(r, reinterpret_cast<vt*>(p));
+    }
+}
+
 template <typename T, int N>
 __device__ __forceinline__ Vec<T, N> vzero()
 {
@@ -1059,18 +1086,90 @@ __device__ __forceinline__ void coarse_row(const T* __restrict__ V, const Geo& g
     c[N + 1] = I0 + N < gc.nx ? hp[cm + N / 2] : (T)0;
 }
 
+// The coarse neighbourhood of fine row (j, k) above coarse cells I0 .. I0+N-1 (coarse rows J, Jn and
+// planes K, Kn; Jn, Kn clamped to the parent row / plane outside the box, where the oracle's cval()
+// factor applies) and the oracle's per-cell prolongation value of its cells.
+template <typename T, int N, int DIM, int LINEAR>
+struct PvRow {
+    T c00[N + 2], c10[N + 2], c01[N + 2], c11[N + 2];  // [z: K / Kn][y: J / Jn]
+    bool oy, oz, interior;
+    int I0, cx;
+    __device__ __forceinline__ void load(const T* __restrict__ V, const Geo& gc, int j, int64_t k, int i0)
+    {
+        I0 = i0;
+        cx = gc.nx;
+        const int J = j >> 1;
+        const int64_t K = DIM == 3 ? (k >> 1) : 0;
+        int Jn = (j & 1) ? J + 1 : J - 1;
+        oy = Jn < 0 || Jn >= gc.ny;
+        if (oy) Jn = J;
+        int64_t Kn = K;
+        oz = false;
+        if (DIM == 3) {
+            Kn = (k & 1) ? K + 1 : K - 1;
+            oz = gc.z0 + Kn < 0 || gc.z0 + Kn >= gc.gnz;
+            if (oz) Kn = K;
+        }
+        coarse_row<T, N>(V, gc, J, K, I0, c00);
+        if (LINEAR) {
+            coarse_row<T, N>(V, gc, Jn, K, I0, c10);
+            if (DIM == 3) {
+                coarse_row<T, N>(V, gc, J, Kn, I0, c01);
+                coarse_row<T, N>(V, gc, Jn, Kn, I0, c11);
+            }
+        }
+        interior = !oy && !oz && I0 > 0 && I0 + N < cx;
+    }
+    // P V at the cell above coarse I0 + e with x parity o
+    __device__ __forceinline__ T value(int e, int o, T cl) const
+    {
+        const T w0 = (T)0.75, w1 = (T)0.25;
+        const int pe = e + 1;  // parent I0 + e
+        if (!LINEAR) return c00[pe];
+        if (interior) {  // no neighbour leaves the box: every factor is 1
+            const T nb00 = o ? c00[e + 2] : c00[e];
+            const T nb10 = o ? c10[e + 2] : c10[e];
+            const T a00 = w0 * c00[pe] + w1 * nb00;
+            const T a10 = w0 * c10[pe] + w1 * nb10;
+            if (DIM == 2) return w0 * a00 + w1 * a10;
+            const T nb01 = o ? c01[e + 2] : c01[e];
+            const T nb11 = o ? c11[e + 2] : c11[e];
+            const T a01 = w0 * c01[pe] + w1 * nb01;
+            const T a11 = w0 * c11[pe] + w1 * nb11;
+            const T b0 = w0 * a00 + w1 * a10;
+            const T b1 = w0 * a01 + w1 * a11;
+            return w0 * b0 + w1 * b1;
+        }
+        auto sv = [&](T val, bool fx, bool fy, bool fz) {
+            T s = (T)1;
+            if (fx) s = -cl * s;
+            if (fy) s = -cl * s;
+            if (fz) s = -cl * s;
+            return s == (T)1 ? val : s * val;
+        };
+        const bool ox = (o == 0 && I0 + e == 0) || (o == 1 && I0 + e == cx - 1);
+        // neighbour column: e (o = 0) or e + 2 (o = 1); the parent when out of the box
+        auto col = [&](const T (&cc)[N + 2]) { return ox ? cc[pe] : (o ? cc[e + 2] : cc[e]); };
+        const T a00 = w0 * c00[pe] + w1 * sv(col(c00), ox, false, false);
+        const T a10 = w0 * sv(c10[pe], false, oy, false) + w1 * sv(col(c10), ox, oy, false);
+        if (DIM == 2) return w0 * a00 + w1 * a10;
+        const T a01 = w0 * sv(c01[pe], false, false, oz) + w1 * sv(col(c01), ox, false, oz);
+        const T a11 = w0 * sv(c11[pe], false, oy, oz) + w1 * sv(col(c11), ox, oy, oz);
+        const T b0 = w0 * a00 + w1 * a10;
+        const T b1 = w0 * a01 + w1 * a11;
+        return w0 * b0 + w1 * b1;
+    }
+};
+
 // Vector form (coarse nx >= N): a thread owns the fine cells of one fine row (j, k) above N
-// consecutive coarse cells I0 .. — fine m = I0 .. in BOTH colours (one N-wide access of u each).
-// It needs the coarse rows J, Jn and planes K, Kn only (Jn, Kn clamped to the parent row/plane
-// outside the box, where the oracle's cval() factor applies) and evaluates exactly the oracle's
-// per-cell expression.
+// consecutive coarse cells I0 .. — fine m = I0 .. in BOTH colours (one N-wide access of u each) —
+// and evaluates exactly the oracle's per-cell expression (PvRow).
 template <typename T, int DIM, int LINEAR>
 __global__ __launch_bounds__(kBlock) void k_prolong_v(T* __restrict__ u, const T* __restrict__ V, Geo g, Geo gc,
                                                       T cl)
 {
     constexpr int N = VN<T>::n;
     constexpr int LN = N == 4 ? 2 : 1;
-    const int cx = gc.nx, cy = gc.ny;
     const int lgpr = gc.lx - LN;
     const int b = xcd_remap(blockIdx.x, gridDim.x);
     const int64_t it = (int64_t)b * kBlock + threadIdx.x;
@@ -1079,84 +1178,92 @@ __global__ __launch_bounds__(kBlock) void k_prolong_v(T* __restrict__ u, const T
     const int64_t k = DIM == 3 ? it >> (lgpr + g.ly) : 0;
     if (k >= g.nz) return;
     const int I0 = grp * N;
-    const int J = j >> 1;
-    const int64_t K = DIM == 3 ? (k >> 1) : 0;
-    int Jn = (j & 1) ? J + 1 : J - 1;
-    const bool oy = Jn < 0 || Jn >= cy;
-    if (oy) Jn = J;
-    int64_t Kn = K;
-    bool oz = false;
-    if (DIM == 3) {
-        Kn = (k & 1) ? K + 1 : K - 1;
-        oz = gc.z0 + Kn < 0 || gc.z0 + Kn >= gc.gnz;
-        if (oz) Kn = K;
-    }
-    T c00[N + 2], c10[N + 2], c01[N + 2], c11[N + 2];  // [z: K / Kn][y: J / Jn]
-    coarse_row<T, N>(V, gc, J, K, I0, c00);
-    if (LINEAR) {
-        coarse_row<T, N>(V, gc, Jn, K, I0, c10);
-        if (DIM == 3) {
-            coarse_row<T, N>(V, gc, J, Kn, I0, c01);
-            coarse_row<T, N>(V, gc, Jn, Kn, I0, c11);
-        }
-    }
-    const T w0 = (T)0.75, w1 = (T)0.25;
-    auto sv = [&](T val, bool fx, bool fy, bool fz) {
-        T s = (T)1;
-        if (fx) s = -cl * s;
-        if (fy) s = -cl * s;
-        if (fz) s = -cl * s;
-        return s == (T)1 ? val : s * val;
-    };
+    PvRow<T, N, DIM, LINEAR> pv;
+    pv.load(V, gc, j, k, I0);
     const int p = (int)((j + g.z0 + k) & 1);
-    const bool interior = !oy && !oz && I0 > 0 && I0 + N < cx;
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
         const int o = c ^ p;  // x parity of this colour's cells in row j
         const int64_t own = k * g.P + c * g.H + (int64_t)j * g.hw + I0;
         Vec<T, N> uv = vload<T, N>(u + own);
 #pragma unroll
-        for (int e = 0; e < N; ++e) {
-            const int pe = e + 1;  // parent I0 + e
-            T v;
-            if (!LINEAR) {
-                v = c00[pe];
-            } else if (interior) {  // no neighbour leaves the box: every factor is 1
-                const T nb00 = o ? c00[e + 2] : c00[e];
-                const T nb10 = o ? c10[e + 2] : c10[e];
-                const T a00 = w0 * c00[pe] + w1 * nb00;
-                const T a10 = w0 * c10[pe] + w1 * nb10;
-                if (DIM == 2) {
-                    v = w0 * a00 + w1 * a10;
-                } else {
-                    const T nb01 = o ? c01[e + 2] : c01[e];
-                    const T nb11 = o ? c11[e + 2] : c11[e];
-                    const T a01 = w0 * c01[pe] + w1 * nb01;
-                    const T a11 = w0 * c11[pe] + w1 * nb11;
-                    const T b0 = w0 * a00 + w1 * a10;
-                    const T b1 = w0 * a01 + w1 * a11;
-                    v = w0 * b0 + w1 * b1;
-                }
-            } else {
-                const bool ox = (o == 0 && I0 + e == 0) || (o == 1 && I0 + e == cx - 1);
-                // neighbour column: e (o = 0) or e + 2 (o = 1); the parent when out of the box
-                auto col = [&](const T (&cc)[N + 2]) { return ox ? cc[pe] : (o ? cc[e + 2] : cc[e]); };
-                const T a00 = w0 * c00[pe] + w1 * sv(col(c00), ox, false, false);
-                const T a10 = w0 * sv(c10[pe], false, oy, false) + w1 * sv(col(c10), ox, oy, false);
-                if (DIM == 2) {
-                    v = w0 * a00 + w1 * a10;
-                } else {
-                    const T a01 = w0 * sv(c01[pe], false, false, oz) + w1 * sv(col(c01), ox, false, oz);
-                    const T a11 = w0 * sv(c11[pe], false, oy, oz) + w1 * sv(col(c11), ox, oy, oz);
-                    const T b0 = w0 * a00 + w1 * a10;
-                    const T b1 = w0 * a01 + w1 * a11;
-                    v = w0 * b0 + w1 * b1;
-                }
-            }
-            uv.v[e] = uv.v[e] + v;
-        }
+        for (int e = 0; e < N; ++e) uv.v[e] = uv.v[e] + pv.value(e, o, cl);
         vstore<T, N>(u + own, uv);
     }
+}
+
+// Prolongation + correction fused with the first (red) half-sweep of the post-smoothing
+// (prolong_correct + the red half of smooth's first sweep).  The red half-sweep replaces every red
+// cell without reading it, and the black half-sweep after it replaces every black cell without
+// reading it, so u + P V is only ever read on black cells by this red half-sweep: each thread
+// evaluates it (PvRow, k_prolong_v's expressions) for the black neighbours of its N red cells —
+// its own row, rows j +- 1 and planes k +- 1, plus one edge cell — and writes only the red cells.
+// The black cells keep u without P V until the black half-sweep overwrites them.  HBM: read black u,
+// red f and V, write red u (the per-piece pair also writes and re-reads both colours of u).
+template <typename T, int DIM, int LINEAR>
+__global__ __launch_bounds__(kBlock) void k_post1(T* __restrict__ u, const T* __restrict__ V,
+                                                  const T* __restrict__ f, Geo g, Geo gc, Op<T, DIM> op, T clc)
+{
+    constexpr int N = VN<T>::n;
+    constexpr int LN = N == 4 ? 2 : 1;
+    const int lgpr = g.lhw - LN;
+    const int b = xcd_remap(blockIdx.x, gridDim.x);
+    const int64_t it = (int64_t)b * kBlock + threadIdx.x;
+    const int grp = (int)(it & ((1 << lgpr) - 1));
+    const int j = (int)((it >> lgpr) & (g.ny - 1));
+    const int64_t k = it >> (lgpr + g.ly);
+    if (k >= g.nz) return;
+    const int m0 = grp * N;
+    const int64_t gk = g.z0 + k;
+    const int orr = (int)((j + gk) & 1);  // x parity of this row's red cells (black: orr ^ 1)
+    // u + P V of black row (jj, kk) at m0 .. m0+N-1 (0 outside the box)
+    auto black_row = [&](int jj, int64_t kk, Vec<T, N>& r) {
+        const int64_t gkk = g.z0 + kk;
+        if (jj < 0 || jj >= g.ny || (DIM == 3 && (gkk < 0 || gkk >= g.gnz))) {
+            r = vzero<T, N>();
+            return;
+        }
+        const int ob = 1 ^ (int)((jj + gkk) & 1);
+        r = vload<T, N>(u + kk * g.P + g.H + (int64_t)jj * g.hw + m0);
+        PvRow<T, N, DIM, LINEAR> pv;
+        pv.load(V, gc, jj, kk, m0);
+#pragma unroll
+        for (int e = 0; e < N; ++e) r.v[e] = r.v[e] + pv.value(e, ob, clc);
+    };
+    Vec<T, N> bc, byl, byr, bzl, bzr;
+    black_row(j, k, bc);
+    black_row(j - 1, k, byl);
+    black_row(j + 1, k, byr);
+    if (DIM == 3) {
+        black_row(j, k - 1, bzl);
+        black_row(j, k + 1, bzr);
+    }
+    // the black x-neighbour outside the segment: m0 - 1 (red cells at even x) or m0 + N (odd x)
+    const int me = orr == 0 ? m0 - 1 : m0 + N;
+    T edge = (T)0;
+    if (me >= 0 && me < g.hw) {
+        const int i = 2 * me + (orr ^ 1);
+        edge = u[k * g.P + g.H + (int64_t)j * g.hw + me] + prolong_value<T, DIM, LINEAR>(V, g, gc, clc, i, j, k);
+    }
+    const int64_t own = k * g.P + (int64_t)j * g.hw + m0;
+    const Vec<T, N> fr = vload<T, N>(f + own);
+    const int nbyz = (j == 0) + (j == g.ny - 1) + (DIM == 3 ? (gk == 0) + (gk == g.gnz - 1) : 0);
+    Vec<T, N> out;
+#pragma unroll
+    for (int e = 0; e < N; ++e) {
+        const int i = 2 * (m0 + e) + orr;
+        const T xl = orr == 0 ? (e == 0 ? edge : bc.v[e - 1]) : bc.v[e];
+        const T xr = orr == 0 ? bc.v[e] : (e == N - 1 ? edge : bc.v[e + 1]);
+        T s = xl + xr;
+        s = s + byl.v[e];
+        s = s + byr.v[e];
+        if (DIM == 3) {
+            s = s + bzl.v[e];
+            s = s + bzr.v[e];
+        }
+        out.v[e] = op.relax(s, fr.v[e], nbyz + (i == 0) + (i == g.nx - 1));
+    }
+    vstore<T, N>(u + own, out);
 }
 
 // ---- z-streamed temporally blocked smoothing (3D, red/black 2+2) -------------------------------
@@ -1258,6 +1365,12 @@ struct ZsTile<double> {
                          NPRE = 2, NPOST = 2;
 };
 constexpr int kZsHX = 8;  // x halo cells per side (>= the trapezoid depth, whole groups)
+// Streaming (non-temporal) level-0 loads / stores of the phases: timing experiments (ZS_NT bit 0:
+// loads, bit 1: stores), so that the level-0 stream does not evict the coarse level it writes
+#ifndef ZS_NT
+#define ZS_NT 0
+#endif
+constexpr bool kZsNTL = (ZS_NT & 1) != 0, kZsNTS = (ZS_NT & 2) != 0;
 
 template <typename T, bool PRE>
 struct ZsShape {
@@ -1661,22 +1774,22 @@ __attribute__((amdgpu_waves_per_eu(1, PRE ? ZS_WPE_PRE : ZS_WPE_POST))) void k_z
 #else
             const int64_t pP = (int64_t)p * P, Pz = P;
 #endif
-            r.u = vload<T, N>(src_black + pP + goff);
-            r.f1 = vload<T, N>(f + (pP - Pz) + goff);
-            r.f2 = vload<T, N>(f + (pP - 2 * Pz) + Hh + goff);
+            r.u = gload<T, N, kZsNTL>(src_black + pP + goff);
+            r.f1 = gload<T, N, kZsNTL>(f + (pP - Pz) + goff);
+            r.f2 = gload<T, N, kZsNTL>(f + (pP - 2 * Pz) + Hh + goff);
             if (!PRE && ERR && tile_xy) {  // psiOld of plane p - 4, for the tile's own columns only
                 const T* dp = dst + (pP - 4 * Pz);
-                r.o0 = vload<T, N>(dp + goff);
-                r.o1 = vload<T, N>(dp + Hh + goff);
+                r.o0 = gload<T, N, kZsNTL>(dp + goff);
+                r.o1 = gload<T, N, kZsNTL>(dp + Hh + goff);
             }
         } else {
-            r.u = vload<T, N>(src_black + (int64_t)ZS_PLANE(pcl(p)) * P + goff);
-            r.f1 = vload<T, N>(f + (int64_t)ZS_PLANE(pcl(p - 1)) * P + goff);
-            r.f2 = vload<T, N>(f + (int64_t)ZS_PLANE(pcl(p - 2)) * P + Hh + goff);
+            r.u = gload<T, N, kZsNTL>(src_black + (int64_t)ZS_PLANE(pcl(p)) * P + goff);
+            r.f1 = gload<T, N, kZsNTL>(f + (int64_t)ZS_PLANE(pcl(p - 1)) * P + goff);
+            r.f2 = gload<T, N, kZsNTL>(f + (int64_t)ZS_PLANE(pcl(p - 2)) * P + Hh + goff);
             if (!PRE && ERR && tile_xy) {
                 const T* dp = dst + (int64_t)pcl(p - 4) * P;
-                r.o0 = vload<T, N>(dp + goff);
-                r.o1 = vload<T, N>(dp + Hh + goff);
+                r.o0 = gload<T, N, kZsNTL>(dp + goff);
+                r.o1 = gload<T, N, kZsNTL>(dp + Hh + goff);
             }
         }
     };
@@ -1801,8 +1914,8 @@ __attribute__((amdgpu_waves_per_eu(1, PRE ? ZS_WPE_PRE : ZS_WPE_POST))) void k_z
                     }
                 }
                 T* dp = dst + (int64_t)q * P;
-                vstore<T, N>(dp + goff, W3[sl(4)]);
-                vstore<T, N>(dp + Hh + goff, o4);
+                gstore<T, N, kZsNTS>(dp + goff, W3[sl(4)]);
+                gstore<T, N, kZsNTS>(dp + Hh + goff, o4);
             }
         }
 
@@ -2763,6 +2876,35 @@ static hipError_t fresh_t(const void* f, void* u, Geo g, double h, double cl, hi
 }
 
 bool fresh_supported(int rb, const Geo& g) { return half_vector(rb, g); }
+
+template <typename T, int D>
+static hipError_t post1_t(int linear, void* u, const void* V, const void* f, Geo g, Geo gc, double h, double cl,
+                          double clc, hipStream_t s)
+{
+    const int64_t items = half_items(sizeof(T), g);
+    const Op<T, D> op = make_op<T, D>(h, cl);
+    if (linear) k_post1<T, D, 1><<<nblk(items), kBlock, 0, s>>>((T*)u, (const T*)V, (const T*)f, g, gc, op, (T)clc);
+    else k_post1<T, D, 0><<<nblk(items), kBlock, 0, s>>>((T*)u, (const T*)V, (const T*)f, g, gc, op, (T)clc);
+    return hipGetLastError();
+}
+
+// the red cells of a row segment and their black neighbours' coarse rows come in whole vectors
+bool post1_supported(int rb, const Geo& g, const Geo& gc)
+{
+    const int n = 16 / rb;
+    return half_vector(rb, g) && gc.nx >= n && 2 * gc.nx == g.nx && g.z0 == 0 && g.gnz == g.nz;
+}
+
+hipError_t launch_post_first(int rb, int dim, int linear, void* u, const void* V, const void* f, Geo g, Geo gc,
+                             double h, double cl, double clc, hipStream_t s)
+{
+    if (!post1_supported(rb, g, gc)) return hipErrorInvalidValue;
+    if (rb == 8)
+        return dim == 3 ? post1_t<double, 3>(linear, u, V, f, g, gc, h, cl, clc, s)
+                        : post1_t<double, 2>(linear, u, V, f, g, gc, h, cl, clc, s);
+    return dim == 3 ? post1_t<float, 3>(linear, u, V, f, g, gc, h, cl, clc, s)
+                    : post1_t<float, 2>(linear, u, V, f, g, gc, h, cl, clc, s);
+}
 
 hipError_t launch_fresh_sweep(int rb, int dim, const void* f, void* u, Geo g, double h, double cl, hipStream_t s)
 {

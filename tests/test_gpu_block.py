@@ -190,3 +190,38 @@ def test_cubic_tail_equals_generic_tail_and_oracle(cfg, monkeypatch):
     for level in range(len(a.levels)):
         assert np.array_equal(a.get_psi(level), b.get_psi(level)), f"psi level {level}"
         assert np.array_equal(a.get_f(level), b.get_f(level)), f"f level {level}"
+
+
+POST1_CONFIGS = [
+    dict(dim=3, n=(64, 64, 64), real="double", nu1=2, nu2=2, prolong="linear", coarse_bc="consistent"),
+    dict(dim=3, n=(128, 64, 32), real="float", nu1=2, nu2=2, prolong="pc", coarse_bc="zero", cycle="F"),
+    dict(dim=3, n=(32, 64, 128), real="float", nu1=1, nu2=3, prolong="linear", coarse_bc="consistent",
+         coarse_init="warm"),
+    dict(dim=2, n=(256, 256, 1), real="float", nu1=2, nu2=2, prolong="linear", coarse_bc="consistent"),
+    dict(dim=2, n=(256, 128, 1), real="double", nu1=2, nu2=1, prolong="linear", coarse_bc="consistent", cycle="F"),
+]
+
+
+@pytest.mark.parametrize("cfg", POST1_CONFIGS, ids=_id)
+def test_post_first_half_sweep_matches_oracle(cfg, monkeypatch):
+    """k_post1 (prolongation + correction fused into the first post red half-sweep; u + P V of the
+    black cells never stored) == prolong_correct + smooth == the oracle, psi on every level, err to
+    summation order (tiled phases off, so every level above the tail runs per piece; 2D level 0 too)."""
+    kw = dict(smoother="rbgs", **cfg)
+    monkeypatch.setenv("MGP_BLK", "0")
+    monkeypatch.setenv("MGP_POST1", "1")
+    a = _ctx(**kw)
+    monkeypatch.setenv("MGP_POST1", "0")
+    b = _ctx(**kw)
+    o = Oracle(threads=8, **kw)
+    for x in (a, b, o):
+        x.init_point_charge()
+    for it in range(3):
+        old = o.get(0)
+        ea, eb, eo = a.cycle(), b.cycle(), o.step()
+        new = o.get(0)
+        assert np.array_equal(a.get_psi(), new), f"psi differs from the oracle after cycle {it + 1}"
+        assert np.array_equal(b.get_psi(), new)
+        _check_err(ea, eo, new, old)
+    for level in range(len(a.levels)):
+        assert np.array_equal(a.get_psi(level), b.get_psi(level)), f"psi level {level}"
