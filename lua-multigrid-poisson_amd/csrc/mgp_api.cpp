@@ -1151,12 +1151,27 @@ int mgp_comm_unique_id(void* out, int64_t nbytes)
     return MGP_OK;
 }
 
+static void select_engines(mgp_ctx* c);
+static int level_engine(const mgp_ctx* c, int l);
+
 int mgp_plan(const mgp_opts* o, int64_t* rows, int max_levels)
 {
     if (!o) return MGP_ERR_ARG;
     std::vector<LevelPlan> plan;
     int rc = plan_levels(*o, plan, g_create_error);
     if (rc != MGP_OK) return rc;
+    // the engines mgp_create would pick, on a device-free context
+    mgp_ctx c;
+    c.o = *o;
+    if (c.o.dim == 2) c.o.n[2] = 1;
+    c.rb = o->real_bytes;
+    for (auto& p : plan) {
+        Level L;
+        L.p = p;
+        L.g = make_geo(p, c.o.dim);
+        c.lev.push_back(L);
+    }
+    select_engines(&c);
     for (int l = 0; l < (int)plan.size() && l < max_levels && rows; ++l) {
         int64_t* r = rows + 8 * l;
         r[0] = plan[l].nx;
@@ -1165,7 +1180,8 @@ int mgp_plan(const mgp_opts* o, int64_t* rows, int max_levels)
         r[3] = plan[l].nz;
         r[4] = plan[l].z0;
         r[5] = plan[l].dist;
-        r[6] = r[7] = 0;
+        r[6] = level_engine(&c, l);
+        r[7] = 0;
     }
     return (int)plan.size();
 }
@@ -1228,6 +1244,53 @@ int mgp_create_loopback(mgp_ctx** out, const mgp_opts* o, mgp_loopback* lb)
         return MGP_ERR_ARG;
     }
     return create_impl(out, o, lb);
+}
+
+// How each level's phases run (host logic only, no device): the temporally blocked phases (k_zs),
+// the tiled one-launch phases (k_blk) and the one-launch coarse tail; shared by mgp_create and mgp_plan.
+static void select_engines(mgp_ctx* c)
+{
+    c->err_fuse = c->o.err_mode && c->o.smoother == MGP_RBGS && c->o.nu1 >= 1 && c->o.nu2 >= 1 && c->lev.size() > 1;
+    {
+        // temporally blocked phases (k_zs): RB-GS 2+2 on 3D levels of >= MGP_FUSED_MIN_CELLS cells (per
+        // rank); MGP_FUSED=0 turns them off (one launch per half-sweep, bit-identical results).  A
+        // distributed fused level exchanges kGhostZs-deep halos, so every level gets that many ghost planes.
+        const char* v = std::getenv("MGP_FUSED");
+        const char* vm = std::getenv("MGP_FUSED_MIN_CELLS");
+        const int64_t min_cells = vm ? std::atoll(vm) : (int64_t(1) << 25);
+        const bool on = !(v && std::atoi(v) == 0) && c->o.smoother == MGP_RBGS && c->o.nu1 == 2 && c->o.nu2 == 2;
+        for (size_t l = 0; l + 1 < c->lev.size(); ++l) {
+            Level& L = c->lev[l];
+            L.fused = on && level_cells(L) >= min_cells && mgp::fused_supported(c->rb, c->o.dim, 2, L.g);
+            if (L.fused) {
+                L.zc = mgp::fused_zc(c->rb, L.g, false);
+                L.zc_pre = mgp::fused_zc(c->rb, L.g, true);
+            }
+            if (L.fused && L.p.dist) c->G = mgp::kGhostZs;
+        }
+    }
+    {
+        // 3D-tiled one-launch phases (k_blk) on replicated RB-GS levels 1 .. of <= MGP_BLK_CELLS cells
+        // (default 2^18 = 64^3) below the finest; MGP_BLK=0 turns them off (bit-identical results)
+        const char* v = std::getenv("MGP_BLK");
+        const char* vm = std::getenv("MGP_BLK_CELLS");
+        const int64_t max_cells = vm ? std::atoll(vm) : (int64_t(1) << 18);
+        const int ns = std::max(c->o.nu1, c->o.nu2);
+        const bool on = !(v && std::atoi(v) == 0) && c->o.smoother == MGP_RBGS && c->o.nu1 >= 1 && c->o.nu2 >= 1;
+        for (size_t l = 1; l + 1 < c->lev.size(); ++l) {
+            Level& L = c->lev[l];
+            L.blk = on && !L.fused && !L.p.dist && level_cells(L) <= max_cells &&
+                    mgp::block_supported(c->rb, c->o.dim, ns, L.g);
+        }
+    }
+    plan_tail(c);
+}
+
+// mgp_level_info / mgp_plan engine code: 0 one launch per piece, 1 coarse tail, 2 k_zs, 3 k_blk
+static int level_engine(const mgp_ctx* c, int l)
+{
+    const Level& L = c->lev[l];
+    return c->tail_level >= 0 && l >= c->tail_level ? 1 : L.fused ? 2 : L.blk ? 3 : 0;
 }
 
 static int create_impl(mgp_ctx** out, const mgp_opts* o, mgp_loopback* lb, ncclComm_t ext_comm)
@@ -1294,39 +1357,7 @@ static int create_impl(mgp_ctx** out, const mgp_opts* o, mgp_loopback* lb, ncclC
         L.g = make_geo(p, c->o.dim);
         c->lev.push_back(L);
     }
-    c->err_fuse = c->o.err_mode && c->o.smoother == MGP_RBGS && c->o.nu1 >= 1 && c->o.nu2 >= 1 && c->lev.size() > 1;
-    {
-        // temporally blocked phases (k_zs): RB-GS 2+2 on 3D levels of >= MGP_FUSED_MIN_CELLS cells (per
-        // rank); MGP_FUSED=0 turns them off (one launch per half-sweep, bit-identical results).  A
-        // distributed fused level exchanges kGhostZs-deep halos, so every level gets that many ghost planes.
-        const char* v = std::getenv("MGP_FUSED");
-        const char* vm = std::getenv("MGP_FUSED_MIN_CELLS");
-        const int64_t min_cells = vm ? std::atoll(vm) : (int64_t(1) << 25);
-        const bool on = !(v && std::atoi(v) == 0) && c->o.smoother == MGP_RBGS && c->o.nu1 == 2 && c->o.nu2 == 2;
-        for (size_t l = 0; l + 1 < c->lev.size(); ++l) {
-            Level& L = c->lev[l];
-            L.fused = on && level_cells(L) >= min_cells && mgp::fused_supported(c->rb, c->o.dim, 2, L.g);
-            if (L.fused) {
-                L.zc = mgp::fused_zc(c->rb, L.g, false);
-                L.zc_pre = mgp::fused_zc(c->rb, L.g, true);
-            }
-            if (L.fused && L.p.dist) c->G = mgp::kGhostZs;
-        }
-    }
-    {
-        // 3D-tiled one-launch phases (k_blk) on replicated RB-GS levels 1 .. of <= MGP_BLK_CELLS cells
-        // (default 2^18 = 64^3) below the finest; MGP_BLK=0 turns them off (bit-identical results)
-        const char* v = std::getenv("MGP_BLK");
-        const char* vm = std::getenv("MGP_BLK_CELLS");
-        const int64_t max_cells = vm ? std::atoll(vm) : (int64_t(1) << 18);
-        const int ns = std::max(c->o.nu1, c->o.nu2);
-        const bool on = !(v && std::atoi(v) == 0) && c->o.smoother == MGP_RBGS && c->o.nu1 >= 1 && c->o.nu2 >= 1;
-        for (size_t l = 1; l + 1 < c->lev.size(); ++l) {
-            Level& L = c->lev[l];
-            L.blk = on && !L.fused && !L.p.dist && level_cells(L) <= max_cells &&
-                    mgp::block_supported(c->rb, c->o.dim, ns, L.g);
-        }
-    }
+    select_engines(c);
     for (auto& L : c->lev) L.alloc = L.g.P * (L.g.nz + 2 * c->G);
     for (size_t l = 0; l < c->lev.size(); ++l) {
         Level& L = c->lev[l];
@@ -1381,7 +1412,6 @@ static int create_impl(mgp_ctx** out, const mgp_opts* o, mgp_loopback* lb, ncclC
         const char* v = std::getenv("MGP_GRAPH");
         c->use_graph = c->o.world == 1 && !(v && std::atoi(v) == 0);
     }
-    plan_tail(c);
     if (c->o.smoother == MGP_RBGS && c->o.coarse_init == MGP_COARSE_FRESH) {
         for (size_t l = 1; l < c->lev.size(); ++l)
             if (!c->lev[l].fused && (c->tail_level < 0 || (int)l < c->tail_level))
@@ -1451,8 +1481,7 @@ int mgp_level_info(const mgp_ctx* c, int level, int64_t info[8])
     info[3] = p.nz;
     info[4] = p.z0;
     info[5] = p.dist;
-    const Level& L = c->lev[level];
-    info[6] = c->tail_level >= 0 && level >= c->tail_level ? 1 : L.fused ? 2 : L.blk ? 3 : 0;  // phase engine
+    info[6] = level_engine(c, level);
     info[7] = c->lev[level].exchanges;
     return MGP_OK;
 }
