@@ -37,8 +37,8 @@ HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=20)
-    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--steps", type=int, default=50)
+    p.add_argument("--warmup", type=int, default=10, help="untimed cycles (graph capture, clocks)")
     p.add_argument("--n", type=int, default=512, help="cells per axis of each rank's cube slab (weak scaling)")
     p.add_argument("--box", default=None, help="NX,NY,NZ global box, strong scaling over the ranks (slab-z)")
     p.add_argument("--dim", type=int, default=3, choices=[2, 3])
