@@ -1271,7 +1271,7 @@ __global__ __launch_bounds__(kBlock) void k_post1(T* __restrict__ u, const T* __
 // k_zs applies a whole smoothing phase of a level in ONE pass over HBM:
 //   PRE : 2 RB-GS sweeps, then residual + restriction (smooth(l, 2) + residual_restrict(l))
 //   POST: prolongation + correction, then 2 RB-GS sweeps (+ err) (prolong_correct + smooth(l, 2))
-// A workgroup owns an x-y tile (plus a halo of H rows and kZsHX cells per side) and a chunk of zc
+// A workgroup owns an x-y tile (plus a halo of H rows and S::HX >= H cells per side) and a chunk of zc
 // planes and streams through z.  Every thread owns one column of the extended tile: N consecutive
 // cells of each colour of one row.  At step p:
 //   stage 0   plane p of the input's BLACK cells (POST: plus the prolongation, k_prolong_v's
@@ -1364,7 +1364,6 @@ struct ZsTile<double> {
     static constexpr int TXPRE = ZS_TXPRE_F64, TXPOST = ZS_TXPOST_F64, TYPRE = ZS_TYPRE_F64, TYPOST = ZS_TYPOST_F64,
                          NPRE = 2, NPOST = 2;
 };
-constexpr int kZsHX = 8;  // x halo cells per side (>= the trapezoid depth, whole groups)
 // Streaming (non-temporal) level-0 loads / stores of the phases: timing experiments (ZS_NT bit 0:
 // loads, bit 1: stores), so that the level-0 stream does not evict the coarse level it writes
 #ifndef ZS_NT
@@ -1378,9 +1377,15 @@ struct ZsShape {
     static constexpr int TX = PRE ? ZsTile<T>::TXPRE : ZsTile<T>::TXPOST;
     static constexpr int TY = PRE ? ZsTile<T>::TYPRE : ZsTile<T>::TYPOST;
     static constexpr int H = PRE ? 5 : 4;              // y/z halo = stages that read neighbours
-    static constexpr int HWE = (TX + 2 * kZsHX) / 2;   // reals per LDS half-row
+    // x halo cells per side: the trapezoid depth H in whole column groups (2 N cells of x each)
+#ifdef ZS_HX_FIXED  // timing experiment: the round-1 fixed 8-cell x halo
+    static constexpr int HX = ZS_HX_FIXED;
+#else
+    static constexpr int HX = 2 * N * ((H + 2 * N - 1) / (2 * N));
+#endif
+    static constexpr int HWE = (TX + 2 * HX) / 2;      // reals per LDS half-row
     static constexpr int G = HWE / N;                  // column groups per row
-    static constexpr int HXG = kZsHX / 2 / N;          // halo groups per side
+    static constexpr int HXG = HX / 2 / N;             // halo groups per side
     static constexpr int YE = TY + 2 * H;
     static constexpr int NT = G * YE;                  // threads with a column
     static constexpr int NTL = (NT + 63) / 64 * 64;    // launched threads
@@ -1677,7 +1682,7 @@ __attribute__((amdgpu_waves_per_eu(1, PRE ? ZS_WPE_PRE : ZS_WPE_POST))) void k_z
     col.lrow = ye * HWE + m0;
     col.lym = (ye > 0 ? ye - 1 : ye) * HWE + m0;
     col.lyp = (ye < YE - 1 ? ye + 1 : ye) * HWE + m0;
-    col.gm = (X0 - kZsHX) / 2 + m0;  // global packed m of my first cell
+    col.gm = (X0 - S::HX) / 2 + m0;  // global packed m of my first cell
     col.x_first = gx == 0;
     col.x_last = gx == G - 1;
     col.lxm = col.x_first ? col.lrow : col.lrow - N;
