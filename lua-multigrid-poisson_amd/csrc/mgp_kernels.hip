@@ -175,6 +175,20 @@ struct Op {
         const T a_u = askew + diag(nb) * uc;
         return fc - a_u;
     }
+    // The same two with the table indexed directly (for an Op that lives in LDS, where a per-lane
+    // index is one read): dg[0] = adiag, ydg[0] = yadiag, and with cl = 0 every entry is those, so
+    // these equal relax / residual for every nb, without the branch or the select chain.
+    __device__ __forceinline__ T relax_idx(T sum, T fc, int nb) const
+    {
+        const T a = fc - sum * inv_hSq;
+        return div_rn(a, dg[nb], ydg[nb]);
+    }
+    __device__ __forceinline__ T residual_idx(T sum, T fc, T uc, int nb) const
+    {
+        const T askew = sum * inv_hSq;
+        const T a_u = askew + dg[nb] * uc;
+        return fc - a_u;
+    }
     // The same two with the diagonal computed and divided by directly (the oracle's expressions):
     // the temporally blocked phases' rare boundary path, where the table selects cost registers.
     __device__ __forceinline__ T diag_direct(int nb) const
@@ -2213,6 +2227,9 @@ constexpr int tc_levels()
 template <int DIM>
 constexpr int tc_top() { return DIM == 3 ? 16 : 64; }
 constexpr int kTcThreads = 1024;
+#ifndef TC_MAXL  // timing experiment: skip the ops of levels >= TC_MAXL (wrong results)
+#define TC_MAXL 16
+#endif
 
 template <typename T, int DIM, int N>
 __device__ __forceinline__ void tc_half(T* U, const T* F, const Op<T, DIM>& op, int c, int tid)
@@ -2236,7 +2253,7 @@ __device__ __forceinline__ void tc_half(T* U, const T* F, const Op<T, DIM>& op, 
                 sm = sm + U[x + L::W * L::W];
             }
             const int nb = (i == 0) + (i == N - 1) + (j == 0) + (j == N - 1) + (DIM == 3 ? (k == 0) + (k == N - 1) : 0);
-            U[x] = op.relax(sm, F[x], nb);
+            U[x] = op.relax_idx(sm, F[x], nb);
         }
     }
 }
@@ -2257,7 +2274,7 @@ __device__ __forceinline__ void tc_rr(const T* U, const T* F, T* Fc, const Op<T,
             sm = sm + U[x + L::W * L::W];
         }
         const int nb = (i == 0) + (i == N - 1) + (j == 0) + (j == N - 1) + (DIM == 3 ? (k == 0) + (k == N - 1) : 0);
-        return op.residual(sm, F[x], U[x], nb);
+        return op.residual_idx(sm, F[x], U[x], nb);
     };
     for (int q = tid; q < CNT; q += kTcThreads) {
         const int I = q % M, J = (q / M) % M, K = DIM == 3 ? q / (M * M) : 0;
@@ -2372,7 +2389,7 @@ __global__ __launch_bounds__(kTcThreads) void k_tail_c(const TailArgs<T, DIM> a)
         asm volatile("" : "+v"(tid));
 #define TC_CASE(L)                                                                                     \
     case L:                                                                                            \
-        if constexpr ((L) < NL) {                                                                      \
+        if constexpr ((L) < NL && (L) < TC_MAXL) {                                                     \
             constexpr int N = TN >> (L);                                                               \
             if (op == TAIL_SMOOTH) {                                                                   \
                 for (int sw = 0; sw < arg; ++sw) {                                                     \
@@ -2471,6 +2488,8 @@ __global__ __launch_bounds__(blk_threads<DIM>()) void k_blk(const T* __restrict_
     T* const F = U + S::cells;
     T* const RS = F + S::cells;  // PRE: residuals of the owned cells (x fastest)
     const int tid = threadIdx.x;
+    __shared__ Op<T, DIM> sop;  // the operator in LDS: its diagonal table is indexed per cell
+    if (tid == 0) sop = op;
     const int ntx = g.nx / B, nty = g.ny / B;
     const int b = blockIdx.x;
     const int X0 = (b % ntx) * B, Y0 = ((b / ntx) % nty) * B, Z0 = (b / (ntx * nty)) * BZ;
@@ -2550,7 +2569,7 @@ __global__ __launch_bounds__(blk_threads<DIM>()) void k_blk(const T* __restrict_
                 gkl < nzl) {
                 const T sum = nbsum(lx, ly, lz, c);
                 const int own = S::lidx(lz, ly, c, mm);
-                U[own] = op.relax(sum, F[own], faces(gi, gj, gz0 + gkl));
+                U[own] = sop.relax_idx(sum, F[own], faces(gi, gj, gz0 + gkl));
             }
         }
         __syncthreads();
@@ -2567,7 +2586,7 @@ __global__ __launch_bounds__(blk_threads<DIM>()) void k_blk(const T* __restrict_
                 const int c = (lx & 1) ^ ((ly + lz + p0) & 1);
                 const int own = S::lidx(lz, ly, c, lx >> 1);
                 const T sum = nbsum(lx, ly, lz, c);
-                RS[it] = op.residual(sum, F[own], U[own], faces(X0 + x, Y0 + y, gz0 + Z0 + z));
+                RS[it] = sop.residual_idx(sum, F[own], U[own], faces(X0 + x, Y0 + y, gz0 + Z0 + z));
             }
         }
         __syncthreads();
