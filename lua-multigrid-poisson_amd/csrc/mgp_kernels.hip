@@ -2238,7 +2238,7 @@ __device__ __forceinline__ void tc_half(T* U, const T* F, const Op<T, DIM>& op, 
     constexpr int HN = N >= 2 ? N / 2 : 1;
     constexpr int CNT = N >= 2 ? L::CELLS / 2 : 1;
     if (N == 1 && c == 1) return;  // the single cell is red
-#pragma unroll 1
+#pragma unroll
     for (int q0 = 0; q0 < CNT; q0 += kTcThreads) {
         const int q = q0 + tid;
         if (q < CNT) {
@@ -2342,23 +2342,38 @@ __device__ __forceinline__ void tc_prolong(T* U, const T* V, T cl, int tid)
     }
 }
 
-// level l of the tail: copy in (zero halo; zero_u: a fresh guess) or out, packed global layout
+// level l of the tail: copy in (zero halo; zero_u: a fresh guess) or out, packed global layout; a
+// thread's loads are all issued before its LDS stores (compile-time trip count)
 template <typename T, int DIM, int N>
 __device__ __forceinline__ void tc_copy(T* U, T* F, T* gu, T* gf, bool in, bool zero_u, int tid)
 {
     using L = TcLev<DIM, N>;
     constexpr int HW = N >= 2 ? N / 2 : 1;
     constexpr int64_t H = (int64_t)HW * N, P = 2 * H;
-    for (int q = tid; q < L::P; q += kTcThreads) {
+    constexpr int IT = (L::P + kTcThreads - 1) / kTcThreads;
+    T uv[IT], fv[IT];
+#pragma unroll
+    for (int r = 0; r < IT; ++r) {
+        const int q = tid + r * kTcThreads;
         const int i = q % L::W - 1, j = (q / L::W) % L::W - 1, k = DIM == 3 ? q / (L::W * L::W) - 1 : 0;
-        const bool inside = i >= 0 && i < N && j >= 0 && j < N && k >= 0 && k < N;
+        const bool inside = q < L::P && i >= 0 && i < N && j >= 0 && j < N && k >= 0 && k < N;
         const int64_t gi = (int64_t)k * P + ((i + j + k) & 1) * H + (int64_t)j * HW + (i >> 1);
         if (in) {
-            U[q] = inside && !zero_u ? gu[gi] : (T)0;
-            F[q] = inside ? gf[gi] : (T)0;
+            uv[r] = inside && !zero_u ? gu[gi] : (T)0;
+            fv[r] = inside ? gf[gi] : (T)0;
         } else if (inside) {
             gu[gi] = U[q];
             gf[gi] = F[q];
+        }
+    }
+    if (in) {
+#pragma unroll
+        for (int r = 0; r < IT; ++r) {
+            const int q = tid + r * kTcThreads;
+            if (q < L::P) {
+                U[q] = uv[r];
+                F[q] = fv[r];
+            }
         }
     }
 }
