@@ -156,6 +156,7 @@ struct mgp_ctx {
     bool deep_halo = true;  // smooth_deep on distributed levels below the finest
     bool fresh_sweep = true;        // k_fresh for the first sweep of a lazily zeroed level (MGP_FRESH=0: off)
     bool lazy_zero = true;          // fresh coarse guesses without a memset where a reader can take it (MGP_LAZY_ZERO=0: off)
+    bool post_black = true;         // the cycle's prolongation corrects the black cells only (MGP_POST_BLACK=0: both)
     bool post1 = false;             // k_post1: prolongation fused into the first post red half-sweep (MGP_POST1=1;
                                     // measured slower: 5 rows of P V per thread cost more VALU and L2 loads
                                     // than the prolongation pass it saves)
@@ -594,7 +595,9 @@ int residual_restrict(mgp_ctx* c, int l, double h)
     return MGP_OK;
 }
 
-int prolong_correct(mgp_ctx* c, int l)
+// black_only: the cycle's correction before a red/black post-smoothing (k_prolong_v skips the red
+// cells, which the first post half-sweep replaces without reading)
+int prolong_correct(mgp_ctx* c, int l, bool black_only = false)
 {
     Level& L = c->lev[l];
     Level& C = c->lev[l + 1];
@@ -606,7 +609,7 @@ int prolong_correct(mgp_ctx* c, int l)
     const Geo gc = coarse_view(L, C, &zc);
     char* V = c->ui(C, C.u) + (size_t)(zc * C.g.P) * c->rb;
     HIP_TRY(c, mgp::launch_prolong_correct(c->rb, c->o.dim, linear, c->ui(L, L.u), V, L.g, gc,
-                                           coarse_coef(c->o.coarse_bc, l + 1), c->s));
+                                           coarse_coef(c->o.coarse_bc, l + 1), c->s, black_only));
     L.ghost_ok = !L.p.dist;
     L.ghost_zero = false;
     return MGP_OK;
@@ -970,7 +973,7 @@ int cycle_rec(mgp_ctx* c, int l, double h, bool fcycle)
         TRY(post_first(c, l, h));
         TRY(smooth(c, l, c->o.nu2, h, want_err, true));
     } else {
-        TRY(prolong_correct(c, l));
+        TRY(prolong_correct(c, l, c->post_black && c->o.smoother == MGP_RBGS && c->o.nu2 >= 1));
         TRY(smooth(c, l, c->o.nu2, h, want_err));
     }
     return MGP_OK;
@@ -1313,6 +1316,8 @@ static int create_impl(mgp_ctx** out, const mgp_opts* o, mgp_loopback* lb, ncclC
     {
         const char* v = std::getenv("MGP_FRESH");
         c->fresh_sweep = !(v && std::atoi(v) == 0);
+        const char* vb = std::getenv("MGP_POST_BLACK");
+        c->post_black = !(vb && std::atoi(vb) == 0);
         const char* vp = std::getenv("MGP_POST1");
         c->post1 = vp && std::atoi(vp) != 0;
     }

@@ -77,8 +77,10 @@ hipError_t launch_residual_restrict(int rb, int dim, const void* u, const void* 
                                     double cl, hipStream_t s);
 // u += P V (expandResidual + addTo); V points at the coarse plane gc.z0, which must correspond to
 // this rank's fine plane 0; planes -1 and gc.nz of V must be readable for the linear kind.
+// black_only: the black cells only (before a red/black post-smoothing: its red half-sweep replaces
+// every red cell without reading it).
 hipError_t launch_prolong_correct(int rb, int dim, int linear, void* u, const void* V, Geo g, Geo gc, double clc,
-                                  hipStream_t s);
+                                  hipStream_t s, bool black_only = false);
 // Deterministic two-pass fp64 sum of (a - b)^2 over n elements into *out (ctr != nullptr: into
 // out[*ctr], then ++*ctr on the device).
 hipError_t launch_sqdiff_sum(int rb, const void* a, const void* b, int64_t n, double* partials, double* out,

@@ -1178,7 +1178,9 @@ struct PvRow {
 // Vector form (coarse nx >= N): a thread owns the fine cells of one fine row (j, k) above N
 // consecutive coarse cells I0 .. — fine m = I0 .. in BOTH colours (one N-wide access of u each) —
 // and evaluates exactly the oracle's per-cell expression (PvRow).
-template <typename T, int DIM, int LINEAR>
+// BLACK: only the black cells (the cycle's prolongation before a red/black post-smoothing, whose red
+// half-sweep replaces every red cell without reading it)
+template <typename T, int DIM, int LINEAR, bool BLACK = false>
 __global__ __launch_bounds__(kBlock) void k_prolong_v(T* __restrict__ u, const T* __restrict__ V, Geo g, Geo gc,
                                                       T cl)
 {
@@ -1196,7 +1198,7 @@ __global__ __launch_bounds__(kBlock) void k_prolong_v(T* __restrict__ u, const T
     pv.load(V, gc, j, k, I0);
     const int p = (int)((j + g.z0 + k) & 1);
 #pragma unroll
-    for (int c = 0; c < 2; ++c) {
+    for (int c = BLACK ? 1 : 0; c < 2; ++c) {
         const int o = c ^ p;  // x parity of this colour's cells in row j
         const int64_t own = k * g.P + c * g.H + (int64_t)j * g.hw + I0;
         Vec<T, N> uv = vload<T, N>(u + own);
@@ -2988,16 +2990,22 @@ hipError_t launch_residual_restrict(int rb, int dim, const void* u, const void* 
 }
 
 template <typename T, int D>
-static hipError_t pr_t(int linear, void* u, const void* V, Geo g, Geo gc, double clc, hipStream_t s)
+static hipError_t pr_t(int linear, void* u, const void* V, Geo g, Geo gc, double clc, bool black, hipStream_t s)
 {
     constexpr int n = VN<T>::n;
     if (gc.nx >= n) {
         const int64_t items = (int64_t)(gc.nx / n) * g.ny * g.nz;
-        if (linear) k_prolong_v<T, D, 1><<<nblk(items), kBlock, 0, s>>>((T*)u, (const T*)V, g, gc, (T)clc);
-        else k_prolong_v<T, D, 0><<<nblk(items), kBlock, 0, s>>>((T*)u, (const T*)V, g, gc, (T)clc);
+        const unsigned nb = nblk(items);
+        if (black) {
+            if (linear) k_prolong_v<T, D, 1, true><<<nb, kBlock, 0, s>>>((T*)u, (const T*)V, g, gc, (T)clc);
+            else k_prolong_v<T, D, 0, true><<<nb, kBlock, 0, s>>>((T*)u, (const T*)V, g, gc, (T)clc);
+        } else {
+            if (linear) k_prolong_v<T, D, 1><<<nb, kBlock, 0, s>>>((T*)u, (const T*)V, g, gc, (T)clc);
+            else k_prolong_v<T, D, 0><<<nb, kBlock, 0, s>>>((T*)u, (const T*)V, g, gc, (T)clc);
+        }
         return hipGetLastError();
     }
-    for (int color = 0; color < 2; ++color) {
+    for (int color = black ? 1 : 0; color < 2; ++color) {
         const unsigned nb = nblk(g.H * g.nz);
         if (linear) k_prolong<T, D, 1><<<nb, kBlock, 0, s>>>((T*)u, (const T*)V, g, gc, clc, color);
         else k_prolong<T, D, 0><<<nb, kBlock, 0, s>>>((T*)u, (const T*)V, g, gc, clc, color);
@@ -3008,10 +3016,13 @@ static hipError_t pr_t(int linear, void* u, const void* V, Geo g, Geo gc, double
 }
 
 hipError_t launch_prolong_correct(int rb, int dim, int linear, void* u, const void* V, Geo g, Geo gc, double clc,
-                                  hipStream_t s)
+                                  hipStream_t s, bool black_only)
 {
-    if (rb == 8) return dim == 3 ? pr_t<double, 3>(linear, u, V, g, gc, clc, s) : pr_t<double, 2>(linear, u, V, g, gc, clc, s);
-    return dim == 3 ? pr_t<float, 3>(linear, u, V, g, gc, clc, s) : pr_t<float, 2>(linear, u, V, g, gc, clc, s);
+    if (rb == 8)
+        return dim == 3 ? pr_t<double, 3>(linear, u, V, g, gc, clc, black_only, s)
+                        : pr_t<double, 2>(linear, u, V, g, gc, clc, black_only, s);
+    return dim == 3 ? pr_t<float, 3>(linear, u, V, g, gc, clc, black_only, s)
+                    : pr_t<float, 2>(linear, u, V, g, gc, clc, black_only, s);
 }
 
 // ---- fused smoothing phases ----

@@ -225,3 +225,29 @@ def test_post_first_half_sweep_matches_oracle(cfg, monkeypatch):
         _check_err(ea, eo, new, old)
     for level in range(len(a.levels)):
         assert np.array_equal(a.get_psi(level), b.get_psi(level)), f"psi level {level}"
+
+
+@pytest.mark.parametrize("cfg", FRESH_CONFIGS + [
+    dict(dim=3, n=(64, 64, 64), real="float", nu1=2, nu2=1, prolong="pc", coarse_bc="consistent", coarse_init="warm"),
+], ids=_id)
+def test_black_only_prolongation_matches_oracle(cfg, monkeypatch):
+    """The cycle's prolongation corrects only the black cells before a red/black post-smoothing (its red
+    half-sweep replaces every red cell without reading it): == correcting both colours == the oracle."""
+    kw = dict(smoother="rbgs", **cfg)
+    monkeypatch.setenv("MGP_BLK", "0")
+    monkeypatch.setenv("MGP_POST_BLACK", "1")
+    a = _ctx(**kw)
+    monkeypatch.setenv("MGP_POST_BLACK", "0")
+    b = _ctx(**kw)
+    o = Oracle(threads=8, **kw)
+    for x in (a, b, o):
+        x.init_point_charge()
+    for it in range(3):
+        old = o.get(0)
+        ea, eb, eo = a.cycle(), b.cycle(), o.step()
+        new = o.get(0)
+        assert np.array_equal(a.get_psi(), new), f"psi differs from the oracle after cycle {it + 1}"
+        assert np.array_equal(b.get_psi(), new)
+        _check_err(ea, eo, new, old)
+    for level in range(len(a.levels)):
+        assert np.array_equal(a.get_psi(level), b.get_psi(level)), f"psi level {level}"
