@@ -531,7 +531,9 @@ int smooth(mgp_ctx* c, int l, int sweeps, double h, bool want_err = false, bool 
         if (sw == 0 && L.zero_pending && c->fresh_sweep && !oop && !last_err && !L.p.dist &&
             mgp::fresh_supported(c->rb, L.g)) {
             // the first sweep of a fresh zero guess from f alone (k_fresh: both colours, one pass)
-            HIP_TRY(c, mgp::launch_fresh_sweep(c->rb, c->o.dim, c->ui(L, L.f), c->ui(L, L.u), L.g, h, cl, c->s));
+            // with a second sweep to come its red half-sweep replaces the red cells unread: not stored
+            HIP_TRY(c, mgp::launch_fresh_sweep(c->rb, c->o.dim, c->ui(L, L.f), c->ui(L, L.u), L.g, h, cl, c->s,
+                                               sweeps < 2));
             L.zero_pending = false;
             L.ghost_ok = true;
             L.ghost_zero = false;

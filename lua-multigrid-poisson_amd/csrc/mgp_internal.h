@@ -64,7 +64,9 @@ hipError_t launch_half_sweep(int rb, int dim, bool fine, int color, const void* 
 // The first red/black sweep of a fresh zero guess (cpu.lua:138) in one pass: u (both colours) from f
 // alone, bit-identical to the red and black half-sweeps reading u = 0.  Levels with hw >= 16 / rb.
 bool fresh_supported(int rb, const Geo& g);
-hipError_t launch_fresh_sweep(int rb, int dim, const void* f, void* u, Geo g, double h, double cl, hipStream_t s);
+// store_red = false: the red cells are left as they are (a later sweep's red half-sweep replaces them unread).
+hipError_t launch_fresh_sweep(int rb, int dim, const void* f, void* u, Geo g, double h, double cl, hipStream_t s,
+                              bool store_red = true);
 // prolong_correct + the red half of the first post-smoothing sweep in one pass: red cells of u from black u
 // + P V (never stored: the black half-sweep that follows replaces the black cells without reading
 // them).  Vector levels of one rank's box with coarse nx >= 16 / rb.

@@ -613,7 +613,8 @@ __global__ __launch_bounds__(kBlock) void k_half_s(const T* __restrict__ other, 
 // half-sweeps reading a zero black input.  A thread owns the N red and N black cells at half
 // positions m0 .. m0+N-1 of one row.  HBM: read f, write u (the per-piece pair also reads the
 // zero input and re-reads the red cells).
-template <typename T, int DIM>
+// RED = false: the red cells are not stored (a later sweep's red half-sweep replaces them unread)
+template <typename T, int DIM, bool RED = true>
 __global__ __launch_bounds__(kBlock) void k_fresh(const T* __restrict__ f, T* __restrict__ u, Geo g, Op<T, DIM> op)
 {
     constexpr int N = VN<T>::n;
@@ -678,7 +679,7 @@ __global__ __launch_bounds__(kBlock) void k_fresh(const T* __restrict__ f, T* __
         }
         out.v[e] = op.relax(s, fb.v[e], nbyz + (i == 0) + (i == g.nx - 1));
     }
-    vstore<T, N>(u + own, rc);
+    if (RED) vstore<T, N>(u + own, rc);
     vstore<T, N>(u + own + g.H, out);
 }
 
@@ -2909,10 +2910,11 @@ hipError_t launch_half_sweep(int rb, int dim, bool fine, int color, const void* 
 }
 
 template <typename T, int D>
-static hipError_t fresh_t(const void* f, void* u, Geo g, double h, double cl, hipStream_t s)
+static hipError_t fresh_t(const void* f, void* u, Geo g, double h, double cl, bool red, hipStream_t s)
 {
     const int64_t items = half_items(sizeof(T), g);
-    k_fresh<T, D><<<nblk(items), kBlock, 0, s>>>((const T*)f, (T*)u, g, make_op<T, D>(h, cl));
+    if (red) k_fresh<T, D, true><<<nblk(items), kBlock, 0, s>>>((const T*)f, (T*)u, g, make_op<T, D>(h, cl));
+    else k_fresh<T, D, false><<<nblk(items), kBlock, 0, s>>>((const T*)f, (T*)u, g, make_op<T, D>(h, cl));
     return hipGetLastError();
 }
 
@@ -2947,11 +2949,13 @@ hipError_t launch_post_first(int rb, int dim, int linear, void* u, const void* V
                     : post1_t<float, 2>(linear, u, V, f, g, gc, h, cl, clc, s);
 }
 
-hipError_t launch_fresh_sweep(int rb, int dim, const void* f, void* u, Geo g, double h, double cl, hipStream_t s)
+hipError_t launch_fresh_sweep(int rb, int dim, const void* f, void* u, Geo g, double h, double cl, hipStream_t s,
+                              bool store_red)
 {
     if (!fresh_supported(rb, g)) return hipErrorInvalidValue;
-    if (rb == 8) return dim == 3 ? fresh_t<double, 3>(f, u, g, h, cl, s) : fresh_t<double, 2>(f, u, g, h, cl, s);
-    return dim == 3 ? fresh_t<float, 3>(f, u, g, h, cl, s) : fresh_t<float, 2>(f, u, g, h, cl, s);
+    if (rb == 8)
+        return dim == 3 ? fresh_t<double, 3>(f, u, g, h, cl, store_red, s) : fresh_t<double, 2>(f, u, g, h, cl, store_red, s);
+    return dim == 3 ? fresh_t<float, 3>(f, u, g, h, cl, store_red, s) : fresh_t<float, 2>(f, u, g, h, cl, store_red, s);
 }
 
 template <typename T, int D>
