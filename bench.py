@@ -182,9 +182,11 @@ def main():
                "fused_post": f"k_zs<{tname}, false, {lin}, true, true>"}
     # Algorithmic bytes per level-0 cell of one launch (reals): what the launch must move
     # to and from HBM.  half_sweep: read the other colour and f, write this colour of half the cells.
-    # fused_pre (k_zs: 2 RB-GS sweeps + residual + restriction): read black u and f, write u and R/8.
+    # fused_pre (k_zs: 2 RB-GS sweeps + residual + restriction): read black u and f, write black u and R/8
+    # (its red cells are never read: the only reader, fused_post, loads black cells and its first red
+    # half-sweep replaces the red ones).
     # fused_post (k_zs: prolongation + correction + 2 sweeps + err): read black u, V/8, f, psiOld; write u.
-    algo_reals = {"half_sweep": 1.5, "fused_pre": 2.625, "fused_post": 3.625}
+    algo_reals = {"half_sweep": 1.5, "fused_pre": 2.125, "fused_post": 3.625}
     per_kind = {k: v for k, v in timed.items() if v[1] > 0}
     cells = cells_rank
     if per_kind:

@@ -1387,6 +1387,10 @@ struct ZsTile<double> {
 #define ZS_NT 0
 #endif
 constexpr bool kZsNTL = (ZS_NT & 1) != 0, kZsNTS = (ZS_NT & 2) != 0;
+#ifndef ZS_PRE_RED_STORE  // timing experiment: PRE stores its (unread) red cells too
+#define ZS_PRE_RED_STORE 0
+#endif
+constexpr bool kZsPreRed = ZS_PRE_RED_STORE != 0;
 
 template <typename T, bool PRE>
 struct ZsShape {
@@ -1936,7 +1940,9 @@ __attribute__((amdgpu_waves_per_eu(1, PRE ? ZS_WPE_PRE : ZS_WPE_POST))) void k_z
                     }
                 }
                 T* dp = dst + (int64_t)q * P;
-                gstore<T, N, kZsNTS>(dp + goff, W3[sl(4)]);
+                // PRE: the red cells are not stored.  Its output is read only by POST, whose stage 0
+                // loads the black cells (the first post half-sweep replaces the red ones unread).
+                if (!PRE || kZsPreRed) gstore<T, N, kZsNTS>(dp + goff, W3[sl(4)]);
                 gstore<T, N, kZsNTS>(dp + Hh + goff, o4);
             }
         }
