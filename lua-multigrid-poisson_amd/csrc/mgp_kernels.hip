@@ -2631,14 +2631,16 @@ __global__ __launch_bounds__(blk_threads<DIM>()) void k_blk(const T* __restrict_
             R[pidx(gc, (X0 >> 1) + I, (Y0 >> 1) + J, (int64_t)((Z0 >> 1) + K))] = (DIM == 3 ? (T)0.125 : (T)0.25) * sm;
         }
     }
-    // the owned cells (both colours) to dst
+    // the owned cells to dst: both colours after POST; only the black ones after PRE (its output is read
+    // only by POST, which loads black cells and whose first red half-sweep replaces the red ones)
     {
-        constexpr int H2 = B / 2, n = BZ * B * 2 * H2;
+        constexpr int NC = PRE ? 1 : 2;  // colours stored
+        constexpr int H2 = B / 2, n = BZ * B * NC * H2;
 #pragma unroll
         for (int q = 0; q < (n + NT - 1) / NT; ++q) {
             const int it = tid + q * NT;
             if (it < n) {
-                const int mm = it % H2, c = (it / H2) & 1, ly = (it / (2 * H2)) % B, lz = it / (2 * H2 * B);
+                const int mm = it % H2, c = PRE ? 1 : (it / H2) & 1, ly = (it / (NC * H2)) % B, lz = it / (NC * H2 * B);
                 dst[(int64_t)(Z0 + lz) * g.P + c * g.H + (int64_t)(Y0 + ly) * g.hw + (X0 >> 1) + mm] =
                     U[S::lidx(lz + EZH, ly + E, c, (HX >> 1) + mm)];
             }
