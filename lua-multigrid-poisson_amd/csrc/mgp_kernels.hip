@@ -995,29 +995,27 @@ __global__ __launch_bounds__(kBlock) void k_resrestrict(const T* __restrict__ u,
 
 // ---- prolongation + correction --------------------------------------------------------------
 
-// coarse value at (I, J, K) (K relative to the V pointer), times the ghost factor of the
-// linear kind (oracle cval(): -cl per out-of-box axis, in x, y, z order)
+// The oracle's cval() factor: -cl per out-of-box axis, in x, y, z order, applied to coarse value v
 template <typename T>
-__device__ __forceinline__ T cval(const T* __restrict__ V, const Geo& gc, int I, int J, int64_t K, bool ox, bool oy,
-                                  bool oz, T cl)
+__device__ __forceinline__ T cfac(T v, bool ox, bool oy, bool oz, T cl)
 {
     T s = (T)1;
     if (ox) s = -cl * s;
     if (oy) s = -cl * s;
     if (oz) s = -cl * s;
-    const T v = V[pidx(gc, I, J, K)];
     return s == (T)1 ? v : s * v;
 }
 
-// (P V) at fine cell (i, j, local plane k): the oracle's per-cell prolongation value.
-template <typename T, int DIM, int LINEAR>
-__device__ __forceinline__ T prolong_value(const T* V, const Geo& g, const Geo& gc, T cl, int i, int j, int64_t k)
+// (P V) at fine cell (i, j, local plane k): the oracle's per-cell prolongation value, with the coarse
+// values read through get(I, J, K) (K relative to the V pointer; always inside the box).
+template <typename T, int DIM, int LINEAR, typename Get>
+__device__ __forceinline__ T prolong_eval(const Get& get, const Geo& gc, T cl, int i, int j, int64_t k)
 {
     const int I = i >> 1, J = j >> 1;
     const int64_t K = DIM == 3 ? (k >> 1) : 0;
     T v;
     if (!LINEAR) {
-        v = V[pidx(gc, I, J, K)];
+        v = get(I, J, K);
     } else {
         const T w0 = (T)0.75, w1 = (T)0.25;
         int In = (i & 1) ? I + 1 : I - 1;
@@ -1027,24 +1025,32 @@ __device__ __forceinline__ T prolong_value(const T* V, const Geo& g, const Geo& 
         if (ox) In = I;
         if (oy) Jn = J;
         if (DIM == 2) {
-            const T a0 = w0 * cval(V, gc, I, J, 0, false, false, false, cl) + w1 * cval(V, gc, In, J, 0, ox, false, false, cl);
-            const T a1 = w0 * cval(V, gc, I, Jn, 0, false, oy, false, cl) + w1 * cval(V, gc, In, Jn, 0, ox, oy, false, cl);
+            const T a0 = w0 * cfac(get(I, J, 0), false, false, false, cl) + w1 * cfac(get(In, J, 0), ox, false, false, cl);
+            const T a1 = w0 * cfac(get(I, Jn, 0), false, oy, false, cl) + w1 * cfac(get(In, Jn, 0), ox, oy, false, cl);
             v = w0 * a0 + w1 * a1;
         } else {
             int64_t Kn = (k & 1) ? K + 1 : K - 1;
             const int64_t Kng = gc.z0 + Kn;
             const bool oz = Kng < 0 || Kng >= gc.gnz;
             if (oz) Kn = K;
-            const T a00 = w0 * cval(V, gc, I, J, K, false, false, false, cl) + w1 * cval(V, gc, In, J, K, ox, false, false, cl);
-            const T a10 = w0 * cval(V, gc, I, Jn, K, false, oy, false, cl) + w1 * cval(V, gc, In, Jn, K, ox, oy, false, cl);
-            const T a01 = w0 * cval(V, gc, I, J, Kn, false, false, oz, cl) + w1 * cval(V, gc, In, J, Kn, ox, false, oz, cl);
-            const T a11 = w0 * cval(V, gc, I, Jn, Kn, false, oy, oz, cl) + w1 * cval(V, gc, In, Jn, Kn, ox, oy, oz, cl);
+            const T a00 = w0 * cfac(get(I, J, K), false, false, false, cl) + w1 * cfac(get(In, J, K), ox, false, false, cl);
+            const T a10 = w0 * cfac(get(I, Jn, K), false, oy, false, cl) + w1 * cfac(get(In, Jn, K), ox, oy, false, cl);
+            const T a01 = w0 * cfac(get(I, J, Kn), false, false, oz, cl) + w1 * cfac(get(In, J, Kn), ox, false, oz, cl);
+            const T a11 = w0 * cfac(get(I, Jn, Kn), false, oy, oz, cl) + w1 * cfac(get(In, Jn, Kn), ox, oy, oz, cl);
             const T b0 = w0 * a00 + w1 * a10;
             const T b1 = w0 * a01 + w1 * a11;
             v = w0 * b0 + w1 * b1;
         }
     }
     return v;
+}
+
+// (P V) at fine cell (i, j, local plane k) from the packed coarse level V
+template <typename T, int DIM, int LINEAR>
+__device__ __forceinline__ T prolong_value(const T* V, const Geo& g, const Geo& gc, T cl, int i, int j, int64_t k)
+{
+    auto get = [&](int I, int J, int64_t K) { return V[pidx(gc, I, J, K)]; };
+    return prolong_eval<T, DIM, LINEAR>(get, gc, cl, i, j, k);
 }
 
 // One fine slot of colour `color` of the prolongation + correction (scalar; any sizes).
@@ -2494,6 +2500,9 @@ struct BlkShape {
     static constexpr int BZ = DIM == 3 ? B : 1;  // owned planes
     static constexpr int cells = EX * EY * EZ;
     static constexpr int owned = B * B * BZ;
+    // POST: coarse cells x0/2 - 1 .. of the extended tile's parents and their neighbours
+    static constexpr int CX = EX / 2 + 2, CY = EY / 2 + 3, CZ = DIM == 3 ? EZ / 2 + 3 : 1;
+    static constexpr int ccells = CX * CY * CZ;
     static constexpr int lidx(int lz, int ly, int c, int mm) { return ((lz * EY + ly) * 2 + c) * EH + mm; }
 };
 
@@ -2511,6 +2520,7 @@ __global__ __launch_bounds__(blk_threads<DIM>()) void k_blk(const T* __restrict_
     T* const U = reinterpret_cast<T*>(blk_smem);
     T* const F = U + S::cells;
     T* const RS = F + S::cells;  // PRE: residuals of the owned cells (x fastest)
+    T* const VC = F + S::cells;  // POST: the staged coarse region
     const int tid = threadIdx.x;
     __shared__ Op<T, DIM> sop;  // the operator in LDS: its diagonal table is indexed per cell
     if (tid == 0) sop = op;
@@ -2526,11 +2536,26 @@ __global__ __launch_bounds__(blk_threads<DIM>()) void k_blk(const T* __restrict_
     };
 
     // load: every LDS slot of both colours (u: black cells in the box, 0 elsewhere; f: cells in the
-    // box), all of a thread's global loads in flight at once
+    // box), all of a thread's global loads in flight at once.  POST: the coarse region the tile's
+    // prolongation reads is staged in LDS (VC, unpacked) with the same loads, and P V of the black
+    // slots is evaluated from there (prolong_eval: prolong_value's arithmetic) after one barrier.
     {
         constexpr int n = EZ * EY * 2 * EH;
         constexpr int NB = (n + NT - 1) / NT;
-        T uv[NB], fv[NB];
+        constexpr int CX = S::CX, CY = S::CY, NCB = (S::ccells + NT - 1) / NT;
+        const int cx0 = (xs >> 1) - 1, cy0 = (ys >> 1) - 1, cz0 = DIM == 3 ? (zs >> 1) - 1 : 0;
+        T uv[NB], fv[NB], cv[PRE ? 1 : NCB];
+        if (!PRE) {
+#pragma unroll
+            for (int q = 0; q < NCB; ++q) {
+                const int t = tid + q * NT;
+                const int a = t % CX, bb = (t / CX) % CY, cc = t / (CX * CY);
+                const int I = cx0 + a, J = cy0 + bb, K = cz0 + cc;
+                const bool in = t < S::ccells && I >= 0 && I < gc.nx && J >= 0 && J < gc.ny && K >= 0 &&
+                                (DIM == 2 || K < (int)gc.nz);
+                cv[q] = in ? V[pidx(gc, I, J, (int64_t)K)] : (T)0;
+            }
+        }
 #pragma unroll
         for (int q = 0; q < NB; ++q) {
             const int it = tid + q * NT;
@@ -2542,9 +2567,27 @@ __global__ __launch_bounds__(blk_threads<DIM>()) void k_blk(const T* __restrict_
             const int64_t gi = (int64_t)gk * g.P + c * g.H + (int64_t)gj * g.hw + gm;
             fv[q] = in ? f[gi] : (T)0;
             uv[q] = in && c == 1 && src ? src[gi] : (T)0;
-            if (!PRE && in && c == 1) {
-                const int i = 2 * gm + (1 ^ ((ly + lz + p0) & 1));
-                uv[q] = uv[q] + prolong_value<T, DIM, LINEAR>(V, g, gc, clc, i, gj, (int64_t)gk);
+        }
+        if (!PRE) {
+#pragma unroll
+            for (int q = 0; q < NCB; ++q) {
+                const int t = tid + q * NT;
+                if (t < S::ccells) VC[t] = cv[q];
+            }
+            __syncthreads();
+            auto get = [&](int I, int J, int64_t K) { return VC[(((int)K - cz0) * CY + (J - cy0)) * CX + (I - cx0)]; };
+#pragma unroll
+            for (int q = 0; q < NB; ++q) {
+                const int it = tid + q * NT;
+                const int row = it / (2 * EH), rest = it % (2 * EH);
+                const int lz = row / EY, ly = row % EY;
+                const int c = rest >= EH, mm = rest - c * EH;
+                const int gm = mxs + mm, gj = ys + ly, gk = zs + lz;
+                const bool in = it < n && gm >= 0 && gm < g.hw && gj >= 0 && gj < g.ny && gk >= 0 && gk < nzl;
+                if (in && c == 1) {
+                    const int i = 2 * gm + (1 ^ ((ly + lz + p0) & 1));
+                    uv[q] = uv[q] + prolong_eval<T, DIM, LINEAR>(get, gc, clc, i, gj, (int64_t)gk);
+                }
             }
         }
 #pragma unroll
@@ -3252,7 +3295,7 @@ template <typename T, int DIM, bool PRE, int NS>
 constexpr size_t blk_lds()
 {
     using S = BlkShape<DIM, PRE, blk_tile<DIM>(), NS>;
-    return (2 * (size_t)S::cells + (PRE ? (size_t)S::owned : 0)) * sizeof(T);
+    return (2 * (size_t)S::cells + (PRE ? (size_t)S::owned : (size_t)S::ccells)) * sizeof(T);
 }
 
 // the owned tile edge B divides every axis of the level (3D: B^3 tiles, 2D: B^2)
