@@ -3378,7 +3378,8 @@ hipError_t launch_metrics(int rb, const void* psi, const void* old, int64_t n, d
     return hipGetLastError();
 }
 
-int sum_scratch(int n) { return n <= 8192 ? 0 : (n + 8191) / 8192; }
+// one fixed-order kernel up to 65536 partials (64 per thread), two levels beyond
+int sum_scratch(int n) { return n <= 65536 ? 0 : (n + 8191) / 8192; }
 
 hipError_t launch_sum_partials(const double* partials, int n, double* out, hipStream_t s, int* ctr)
 {
