@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define MGP_API_VERSION 1
+#define MGP_API_VERSION 2  /* 2: mgp_opts.restriction (in the former padding after world) */
 #define MGP_COMM_ID_BYTES 128 /* == NCCL_UNIQUE_ID_BYTES */
 
 typedef enum mgp_status {
@@ -43,6 +43,10 @@ enum { MGP_CYCLE_V = 0, MGP_CYCLE_F = 1 };             /* twoGrid recursion (gam
 enum { MGP_PROLONG_PC = 0, MGP_PROLONG_LINEAR = 1 };   /* cpu.lua:142-150 injection / (tri)linear */
 enum { MGP_COARSE_FRESH = 0, MGP_COARSE_WARM = 1 };    /* cpu.lua:138 zeros / cpu-raw.lua:221 Vs */
 enum { MGP_BC_ZERO = 0, MGP_BC_CONSISTENT = 1 };       /* coarse ghost: 0 (ref) / extrapolated */
+/* restriction: the 2^dim cell average of cpu.lua:127-135 (reduceResidual) or the cell-centred full
+ * weighting (north_star "full-weighting restriction"): the adjoint of the linear prolongation, per axis
+ * (1, 3, 3, 1) / 8 over fine cells 2I-1 .. 2I+2, face weight (3 - c) next to the box boundary */
+enum { MGP_RESTRICT_AVERAGE = 0, MGP_RESTRICT_FULL_WEIGHTING = 1 };
 /* Fields of a level, by cpu-raw.lua's names (cpu-raw.lua:148-171).  U and F are the stored, writable
  * state; the others are read-only views computed on request from it:
  *   MGP_FIELD_U          psi on level 0, Vs[L] below (the coarse correction)
@@ -52,8 +56,8 @@ enum { MGP_BC_ZERO = 0, MGP_BC_CONSISTENT = 1 };       /* coarse ghost: 0 (ref) 
  *   MGP_FIELD_PSI_OLD    psiOld (level 0): the iterate before the last outer iteration (cpu.lua:200)
  *   MGP_FIELD_ERROR      errorBuf (level 0) = (psi - psiOld)^2 per cell (calcFrobErr, gpu.lua:189-200)
  *   MGP_FIELD_TMP        tmpU: the Jacobi target buffer (cpu-raw.lua:153, 176-184)
- * PSI_OLD / ERROR need err_mode 1 and a psiOld that the cycle kept (not after a temporally blocked
- * finest level, which overwrites it in place): MGP_ERR_STATE otherwise.  TMP: MGP_ERR_STATE when the
+ * PSI_OLD / ERROR need err_mode 1 (MGP_ERR_STATE otherwise; a temporally blocked finest level keeps psiOld
+ * in a buffer of its own, unless the environment sets MGP_KEEP_PSI_OLD=0).  TMP: MGP_ERR_STATE when the
  * level has no second buffer (red/black Gauss-Seidel works in place). */
 enum { MGP_FIELD_U = 0, MGP_FIELD_F = 1, MGP_FIELD_RESIDUAL = 2, MGP_FIELD_CORRECTION = 3, MGP_FIELD_PSI_OLD = 4,
        MGP_FIELD_ERROR = 5, MGP_FIELD_TMP = 6, MGP_FIELD_KINDS = 7 };
@@ -74,6 +78,7 @@ typedef struct mgp_opts {
     int32_t err_mode;      /* 1: psiOld snapshot + RMS update per cycle (cpu.lua:200-203); 0: off */
     int32_t device;        /* HIP device ordinal; -1 = current device */
     int32_t rank, world;   /* slab-z domain decomposition over `world` GPUs (3D only) */
+    int32_t restriction;   /* MGP_RESTRICT_AVERAGE (reference) | MGP_RESTRICT_FULL_WEIGHTING */
     int64_t gather_cells;  /* a level with <= this many cells is replicated on every rank */
     uint8_t comm_id[MGP_COMM_ID_BYTES]; /* from mgp_comm_unique_id() on rank 0 (world > 1) */
 } mgp_opts;

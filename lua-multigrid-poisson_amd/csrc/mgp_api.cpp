@@ -12,6 +12,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <condition_variable>
 #include <mutex>
@@ -68,6 +69,10 @@ int plan_levels(const mgp_opts& o, std::vector<LevelPlan>& out, std::string& err
     if (o.prolong != MGP_PROLONG_PC && o.prolong != MGP_PROLONG_LINEAR) { err = "unknown prolong"; return MGP_ERR_ARG; }
     if (o.coarse_init != MGP_COARSE_FRESH && o.coarse_init != MGP_COARSE_WARM) { err = "unknown coarse_init"; return MGP_ERR_ARG; }
     if (o.coarse_bc != MGP_BC_ZERO && o.coarse_bc != MGP_BC_CONSISTENT) { err = "unknown coarse_bc"; return MGP_ERR_ARG; }
+    if (o.restriction != MGP_RESTRICT_AVERAGE && o.restriction != MGP_RESTRICT_FULL_WEIGHTING) {
+        err = "unknown restriction";
+        return MGP_ERR_ARG;
+    }
     if (o.nu1 < 0 || o.nu2 < 0 || o.coarse_sweeps < 1) { err = "nu1/nu2 >= 0 and coarse_sweeps >= 1 required"; return MGP_ERR_ARG; }
     if (o.world < 1 || o.rank < 0 || o.rank >= o.world) { err = "need 0 <= rank < world"; return MGP_ERR_ARG; }
     if (o.world > 1) {
@@ -174,6 +179,12 @@ struct mgp_ctx {
     double* d_rn = nullptr;       // residual-norm partials (+ 2 results), d_rn_cap doubles
     int64_t d_rn_cap = 0;
     char* psi_old = nullptr;  // snapshot buffer (Jacobi path)
+    // full-weighting restriction: the residual of the level being restricted (level-0 sized, with ghost planes)
+    char* rscratch = nullptr;
+    // temporally blocked finest level with err: POST's output buffer, so that psiOld (t) survives the cycle
+    // for the reference's metrics (mgp_metrics, psiOld / errorBuf: cpu-raw.lua:148-153, gpu.lua:173-200);
+    // rotates with u (MGP_KEEP_PSI_OLD=0: POST writes over psiOld in place and no metrics are kept)
+    char* xbuf = nullptr;
     // an all-zero buffer of the largest lazily zeroed level's layout: a fresh coarse guess (cpu.lua:138)
     // costs no memset, the first red half-sweep reads its black neighbours from here
     char* zbuf = nullptr;
@@ -190,6 +201,9 @@ struct mgp_ctx {
     // accumulate (psi - psiOld)^2 (cpu.lua:200-203 without the copy and the extra pass).
     bool err_fuse = false;
     bool in_cycle = false;  // a one_cycle() is running (level-0 first sweep goes out of place)
+    // set by the owning group when another rank failed: no new exchange / collective is issued, and the
+    // communicator (aborted by the group) is not touched again
+    const std::atomic<bool>* group_stop = nullptr;
     bool first_done = false;
     bool err_done = false;
     // hipGraph replay of whole cycles (single GPU): one instantiated graph per pointer state of
@@ -369,6 +383,7 @@ int exchange_buf(mgp_ctx* c, Level& L, char* buf, int depth = 1, int colour = -1
 {
     if (depth > c->G || depth > L.g.nz)
         return c->fail(MGP_ERR_STATE, "internal: exchange depth %d (ghost %d, slab %d)", depth, c->G, (int)L.g.nz);
+    if (c->group_stop && c->group_stop->load()) return c->fail(MGP_ERR_STATE, "group aborted: another rank failed");
     ++L.exchanges;
     if (c->lb) return lb_exchange(c, (int)(&L - c->lev.data()), buf, depth, colour);
     const size_t rb = (size_t)c->rb;
@@ -574,8 +589,39 @@ Geo coarse_view(const Level& L, const Level& C, int64_t* zc_local)
     return gc;
 }
 
+// agglomerate: every rank gets the whole coarse right-hand side R (cf. cpu-gpu.lua:22-32)
+int gather_coarse_rhs(mgp_ctx* c, Level& L, Level& C, char* R)
+{
+    const size_t count = (size_t)((L.g.nz / 2) * C.g.P);
+    if (c->lb) return lb_allgather(c, c->ui(C, C.f), count);
+    NCCL_TRY(c, ncclAllGather(R, c->ui(C, C.f), count, c->nccl_real(), c->comm, c->s));
+    return MGP_OK;
+}
+
+// calcResidual + the full-weighting restriction (MGP_RESTRICT_FULL_WEIGHTING): r of the level's own planes
+// into the scratch, one ghost plane of r from each z-neighbour on a slab level, then R from r
+int residual_restrict_fw(mgp_ctx* c, int l, double h)
+{
+    Level& L = c->lev[l];
+    Level& C = c->lev[l + 1];
+    TRY(materialize_zero(c, L));
+    TRY(exchange(c, L));
+    HIP_TRY(c, mgp::launch_residual_field_v(c->rb, c->o.dim, c->ui(L, L.u), c->ui(L, L.f), c->ui(L, c->rscratch), L.g,
+                                            h, coarse_coef(c->o.coarse_bc, l), c->s));
+    if (L.p.dist) TRY(exchange_buf(c, L, c->rscratch, 1));
+    int64_t zc = 0;
+    const Geo gc = coarse_view(L, C, &zc);
+    char* R = c->ui(C, C.f) + (size_t)(zc * C.g.P) * c->rb;
+    HIP_TRY(c, mgp::launch_fw_restrict(c->rb, c->o.dim, c->ui(L, c->rscratch), R, L.g, gc,
+                                       coarse_coef(c->o.coarse_bc, l + 1), c->s));
+    C.fghost_ok = !C.p.dist;
+    if (L.p.dist && !C.p.dist) TRY(gather_coarse_rhs(c, L, C, R));
+    return MGP_OK;
+}
+
 int residual_restrict(mgp_ctx* c, int l, double h)
 {
+    if (c->o.restriction == MGP_RESTRICT_FULL_WEIGHTING) return residual_restrict_fw(c, l, h);
     Level& L = c->lev[l];
     Level& C = c->lev[l + 1];
     TRY(materialize_zero(c, L));
@@ -586,14 +632,7 @@ int residual_restrict(mgp_ctx* c, int l, double h)
     HIP_TRY(c, mgp::launch_residual_restrict(c->rb, c->o.dim, c->ui(L, L.u), c->ui(L, L.f), R, L.g, gc, h,
                                              coarse_coef(c->o.coarse_bc, l), c->s));
     C.fghost_ok = !C.p.dist;
-    if (L.p.dist && !C.p.dist) {
-        // agglomerate: every rank gets the whole coarse right-hand side (cf. cpu-gpu.lua:22-32)
-        const size_t count = (size_t)((L.g.nz / 2) * C.g.P);
-        if (c->lb)
-            TRY(lb_allgather(c, c->ui(C, C.f), count));
-        else
-            NCCL_TRY(c, ncclAllGather(R, c->ui(C, C.f), count, c->nccl_real(), c->comm, c->s));
-    }
+    if (L.p.dist && !C.p.dist) TRY(gather_coarse_rhs(c, L, C, R));
     return MGP_OK;
 }
 
@@ -706,8 +745,10 @@ int fused_pre(mgp_ctx* c, int l, double h)
     }
     int64_t zc = 0;
     const Geo gc = coarse_view(L, C, &zc);
+    const bool fw = c->o.restriction == MGP_RESTRICT_FULL_WEIGHTING;
     mgp::FusedArgs a{};
     a.pre = true;
+    a.linear = fw;  // PRE: 1 = smoothing only (both colours stored), the full weighting follows
     a.src = c->ui(L, L.u);
     a.f = c->ui(L, L.f);
     a.dst = c->ui(L, L.t);
@@ -722,19 +763,14 @@ int fused_pre(mgp_ctx* c, int l, double h)
     TRY(timed_begin(c, l, &e));
     HIP_TRY(c, mgp::launch_fused(c->rb, a, c->s));
     // algorithmic bytes: nu1 sweeps x 3 reals + (2 + 1/8) reals of residual/restriction
-    TRY(timed_end(c, e, MGP_TIMING_FUSED_PRE, (3.0 * c->o.nu1 + 2.125) * c->rb * (double)level_cells(L)));
+    TRY(timed_end(c, e, MGP_TIMING_FUSED_PRE, (3.0 * c->o.nu1 + (fw ? 0.0 : 2.125)) * c->rb * (double)level_cells(L)));
     std::swap(L.u, L.t);  // u = smoothed; t = the previous iterate (psiOld on level 0)
     L.ghost_ok = !L.p.dist;
     L.ghost_zero = false;
-    C.fghost_ok = !C.p.dist;
-    if (L.p.dist && !C.p.dist) {  // agglomerate the coarse right-hand side, as residual_restrict
-        const size_t count = (size_t)((L.g.nz / 2) * C.g.P);
-        if (c->lb)
-            TRY(lb_allgather(c, c->ui(C, C.f), count));
-        else
-            NCCL_TRY(c, ncclAllGather(a.R, c->ui(C, C.f), count, c->nccl_real(), c->comm, c->s));
-    }
     if (l == 0 && c->in_cycle) c->first_done = true;
+    if (fw) return residual_restrict_fw(c, l, h);
+    C.fghost_ok = !C.p.dist;
+    if (L.p.dist && !C.p.dist) TRY(gather_coarse_rhs(c, L, C, (char*)a.R));  // as residual_restrict
     return MGP_OK;
 }
 
@@ -756,7 +792,10 @@ int fused_post(mgp_ctx* c, int l, double h, bool want_err)
     a.linear = c->o.prolong == MGP_PROLONG_LINEAR;
     a.src = c->ui(L, L.u);
     a.f = c->ui(L, L.f);
-    a.dst = c->ui(L, L.t);
+    // with err on level 0: t holds psiOld; the output goes to xbuf when psiOld is kept, else over t
+    const bool keep = want_err && l == 0 && c->xbuf;
+    a.dst = c->ui(L, keep ? c->xbuf : L.t);
+    a.old = want_err ? c->ui(L, L.t) : nullptr;
     a.V = c->ui(C, C.u) + (size_t)(zc * C.g.P) * c->rb;
     a.partials = want_err ? c->d_part : nullptr;
     a.g = L.g;
@@ -771,7 +810,10 @@ int fused_post(mgp_ctx* c, int l, double h, bool want_err)
     HIP_TRY(c, mgp::launch_fused(c->rb, a, c->s));
     TRY(timed_end(c, e, MGP_TIMING_FUSED_POST,
                   (3.0 * c->o.nu2 + 2.125 + (want_err ? 2.0 : 0.0)) * c->rb * (double)level_cells(L)));
-    std::swap(L.u, L.t);
+    if (keep)
+        std::swap(L.u, c->xbuf);  // u = new iterate, t = psiOld (kept), xbuf = the smoothed PRE output (scratch)
+    else
+        std::swap(L.u, L.t);
     L.ghost_ok = !L.p.dist;
     L.ghost_zero = false;
     if (want_err) {
@@ -800,6 +842,8 @@ int block_pre(mgp_ctx* c, int l, double h)
     a.R = c->ui(C, C.f) + (size_t)(zc * C.g.P) * c->rb;
     a.h = h;
     a.cl = coarse_coef(c->o.coarse_bc, l);
+    a.linear = c->o.restriction == MGP_RESTRICT_FULL_WEIGHTING;  // PRE: the restriction
+    a.clc = coarse_coef(c->o.coarse_bc, l + 1);
     HIP_TRY(c, mgp::launch_block(c->rb, c->o.dim, a, c->s));
     L.zero_pending = false;
     std::swap(L.u, L.t);
@@ -939,6 +983,7 @@ int run_tail(mgp_ctx* c, bool fcycle)
         L.ghost_zero = false;
     }
     t.zero_first = c->lev[T].zero_pending;
+    t.fw = c->o.restriction == MGP_RESTRICT_FULL_WEIGHTING;
     c->lev[T].zero_pending = false;
     const std::vector<uint32_t>& p = fcycle ? c->tail_f : c->tail_v;
     t.nops = (int)p.size();
@@ -991,7 +1036,7 @@ void update_metrics_old(mgp_ctx* c)
     if (!c->o.err_mode) return;
     if (!c->err_fuse)
         c->metrics_old = c->psi_old;
-    else if (!L0.fused)
+    else if (!L0.fused || c->xbuf)
         c->metrics_old = c->ui(L0, L0.t);
 }
 
@@ -1034,6 +1079,7 @@ std::vector<char*> level_state(const mgp_ctx* c)
         v.push_back(L.u);
         v.push_back(L.t);
     }
+    v.push_back(c->xbuf);
     return v;
 }
 
@@ -1043,6 +1089,7 @@ void set_level_state(mgp_ctx* c, const std::vector<char*>& v)
         c->lev[l].u = v[2 * l];
         c->lev[l].t = v[2 * l + 1];
     }
+    c->xbuf = v[2 * c->lev.size()];
 }
 
 // One cycle through a cached hipGraph (captured on first use of a buffer-pointer state).
@@ -1100,6 +1147,7 @@ int check_level(const mgp_ctx* c, int level)
 int sync_and_check(mgp_ctx* c)
 {
     HIP_TRY(c, hipStreamSynchronize(c->s));
+    if (c->group_stop && c->group_stop->load()) return c->fail(MGP_ERR_STATE, "group aborted: another rank failed");
     if (c->comm) {
         ncclResult_t ar = ncclSuccess;
         NCCL_TRY(c, ncclCommGetAsyncError(c->comm, &ar));
@@ -1138,6 +1186,7 @@ void mgp_opts_default(mgp_opts* o)
     o->rank = 0;
     o->world = 1;
     o->gather_cells = 32768;
+    o->restriction = MGP_RESTRICT_AVERAGE;  // cpu.lua:127-135
 }
 
 int mgp_comm_unique_id(void* out, int64_t nbytes)
@@ -1203,6 +1252,8 @@ static void destroy_impl(mgp_ctx* c)
     }
     if (c->zbuf) (void)hipFree(c->zbuf);
     if (c->psi_old) (void)hipFree(c->psi_old);
+    if (c->rscratch) (void)hipFree(c->rscratch);
+    if (c->xbuf) (void)hipFree(c->xbuf);
     if (c->stage) (void)hipFree(c->stage);
     if (c->d_stats_h) (void)hipFree(c->d_stats_h);
     if (c->d_part) (void)hipFree(c->d_part);
@@ -1390,6 +1441,23 @@ static int create_impl(mgp_ctx** out, const mgp_opts* o, mgp_loopback* lb, ncclC
         return bail(MGP_ERR_OOM);
     }
     {
+        const char* v = std::getenv("MGP_KEEP_PSI_OLD");
+        if (c->o.err_mode && c->err_fuse && L0.fused && !(v && std::atoi(v) == 0)) {
+            if (hipMalloc(&c->xbuf, (size_t)L0.alloc * rb) != hipSuccess ||
+                hipMemsetAsync(c->xbuf, 0, (size_t)L0.alloc * rb, c->s) != hipSuccess) {
+                c->err = "hipMalloc failed for the psiOld-keeping output buffer";
+                return bail(MGP_ERR_OOM);
+            }
+        }
+    }
+    // the full weighting reads residuals of neighbouring coarse cells' children: r is materialised once per
+    // level in this scratch (level 0 is the largest level; the kernels never read its physical ghost planes)
+    if (c->o.restriction == MGP_RESTRICT_FULL_WEIGHTING && c->lev.size() > 1 &&
+        hipMalloc(&c->rscratch, (size_t)L0.alloc * rb) != hipSuccess) {
+        c->err = "hipMalloc failed for the full-weighting residual scratch";
+        return bail(MGP_ERR_OOM);
+    }
+    {
         // staging for host I/O: at least one level-0 plane, at most ~256 MiB (or the whole interior)
         const size_t plane = (size_t)(L0.p.nx * L0.p.ny) * rb;
         c->stage_bytes = std::min(interior, std::max(plane, (size_t)256 << 20));
@@ -1527,7 +1595,7 @@ static int field_source(mgp_ctx* c, int level, int which, char** src, char** scr
     case MGP_FIELD_ERROR:
         if (level != 0 || !c->metrics_old)
             return c->fail(MGP_ERR_STATE, "psiOld / errorBuf: level 0 only, after an outer iteration with err_mode 1 "
-                                          "that kept psiOld (not with the temporally blocked finest level)");
+                                          "that kept psiOld (not with MGP_KEEP_PSI_OLD=0 on the temporally blocked finest level)");
         break;
     case MGP_FIELD_CORRECTION:
         if (level + 1 >= (int)c->lev.size()) return c->fail(MGP_ERR_ARG, "vs: the coarsest level has none");
@@ -1851,7 +1919,7 @@ int mgp_metrics(mgp_ctx* c, double* rel_err, int64_t* count, double* frob)
     if (!c) return MGP_ERR_ARG;
     if (!c->metrics_old)
         return c->fail(MGP_ERR_STATE, "mgp_metrics: no psiOld of a last outer iteration (run mgp_cycle with err_mode 1; "
-                                      "not available with the temporally blocked phases)");
+                                      "not kept with MGP_KEEP_PSI_OLD=0 on the temporally blocked finest level)");
     if (!c->d_metrics) HIP_TRY(c, hipMalloc(&c->d_metrics, sizeof(double) * (3 * mgp::kSumBlocks + 3)));
     const Level& L0 = c->lev[0];
     double* out = c->d_metrics + 3 * mgp::kSumBlocks;
@@ -2000,27 +2068,88 @@ struct mgp_group {
     std::vector<int> dev;
     mgp_loopback* lb = nullptr;  // all ranks on one device: loopback transport
     std::string err;
+    std::atomic<bool> stop{false};  // a rank failed and the others were woken: the group is unusable
+};
+
+// Restores the caller's current device on scope exit (the group switches devices per rank).
+struct DeviceGuard {
+    int dev = -1;
+    DeviceGuard() { (void)hipGetDevice(&dev); }
+    ~DeviceGuard()
+    {
+        if (dev >= 0) (void)hipSetDevice(dev);
+    }
 };
 
 static thread_local std::string g_group_error;
 
+// Wake the ranks still blocked on a failed rank: they would otherwise wait forever in a halo exchange or
+// collective that rank never joined.  Loopback: break the host barrier.  RCCL: ncclCommAbort every
+// communicator (its outstanding kernels exit); the ranks see `stop` before touching their comm again.
+static void group_abort(mgp_group* g)
+{
+    g->stop.store(true);
+    if (g->lb) {
+        std::lock_guard<std::mutex> lk(g->lb->m);
+        g->lb->broken = true;
+        g->lb->cv.notify_all();
+        return;
+    }
+    for (size_t r = 0; r < g->ranks.size(); ++r)
+        if (g->ranks[r] && g->ranks[r]->comm) {
+            (void)hipSetDevice(g->dev[r]);
+            (void)ncclCommAbort(g->ranks[r]->comm);
+        }
+}
+
 // Run fn(rank context, r) on every rank, each in its own host thread with its device current (the
-// ranks' halo exchanges and collectives must be issued concurrently).  First failure wins.
+// ranks' halo exchanges and collectives must be issued concurrently).  First failure wins.  When a rank
+// fails and the others have not returned within a short grace period, they are blocked on it: the group
+// is aborted (group_abort) and unusable afterwards (every later call fails with MGP_ERR_STATE).
 static int group_run(mgp_group* g, const std::function<int(mgp_ctx*, int)>& fn)
 {
+    if (g->stop.load()) {
+        g->err = "group aborted after a rank failed: destroy it";
+        return MGP_ERR_STATE;
+    }
+    DeviceGuard keep_device;
     const int n = (int)g->ranks.size();
     std::vector<int> rc((size_t)n, MGP_OK);
+    std::mutex m;
+    std::condition_variable cv;
+    int done = 0;
+    bool failed = false;
+    // test hook: this rank fails at once, before any exchange (tests/test_gpu_group.py)
+    const char* fr = std::getenv("MGP_TEST_FAIL_RANK");
+    const int fail_rank = fr ? std::atoi(fr) : -1;
     std::vector<std::thread> th;
     th.reserve((size_t)n);
     for (int r = 0; r < n; ++r)
         th.emplace_back([&, r] {
-            if (hipSetDevice(g->dev[(size_t)r]) != hipSuccess) {
-                rc[(size_t)r] = MGP_ERR_HIP;
-                return;
-            }
-            rc[(size_t)r] = fn(g->ranks[(size_t)r], r);
+            int v;
+            if (hipSetDevice(g->dev[(size_t)r]) != hipSuccess)
+                v = MGP_ERR_HIP;
+            else if (r == fail_rank)
+                v = g->ranks[(size_t)r]->fail(MGP_ERR_STATE, "injected failure (MGP_TEST_FAIL_RANK)");
+            else
+                v = fn(g->ranks[(size_t)r], r);
+            rc[(size_t)r] = v;
+            std::lock_guard<std::mutex> lk(m);
+            ++done;
+            if (v != MGP_OK) failed = true;
+            cv.notify_all();
         });
+    {
+        std::unique_lock<std::mutex> lk(m);
+        cv.wait(lk, [&] { return done == n || failed; });
+        if (done < n && !cv.wait_for(lk, std::chrono::seconds(2), [&] { return done == n; })) {
+            lk.unlock();
+            group_abort(g);
+        }
+    }
     for (auto& t : th) t.join();
+    if (g->stop.load() && !g->lb)
+        for (auto* c : g->ranks) c->comm = nullptr;  // freed by ncclCommAbort
     for (int r = 0; r < n; ++r)
         if (rc[(size_t)r] != MGP_OK) {
             g->err = "rank " + std::to_string(r) + ": " + g->ranks[(size_t)r]->err;
@@ -2032,6 +2161,7 @@ static int group_run(mgp_group* g, const std::function<int(mgp_ctx*, int)>& fn)
 void mgp_group_destroy(mgp_group* g)
 {
     if (!g) return;
+    DeviceGuard keep_device;
     for (auto* c : g->ranks)
         if (c) {
             (void)hipSetDevice(c->device);
@@ -2048,6 +2178,7 @@ int mgp_group_create(mgp_group** out, const mgp_opts* o, int ngpu, const int* de
         return MGP_ERR_ARG;
     }
     *out = nullptr;
+    DeviceGuard keep_device;
     mgp_group* g = new mgp_group();
     for (int r = 0; r < ngpu; ++r) g->dev.push_back(devices ? devices[r] : r);
     bool same = true;
@@ -2079,6 +2210,7 @@ int mgp_group_create(mgp_group** out, const mgp_opts* o, int ngpu, const int* de
         ro.rank = r;
         ro.device = g->dev[(size_t)r];
         const int rc = create_impl(&g->ranks[(size_t)r], &ro, g->lb, comms[(size_t)r]);
+        if (rc == MGP_OK) g->ranks[(size_t)r]->group_stop = &g->stop;
         if (rc != MGP_OK) {
             for (int q = r + 1; q < ngpu; ++q)
                 if (comms[(size_t)q]) (void)ncclCommDestroy(comms[(size_t)q]);

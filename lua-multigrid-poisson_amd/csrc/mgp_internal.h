@@ -77,6 +77,13 @@ hipError_t launch_post_first(int rb, int dim, int linear, void* u, const void* V
 // coarse plane of this rank's fine plane 0; its Geo is gc) from u, f of the fine level.
 hipError_t launch_residual_restrict(int rb, int dim, const void* u, const void* f, void* R, Geo g, Geo gc, double h,
                                     double cl, hipStream_t s);
+// Full-weighting restriction (mgp_opts.restriction, build-defined): r = f - A u of the level's own planes
+// into the scratch r (same packed layout and ghost planes as the level), then R (coarse packed, Geo gc)
+// from r, which must have current planes -1 and g.nz (zero at the physical boundary, the neighbours'
+// planes across a slab edge).  clc: the coarse level's boundary coefficient (face weight 3 - clc).
+hipError_t launch_residual_field_v(int rb, int dim, const void* u, const void* f, void* r, Geo g, double h, double cl,
+                                   hipStream_t s);
+hipError_t launch_fw_restrict(int rb, int dim, const void* r, void* R, Geo g, Geo gc, double clc, hipStream_t s);
 // u += P V (expandResidual + addTo); V points at the coarse plane gc.z0, which must correspond to
 // this rank's fine plane 0; planes -1 and gc.nz of V must be readable for the linear kind.
 // black_only: the black cells only (before a red/black post-smoothing: its red half-sweep replaces
@@ -107,10 +114,11 @@ hipError_t launch_sum_partials(const double* partials, int n, double* out, hipSt
 // src and dst are different buffers (tiles read each other's halos of src).
 struct FusedArgs {
     bool pre;
-    int linear;
+    int linear;  // POST: linear prolongation; PRE: 1 = no restriction (both colours stored, full weighting after)
     const void* src;
     const void* f;
     void* dst;
+    const void* old;  // POST + err: psiOld (nullptr: dst, overwritten plane by plane as the output is stored)
     void* R;
     const void* V;
     double* partials;
@@ -136,7 +144,7 @@ constexpr int kBlkTile = 8;     // 3D owned tile edge (every axis of a tiled lev
 constexpr int kBlkTile2D = 32;  // 2D owned tile edge
 struct BlockArgs {
     bool pre;
-    int linear;
+    int linear;  // POST: linear prolongation; PRE: 1 = full-weighting restriction (face weight 3 - clc)
     int ns;
     const void* src;
     const void* f;
@@ -158,6 +166,7 @@ enum TailOp { TAIL_SMOOTH = 1, TAIL_RR = 2, TAIL_ZERO = 3, TAIL_PROLONG = 4 };
 struct TailSpec {
     int nlev, nops, jacobi, linear;
     int zero_first;  // the first level's u is logically 0 (a fresh guess): loaded as zeros
+    int fw;          // TAIL_RR restricts by full weighting (mgp_opts.restriction)
     void* u[kTailMaxLevels];  // interior plane 0 of each level's u / f (global)
     void* f[kTailMaxLevels];
     Geo g[kTailMaxLevels];

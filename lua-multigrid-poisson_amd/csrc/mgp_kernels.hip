@@ -993,6 +993,187 @@ __global__ __launch_bounds__(kBlock) void k_resrestrict(const T* __restrict__ u,
     }
 }
 
+// ---- full-weighting restriction (build-defined option, north_star) ------------------------------
+//
+// The cell-centred adjoint of the linear prolongation (oracle: restrict_fw in mgp_oracle_impl.h): per
+// axis coarse I takes fine 2I-1 .. 2I+2 as ((r_a + w_b r_b) + w_c r_c) + r_d, w = 3 or, next to a box
+// face, 3 - clc; fine cells outside the box are +0; x, then y, then z; times 1/8^DIM.  The residual is
+// materialised first (k_resfield_v / k_residual_field into the level-sized scratch), because each fine
+// residual feeds 2^DIM coarse cells; on a slab level one ghost plane of r is exchanged in between.
+
+template <typename T>
+__device__ __forceinline__ T fw_axis(T a, T b, T c, T d, T wb, T wc)
+{
+    T s = a + wb * b;
+    s = s + wc * c;
+    s = s + d;
+    return s;
+}
+
+// Coarse cell (I, J, local plane K) from fine residuals get(i, j, k) (k local; called only for cells
+// inside the box).  gc.z0 = g.z0 / 2 (the coarse plane of this rank's fine plane 0).
+template <typename T, int DIM, typename Get>
+__device__ __forceinline__ T fw_eval(const Get& get, const Geo& g, const Geo& gc, T wf, int I, int J, int64_t K)
+{
+    const T w3 = (T)3;
+    T az = (T)0;
+#pragma unroll
+    for (int dz = 0; dz < (DIM == 3 ? 4 : 1); ++dz) {
+        const int64_t k = DIM == 3 ? 2 * K - 1 + dz : 0;
+        const bool kin = DIM == 2 || (g.z0 + k >= 0 && g.z0 + k < g.gnz);
+        T ay = (T)0;
+#pragma unroll
+        for (int dy = 0; dy < 4; ++dy) {
+            const int j = 2 * J - 1 + dy;
+            const bool jin = kin && j >= 0 && j < g.ny;
+            T x[4];
+#pragma unroll
+            for (int dx = 0; dx < 4; ++dx) {
+                const int i = 2 * I - 1 + dx;
+                x[dx] = (jin && i >= 0 && i < g.nx) ? get(i, j, k) : (T)0;
+            }
+            const T ax = fw_axis(x[0], x[1], x[2], x[3], I == 0 ? wf : w3, I == gc.nx - 1 ? wf : w3);
+            // ay = ((ax0 + wb ax1) + wc ax2) + ax3, accumulated row by row
+            if (dy == 0) ay = ax;
+            else if (dy == 1) ay = ay + (J == 0 ? wf : w3) * ax;
+            else if (dy == 2) ay = ay + (J == gc.ny - 1 ? wf : w3) * ax;
+            else ay = ay + ax;
+        }
+        if (DIM == 2) {
+            az = ay;
+        } else {
+            const int64_t gK = gc.z0 + K;
+            if (dz == 0) az = ay;
+            else if (dz == 1) az = az + (gK == 0 ? wf : w3) * ay;
+            else if (dz == 2) az = az + (gK == gc.gnz - 1 ? wf : w3) * ay;
+            else az = az + ay;
+        }
+    }
+    return (DIM == 3 ? (T)(1.0 / 512.0) : (T)(1.0 / 64.0)) * az;
+}
+
+// r = f - A u at both colours of a level (vector form, k_half's item): the scratch of the full weighting
+template <typename T, int DIM>
+__global__ __launch_bounds__(kBlock) void k_resfield_v(const T* __restrict__ u, const T* __restrict__ f,
+                                                       T* __restrict__ r, Geo g, Op<T, DIM> op, int64_t items)
+{
+    constexpr int N = VN<T>::n;
+    const int b = xcd_remap(blockIdx.x, gridDim.x);
+    const int64_t it = (int64_t)b * kBlock + threadIdx.x;
+    if (it >= 2 * items) return;
+    const int color = it >= items;
+    HalfIn<T, N> in;
+    half_load<T, DIM>(in, u, f, g, color, it - color * items);
+    const Vec<T, N> uc = vload<T, N>(u + in.own);
+    const bool fast = op.cl == (T)0;
+    Vec<T, N> out;
+#pragma unroll
+    for (int e = 0; e < N; ++e) {
+        const int o = in.o;
+        const int i = 2 * (in.m0 + e) + o;
+        const T xl = o == 0 ? (e == 0 ? in.edge : in.cen.v[e - 1]) : in.cen.v[e];
+        const T xr = o == 0 ? in.cen.v[e] : (e == N - 1 ? in.edge : in.cen.v[e + 1]);
+        T sm = xl + xr;
+        sm = sm + in.yl.v[e];
+        sm = sm + in.yr.v[e];
+        if (DIM == 3) {
+            sm = sm + in.zl.v[e];
+            sm = sm + in.zr.v[e];
+        }
+        out.v[e] = fast ? op.residual(sm, in.fv.v[e], uc.v[e], 0)
+                        : op.residual(sm, in.fv.v[e], uc.v[e], in.nbyz + (i == 0) + (i == g.nx - 1));
+    }
+    vstore<T, N>(r + in.own, out);
+}
+
+// Scalar form: a thread per coarse cell (any sizes), r packed with readable planes -1 and g.nz
+template <typename T, int DIM>
+__global__ __launch_bounds__(kBlock) void k_fw_s(const T* __restrict__ r, T* __restrict__ R, Geo g, Geo gc, T wf)
+{
+    const int64_t it = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (it >= resrestrict_items<T, DIM>(g)) return;
+    const int cx = g.nx >> 1, cy = g.ny >> 1;
+    const int I = (int)(it % cx), J = (int)((it / cx) % cy);
+    const int64_t K = it / ((int64_t)cx * cy);
+    auto get = [&](int i, int j, int64_t k) { return r[pidx(g, i, j, k)]; };
+    R[pidx(gc, I, J, K)] = fw_eval<T, DIM>(get, g, gc, wf, I, J, K);
+}
+
+// Vector form (coarse nx >= N): a thread owns N consecutive coarse cells I0 .. of one coarse row; each
+// of its 4 (2D) / 16 (3D) fine rows is two N-wide loads (even and odd x of fine cells 2 I0 .. 2 I0 + 2N - 1)
+// plus the two edge cells, reduced along x at once and accumulated in fw_eval's order.
+template <typename T, int DIM>
+__global__ __launch_bounds__(kBlock) void k_fw_v(const T* __restrict__ r, T* __restrict__ R, Geo g, Geo gc, T wf)
+{
+    constexpr int N = VN<T>::n;
+    constexpr int LN = N == 4 ? 2 : 1;
+    const int cx = g.nx >> 1, cy = g.ny >> 1;
+    const int lgpr = (g.lx - 1) - LN;
+    const int64_t ncz = DIM == 3 ? (g.nz >> 1) : 1;
+    const int b = xcd_remap(blockIdx.x, gridDim.x);
+    const int64_t it = (int64_t)b * kBlock + threadIdx.x;
+    const int grp = (int)(it & ((1 << lgpr) - 1));
+    const int J = (int)((it >> lgpr) & (cy - 1));
+    const int64_t K = it >> (lgpr + g.ly - 1);
+    if (K >= ncz) return;
+    const int I0 = grp * N;
+    const T w3 = (T)3;
+    T az[N], ay[N];
+#pragma unroll
+    for (int e = 0; e < N; ++e) az[e] = (T)0;
+#pragma unroll
+    for (int dz = 0; dz < (DIM == 3 ? 4 : 1); ++dz) {
+        const int64_t k = DIM == 3 ? 2 * K - 1 + dz : 0;
+        const int64_t gk = g.z0 + k;
+        const bool kin = DIM == 2 || (gk >= 0 && gk < g.gnz);
+#pragma unroll
+        for (int dy = 0; dy < 4; ++dy) {
+            const int j = 2 * J - 1 + dy;
+            Vec<T, N> ev = vzero<T, N>(), od = vzero<T, N>();
+            T left = (T)0, right = (T)0;
+            if (kin && j >= 0 && j < g.ny) {
+                const int pe = (int)((j + gk) & 1);  // colour of the row's even x
+                const T* row = r + k * g.P + (int64_t)j * g.hw;
+                ev = vload<T, N>(row + pe * g.H + I0);
+                od = vload<T, N>(row + (pe ^ 1) * g.H + I0);
+                if (I0 > 0) left = row[(pe ^ 1) * g.H + I0 - 1];  // fine 2 I0 - 1
+                if (I0 + N < cx) right = row[pe * g.H + I0 + N];  // fine 2 I0 + 2N
+            }
+#pragma unroll
+            for (int e = 0; e < N; ++e) {
+                const int I = I0 + e;
+                const T a = e == 0 ? left : od.v[e - 1];
+                const T d = e == N - 1 ? right : ev.v[e + 1];
+                const T ax = fw_axis(a, ev.v[e], od.v[e], d, I == 0 ? wf : w3, I == cx - 1 ? wf : w3);
+                if (dy == 0) ay[e] = ax;
+                else if (dy == 1) ay[e] = ay[e] + (J == 0 ? wf : w3) * ax;
+                else if (dy == 2) ay[e] = ay[e] + (J == cy - 1 ? wf : w3) * ax;
+                else ay[e] = ay[e] + ax;
+            }
+        }
+#pragma unroll
+        for (int e = 0; e < N; ++e) {
+            if (DIM == 2) {
+                az[e] = ay[e];
+            } else {
+                const int64_t gK = gc.z0 + K;
+                if (dz == 0) az[e] = ay[e];
+                else if (dz == 1) az[e] = az[e] + (gK == 0 ? wf : w3) * ay[e];
+                else if (dz == 2) az[e] = az[e] + (gK == gc.gnz - 1 ? wf : w3) * ay[e];
+                else az[e] = az[e] + ay[e];
+            }
+        }
+    }
+    const int64_t gK = gc.z0 + K;
+    const int pc = (int)((J + gK) & 1);
+    const int64_t rowc = K * gc.P + (int64_t)J * gc.hw;
+#pragma unroll
+    for (int e = 0; e < N; ++e) {
+        const int I = I0 + e;
+        R[rowc + ((I + pc) & 1) * gc.H + (I >> 1)] = (DIM == 3 ? (T)(1.0 / 512.0) : (T)(1.0 / 64.0)) * az[e];
+    }
+}
+
 // ---- prolongation + correction --------------------------------------------------------------
 
 // The oracle's cval() factor: -cl per out-of-box axis, in x, y, z order, applied to coarse value v
@@ -1663,8 +1844,9 @@ __device__ __forceinline__ void block_partial_t(double acc, double* partials)
     if (threadIdx.x == 0) partials[blockIdx.x] = red[0];
 }
 
-// src: the level's u before the phase; dst: the phase's output (POST with ERR reads psiOld from
-// dst first).  V/gc: coarse correction (POST); R/gc: restricted residual (PRE); both point at the
+// src: the level's u before the phase; dst: the phase's output; old (POST with ERR): psiOld, either dst
+// itself (read plane by plane just before the output overwrites it) or a buffer of its own (kept for the
+// reference's metrics, mgp_metrics / psiOld / errorBuf).  V/gc: coarse correction (POST); R/gc: restricted residual (PRE); both point at the
 // coarse plane of local fine plane 0 (gc.z0 = g.z0 / 2).  zc: planes per z-chunk.  gz: readable
 // ghost planes per side of src / f / dst (on a distributed level they must hold the neighbours'
 // current H planes).  CLZ: the level operator has no boundary modification (cl == 0, level 0).
@@ -1677,13 +1859,16 @@ __device__ __forceinline__ void block_partial_t(double acc, double* partials)
 template <typename T, bool PRE, int LINEAR, bool ERR, bool CLZ>
 __global__ __launch_bounds__((ZsShape<T, PRE>::NTL))
 __attribute__((amdgpu_waves_per_eu(1, PRE ? ZS_WPE_PRE : ZS_WPE_POST))) void k_zs(const T* __restrict__ src, const T* __restrict__ f,
-                                                                T* __restrict__ dst, T* __restrict__ R,
+                                                                T* __restrict__ dst, const T* old, T* __restrict__ R,
                                                                 const T* __restrict__ V, double* __restrict__ partials,
                                                                 Geo g, Geo gc, Op<T, 3> op, T clc, int zc, int gz)
 {
     using S = ZsShape<T, PRE>;
     constexpr int N = S::N, H = S::H, HWE = S::HWE, G = S::G, YE = S::YE, SLOT = S::SLOT, TX = S::TX,
                   TY = S::TY, NS3 = S::NS3, NTL = S::NTL;
+    // PRE: LINEAR selects the restriction: 0 = residual + 2^3 average here; 1 = none (both colours of the
+    // smoothed level stored; the host runs the full-weighting restriction after the phase)
+    constexpr bool RR = PRE && LINEAR == 0;
     using VT = Vec<T, N>;
     using PF = ZsPrefetch<T, N>;
     extern __shared__ __align__(16) unsigned char zs_smem[];
@@ -1810,7 +1995,7 @@ __attribute__((amdgpu_waves_per_eu(1, PRE ? ZS_WPE_PRE : ZS_WPE_POST))) void k_z
             r.f1 = gload<T, N, kZsNTL>(f + (pP - Pz) + goff);
             r.f2 = gload<T, N, kZsNTL>(f + (pP - 2 * Pz) + Hh + goff);
             if (!PRE && ERR && tile_xy) {  // psiOld of plane p - 4, for the tile's own columns only
-                const T* dp = dst + (pP - 4 * Pz);
+                const T* dp = old + (pP - 4 * Pz);
                 r.o0 = gload<T, N, kZsNTL>(dp + goff);
                 r.o1 = gload<T, N, kZsNTL>(dp + Hh + goff);
             }
@@ -1819,7 +2004,7 @@ __attribute__((amdgpu_waves_per_eu(1, PRE ? ZS_WPE_PRE : ZS_WPE_POST))) void k_z
             r.f1 = gload<T, N, kZsNTL>(f + (int64_t)ZS_PLANE(pcl(p - 1)) * P + goff);
             r.f2 = gload<T, N, kZsNTL>(f + (int64_t)ZS_PLANE(pcl(p - 2)) * P + Hh + goff);
             if (!PRE && ERR && tile_xy) {
-                const T* dp = dst + (int64_t)pcl(p - 4) * P;
+                const T* dp = old + (int64_t)pcl(p - 4) * P;
                 r.o0 = gload<T, N, kZsNTL>(dp + goff);
                 r.o1 = gload<T, N, kZsNTL>(dp + Hh + goff);
             }
@@ -1927,7 +2112,7 @@ __attribute__((amdgpu_waves_per_eu(1, PRE ? ZS_WPE_PRE : ZS_WPE_POST))) void k_z
             vstore<T, N>(slot(S::OFF1, 2, p - 1) + col.lrow, o1);
             vstore<T, N>(slot(S::OFF2, 2, p - 2) + col.lrow, o2);
             vstore<T, N>(slot(S::OFF3, NS3, p - 3) + col.lrow, o3);
-            if (PRE) vstore<T, N>(slot(S::OFF4, 2, p - 4) + col.lrow, o4);
+            if (RR) vstore<T, N>(slot(S::OFF4, 2, p - 4) + col.lrow, o4);
         }
 
         // ---- the smoothed plane p - 4: red final after stage 3, black after stage 4 ----
@@ -1948,13 +2133,13 @@ __attribute__((amdgpu_waves_per_eu(1, PRE ? ZS_WPE_PRE : ZS_WPE_POST))) void k_z
                 T* dp = dst + (int64_t)q * P;
                 // PRE: the red cells are not stored.  Its output is read only by POST, whose stage 0
                 // loads the black cells (the first post half-sweep replaces the red ones unread).
-                if (!PRE || kZsPreRed) gstore<T, N, kZsNTS>(dp + goff, W3[sl(4)]);
+                if (!RR || kZsPreRed) gstore<T, N, kZsNTS>(dp + goff, W3[sl(4)]);
                 gstore<T, N, kZsNTS>(dp + Hh + goff, o4);
             }
         }
 
         // ---- PRE: residual + restriction of plane p - 5 ----
-        if (PRE) {
+        if (RR) {
             const int q = p - 5;
             const int pq = par(q);
             zs_nb_load<T, N>(nr, slot(S::OFF3, NS3, q), col);  // red of A4 at q
@@ -2092,6 +2277,7 @@ constexpr int tail_threads() { return sizeof(T) == 4 ? TAIL_THREADS_F32 : 512; }
 template <typename T, int DIM>
 struct TailArgs {
     int nlev, nops, jacobi, zero0;  // zero0: level 0's u is a fresh zero guess (not read)
+    int fw;                          // full-weighting restriction (TAIL_RR)
     int64_t off[kTailMaxLevels];     // element offset of the level's LDS region
     int64_t region[kTailMaxLevels];  // elements of one LDS array of the level (ghost planes included)
     T* u[kTailMaxLevels];            // global interior plane 0 of u / f
@@ -2171,8 +2357,22 @@ __global__ __launch_bounds__(tail_threads<T>()) void k_tail(const TailArgs<T, DI
             }
         } else if (op == TAIL_RR) {
             const int64_t n = resrestrict_items<T, DIM>(g);
-            for (int64_t it = tid; it < n; it += kTailThreads)
-                resrestrict_item<T, DIM>(cur(l), rhs(l), rhs(l + 1), g, a.g[l + 1], a.op[l], it);
+            if (a.fw) {  // full weighting: every fine residual evaluated where a coarse cell reads it
+                const Geo gc = a.g[l + 1];
+                const T* U = cur(l);
+                const T* F = rhs(l);
+                const T wf = (T)3 - a.op[l + 1].cl;
+                auto get = [&](int i, int j, int64_t k) { return residual_at<T, DIM>(U, F, g, a.op[l], i, j, k); };
+                for (int64_t it = tid; it < n; it += kTailThreads) {
+                    const int cx = g.nx >> 1, cy = g.ny >> 1;
+                    const int I = (int)(it % cx), J = (int)((it / cx) % cy);
+                    const int64_t K = it / ((int64_t)cx * cy);
+                    rhs(l + 1)[pidx(gc, I, J, K)] = fw_eval<T, DIM>(get, g, gc, wf, I, J, K);
+                }
+            } else {
+                for (int64_t it = tid; it < n; it += kTailThreads)
+                    resrestrict_item<T, DIM>(cur(l), rhs(l), rhs(l + 1), g, a.g[l + 1], a.op[l], it);
+            }
             __syncthreads();
         } else if (op == TAIL_ZERO) {
             T* U = cur(l);
@@ -2307,6 +2507,37 @@ __device__ __forceinline__ void tc_rr(const T* U, const T* F, T* Fc, const Op<T,
     }
 }
 
+// tc_rr with the full-weighting restriction (fw_eval over the residuals of the 4^DIM fine cells)
+template <typename T, int DIM, int N>
+__device__ __forceinline__ void tc_rr_fw(const T* U, const T* F, T* Fc, const Op<T, DIM>& op, T wf, int tid)
+{
+    using L = TcLev<DIM, N>;
+    using C = TcLev<DIM, N / 2>;
+    constexpr int M = N / 2, CNT = C::CELLS;
+    Geo g{}, gc{};
+    g.nx = g.ny = N;
+    g.gnz = DIM == 3 ? N : 1;
+    gc.nx = gc.ny = M;
+    gc.gnz = DIM == 3 ? M : 1;
+    auto res = [&](int i, int j, int64_t k64) {
+        const int k = (int)k64;
+        const int x = L::idx(i, j, k);
+        T sm = U[x - 1] + U[x + 1];
+        sm = sm + U[x - L::W];
+        sm = sm + U[x + L::W];
+        if (DIM == 3) {
+            sm = sm + U[x - L::W * L::W];
+            sm = sm + U[x + L::W * L::W];
+        }
+        const int nb = (i == 0) + (i == N - 1) + (j == 0) + (j == N - 1) + (DIM == 3 ? (k == 0) + (k == N - 1) : 0);
+        return op.residual_idx(sm, F[x], U[x], nb);
+    };
+    for (int q = tid; q < CNT; q += kTcThreads) {
+        const int I = q % M, J = (q / M) % M, K = DIM == 3 ? q / (M * M) : 0;
+        Fc[C::idx(I, J, K)] = fw_eval<T, DIM>(res, g, gc, wf, I, J, (int64_t)K);
+    }
+}
+
 template <typename T, int DIM, int N, int LINEAR>
 __device__ __forceinline__ void tc_prolong(T* U, const T* V, T cl, int tid)
 {
@@ -2437,7 +2668,10 @@ __global__ __launch_bounds__(kTcThreads) void k_tail_c(const TailArgs<T, DIM> a)
                 __syncthreads();                                                                       \
             } else if constexpr (N >= 2 && (L) + 1 < NL) {                                             \
                 if (op == TAIL_RR) {                                                                   \
-                    tc_rr<T, DIM, N>(TC_U(L), TC_F(L), TC_F((L) + 1), sop[L], tid);                    \
+                    if (a.fw)                                                                          \
+                        tc_rr_fw<T, DIM, N>(TC_U(L), TC_F(L), TC_F((L) + 1), sop[L], (T)3 - sop[(L) + 1].cl, tid); \
+                    else                                                                               \
+                        tc_rr<T, DIM, N>(TC_U(L), TC_F(L), TC_F((L) + 1), sop[L], tid);                \
                     __syncthreads();                                                                   \
                 } else if (op == TAIL_PROLONG) {                                                       \
                     tc_prolong<T, DIM, N, LINEAR>(TC_U(L), TC_U((L) + 1), sop[(L) + 1].cl, tid);       \
@@ -2491,28 +2725,34 @@ constexpr size_t tc_lds(int rb)
 template <int DIM>
 constexpr int blk_threads() { return DIM == 3 ? 1024 : 256; }
 
-// Compile-time shape of a phase: owned B^DIM tile, halo E (y, z) and HX (x, even), NS sweeps.
-template <int DIM, bool PRE, int B, int NS>
+// Compile-time shape of a phase: owned B^DIM tile, halo E (y, z) and HX (x, even), NS sweeps.  FW (PRE):
+// the full-weighting restriction reads the residuals of a one-cell ring around the tile, so the swept
+// region ends one cell wider.
+template <int DIM, bool PRE, int B, int NS, bool FW = false>
 struct BlkShape {
-    static constexpr int E = PRE ? 2 * NS + 1 : 2 * NS;
+    static constexpr int E = PRE ? 2 * NS + 1 + (FW ? 1 : 0) : 2 * NS;
     static constexpr int HX = (E + 1) & ~1;
     static constexpr int EX = B + 2 * HX, EY = B + 2 * E, EZ = DIM == 3 ? B + 2 * E : 1, EH = EX / 2;
     static constexpr int BZ = DIM == 3 ? B : 1;  // owned planes
     static constexpr int cells = EX * EY * EZ;
     static constexpr int owned = B * B * BZ;
+    static constexpr int RB = FW ? B + 2 : B, RBZ = DIM == 3 ? RB : 1;  // residual region edge (PRE)
+    static constexpr int rcells = RB * RB * RBZ;
     // POST: coarse cells x0/2 - 1 .. of the extended tile's parents and their neighbours
     static constexpr int CX = EX / 2 + 2, CY = EY / 2 + 3, CZ = DIM == 3 ? EZ / 2 + 3 : 1;
     static constexpr int ccells = CX * CY * CZ;
     static constexpr int lidx(int lz, int ly, int c, int mm) { return ((lz * EY + ly) * 2 + c) * EH + mm; }
 };
 
+// PRE: LINEAR selects the restriction (0: the 2^DIM average, 1: full weighting with face weight 3 - clc)
 template <typename T, int DIM, bool PRE, int LINEAR, int B, int NS>
 __global__ __launch_bounds__(blk_threads<DIM>()) void k_blk(const T* __restrict__ src, const T* __restrict__ f,
                                                             T* __restrict__ dst, T* __restrict__ R,
                                                             const T* __restrict__ V, Geo g, Geo gc, Op<T, DIM> op,
                                                             T clc)
 {
-    using S = BlkShape<DIM, PRE, B, NS>;
+    constexpr bool FW = PRE && LINEAR == 1;
+    using S = BlkShape<DIM, PRE, B, NS, FW>;
     constexpr int E = S::E, HX = S::HX, EY = S::EY, EZ = S::EZ, EH = S::EH, BZ = S::BZ;
     constexpr int EZH = DIM == 3 ? E : 0;  // z halo
     constexpr int NT = blk_threads<DIM>();
@@ -2642,7 +2882,39 @@ __global__ __launch_bounds__(blk_threads<DIM>()) void k_blk(const T* __restrict_
         __syncthreads();
     }
 
-    if (PRE) {
+    if (FW) {
+        // residual of the owned cells and a one-cell ring (0 outside the box) into RS ...
+        constexpr int RB = S::RB;
+#pragma unroll
+        for (int q = 0; q < (S::rcells + NT - 1) / NT; ++q) {
+            const int it = tid + q * NT;
+            if (it < S::rcells) {
+                const int x = it % RB - 1, y = (it / RB) % RB - 1, z = DIM == 3 ? it / (RB * RB) - 1 : 0;
+                const int gi = X0 + x, gj = Y0 + y, gk = Z0 + z;  // gk local
+                T v = (T)0;
+                if (gi >= 0 && gi < g.nx && gj >= 0 && gj < g.ny && (DIM == 2 || (gk >= 0 && gk < nzl))) {
+                    const int lx = HX + x, ly = E + y, lz = EZH + z;
+                    const int c = (lx & 1) ^ ((ly + lz + p0) & 1);
+                    const int own = S::lidx(lz, ly, c, lx >> 1);
+                    v = sop.residual_idx(nbsum(lx, ly, lz, c), F[own], U[own], faces(gi, gj, gz0 + gk));
+                }
+                RS[it] = v;
+            }
+        }
+        __syncthreads();
+        // ... then one coarse cell per thread by full weighting (fw_eval's order)
+        constexpr int C = B / 2, CZ = DIM == 3 ? C : 1;
+        const T wf = (T)3 - clc;
+        for (int it = tid; it < C * C * CZ; it += NT) {
+            const int I = it % C, J = (it / C) % C, K = it / (C * C);
+            const int gI = (X0 >> 1) + I, gJ = (Y0 >> 1) + J, gK = (Z0 >> 1) + K;
+            // RS holds fine local cell x at x + 1: coarse I reads RS columns 2I .. 2I + 3
+            auto get = [&](int i, int j, int64_t k) {
+                return RS[((DIM == 3 ? (int)k - Z0 + 1 : 0) * RB + (j - Y0 + 1)) * RB + (i - X0 + 1)];
+            };
+            R[pidx(gc, gI, gJ, (int64_t)gK)] = fw_eval<T, DIM>(get, g, gc, wf, gI, gJ, (int64_t)gK);
+        }
+    } else if (PRE) {
         // residual of every owned cell into RS (residual_at's expressions) ...
 #pragma unroll
         for (int q = 0; q < (S::owned + NT - 1) / NT; ++q) {
@@ -3045,6 +3317,59 @@ hipError_t launch_residual_restrict(int rb, int dim, const void* u, const void* 
 }
 
 template <typename T, int D>
+static void resfield_t(const void* u, const void* f, void* r, Geo g, double h, double cl, hipStream_t s)
+{
+    const Op<T, D> op = make_op<T, D>(h, cl);
+    if (half_vector(sizeof(T), g)) {
+        const int64_t items = half_items(sizeof(T), g);
+        k_resfield_v<T, D><<<nblk(2 * items), kBlock, 0, s>>>((const T*)u, (const T*)f, (T*)r, g, op, items);
+    } else {
+        k_residual_field<T, D><<<nblk_gs(g.P * g.nz), kBlock, 0, s>>>((const T*)u, (const T*)f, (T*)r, g, op);
+    }
+}
+
+hipError_t launch_residual_field_v(int rb, int dim, const void* u, const void* f, void* r, Geo g, double h, double cl,
+                                   hipStream_t s)
+{
+    if (rb == 8) {
+        if (dim == 3) resfield_t<double, 3>(u, f, r, g, h, cl, s);
+        else resfield_t<double, 2>(u, f, r, g, h, cl, s);
+    } else {
+        if (dim == 3) resfield_t<float, 3>(u, f, r, g, h, cl, s);
+        else resfield_t<float, 2>(u, f, r, g, h, cl, s);
+    }
+    return hipGetLastError();
+}
+
+template <typename T, int D>
+static void fw_t(const void* r, void* R, Geo g, Geo gc, double clc, hipStream_t s)
+{
+    constexpr int n = VN<T>::n;
+    const int cx = g.nx / 2;
+    const int64_t ncz = D == 3 ? g.nz / 2 : 1;
+    const T wf = (T)3 - (T)clc;
+    if (cx >= n) {
+        const int64_t items = (int64_t)(cx / n) * (g.ny / 2) * ncz;
+        k_fw_v<T, D><<<nblk(items), kBlock, 0, s>>>((const T*)r, (T*)R, g, gc, wf);
+    } else {
+        const int64_t items = (int64_t)cx * (g.ny / 2) * ncz;
+        k_fw_s<T, D><<<nblk(items), kBlock, 0, s>>>((const T*)r, (T*)R, g, gc, wf);
+    }
+}
+
+hipError_t launch_fw_restrict(int rb, int dim, const void* r, void* R, Geo g, Geo gc, double clc, hipStream_t s)
+{
+    if (rb == 8) {
+        if (dim == 3) fw_t<double, 3>(r, R, g, gc, clc, s);
+        else fw_t<double, 2>(r, R, g, gc, clc, s);
+    } else {
+        if (dim == 3) fw_t<float, 3>(r, R, g, gc, clc, s);
+        else fw_t<float, 2>(r, R, g, gc, clc, s);
+    }
+    return hipGetLastError();
+}
+
+template <typename T, int D>
 static hipError_t pr_t(int linear, void* u, const void* V, Geo g, Geo gc, double clc, bool black, hipStream_t s)
 {
     constexpr int n = VN<T>::n;
@@ -3089,7 +3414,8 @@ static hipError_t zs_launch(const FusedArgs& a, hipStream_t s)
     const Op<T, 3> op = make_op<T, 3>(a.h, a.cl);
     const unsigned nb = (unsigned)((a.g.nx / S::TX) * (a.g.ny / S::TY) * (a.g.nz / a.zc));
     k_zs<T, PRE, LINEAR, ERR, CLZ><<<nb, S::NTL, S::lds_bytes, s>>>((const T*)a.src, (const T*)a.f, (T*)a.dst,
-                                                                     (T*)a.R, (const T*)a.V, a.partials, a.g, a.gc,
+                                                                     (const T*)(a.old ? a.old : a.dst), (T*)a.R,
+                                                                     (const T*)a.V, a.partials, a.g, a.gc,
                                                                      op, (T)a.clc, a.zc, a.ghost);
     return hipGetLastError();
 }
@@ -3098,7 +3424,7 @@ template <typename T, bool CLZ>
 static hipError_t fused_dispatch(const FusedArgs& a, hipStream_t s)
 {
     const bool err = a.partials != nullptr;
-    if (a.pre) return zs_launch<T, true, 0, false, CLZ>(a, s);
+    if (a.pre) return a.linear ? zs_launch<T, true, 1, false, CLZ>(a, s) : zs_launch<T, true, 0, false, CLZ>(a, s);
     if (a.linear) return err ? zs_launch<T, false, 1, true, CLZ>(a, s) : zs_launch<T, false, 1, false, CLZ>(a, s);
     return err ? zs_launch<T, false, 0, true, CLZ>(a, s) : zs_launch<T, false, 0, false, CLZ>(a, s);
 }
@@ -3153,6 +3479,7 @@ static hipError_t fused_attr()
     const int pre = (int)ZsShape<T, true>::lds_bytes, post = (int)ZsShape<T, false>::lds_bytes;
     const auto A = hipFuncAttributeMaxDynamicSharedMemorySize;
     hipError_t e = hipFuncSetAttribute((const void*)k_zs<T, true, 0, false, CLZ>, A, pre);
+    if (e == hipSuccess) e = hipFuncSetAttribute((const void*)k_zs<T, true, 1, false, CLZ>, A, pre);
     if (e == hipSuccess) e = hipFuncSetAttribute((const void*)k_zs<T, false, 0, false, CLZ>, A, post);
     if (e == hipSuccess) e = hipFuncSetAttribute((const void*)k_zs<T, false, 0, true, CLZ>, A, post);
     if (e == hipSuccess) e = hipFuncSetAttribute((const void*)k_zs<T, false, 1, false, CLZ>, A, post);
@@ -3244,6 +3571,7 @@ static hipError_t tail_t(const TailSpec& t, hipStream_t s)
     a.nops = t.nops;
     a.jacobi = t.jacobi;
     a.zero0 = t.zero_first;
+    a.fw = t.fw;
     const int G = D == 3 ? kGhost3D : 0;
     int64_t off = 0;
     for (int l = 0; l < t.nlev; ++l) {
@@ -3291,11 +3619,11 @@ hipError_t launch_tail(int rb, int dim, const TailSpec& t, hipStream_t s)
 template <int DIM>
 constexpr int blk_tile() { return DIM == 3 ? kBlkTile : kBlkTile2D; }
 
-template <typename T, int DIM, bool PRE, int NS>
+template <typename T, int DIM, bool PRE, int NS, bool FW = false>
 constexpr size_t blk_lds()
 {
-    using S = BlkShape<DIM, PRE, blk_tile<DIM>(), NS>;
-    return (2 * (size_t)S::cells + (PRE ? (size_t)S::owned : (size_t)S::ccells)) * sizeof(T);
+    using S = BlkShape<DIM, PRE, blk_tile<DIM>(), NS, FW>;
+    return (2 * (size_t)S::cells + (PRE ? (size_t)S::rcells : (size_t)S::ccells)) * sizeof(T);
 }
 
 // the owned tile edge B divides every axis of the level (3D: B^3 tiles, 2D: B^2)
@@ -3304,8 +3632,8 @@ bool block_supported(int rb, int dim, int ns, const Geo& g)
     if ((dim != 2 && dim != 3) || ns < 1 || ns > kBlkMaxSweeps) return false;
     const int B = dim == 3 ? kBlkTile : kBlkTile2D;
     if (g.nx < B || g.ny < B || (dim == 3 && g.nz < B) || g.z0 != 0 || g.gnz != g.nz) return false;
-    const size_t lds = rb == 8 ? (dim == 3 ? blk_lds<double, 3, true, kBlkMaxSweeps>() : blk_lds<double, 2, true, kBlkMaxSweeps>())
-                               : (dim == 3 ? blk_lds<float, 3, true, kBlkMaxSweeps>() : blk_lds<float, 2, true, kBlkMaxSweeps>());
+    const size_t lds = rb == 8 ? (dim == 3 ? blk_lds<double, 3, true, kBlkMaxSweeps, true>() : blk_lds<double, 2, true, kBlkMaxSweeps, true>())
+                               : (dim == 3 ? blk_lds<float, 3, true, kBlkMaxSweeps, true>() : blk_lds<float, 2, true, kBlkMaxSweeps, true>());
     return lds <= kTailMaxLds;
 }
 
@@ -3315,7 +3643,9 @@ static hipError_t blk_attr_ns()
     constexpr int B = blk_tile<D>();
     const auto A = hipFuncAttributeMaxDynamicSharedMemorySize;
     const int pre = (int)blk_lds<T, D, true, NS>(), post = (int)blk_lds<T, D, false, NS>();
+    const int pre_fw = (int)blk_lds<T, D, true, NS, true>();
     hipError_t e = hipFuncSetAttribute((const void*)k_blk<T, D, true, 0, B, NS>, A, pre);
+    if (e == hipSuccess) e = hipFuncSetAttribute((const void*)k_blk<T, D, true, 1, B, NS>, A, pre_fw);
     if (e == hipSuccess) e = hipFuncSetAttribute((const void*)k_blk<T, D, false, 0, B, NS>, A, post);
     if (e == hipSuccess) e = hipFuncSetAttribute((const void*)k_blk<T, D, false, 1, B, NS>, A, post);
     return e;
@@ -3339,7 +3669,10 @@ static hipError_t blk_t(const BlockArgs& a, hipStream_t s)
     const Op<T, D> op = make_op<T, D>(a.h, a.cl);
     const unsigned nb = (unsigned)((a.g.nx / B) * (a.g.ny / B) * (D == 3 ? a.g.nz / B : 1));
     const T* src = (const T*)a.src;
-    if (a.pre)
+    if (a.pre && a.linear)  // PRE: linear = full-weighting restriction
+        k_blk<T, D, true, 1, B, NS><<<nb, NT, blk_lds<T, D, true, NS, true>(), s>>>(
+            src, (const T*)a.f, (T*)a.dst, (T*)a.R, (const T*)a.V, a.g, a.gc, op, (T)a.clc);
+    else if (a.pre)
         k_blk<T, D, true, 0, B, NS><<<nb, NT, blk_lds<T, D, true, NS>(), s>>>(
             src, (const T*)a.f, (T*)a.dst, (T*)a.R, (const T*)a.V, a.g, a.gc, op, (T)a.clc);
     else if (a.linear)

@@ -30,8 +30,8 @@ mg:metrics() returns relErr, count, frobErr of the last outer iteration (gpu.lua
 mg:residualNorm() returns ||f - A psi||, ||f|| (device reduction).
 Extra table fields select the build's configurations: dim (2|3), real, smoother ('jacobi'|'rbgs'),
 cycle ('V'|'F'), prolong ('pc'|'linear'), coarse_init ('fresh'|'warm'), coarse_bc
-('zero'|'consistent'), device.  Defaults reproduce cpu.lua (2D, double, Jacobi 7+7, V-cycle,
-injection, fresh zero coarse guess, ghost value 0).
+('zero'|'consistent'), restriction ('average'|'full_weighting'), device.  Defaults reproduce cpu.lua
+(2D, double, Jacobi 7+7, V-cycle, injection, 2x2 average, fresh zero coarse guess, ghost value 0).
 Errors from the library raise Lua errors (error()), as the reference's own failures do.
 
 Not executable in this repository's CI (no Lua runtime in the image): tests/test_lua_binding.py
@@ -59,6 +59,7 @@ typedef struct mgp_opts {
     int32_t err_mode;
     int32_t device;
     int32_t rank, world;
+    int32_t restriction;
     int64_t gather_cells;
     uint8_t comm_id[128];
 } mgp_opts;
@@ -82,6 +83,7 @@ int         mgp_set_coarse_handoff(mgp_ctx* c, int64_t size, mgp_coarse_fn fn, v
 int         mgp_metrics(mgp_ctx* c, double* rel_err, int64_t* count, double* frob);
 int         mgp_residual_norm(mgp_ctx* c, int level, double* rnorm, double* fnorm);
 int         mgp_group_create(mgp_group** out, const mgp_opts* o, int ngpu, const int* devices);
+mgp_ctx*    mgp_group_rank(mgp_group* g, int rank);
 void        mgp_group_destroy(mgp_group* g);
 const char* mgp_group_last_error(const mgp_group* g);
 int         mgp_group_init_point_charge(mgp_group* g);
@@ -100,6 +102,7 @@ local CODES = {
 	prolong = {pc = 0, linear = 1},
 	coarse_init = {fresh = 0, warm = 1},
 	coarse_bc = {zero = 0, consistent = 1},
+	restriction = {average = 0, full_weighting = 1},
 }
 -- include/mgpoisson.h MGP_FIELD_*; names of cpu-raw.lua:148-171
 local FIELD = {psi = 0, f = 1, rs = 2, vs = 3, psiOld = 4, errorBuf = 5, tmpU = 6, Vs = 0, Rs = 1}
@@ -134,7 +137,11 @@ MultigridHIP.__index = function(self, k)
 		local mg = self
 		return setmetatable({}, {__index = function(_, L) return mg:getImage(FIELD[k], mg:levelOf(L)) end})
 	end
-	if k == 'inPlaceIterativeSolver' then return rawget(self, 'build').smoother end
+	if k == 'inPlaceIterativeSolver' then
+		return rawget(self, 'pendingSmoother') or rawget(self, 'build').smoother
+	end
+	-- the value last assigned, as a plain field of cpu.lua's object would read back
+	if k == 'smooth' then return rawget(self, 'pendingSmooth') or rawget(self, 'build').smooth end
 	return rawget(MultigridHIP, k)
 end
 
@@ -194,6 +201,30 @@ function MultigridHIP:createContext()
 		local pp = ffi.new('mgp_ctx*[1]')
 		check(lib.mgp_create(pp, o), nil)
 		rawset(self, 'ctx', ffi.gc(pp[0], lib.mgp_destroy))
+		self:applyCoarse()
+	end
+end
+
+-- cpu-gpu.lua:55-72 cpuDepth: the GPU's one-launch coarse engine from size 2^cpuDepth, or the hand-off of
+-- that level to engine:twoGrid (re-applied whenever the context is rebuilt)
+function MultigridHIP:applyCoarse()
+	local cpuDepth, engine = rawget(self, 'cpuDepth'), rawget(self, 'engine')
+	if not cpuDepth then return end
+	local L = bit.lshift(1, cpuDepth)
+	if engine then
+		-- cpu-gpu.lua:17-52: the callback runs engine:twoGrid on the level's host copies
+		local cb = rawget(self, 'handoff')
+		if not cb then
+			local pt = rawget(self, 'ptype')
+			cb = ffi.cast('mgp_coarse_fn', function(user, h, u, f, size)
+				local ok = pcall(engine.twoGrid, engine, h, ffi.cast(pt, u), ffi.cast(pt, f), tonumber(size))
+				return ok and 0 or 1
+			end)
+			rawset(self, 'handoff', cb)  -- keep the callback alive
+		end
+		check(lib.mgp_set_coarse_handoff(self.ctx, L, cb, nil), self.ctx)
+	else
+		lib.mgp_set_coarse_level(self.ctx, L)  -- keeps the default switch when it does not fit
 	end
 end
 
@@ -211,6 +242,7 @@ function MultigridHIP:init(a, real, cpuDepth, engine)
 		-- cpu-raw.lua positional protocol: persistent coarse buffers (cpu-raw.lua:221)
 		args = {size = a, real = real, coarse_init = 'warm'}
 		rawset(self, 'cpuDepth', cpuDepth)
+		rawset(self, 'engine', engine)
 	end
 	local n = assert(tonumber(args.size), 'size is required')
 	local dim = args.dim or 2
@@ -227,27 +259,13 @@ function MultigridHIP:init(a, real, cpuDepth, engine)
 	end
 	rawset(self, 'build', {real = rawget(self, 'real'), smooth = args.smooth or MultigridHIP.smooth,
 		smoother = smoother or 'jacobi', cycle = args.cycle, prolong = args.prolong,
-		coarse_init = args.coarse_init, coarse_bc = args.coarse_bc, device = args.device})
-	self:createContext()
+		coarse_init = args.coarse_init, coarse_bc = args.coarse_bc, restriction = args.restriction,
+		device = args.device})
 	local cells = n * n * (dim == 3 and n or 1)
 	rawset(self, 'count', cells)
 	rawset(self, 'ctype', (rawget(self, 'real') == 'float') and 'float[?]' or 'double[?]')
 	rawset(self, 'ptype', (rawget(self, 'real') == 'float') and 'float*' or 'double*')
-	if cpuDepth and not rawget(self, 'group') then
-		local L = bit.lshift(1, cpuDepth)
-		if engine then
-			-- cpu-gpu.lua:17-52: the callback runs engine:twoGrid on the level's host copies
-			local pt = rawget(self, 'ptype')
-			local cb = ffi.cast('mgp_coarse_fn', function(user, h, u, f, size)
-				local ok = pcall(engine.twoGrid, engine, h, ffi.cast(pt, u), ffi.cast(pt, f), tonumber(size))
-				return ok and 0 or 1
-			end)
-			rawset(self, 'handoff', cb)  -- keep the callback alive
-			check(lib.mgp_set_coarse_handoff(self.ctx, L, cb, nil), self.ctx)
-		else
-			lib.mgp_set_coarse_level(self.ctx, L)  -- keeps the default switch when it does not fit
-		end
-	end
+	self:createContext()
 	self:initPointCharge()
 end
 
@@ -276,17 +294,26 @@ function MultigridHIP:applyKnobs()
 	self:setBuffer(1, f)
 end
 
+-- the context that answers level queries: the solver's own, or rank 0's of a multi-GPU group
+function MultigridHIP:infoCtx()
+	local g = rawget(self, 'group')
+	if g then return lib.mgp_group_rank(g, 0) end
+	return self.ctx
+end
+
 function MultigridHIP:levelOf(size)
 	local info = ffi.new('int64_t[8]')
-	local n = check(lib.mgp_num_levels(self.ctx), self.ctx)
+	local ctx = self:infoCtx()
+	local n = check(lib.mgp_num_levels(ctx), ctx)
 	for l = 0, n - 1 do
-		check(lib.mgp_level_info(self.ctx, l, info), self.ctx)
+		check(lib.mgp_level_info(ctx, l, info), ctx)
 		if tonumber(info[0]) == size then return l end
 	end
 	error('no level of size ' .. tostring(size))
 end
 
 function MultigridHIP:metrics()
+	if rawget(self, 'group') then error('metrics: single-GPU solvers only (ngpu > 1 runs mgp_group_*)', 2) end
 	local rel, n, frob = ffi.new('double[1]'), ffi.new('int64_t[1]'), ffi.new('double[1]')
 	check(lib.mgp_metrics(self.ctx, rel, n, frob), self.ctx)
 	return rel[0], tonumber(n[0]), frob[0]
@@ -304,9 +331,11 @@ function MultigridHIP:getBuffer(which, level)
 	level = level or 0
 	local count = self.count
 	if level ~= 0 then
+		-- a group's fields are the global box: nz_global (info[2]); one context's are its planes (info[3])
 		local info = ffi.new('int64_t[8]')
-		check(lib.mgp_level_info(self.ctx, level, info), self.ctx)
-		count = tonumber(info[0] * info[1] * info[3])
+		local ctx = self:infoCtx()
+		check(lib.mgp_level_info(ctx, level, info), ctx)
+		count = tonumber(info[0] * info[1] * (rawget(self, 'group') and info[2] or info[3]))
 	end
 	local buf = ffi.new(self.ctype, count)
 	local g = rawget(self, 'group')

@@ -38,6 +38,7 @@ CYCLE_V, CYCLE_F = 0, 1
 PROLONG_PC, PROLONG_LINEAR = 0, 1
 COARSE_FRESH, COARSE_WARM = 0, 1
 BC_ZERO, BC_CONSISTENT = 0, 1
+RESTRICT_AVERAGE, RESTRICT_FULL_WEIGHTING = 0, 1
 FIELD_U, FIELD_F = 0, 1
 FIELD_RESIDUAL, FIELD_CORRECTION, FIELD_PSI_OLD, FIELD_ERROR, FIELD_TMP = 2, 3, 4, 5, 6
 # cpu-raw.lua:148-171 names of the level fields (Vs/Rs are U/F below the finest level)
@@ -70,6 +71,7 @@ class MGPOpts(ctypes.Structure):
         ("device", ctypes.c_int32),
         ("rank", ctypes.c_int32),
         ("world", ctypes.c_int32),
+        ("restriction", ctypes.c_int32),
         ("gather_cells", ctypes.c_int64),
         ("comm_id", ctypes.c_uint8 * COMM_ID_BYTES),
     ]

@@ -17,12 +17,14 @@ CYCLES = {"V": L.CYCLE_V, "F": L.CYCLE_F}
 PROLONGS = {"pc": L.PROLONG_PC, "linear": L.PROLONG_LINEAR}
 COARSE_INITS = {"fresh": L.COARSE_FRESH, "warm": L.COARSE_WARM}
 COARSE_BCS = {"zero": L.BC_ZERO, "consistent": L.BC_CONSISTENT}
+RESTRICTIONS = {"average": L.RESTRICT_AVERAGE, "full_weighting": L.RESTRICT_FULL_WEIGHTING}
 REALS = {"double": 8, "float": 4}
 
 
 def make_opts(dim=2, n=(8, 8, 1), real="double", nu1=7, nu2=7, smoother="jacobi", cycle="V",
               prolong="pc", coarse_init="fresh", coarse_bc="zero", coarse_sweeps=48, err_mode=1,
-              device=-1, rank=0, world=1, gather_cells=32768, comm_id: bytes | None = None) -> L.MGPOpts:
+              device=-1, rank=0, world=1, gather_cells=32768, comm_id: bytes | None = None,
+              restriction="average") -> L.MGPOpts:
     """Build mgp_opts from keyword names (defaults = the reference cpu.lua configuration)."""
     o = L.default_opts()
     o.dim = dim
@@ -40,6 +42,7 @@ def make_opts(dim=2, n=(8, 8, 1), real="double", nu1=7, nu2=7, smoother="jacobi"
     o.device = device
     o.rank, o.world = rank, world
     o.gather_cells = gather_cells
+    o.restriction = RESTRICTIONS[restriction] if isinstance(restriction, str) else restriction
     if comm_id is not None:
         ctypes.memmove(o.comm_id, comm_id, L.COMM_ID_BYTES)
     return o

@@ -95,8 +95,9 @@ class MultigridHIP(_RawFields):
     'debug': ...})`` or the same as keyword arguments.  A missing (None) field falls back to
     the class default exactly as the Lua ``self.maxiter = args.maxiter`` does (cpu.lua:174-177
     with the class fields of cpu.lua:18-22).  Build options beyond the reference's (``dim``,
-    ``real``, ``smoother``, ``cycle``, ``prolong``, ``coarse_init``, ``coarse_bc``) default to
-    the reference configuration: 2D, double, Jacobi 7+7, V-cycle, injection, fresh zero guess.
+    ``real``, ``smoother``, ``cycle``, ``prolong``, ``coarse_init``, ``coarse_bc``, ``restriction``)
+    default to the reference configuration: 2D, double, Jacobi 7+7, V-cycle, injection, 2x2 average,
+    fresh zero guess.
     """
 
     debug = False
@@ -126,7 +127,7 @@ class MultigridHIP(_RawFields):
         self._build = dict(dim=self.dim, real=a.get("real", "double"), smoother=_smoother_name(sm),
                            cycle=a.get("cycle", "V"), prolong=a.get("prolong", "pc"),
                            coarse_init=a.get("coarse_init", "fresh"), coarse_bc=a.get("coarse_bc", "zero"),
-                           device=a.get("device", -1))
+                           restriction=a.get("restriction", "average"), device=a.get("device", -1))
         self._ctx = None
         self._ctx_smooth = None
         self._ensure_ctx()

@@ -52,6 +52,7 @@ void mgo_opts_default(mgo_opts* o)
     o->coarse_sweeps = 48;
     o->coarse_bc = MGO_BC_ZERO;       /* ghost 0 on every level, cpu.lua:28-31 */
     o->threads = 1;
+    o->restriction = MGO_RESTRICT_AVERAGE; /* cpu.lua:127-135 */
 }
 
 static int64_t ncell(const mgo_level* L) { return L->nx * L->ny * L->nz; }
@@ -181,6 +182,15 @@ static void restrict_any(int dim, int64_t nx, int64_t ny, int64_t nz, int rb, co
         restrict__f(dim, nx, ny, nz, (const float*)r, (float*)R, threads);
 }
 
+static void restrict_fw_any(int dim, int64_t nx, int64_t ny, int64_t nz, int rb, double clc, const void* r,
+                            void* R, int threads)
+{
+    if (rb == 8)
+        restrict_fw_d(dim, nx, ny, nz, clc, (const double*)r, (double*)R, threads);
+    else
+        restrict_fw_f(dim, nx, ny, nz, clc, (const float*)r, (float*)R, threads);
+}
+
 static void prolong_any(int dim, int64_t nx, int64_t ny, int64_t nz, int rb, int prolong, double clc,
                         void* u, const void* V, int threads)
 {
@@ -224,7 +234,10 @@ static void cycle_rec(mgo_ctx* c, int l, double h, int fcycle)
     smooth_any(o->dim, L->nx, L->ny, L->nz, o->real_bytes, o->smoother, o->nu1, h, cl, L->u, L->f,
                L->tmp, o->threads);
     residual_any(o->dim, L->nx, L->ny, L->nz, o->real_bytes, h, cl, L->u, L->f, L->r, o->threads);
-    restrict_any(o->dim, L->nx, L->ny, L->nz, o->real_bytes, L->r, C->f, o->threads);
+    if (o->restriction == MGO_RESTRICT_FULL_WEIGHTING)
+        restrict_fw_any(o->dim, L->nx, L->ny, L->nz, o->real_bytes, clc, L->r, C->f, o->threads);
+    else
+        restrict_any(o->dim, L->nx, L->ny, L->nz, o->real_bytes, L->r, C->f, o->threads);
     if (o->coarse_init == MGO_COARSE_FRESH) /* V = matrix.zeros (cpu.lua:138) */
         memset(C->u, 0, (size_t)ncell(C) * (size_t)o->real_bytes);
     if (fcycle) {
@@ -303,6 +316,20 @@ void mgo_restrict_arr(int dim, int64_t nx, int64_t ny, int64_t nz, int real_byte
                       void* R)
 {
     restrict_any(dim, nx, ny, dim == 2 ? 1 : nz, real_bytes, r, R, 1);
+}
+
+double mgo_residual_sumsq_arr(int dim, int64_t nx, int64_t ny, int64_t nz, int real_bytes, double h, double cl,
+                              const void* u, const void* f, int64_t z_lo, int64_t z_hi, int threads)
+{
+    if (dim == 2) nz = 1;
+    return real_bytes == 8 ? residual_sumsq_d(dim, nx, ny, nz, h, cl, (const double*)u, (const double*)f, z_lo, z_hi, threads)
+                           : residual_sumsq_f(dim, nx, ny, nz, h, cl, (const float*)u, (const float*)f, z_lo, z_hi, threads);
+}
+
+void mgo_restrict_fw_arr(int dim, int64_t nx, int64_t ny, int64_t nz, int real_bytes, double cl_coarse,
+                         const void* r, void* R)
+{
+    restrict_fw_any(dim, nx, ny, dim == 2 ? 1 : nz, real_bytes, cl_coarse, r, R, 1);
 }
 
 void mgo_prolong_correct_arr(int dim, int64_t nx, int64_t ny, int64_t nz, int real_bytes,

@@ -17,7 +17,8 @@
  *   cpu-raw.lua:221    persistent (warm) coarse buffers  -> MGO_COARSE_WARM
  * Build-defined extensions (no reference counterpart; pinned only by known-answer tests):
  *   3D 7-point form (-6/h^2, 2x2x2 average x1/8, 2x2x2 injection), red/black GS, F-cycle,
- *   cell-centred (bi/tri)linear prolongation, non-cubic boxes and their line/plane coarse solve.
+ *   cell-centred (bi/tri)linear prolongation and its adjoint, the cell-centred full-weighting
+ *   restriction (north_star), non-cubic boxes and their line/plane coarse solve.
  *
  * PARITY STATUS: "parity unpinned" against the reference itself.  The reference is Lua and
  * neither Lua nor its (unvendored) libraries exist in this image, and the reference ships no
@@ -39,6 +40,7 @@ enum { MGO_CYCLE_V = 0, MGO_CYCLE_F = 1 };
 enum { MGO_PROLONG_PC = 0, MGO_PROLONG_LINEAR = 1 };
 enum { MGO_COARSE_FRESH = 0, MGO_COARSE_WARM = 1 };
 enum { MGO_BC_ZERO = 0, MGO_BC_CONSISTENT = 1 };
+enum { MGO_RESTRICT_AVERAGE = 0, MGO_RESTRICT_FULL_WEIGHTING = 1 };
 
 typedef struct mgo_opts {
     int dim;            /* 2 or 3 */
@@ -55,6 +57,9 @@ typedef struct mgo_opts {
                            c_l = (2^l - 1)/(2^l + 1), so the coarse operator sees u = 0 where the
                            fine grid's ghost sits (build-defined; level 0 is unchanged) */
     int threads;        /* OpenMP threads (1 = the reference's single thread) */
+    int restriction;    /* MGO_RESTRICT_AVERAGE: 2^d cell average (reference, cpu.lua:127-135)
+                           MGO_RESTRICT_FULL_WEIGHTING: cell-centred full weighting, the adjoint of
+                           the linear prolongation (build-defined; restrict_fw in mgp_oracle_impl.h) */
 } mgo_opts;
 
 typedef struct mgo_ctx mgo_ctx;
@@ -84,6 +89,13 @@ void mgo_residual_arr(int dim, int64_t nx, int64_t ny, int64_t nz, int real_byte
                       double cl, const void* u, const void* f, void* r);
 void mgo_restrict_arr(int dim, int64_t nx, int64_t ny, int64_t nz, int real_bytes,
                       const void* r, void* R);
+/* sum of (f - A u)^2 in fp64 over planes [z_lo, z_hi) of an nx x ny x nz array (its ends are the
+ * Dirichlet ghost): the independent check of mgp_residual_norm on fields read back in plane chunks */
+double mgo_residual_sumsq_arr(int dim, int64_t nx, int64_t ny, int64_t nz, int real_bytes, double h, double cl,
+                              const void* u, const void* f, int64_t z_lo, int64_t z_hi, int threads);
+/* full-weighting restriction of r (cl_coarse = the coarse level's boundary coefficient) */
+void mgo_restrict_fw_arr(int dim, int64_t nx, int64_t ny, int64_t nz, int real_bytes, double cl_coarse,
+                         const void* r, void* R);
 void mgo_prolong_correct_arr(int dim, int64_t nx, int64_t ny, int64_t nz, int real_bytes,
                              int prolong, double cl_coarse, void* u, const void* V);
 /* c_l for level l under coarse_bc (0 for level 0 and for MGO_BC_ZERO) */

@@ -174,6 +174,55 @@ static void FN(restrict_)(int dim, int64_t nx, int64_t ny, int64_t nz, const MGO
             }
 }
 
+/* Full-weighting restriction (build-defined option, BASELINE north_star "full-weighting restriction"):
+ * the cell-centred adjoint of the linear prolongation below, R = 2^-d P^T r.  Per axis a coarse cell I
+ * takes fine cells 2I-1, 2I, 2I+1, 2I+2 with weights 1, w_lo, w_hi, 1 (then / 8), where w = 3, and at
+ * the box faces (I = 0 for 2I, I = m-1 for 2I+1) w = 3 - clc: the -clc ghost factor of cval() (clc =
+ * the coarse level's coefficient, 0 for MGO_BC_ZERO).  Fine cells outside the box count as r = +0.
+ * Separable, x first, then y, then z, each axis summed ((r_a + w_b r_b) + w_c r_c) + r_d, and the
+ * result scaled by 1/8^d (exact).  The 2x2x2 average above stays the default (cpu.lua:127-135). */
+static inline MGO_T FN(fw_axis)(MGO_T a, MGO_T b, MGO_T c, MGO_T d, MGO_T wb, MGO_T wc)
+{
+    MGO_T s = a + wb * b;
+    s = s + wc * c;
+    s = s + d;
+    return s;
+}
+
+static void FN(restrict_fw)(int dim, int64_t nx, int64_t ny, int64_t nz, double clc, const MGO_T* r,
+                            MGO_T* R, int threads)
+{
+    const int64_t cx = nx / 2, cy = ny / 2, cz = dim == 3 ? nz / 2 : 1;
+    const int64_t pl = nx * ny, cpl = cx * cy;
+    const MGO_T w3 = (MGO_T)3, wf = (MGO_T)3 - (MGO_T)clc;
+    const MGO_T scale = dim == 3 ? (MGO_T)(1.0 / 512.0) : (MGO_T)(1.0 / 64.0);
+#pragma omp parallel for num_threads(threads) schedule(static) if (threads > 1 && pl * nz > 65536)
+    for (int64_t K = 0; K < cz; ++K)
+        for (int64_t J = 0; J < cy; ++J)
+            for (int64_t I = 0; I < cx; ++I) {
+                MGO_T az[4];
+                const int nzz = dim == 3 ? 4 : 1;
+                for (int dz = 0; dz < nzz; ++dz) {
+                    const int64_t k = dim == 3 ? 2 * K - 1 + dz : 0;
+                    MGO_T ay[4];
+                    for (int dy = 0; dy < 4; ++dy) {
+                        const int64_t j = 2 * J - 1 + dy;
+                        MGO_T x[4];
+                        for (int dx = 0; dx < 4; ++dx) {
+                            const int64_t i = 2 * I - 1 + dx;
+                            const int in = i >= 0 && i < nx && j >= 0 && j < ny && k >= 0 && k < nz;
+                            x[dx] = in ? r[i + nx * j + pl * k] : (MGO_T)0;
+                        }
+                        ay[dy] = FN(fw_axis)(x[0], x[1], x[2], x[3], I == 0 ? wf : w3, I == cx - 1 ? wf : w3);
+                    }
+                    az[dz] = FN(fw_axis)(ay[0], ay[1], ay[2], ay[3], J == 0 ? wf : w3, J == cy - 1 ? wf : w3);
+                }
+                const MGO_T s = dim == 3 ? FN(fw_axis)(az[0], az[1], az[2], az[3], K == 0 ? wf : w3, K == cz - 1 ? wf : w3)
+                                         : az[0];
+                R[I + cx * J + cpl * K] = scale * s;
+            }
+}
+
 /* Coarse value for the linear prolongation.  Outside the box the ghost is -cl times the
  * value of the nearest cell inside (cl = 0: the reference's ghost 0).  Only one axis can be
  * outside at a time for the separable weights used below, but the clamp is applied per axis. */
@@ -225,6 +274,36 @@ static void FN(prolong_correct)(int dim, int64_t nx, int64_t ny, int64_t nz, int
                 }
                 u[c] = u[c] + v;
             }
+}
+
+/* sum of r^2 (r = f - A u in the real type, residual()'s expressions) over planes [z_lo, z_hi) of an
+ * nx x ny x nz array whose ends are the Dirichlet ghost (a caller that passes a chunk of a larger field
+ * with one halo plane per side gets that field's residual on the chunk's inner planes); per-plane fp64
+ * partials, then summed in plane order. */
+static double FN(residual_sumsq)(int dim, int64_t nx, int64_t ny, int64_t nz, double h, double cl, const MGO_T* u,
+                                 const MGO_T* f, int64_t z_lo, int64_t z_hi, int threads)
+{
+    const MGO_T hh = (MGO_T)h, hSq = hh * hh, adiag = (MGO_T)(-2 * dim) / hSq, c = (MGO_T)cl;
+    const int64_t pl = nx * ny, np_ = z_hi - z_lo;
+    double* part = (double*)calloc((size_t)(np_ > 0 ? np_ : 1), sizeof(double));
+#pragma omp parallel for num_threads(threads) schedule(static) if (threads > 1)
+    for (int64_t q = 0; q < np_; ++q) {
+        const int64_t k = z_lo + q;
+        double s = 0.0;
+        for (int64_t j = 0; j < ny; ++j)
+            for (int64_t i = 0; i < nx; ++i) {
+                const int64_t cc = i + nx * j + pl * k;
+                const MGO_T askew = FN(nbsum)(u, dim, nx, ny, nz, i, j, k) / hSq;
+                const MGO_T dg = FN(diag)(dim, FN(nfaces)(dim, nx, ny, nz, i, j, k), c, hSq, adiag);
+                const MGO_T r = f[cc] - (askew + dg * u[cc]);
+                s += (double)r * (double)r;
+            }
+        part[q] = s;
+    }
+    double t = 0.0;
+    for (int64_t q = 0; q < np_; ++q) t += part[q];
+    free(part);
+    return t;
 }
 
 /* sum over cells of (psi - psiOld)^2 in double; per-plane partials then in-order total. */

@@ -26,6 +26,7 @@ CYCLE_V, CYCLE_F = 0, 1
 PROLONG_PC, PROLONG_LINEAR = 0, 1
 COARSE_FRESH, COARSE_WARM = 0, 1
 BC_ZERO, BC_CONSISTENT = 0, 1
+RESTRICT_AVERAGE, RESTRICT_FULL_WEIGHTING = 0, 1
 
 
 def _nbsum(u: np.ndarray, dim: int) -> np.ndarray:
@@ -136,6 +137,35 @@ def restrict(r, dim):
     return r.dtype.type(0.125) * s
 
 
+def restrict_fw(r, dim, clc=0.0):
+    """Full weighting (build-defined option): the cell-centred adjoint of the linear prolongation.
+
+    Per axis, coarse cell I gets fine cells 2I-1 .. 2I+2 as ((r_a + w_b r_b) + w_c r_c) + r_d with
+    w = 3, or 3 - clc next to a box face (I = 0 for 2I, I = m-1 for 2I+1); fine cells outside the box
+    are +0.  x, then y, then z; finally times 1/8^d (mgp_oracle_impl.h restrict_fw()).
+    """
+    dt = r.dtype.type
+    w3, wf = dt(3), dt(3) - dt(clc)
+    axes = (2, 1, 0) if dim == 3 else (2, 1)
+    p = np.pad(r, 1) if dim == 3 else np.pad(r, ((0, 0), (1, 1), (1, 1)))
+    for ax in axes:
+        n = p.shape[ax] - 2
+        m = n // 2
+        take = lambda off: np.take(p, np.arange(m) * 2 + off, axis=ax)  # noqa: E731
+        wb = np.full(m, w3, r.dtype)
+        wc = np.full(m, w3, r.dtype)
+        wb[0] = wf
+        wc[m - 1] = wf
+        shp = [1, 1, 1]
+        shp[ax] = m
+        wb, wc = wb.reshape(shp), wc.reshape(shp)
+        s = take(0) + wb * take(1)
+        s = s + wc * take(2)
+        p = s + take(3)  # the axes still to be reduced keep their zero border
+    scale = dt(1.0 / 512.0) if dim == 3 else dt(1.0 / 64.0)
+    return scale * p
+
+
 def _axis_idx(n_fine, n_coarse):
     idx = np.arange(n_fine)
     parent = idx >> 1
@@ -203,7 +233,7 @@ class Multigrid:
 
     def __init__(self, dim=2, n=(8, 8, 1), dtype=np.float64, nu1=7, nu2=7, smoother=JACOBI,
                  cycle=CYCLE_V, prolong_kind=PROLONG_PC, coarse_init=COARSE_FRESH,
-                 coarse_sweeps=48, coarse_bc=BC_ZERO):
+                 coarse_sweeps=48, coarse_bc=BC_ZERO, restriction=RESTRICT_AVERAGE):
         nx, ny, nz = n
         if dim == 2:
             nz = 1
@@ -211,6 +241,7 @@ class Multigrid:
         self.nu1, self.nu2, self.smoother, self.cycle = nu1, nu2, smoother, cycle
         self.prolong_kind, self.coarse_init, self.coarse_sweeps = prolong_kind, coarse_init, coarse_sweeps
         self.coarse_bc = coarse_bc
+        self.restriction = restriction
         shapes = []
         s = (nz, ny, nx)
         while True:
@@ -237,7 +268,11 @@ class Multigrid:
             sweeps = 1 if u.size == 1 else self.coarse_sweeps
             return smooth(u, f, h, self.dim, self.smoother, sweeps, cl)
         u = smooth(u, f, h, self.dim, self.smoother, self.nu1, cl)
-        R = restrict(residual(u, f, h, self.dim, cl), self.dim)
+        r = residual(u, f, h, self.dim, cl)
+        if self.restriction == RESTRICT_FULL_WEIGHTING:
+            R = restrict_fw(r, self.dim, coarse_coef(self.coarse_bc, l + 1))
+        else:
+            R = restrict(r, self.dim)
         V = np.zeros_like(R) if self.coarse_init == COARSE_FRESH else self.V[l + 1]
         if fcycle:
             V = self._cycle(l + 1, V, R, 2 * h, True)

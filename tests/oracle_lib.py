@@ -20,6 +20,7 @@ CYCLES = {"V": 0, "F": 1}
 PROLONGS = {"pc": 0, "linear": 1}
 INITS = {"fresh": 0, "warm": 1}
 BCS = {"zero": 0, "consistent": 1}
+RESTRICTIONS = {"average": 0, "full_weighting": 1}
 
 
 class Opts(ctypes.Structure):
@@ -27,7 +28,7 @@ class Opts(ctypes.Structure):
                 ("real_bytes", ctypes.c_int), ("nu1", ctypes.c_int), ("nu2", ctypes.c_int),
                 ("smoother", ctypes.c_int), ("cycle", ctypes.c_int), ("prolong", ctypes.c_int),
                 ("coarse_init", ctypes.c_int), ("coarse_sweeps", ctypes.c_int), ("coarse_bc", ctypes.c_int),
-                ("threads", ctypes.c_int)]
+                ("threads", ctypes.c_int), ("restriction", ctypes.c_int)]
 
 
 def _load():
@@ -50,6 +51,9 @@ def _load():
     lib.mgo_smooth_arr.argtypes = [ctypes.c_int, i64, i64, i64, ctypes.c_int, ctypes.c_int, ctypes.c_int, d, d, vp, vp]
     lib.mgo_residual_arr.argtypes = [ctypes.c_int, i64, i64, i64, ctypes.c_int, d, d, vp, vp, vp]
     lib.mgo_restrict_arr.argtypes = [ctypes.c_int, i64, i64, i64, ctypes.c_int, vp, vp]
+    lib.mgo_residual_sumsq_arr.restype = d
+    lib.mgo_residual_sumsq_arr.argtypes = [ctypes.c_int, i64, i64, i64, ctypes.c_int, d, d, vp, vp, i64, i64, ctypes.c_int]
+    lib.mgo_restrict_fw_arr.argtypes = [ctypes.c_int, i64, i64, i64, ctypes.c_int, d, vp, vp]
     lib.mgo_prolong_correct_arr.argtypes = [ctypes.c_int, i64, i64, i64, ctypes.c_int, ctypes.c_int, d, vp, vp]
     lib.mgo_coarse_coef.restype = d
     lib.mgo_coarse_coef.argtypes = [ctypes.c_int, ctypes.c_int]
@@ -65,7 +69,8 @@ class Oracle:
     """The C oracle configured like mgpoisson.make_opts (same keyword names)."""
 
     def __init__(self, dim=2, n=(8, 8, 1), real="double", nu1=7, nu2=7, smoother="jacobi", cycle="V",
-                 prolong="pc", coarse_init="fresh", coarse_bc="zero", coarse_sweeps=48, threads=1):
+                 prolong="pc", coarse_init="fresh", coarse_bc="zero", coarse_sweeps=48, threads=1,
+                 restriction="average"):
         o = Opts()
         lib.mgo_opts_default(ctypes.byref(o))
         nn = tuple(n) + (1,) * (3 - len(n))
@@ -74,6 +79,7 @@ class Oracle:
         o.nu1, o.nu2 = nu1, nu2
         o.smoother, o.cycle, o.prolong = SMOOTHERS[smoother], CYCLES[cycle], PROLONGS[prolong]
         o.coarse_init, o.coarse_bc, o.coarse_sweeps, o.threads = INITS[coarse_init], BCS[coarse_bc], coarse_sweeps, threads
+        o.restriction = RESTRICTIONS[restriction]
         self.o = o
         self.dtype = np.dtype(np.float64 if o.real_bytes == 8 else np.float32)
         self.shape = (o.nz, o.ny, o.nx) if dim == 3 else (o.ny, o.nx)
@@ -122,12 +128,32 @@ def residual_arr(dim, u, f, h, cl=0.0):
     return r
 
 
+def residual_sumsq_arr(dim, u, f, h, cl=0.0, z_lo=0, z_hi=None, threads=1):
+    """sum of (f - A u)^2 (fp64) over planes [z_lo, z_hi) of a 3D (nz, ny, nx) array; its ends are the ghost."""
+    u = np.ascontiguousarray(u)
+    f = np.ascontiguousarray(f, u.dtype)
+    nz, ny, nx = (u.shape if dim == 3 else (1,) + u.shape)
+    z_hi = nz if z_hi is None else z_hi
+    return lib.mgo_residual_sumsq_arr(dim, nx, ny, nz, u.itemsize, h, cl, u.ctypes.data, f.ctypes.data, z_lo, z_hi,
+                                      threads)
+
+
 def restrict_arr(dim, r):
     r = np.ascontiguousarray(r)
     shp = tuple(s // 2 for s in r.shape)
     R = np.empty(shp, r.dtype)
     nz, ny, nx = (r.shape if dim == 3 else (1,) + r.shape)
     lib.mgo_restrict_arr(dim, nx, ny, nz, r.itemsize, r.ctypes.data, R.ctypes.data)
+    return R
+
+
+def restrict_fw_arr(dim, r, cl_coarse=0.0):
+    """Full-weighting restriction (the adjoint of the linear prolongation), mgp_oracle_impl.h restrict_fw."""
+    r = np.ascontiguousarray(r)
+    shp = tuple(s // 2 for s in r.shape)
+    R = np.empty(shp, r.dtype)
+    nz, ny, nx = (r.shape if dim == 3 else (1,) + r.shape)
+    lib.mgo_restrict_fw_arr(dim, nx, ny, nz, r.itemsize, cl_coarse, r.ctypes.data, R.ctypes.data)
     return R
 
 

@@ -60,8 +60,10 @@ def test_opts_struct_layout_matches_header():
     assert o.struct_size == ctypes.sizeof(mg._lib.MGPOpts) == 224
     # defaults = the reference cpu.lua configuration
     assert (o.dim, o.real_bytes, o.nu1, o.nu2) == (2, 8, 7, 7)
-    assert (o.smoother, o.cycle, o.prolong, o.coarse_init, o.coarse_bc) == (0, 0, 0, 0, 0)
-    assert mg._lib.lib.mgp_version() == 1
+    assert (o.smoother, o.cycle, o.prolong, o.coarse_init, o.coarse_bc, o.restriction) == (0, 0, 0, 0, 0, 0)
+    assert mg._lib.lib.mgp_version() == 2
+    # restriction sits in the former padding after world, before the 8-byte gather_cells
+    assert mg._lib.MGPOpts.restriction.offset == 84 and mg._lib.MGPOpts.gather_cells.offset == 88
 
 
 def test_plan_single_cube():

@@ -56,3 +56,29 @@ def test_group_rejects_bad_split():
     mg = _mg()
     with pytest.raises(mg.MGPError):
         mg.Group(mg.make_opts(dim=3, n=(16, 16, 16)), 16, devices=[0] * 16)
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_group_rank_failure_aborts_instead_of_hanging(world, monkeypatch):
+    """a rank that fails before its exchange must not leave the other ranks blocked in it.
+    One rank fails at once (test hook MGP_TEST_FAIL_RANK); the call returns the error within seconds (not the
+    loopback barrier's 120 s), the group is marked unusable, and the caller's device is unchanged."""
+    import time
+
+    import torch
+
+    mg = _mg()
+    cfg = dict(real="float", smoother="rbgs", nu1=2, nu2=2, prolong="linear", coarse_bc="consistent")
+    g = mg.Group(mg.make_opts(dim=3, n=(64, 64, 128), **cfg), world, devices=[0] * world)
+    g.init_point_charge()
+    g.cycles(1)  # healthy first
+    monkeypatch.setenv("MGP_TEST_FAIL_RANK", str(world - 1))
+    t0 = time.perf_counter()
+    with pytest.raises(mg.MGPError, match="injected failure"):
+        g.cycles(3)
+    assert time.perf_counter() - t0 < 30
+    monkeypatch.delenv("MGP_TEST_FAIL_RANK")
+    with pytest.raises(mg.MGPError, match="aborted"):
+        g.cycle()
+    assert torch.cuda.current_device() == 0
+    g.close()

@@ -526,6 +526,42 @@ def test_metrics_match_reference_formulas(kw):
     assert abs(frob - r_frob) <= 1e-12 * r_frob and abs(frob - e) <= 1e-12 * e
 
 
+@pytest.mark.parametrize("real,cycle", [("float", "V"), ("double", "F")])
+def test_metrics_under_temporally_blocked_finest_level(real, cycle, monkeypatch):
+    """k_zs on level 0 (forced down to 128^3): POST writes a buffer of its own, so psiOld survives the cycle and
+    the reference's metrics (gpu.lua:173-200, test-gpu-obj.lua:222-243) and the psiOld / errorBuf fields
+    (cpu-raw.lua:148-153) work on the north-star path; psi equals MGP_KEEP_PSI_OLD=0 (in place) bit for bit."""
+    monkeypatch.setenv("MGP_FUSED_MIN_CELLS", "65536")
+    kw = dict(dim=3, n=(128, 128, 128), real=real, cycle=cycle, smoother="rbgs", nu1=2, nu2=2, prolong="linear",
+              coarse_bc="consistent")
+    ctx = _ctx(**kw)
+    monkeypatch.setenv("MGP_KEEP_PSI_OLD", "0")
+    inplace = _ctx(**kw)
+    assert ctx.levels[0]["engine"] == "zs"
+    mg = _mg()
+    for x in (ctx, inplace):
+        x.init_point_charge()
+        x.cycles(2)
+    old = ctx.get_psi()
+    e, e2 = ctx.cycle(), inplace.cycle()
+    assert e == e2 and np.array_equal(ctx.get_psi(), inplace.get_psi())
+    rel, n, frob = ctx.metrics()
+    r_rel, r_n, r_frob = _ref_metrics(ctx.get_psi(), old)
+    assert n == r_n
+    assert abs(rel - r_rel) <= 1e-12 * abs(r_rel)
+    assert abs(frob - r_frob) <= 1e-12 * r_frob and abs(frob - e) <= 1e-12 * e
+    assert np.array_equal(ctx.get_field(mg.FIELD_PSI_OLD), old)
+    d = ctx.get_psi() - old
+    assert np.array_equal(ctx.get_field(mg.FIELD_ERROR), d * d)
+    with pytest.raises(mg.MGPError):
+        inplace.metrics()
+    # graph replay keeps the rotation: two more cycles, psiOld = the iterate before the last one
+    ctx.cycles(1)
+    old = ctx.get_psi()
+    ctx.cycles(1)
+    assert np.array_equal(ctx.get_field(mg.FIELD_PSI_OLD), old)
+
+
 def test_metrics_need_err_mode():
     ctx = _ctx(dim=2, n=(16, 16, 1), err_mode=0)
     ctx.init_point_charge()

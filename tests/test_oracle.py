@@ -13,7 +13,7 @@ import numpy as np
 import pytest
 
 import mgp_oracle_np as N
-from oracle_lib import Oracle, coarse_coef, prolong_correct_arr, residual_arr, restrict_arr, smooth_arr
+from oracle_lib import Oracle, coarse_coef, prolong_correct_arr, residual_arr, restrict_arr, restrict_fw_arr, smooth_arr
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
@@ -25,7 +25,8 @@ def _np_model(cfg):
     return N.Multigrid(cfg["dim"], cfg["n"], dt, cfg.get("nu1", 7), cfg.get("nu2", 7),
                        codes["smoother"][cfg.get("smoother", "jacobi")], codes["cycle"][cfg.get("cycle", "V")],
                        codes["prolong"][cfg.get("prolong", "pc")], codes["coarse_init"][cfg.get("coarse_init", "fresh")],
-                       coarse_bc=codes["coarse_bc"][cfg.get("coarse_bc", "zero")])
+                       coarse_bc=codes["coarse_bc"][cfg.get("coarse_bc", "zero")],
+                       restriction={"average": 0, "full_weighting": 1}[cfg.get("restriction", "average")])
 
 
 CROSS = [
@@ -38,6 +39,13 @@ CROSS = [
     dict(dim=3, n=(8, 8, 8), smoother="rbgs", nu1=2, nu2=2, prolong="linear", coarse_bc="consistent"),
     dict(dim=3, n=(8, 8, 16), smoother="rbgs", nu1=2, nu2=2, cycle="F", prolong="linear", coarse_bc="consistent", real="float"),
     dict(dim=3, n=(8, 8, 8), smoother="jacobi", prolong="pc"),
+    # the full-weighting restriction option (build-defined, north_star)
+    dict(dim=2, n=(32, 16, 1), smoother="rbgs", nu1=2, nu2=2, prolong="linear", coarse_bc="consistent",
+         restriction="full_weighting"),
+    dict(dim=2, n=(16, 16, 1), restriction="full_weighting", real="float"),
+    dict(dim=3, n=(8, 8, 16), smoother="rbgs", nu1=2, nu2=2, cycle="F", prolong="linear", coarse_bc="consistent",
+         restriction="full_weighting"),
+    dict(dim=3, n=(8, 8, 8), smoother="rbgs", nu1=2, nu2=2, prolong="linear", real="float", restriction="full_weighting"),
 ]
 
 
@@ -209,3 +217,72 @@ def test_oracle_reproduces_golden(path):
         if it in (1, 2, 10):
             assert np.array_equal(o.get(0), z[f"psi{it}"])
     np.testing.assert_allclose(errs, z["errs"], rtol=1e-13, atol=0)
+
+
+# ---- full-weighting restriction (build-defined option; north_star "full-weighting restriction") ----
+
+@pytest.mark.parametrize("dim,shape", [(2, (16, 32)), (2, (2, 2)), (3, (8, 16, 4)), (3, (2, 2, 2)), (3, (16, 16, 16))])
+@pytest.mark.parametrize("real", [np.float64, np.float32])
+@pytest.mark.parametrize("clc", [0.0, 1 / 3, 7 / 9])
+def test_full_weighting_c_equals_numpy(dim, shape, real, clc):
+    r = np.random.default_rng(5).standard_normal(shape).astype(real)
+    s3 = shape if dim == 3 else (1,) + shape
+    R = restrict_fw_arr(dim, r, clc)
+    Rn = N.restrict_fw(r.reshape(s3), dim, clc)
+    assert np.array_equal(R.reshape(Rn.shape).view(np.uint8), np.ascontiguousarray(Rn).view(np.uint8))
+
+
+@pytest.mark.parametrize("dim,shape", [(2, (16, 32)), (3, (8, 16, 4)), (3, (4, 4, 4))])
+@pytest.mark.parametrize("clc", [0.0, 1 / 3, 7 / 9])
+def test_full_weighting_is_adjoint_of_linear_prolongation(dim, shape, clc):
+    """R = 2^-dim P^T: <R r, V> 2^dim == <r, P V> for the linear P with the same coarse coefficient."""
+    rng = np.random.default_rng(6)
+    r = rng.standard_normal(shape)
+    V = rng.standard_normal(tuple(s // 2 for s in shape))
+    PV = prolong_correct_arr(dim, np.zeros(shape), V, "linear", clc)
+    lhs = float(np.sum(restrict_fw_arr(dim, r, clc) * V)) * 2 ** dim
+    rhs = float(np.sum(r * PV))
+    assert abs(lhs - rhs) <= 1e-12 * max(1.0, abs(rhs))
+
+
+def test_full_weighting_known_answers():
+    """Interior coarse cells of a constant field are that constant (weights (1,3,3,1)/8 per axis); a corner
+    coarse cell with zero ghosts keeps 7/8 per axis (the fine cell outside contributes +0)."""
+    for dim, shape in ((2, (16, 16)), (3, (8, 8, 8))):
+        R = restrict_fw_arr(dim, np.ones(shape), 0.0)
+        inner = R[(slice(1, -1),) * dim]
+        assert np.all(inner == 1.0)
+        assert R[(0,) * dim] == (7 / 8) ** dim
+        # with the consistent boundary coefficient c, the face weight is 3 - c: (7 - c) / 8 per face axis
+        c = 1 / 3
+        Rc = restrict_fw_arr(dim, np.ones(shape), c)
+        assert Rc[(0,) * dim] == pytest.approx(((7 - c) / 8) ** dim, rel=1e-15)
+
+
+@pytest.mark.parametrize("cfg", [
+    dict(dim=2, n=(64, 64, 1), smoother="rbgs", nu1=2, nu2=2, prolong="linear", coarse_bc="consistent"),
+    dict(dim=2, n=(64, 64, 1), smoother="rbgs", nu1=2, nu2=2, cycle="F", prolong="linear", coarse_bc="zero"),
+    dict(dim=3, n=(16, 16, 16), smoother="rbgs", nu1=2, nu2=2, prolong="linear", coarse_bc="consistent"),
+    dict(dim=3, n=(32, 32, 32), smoother="rbgs", nu1=2, nu2=2, prolong="linear", coarse_bc="zero"),
+], ids=["2dV-consistent", "2dF-zero", "3dV-consistent", "3dV-zero"])
+def test_full_weighting_converges_to_dst(cfg):
+    """The full-weighting option shares the fixed point A^-1 f (DST-I exact solution)."""
+    o = Oracle(restriction="full_weighting", threads=4, **cfg)
+    o.init_point_charge()
+    errs = [o.step() for _ in range(25)]
+    ex = _dst(o, cfg["dim"], cfg["n"])
+    assert np.linalg.norm(o.get(0) - ex) <= 1e-9 * np.linalg.norm(ex)
+    assert errs[-1] < errs[5] * 1e-6
+
+
+def test_full_weighting_rescues_the_zero_boundary_v_cycle():
+    """2D 256^2 RB-GS 2+2 V-cycle with linear P and ghost-0 coarse levels: the 2x2 average diverges
+    (SURVEY §7 [probe]), full weighting converges (update-RMS contraction ~0.81 per cycle)."""
+    kw = dict(dim=2, n=(256, 256, 1), smoother="rbgs", nu1=2, nu2=2, prolong="linear", coarse_bc="zero", threads=4)
+    a, f = Oracle(**kw), Oracle(restriction="full_weighting", **kw)
+    a.init_point_charge()
+    f.init_point_charge()
+    ea = [a.step() for _ in range(14)]
+    ef = [f.step() for _ in range(14)]
+    assert ea[-1] > ea[-2]
+    assert ef[-1] < 0.9 * ef[-2] and ef[-1] < 1e-2 * ef[0]
