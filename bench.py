@@ -17,6 +17,9 @@ max-rank time, i.e. 512^3-cell V-cycles per second for the whole job (= plain V-
 --box 2048,2048,2048; configs[4]: --box 4096,4096,4096 --cycle F).  On one GPU, --box 2048,2048,256
 and --box 4096,4096,512 run one rank's slab of those configs.  value = cycles/s of the whole box.
 --dim 2 --n 4096: BASELINE configs[1] (2D 4096^2 RB-GS, cache-resident: flagged in the line).
+--config0: BASELINE configs[0], the reference cpu.lua path (2D 256^2, fp64, Jacobi 7+7 V-cycle, injection,
+ghost-0 coarse levels), with the CPU port timed over the same cycles (1 thread and OpenMP) beside the GPU.
+--restriction full_weighting: the build's full-weighting option instead of the 2^d cell average.
 
 Launch: python bench.py [--gpus N --steps K --warmup W]  (N>1 under torch.distributed.run).
 """
@@ -45,6 +48,14 @@ def parse():
     p.add_argument("--real", default="float", choices=["float", "double"])
     p.add_argument("--cycle", default="V", choices=["V", "F"])
     p.add_argument("--nu", type=int, default=2)
+    p.add_argument("--smoother", default="rbgs", choices=["rbgs", "jacobi"])
+    p.add_argument("--prolong", default="linear", choices=["linear", "pc"])
+    p.add_argument("--coarse-bc", default="consistent", choices=["consistent", "zero"])
+    p.add_argument("--restriction", default="average", choices=["average", "full_weighting"])
+    p.add_argument("--config0", action="store_true",
+                   help="BASELINE configs[0]: 2D 256^2 fp64 Jacobi 7+7 V-cycle, injection, ghost 0 (cpu.lua path)")
+    p.add_argument("--copy-probe-mb", type=int, default=2048,
+                   help="buffer size of the measured copy-bandwidth probe reported beside the roofline (0 = skip)")
     p.add_argument("--no-timing", action="store_true", help="skip the per-launch smoother events")
     p.add_argument("--cpu-cycles", type=int, default=4, help="oracle cycles timed for cpu_baseline (0 = skip)")
     p.add_argument("--cpu-threads", type=int, default=0,
@@ -52,7 +63,10 @@ def parse():
     p.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "pmc_traffic_current.json"),
                    help="JSON with the PMC-measured HBM bytes per launch of the dominant kernel (tools/pmc_traffic.py); "
                         "used only when its kernel name matches")
-    return p.parse_args()
+    a = p.parse_args()
+    if a.config0:
+        a.dim, a.n, a.real, a.smoother, a.nu, a.prolong, a.coarse_bc, a.cycle = 2, 256, "double", "jacobi", 7, "pc", "zero", "V"
+    return a
 
 
 def main():
@@ -87,9 +101,9 @@ def main():
         box, strong = (n, n, 1), False
     else:
         box, strong = (n, n, n * world), False
-    cfg = dict(dim=a.dim if not a.box else 3, n=box, real=a.real, smoother="rbgs", nu1=a.nu, nu2=a.nu, cycle=a.cycle,
-               prolong="linear", coarse_bc="consistent", coarse_init="fresh", err_mode=1, device=local,
-               rank=rank, world=world, comm_id=comm_id)
+    cfg = dict(dim=a.dim if not a.box else 3, n=box, real=a.real, smoother=a.smoother, nu1=a.nu, nu2=a.nu, cycle=a.cycle,
+               prolong=a.prolong, coarse_bc=a.coarse_bc, coarse_init="fresh", err_mode=1, device=local,
+               rank=rank, world=world, comm_id=comm_id, restriction=a.restriction)
     ctx = mgpoisson.Context(mgpoisson.make_opts(**cfg))
     ctx.init_point_charge()
     rb = 4 if a.real == "float" else 8
@@ -123,6 +137,9 @@ def main():
         ctx.timing(False)
         barrier_sync()
 
+    copy_peak = None
+    if a.copy_probe_mb > 0 and local == 0 and rank == 0:
+        copy_peak = mgpoisson.copy_bandwidth(local, a.copy_probe_mb << 20, 10)
     if world > 1:
         t = torch.tensor([dt], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -131,24 +148,31 @@ def main():
     value = (1 if strong else world) * a.steps / dt
     kind = "V" if a.cycle == "V" else "F"
     gcells = box[0] * box[1] * box[2]
+    sm = "RB-GS" if a.smoother == "rbgs" else "Jacobi"
+    pr = ("trilinear P" if cfg["dim"] == 3 else "bilinear P") if a.prolong == "linear" else "injection P"
+    rs = (f"{'2x2x2' if cfg['dim'] == 3 else '2x2'}-average R" if a.restriction == "average"
+          else "full-weighting R (adjoint of the linear P)")
+    bc = "consistent coarse boundary" if a.coarse_bc == "consistent" else "ghost-0 coarse boundary"
+    algo = f"{sm} {a.nu}+{a.nu}, {kind}-cycle, {pr}, {rs}, {bc}, per-cycle RMS-update err"
     if strong:
         named = {(2048, 2048, 2048): "BASELINE configs[3]: 3D Poisson 2048^3",
                  (4096, 4096, 4096): "BASELINE configs[4]: 3D Poisson 4096^3 fp32 F-cycle"}
         slab = {(2048, 2048, 256): "one rank's slab of BASELINE configs[3] (2048^3 / 8 ranks)",
                 (4096, 4096, 512): "one rank's slab of BASELINE configs[4] (4096^3 / 8 ranks)"}
         wl = named.get(box) or (slab.get(box) if world == 1 else None) or f"3D Poisson {box[0]}x{box[1]}x{box[2]}"
-        workload = f"{wl}, 7-point, RB-GS {a.nu}+{a.nu}, {kind}-cycle, trilinear P, 2x2x2-average R, per-cycle RMS-update err"
+        workload = f"{wl}, 7-point, {algo}"
         unit = f"{kind}-cycles/s ({box[0]}x{box[1]}x{box[2]} box, whole job)"
     elif cfg["dim"] == 2:
         uf_mb = 2 * n * n * rb / 1e6
-        workload = (f"BASELINE configs[1]: 2D Poisson {n}^2, 5-point, RB-GS {a.nu}+{a.nu}, {kind}-cycle, bilinear P, "
-                    f"2x2-average R, per-cycle RMS-update err; u+f = {uf_mb:.0f} MB "
+        tag = ("BASELINE configs[0] (the cpu.lua reference path)" if a.config0
+               else "BASELINE configs[1]" if n == 4096 else "2D")
+        workload = (f"{tag}: 2D Poisson {n}^2, 5-point, {algo}; u+f = {uf_mb:.0f} MB "
                     + ("fit the 256 MB Infinity Cache (MALL-resident: GB/s can exceed HBM)" if uf_mb < 256
                        else "exceed the 256 MB Infinity Cache"))
         unit = f"{kind}-cycles/s ({n}^2)"
     else:
-        workload = (f"BASELINE configs[2]: 3D Poisson {n}^3 per GPU, 7-point, RB-GS {a.nu}+{a.nu}, {kind}-cycle, "
-                    "trilinear P, 2x2x2-average R, per-cycle RMS-update err")
+        tag = "BASELINE configs[2]: " if n == 512 else ""
+        workload = f"{tag}3D Poisson {n}^3 per GPU, 7-point, {algo}"
         unit = f"{kind}-cycles/s ({n}^3-cell slabs, whole job)"
     rnorm, fnorm = ctx.residual_norm()
     line = {
@@ -176,9 +200,10 @@ def main():
         "hbm_used_GB_rank0": (total_b - free_b) / 1e9,
     }
     tname = "float" if a.real == "float" else "double"
-    lin = 1
+    lin = 1 if a.prolong == "linear" else 0
+    fw = a.restriction == "full_weighting"
     kernels = {"half_sweep": f"k_half<{tname}, {cfg['dim']}, 1, false>",
-               "fused_pre": f"k_zs<{tname}, true, 0, false, true>",
+               "fused_pre": f"k_zs<{tname}, true, {1 if fw else 0}, false, true>",
                "fused_post": f"k_zs<{tname}, false, {lin}, true, true>"}
     # Algorithmic bytes per level-0 cell of one launch (reals): what the launch must move
     # to and from HBM.  half_sweep: read the other colour and f, write this colour of half the cells.
@@ -186,7 +211,8 @@ def main():
     # (its red cells are never read: the only reader, fused_post, loads black cells and its first red
     # half-sweep replaces the red ones).
     # fused_post (k_zs: prolongation + correction + 2 sweeps + err): read black u, V/8, f, psiOld; write u.
-    algo_reals = {"half_sweep": 1.5, "fused_pre": 2.125, "fused_post": 3.625}
+    # (full weighting: PRE smooths only and stores both colours, 2.5 reals; the restriction runs after it)
+    algo_reals = {"half_sweep": 1.5, "fused_pre": 2.5 if fw else 2.125, "fused_post": 3.625}
     per_kind = {k: v for k, v in timed.items() if v[1] > 0}
     cells = cells_rank
     if per_kind:
@@ -208,6 +234,11 @@ def main():
                 "window": f"{a.steps} cycles after the timed region, HIP events around each launch"}
         # PMC traffic is measured by a separate rocprofv3 pass (tools/gpu_round.sh), never in this run; it
         # is used only when it was measured on this exact kernel source and workload
+        if copy_peak:
+            roof["measured_copy_peak"] = copy_peak
+            roof["frac_of_measured_copy_peak"] = achieved / copy_peak
+            roof["copy_probe"] = (f"mgp_copy_bandwidth: 16-byte streaming copy of {a.copy_probe_mb} MiB, best of 10, "
+                                  "read + write bytes (BASELINE.md: measured copy-kernel peak)")
         roof["traffic_measured_this_run"] = False
         if a.traffic and os.path.exists(a.traffic):
             with open(a.traffic) as fh:
@@ -223,8 +254,10 @@ def main():
 
     if rank == 0 and world == 1 and a.cpu_cycles > 0:
         thr = a.cpu_threads or int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
-        line["cpu_baseline"] = cpu_baseline(cfg, a.cpu_cycles * 2, thr, gcells)
-        line["cpu_baseline_1thread"] = cpu_baseline(cfg, a.cpu_cycles, 1, gcells)
+        # configs[0] is small: the CPU port runs the same cycles the GPU timed, in full
+        c_omp, c_one = (a.steps, a.steps) if a.config0 else (a.cpu_cycles * 2, a.cpu_cycles)
+        line["cpu_baseline"] = cpu_baseline(cfg, c_omp, thr, gcells)
+        line["cpu_baseline_1thread"] = cpu_baseline(cfg, c_one, 1, gcells)
     if rank == 0:
         print(json.dumps(line), flush=True)
     ctx.close()
@@ -251,7 +284,8 @@ def cpu_baseline(cfg, cycles, threads, gcells):
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     from oracle_lib import Oracle
 
-    kw = {k: cfg[k] for k in ("dim", "n", "real", "smoother", "nu1", "nu2", "cycle", "prolong", "coarse_bc", "coarse_init")}
+    kw = {k: cfg[k] for k in ("dim", "n", "real", "smoother", "nu1", "nu2", "cycle", "prolong", "coarse_bc", "coarse_init",
+                              "restriction")}
     scale = 1.0
     if gcells > 512 ** 3:
         kw["n"] = (512, 512, 512)

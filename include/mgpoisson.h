@@ -232,6 +232,11 @@ enum { MGP_TIMING_HALF_SWEEP = 0, MGP_TIMING_FUSED_PRE = 1, MGP_TIMING_FUSED_POS
 int         mgp_timing(mgp_ctx* c, int enable);
 int         mgp_timing_read(mgp_ctx* c, int kind, double* ms_total, int64_t* launches, double* bytes);
 
+/* Measurement helper (BASELINE.md "a measured copy-kernel peak"): the best of `reps` 16-byte streaming copies
+ * of `bytes` between two fresh device buffers on `device` (-1: current), over three copy-kernel shapes
+ * (grid-stride, one pass, one pass non-temporal), in GB/s of read + write bytes. */
+int         mgp_copy_bandwidth(int device, int64_t bytes, int32_t reps, double* gbps);
+
 #ifdef __cplusplus
 }
 #endif

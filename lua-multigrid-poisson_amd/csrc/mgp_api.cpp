@@ -33,6 +33,15 @@ using mgp::Geo;
 namespace {
 
 thread_local std::string g_create_error;
+// Restores the caller's current device on scope exit (the group switches devices per rank).
+struct DeviceGuard {
+    int dev = -1;
+    DeviceGuard() { (void)hipGetDevice(&dev); }
+    ~DeviceGuard()
+    {
+        if (dev >= 0) (void)hipSetDevice(dev);
+    }
+};
 
 struct LevelPlan {
     int64_t nx, ny, gnz;  // global dims
@@ -1092,6 +1101,54 @@ void set_level_state(mgp_ctx* c, const std::vector<char*>& v)
     c->xbuf = v[2 * c->lev.size()];
 }
 
+// Capture one cycle from the current buffer-pointer state into a new cache entry (nothing runs); the host
+// state advances as if the cycle had run.
+int capture_cycle(mgp_ctx* c, mgp_ctx::GraphEntry** out)
+{
+    const std::vector<char*> pre = level_state(c);
+    HIP_TRY(c, hipStreamBeginCapture(c->s, hipStreamCaptureModeThreadLocal));
+    const int rc = one_cycle(c, c->d_errs);  // err into d_errs[*d_slot] (mgp_cycles set err_ctr)
+    hipGraph_t graph = nullptr;
+    const hipError_t ec = hipStreamEndCapture(c->s, &graph);
+    if (rc != MGP_OK) {
+        if (graph) (void)hipGraphDestroy(graph);
+        set_level_state(c, pre);
+        return rc;
+    }
+    HIP_TRY(c, ec);
+    mgp_ctx::GraphEntry e;
+    e.pre = pre;
+    e.post = level_state(c);
+    const hipError_t ei = hipGraphInstantiate(&e.exec, graph, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(graph);
+    HIP_TRY(c, ei);
+    c->graphs.push_back(e);
+    *out = &c->graphs.back();
+    return MGP_OK;
+}
+
+// Capture the cycle graphs of every pointer state the cycle goes through (the finest level's buffers
+// rotate with a period of 2 or 3 cycles) when the context is created, so that the first cycles replay
+// back to back instead of idling the GPU during their captures.  The state ends where it began.
+int precapture(mgp_ctx* c)
+{
+    const char* v = std::getenv("MGP_PRECAPTURE");
+    if (!c->use_graph || c->handoff_fn || (v && std::atoi(v) == 0)) return MGP_OK;
+    const std::vector<char*> s0 = level_state(c);
+    c->err_ctr = c->o.err_mode && c->o.world == 1 ? c->d_slot : nullptr;  // as mgp_cycles captures
+    int rc = MGP_OK;
+    for (int i = 0; i < 8 && rc == MGP_OK; ++i) {
+        mgp_ctx::GraphEntry* e = nullptr;
+        rc = capture_cycle(c, &e);
+        if (rc == MGP_OK && e->post == s0) break;
+    }
+    c->err_ctr = nullptr;
+    set_level_state(c, s0);
+    c->metrics_old = nullptr;  // no outer iteration has run
+    if (rc != MGP_OK) drop_graphs(c);
+    return rc;
+}
+
 // One cycle through a cached hipGraph (captured on first use of a buffer-pointer state).
 int graph_cycle(mgp_ctx* c, int slot)
 {
@@ -1101,24 +1158,7 @@ int graph_cycle(mgp_ctx* c, int slot)
         if (e.pre == pre) hit = &e;
     if (!hit) {
         if (c->graphs.size() >= 8) return one_cycle(c, c->d_errs);  // unusual state churn: eager
-        HIP_TRY(c, hipStreamBeginCapture(c->s, hipStreamCaptureModeThreadLocal));
-        const int rc = one_cycle(c, c->d_errs);  // err into d_errs[*d_slot] (mgp_cycles set err_ctr)
-        hipGraph_t graph = nullptr;
-        const hipError_t ec = hipStreamEndCapture(c->s, &graph);
-        if (rc != MGP_OK) {
-            if (graph) (void)hipGraphDestroy(graph);
-            set_level_state(c, pre);
-            return rc;
-        }
-        HIP_TRY(c, ec);
-        mgp_ctx::GraphEntry e;
-        e.pre = pre;
-        e.post = level_state(c);
-        const hipError_t ei = hipGraphInstantiate(&e.exec, graph, nullptr, nullptr, 0);
-        (void)hipGraphDestroy(graph);
-        HIP_TRY(c, ei);
-        c->graphs.push_back(e);
-        hit = &c->graphs.back();
+        TRY(capture_cycle(c, &hit));
     }
     set_level_state(c, hit->post);
     update_metrics_old(c);
@@ -1133,7 +1173,7 @@ int ensure_errs(mgp_ctx* c, int k)
     drop_graphs(c);  // captured graphs write into d_errs
     if (c->d_errs) HIP_TRY(c, hipFree(c->d_errs));
     c->d_errs = nullptr;
-    int cap = std::max(k, 64);
+    int cap = std::max(k, 4096);
     HIP_TRY(c, hipMalloc(&c->d_errs, sizeof(double) * cap));
     c->errs_cap = cap;
     return MGP_OK;
@@ -1308,12 +1348,14 @@ static void select_engines(mgp_ctx* c)
 {
     c->err_fuse = c->o.err_mode && c->o.smoother == MGP_RBGS && c->o.nu1 >= 1 && c->o.nu2 >= 1 && c->lev.size() > 1;
     {
-        // temporally blocked phases (k_zs): RB-GS 2+2 on 3D levels of >= MGP_FUSED_MIN_CELLS cells (per
-        // rank); MGP_FUSED=0 turns them off (one launch per half-sweep, bit-identical results).  A
-        // distributed fused level exchanges kGhostZs-deep halos, so every level gets that many ghost planes.
+        // temporally blocked phases: RB-GS 2+2 on 3D levels of >= MGP_FUSED_MIN_CELLS cells per rank (k_zs,
+        // default 2^25) and on 2D levels of >= MGP_YS_MIN_CELLS cells (k_ys, default 2^24); MGP_FUSED=0 turns
+        // them off (one launch per half-sweep, bit-identical results).  A distributed fused level exchanges
+        // kGhostZs-deep halos, so every level gets that many ghost planes.
         const char* v = std::getenv("MGP_FUSED");
-        const char* vm = std::getenv("MGP_FUSED_MIN_CELLS");
-        const int64_t min_cells = vm ? std::atoll(vm) : (int64_t(1) << 25);
+        const char* vm = std::getenv(c->o.dim == 2 ? "MGP_YS_MIN_CELLS" : "MGP_FUSED_MIN_CELLS");
+        // (2D: 4096^2 measured 0.285 ms per cycle with only level 0 streamed, 0.406 with 2048^2 as well)
+        const int64_t min_cells = vm ? std::atoll(vm) : (int64_t(1) << (c->o.dim == 2 ? 24 : 25));
         const bool on = !(v && std::atoi(v) == 0) && c->o.smoother == MGP_RBGS && c->o.nu1 == 2 && c->o.nu2 == 2;
         for (size_t l = 0; l + 1 < c->lev.size(); ++l) {
             Level& L = c->lev[l];
@@ -1537,6 +1579,7 @@ static int create_impl(mgp_ctx** out, const mgp_opts* o, mgp_loopback* lb, ncclC
         c->err = "stream synchronisation after allocation failed";
         return bail(MGP_ERR_HIP);
     }
+    if (precapture(c) != MGP_OK) return bail(MGP_ERR_HIP);
     *out = c;
     return MGP_OK;
 }
@@ -2059,6 +2102,51 @@ int mgp_timing_read(mgp_ctx* c, int kind, double* ms_total, int64_t* launches, d
     return MGP_OK;
 }
 
+int mgp_copy_bandwidth(int device, int64_t bytes, int32_t reps, double* gbps)
+{
+    if (bytes < 16 || reps < 1 || !gbps) {
+        g_create_error = "mgp_copy_bandwidth: bytes >= 16, reps >= 1 and an output are required";
+        return MGP_ERR_ARG;
+    }
+    DeviceGuard keep_device;
+    if (device >= 0 && hipSetDevice(device) != hipSuccess) {
+        g_create_error = "mgp_copy_bandwidth: hipSetDevice failed";
+        return MGP_ERR_HIP;
+    }
+    bytes &= ~(int64_t)15;
+    void *a = nullptr, *b = nullptr;
+    hipStream_t s = nullptr;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    int rc = MGP_OK;
+    double best = 0.0;
+    if (hipMalloc(&a, (size_t)bytes) != hipSuccess || hipMalloc(&b, (size_t)bytes) != hipSuccess ||
+        hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess || hipEventCreate(&e0) != hipSuccess ||
+        hipEventCreate(&e1) != hipSuccess || hipMemsetAsync(a, 0, (size_t)bytes, s) != hipSuccess) {
+        g_create_error = "mgp_copy_bandwidth: allocation failed";
+        rc = MGP_ERR_OOM;
+    }
+    // every copy kernel shape, reps timed launches each after an untimed first touch; the best counts
+    for (int kind = 0; kind < mgp::kCopyKinds && rc == MGP_OK; ++kind)
+        for (int r = -1; r < reps && rc == MGP_OK; ++r) {
+            if (hipEventRecord(e0, s) != hipSuccess || mgp::launch_copy16(kind, a, b, bytes, s) != hipSuccess ||
+                hipEventRecord(e1, s) != hipSuccess || hipEventSynchronize(e1) != hipSuccess) {
+                g_create_error = "mgp_copy_bandwidth: copy kernel failed";
+                rc = MGP_ERR_HIP;
+                break;
+            }
+            float ms = 0.f;
+            (void)hipEventElapsedTime(&ms, e0, e1);
+            if (r >= 0 && ms > 0.f) best = std::max(best, 2.0 * (double)bytes / (ms * 1e-3) / 1e9);
+        }
+    if (e0) (void)hipEventDestroy(e0);
+    if (e1) (void)hipEventDestroy(e1);
+    if (s) (void)hipStreamDestroy(s);
+    if (a) (void)hipFree(a);
+    if (b) (void)hipFree(b);
+    if (rc == MGP_OK) *gbps = best;
+    return rc;
+}
+
 // =====================================================================================
 // Single-process multi-GPU group (one Lua host driving the node's GPUs)
 // =====================================================================================
@@ -2071,15 +2159,6 @@ struct mgp_group {
     std::atomic<bool> stop{false};  // a rank failed and the others were woken: the group is unusable
 };
 
-// Restores the caller's current device on scope exit (the group switches devices per rank).
-struct DeviceGuard {
-    int dev = -1;
-    DeviceGuard() { (void)hipGetDevice(&dev); }
-    ~DeviceGuard()
-    {
-        if (dev >= 0) (void)hipSetDevice(dev);
-    }
-};
 
 static thread_local std::string g_group_error;
 
@@ -2119,6 +2198,7 @@ static int group_run(mgp_group* g, const std::function<int(mgp_ctx*, int)>& fn)
     std::condition_variable cv;
     int done = 0;
     bool failed = false;
+    int first = -1;  // the rank that failed first: the root cause (the others may fail because of it)
     // test hook: this rank fails at once, before any exchange (tests/test_gpu_group.py)
     const char* fr = std::getenv("MGP_TEST_FAIL_RANK");
     const int fail_rank = fr ? std::atoi(fr) : -1;
@@ -2136,7 +2216,10 @@ static int group_run(mgp_group* g, const std::function<int(mgp_ctx*, int)>& fn)
             rc[(size_t)r] = v;
             std::lock_guard<std::mutex> lk(m);
             ++done;
-            if (v != MGP_OK) failed = true;
+            if (v != MGP_OK && !failed) {
+                failed = true;
+                first = r;
+            }
             cv.notify_all();
         });
     {
@@ -2150,11 +2233,10 @@ static int group_run(mgp_group* g, const std::function<int(mgp_ctx*, int)>& fn)
     for (auto& t : th) t.join();
     if (g->stop.load() && !g->lb)
         for (auto* c : g->ranks) c->comm = nullptr;  // freed by ncclCommAbort
-    for (int r = 0; r < n; ++r)
-        if (rc[(size_t)r] != MGP_OK) {
-            g->err = "rank " + std::to_string(r) + ": " + g->ranks[(size_t)r]->err;
-            return rc[(size_t)r];
-        }
+    if (first >= 0) {
+        g->err = "rank " + std::to_string(first) + ": " + g->ranks[(size_t)first]->err;
+        return rc[(size_t)first];
+    }
     return MGP_OK;
 }
 

@@ -1718,9 +1718,9 @@ __device__ __forceinline__ Vec<T, N> zs_relax(const Vec<T, N>& zl, const Vec<T, 
                                               const ZsNb<T, N>& nb, const Vec<T, N>& fv, const ZsCol& c, int o,
                                               int nbyz, int nx, const Op<T, 3>& op, const ZsDiag<T>& dz)
 {
+    Vec<T, N> out;
     T t[N];
     zs_nbsum<T, N>(zl, cen, zr, nb, o, t);
-    Vec<T, N> out;
     if (!CLZ && ST) {
 #pragma unroll
         for (int e = 0; e < N; ++e) {
@@ -2254,6 +2254,283 @@ __attribute__((amdgpu_waves_per_eu(1, PRE ? ZS_WPE_PRE : ZS_WPE_POST))) void k_z
         if (p + 1 <= p_end) step(GEN, R1, pb, pa, p + 1);
         if (p + 2 <= p_end) step(GEN, R2, pa, pb, p + 2);
         if (p + 3 <= p_end) step(GEN, R3, pb, pa, p + 3);
+    }
+    if (ERR) block_partial_t<NTL>(err + err1, partials);
+}
+
+// ---- y-streamed temporally blocked smoothing (2D, red/black 2+2) -------------------------------
+//
+// k_ys is k_zs for a 2D level: rows take the place of planes.  A workgroup owns an x-segment of TX cells
+// (plus HX halo cells per side) and a chunk of yc rows, and streams through y; every thread owns one
+// column group of the segment: N consecutive cells of each colour (packed m0 .. m0 + N - 1).  At step p:
+//   stage 0   black cells of row p (POST: plus the prolongation, PvRow: k_prolong_v's expressions)
+//   stage k   half-sweep k (k = 1..4, red first) on row p - k
+//   last      row p - 4 is final and stored; PRE: residual of row p - 5 and the restriction (both fine rows
+//             of a coarse row belong to the same thread, so the children are summed in registers in the
+//             reference order); POST: (psi - psiOld)^2 partials.
+// The y-neighbours of stage k are the thread's own register windows of stage k - 1; the only operands
+// from other threads are the two x-edge cells, which every stage leaves in LDS (first and last cell of
+// its group) for the next stage one step later: one barrier per step.  Halo cells are recomputed by the
+// neighbouring segments (the trapezoid shrinks by one cell per stage); rows outside the box are 0.  With
+// yc even, Y0 is even and the parity of row p is a compile-time function of the ring slot.  Arithmetic is
+// k_half's / k_resrestrict's / k_prolong_v's, so results are bit-identical to the per-piece path.
+#ifndef YS_TX_F32
+#define YS_TX_F32 1024
+#endif
+#ifndef YS_TX_F64
+#define YS_TX_F64 512
+#endif
+template <typename T, bool PRE>
+struct YsShape {
+    static constexpr int N = 16 / sizeof(T);
+    static constexpr int TX = sizeof(T) == 4 ? YS_TX_F32 : YS_TX_F64;
+    static constexpr int H = PRE ? 5 : 4;
+    static constexpr int HX = 2 * N * ((H + 2 * N - 1) / (2 * N));  // whole column groups
+    static constexpr int HWE = TX / 2 + HX;                          // packed cells per colour of a row
+    static constexpr int G = HWE / N;                                // column groups (threads with work)
+    static constexpr int HXG = HX / 2 / N;
+    static constexpr int NTL = (G + 63) / 64 * 64;
+    // edge slots (first, last cell of every group): stages 0..2 two rows each, stage 3 four (PRE reads
+    // its row p - 5 at step p), stage 4 two (PRE)
+    static constexpr int ES = 2 * G;
+    static constexpr int OFF1 = 2 * ES, OFF2 = 4 * ES, OFF3 = 6 * ES, OFF4 = 10 * ES;
+    static constexpr size_t lds_floats = 12 * ES;
+    static_assert(NTL <= 1024, "too many threads");
+    static_assert(2 * N * HXG >= H, "x halo too small");
+};
+
+template <typename T>
+struct YsPrefetch {
+    Vec<T, 16 / sizeof(T)> u, f1, f2, o0, o1;  // black u of row p; red f of p - 1; black f of p - 2; psiOld of p - 4
+};
+
+// relax of my N cells of x parity o: rows ym / yp above and below (other colour), cen my row's other
+// colour, ep / en the x-edge cells beyond my group; nby = y faces of the row (0 with CLZ)
+template <typename T, int N, bool CLZ, bool RES>
+__device__ __forceinline__ void ys_cells(const Vec<T, N>& ym, const Vec<T, N>& cen, const Vec<T, N>& yp, T ep, T en,
+                                         const Vec<T, N>& fv, const Vec<T, N>& uc, int o, int nby, int gm, int nx,
+                                         bool xin, const Op<T, 2>& op, T (&out)[N])
+{
+    ZsNb<T, N> nb;
+    nb.yl = ym;
+    nb.yr = yp;
+    nb.ep = ep;
+    nb.en = en;
+    T t[N];
+    zs_xsum<T, N>(cen, nb, o, t);
+#pragma unroll
+    for (int e = 0; e < N; ++e) {
+        t[e] = t[e] + ym.v[e];
+        t[e] = t[e] + yp.v[e];
+    }
+    if (CLZ || __all(nby == 0 && xin)) {
+#pragma unroll
+        for (int e = 0; e < N; ++e) {
+            if (RES) {
+                const T askew = t[e] * op.inv_hSq;
+                const T a_u = askew + op.adiag * uc.v[e];
+                out[e] = fv.v[e] - a_u;
+            } else {
+                out[e] = div_rn(fv.v[e] - t[e] * op.inv_hSq, op.adiag, op.yadiag);
+            }
+        }
+    } else {
+#pragma unroll
+        for (int e = 0; e < N; ++e) {
+            const int i = 2 * (gm + e) + o;
+            const int nbc = nby + (i == 0) + (i == nx - 1);
+            out[e] = RES ? op.residual_direct(t[e], fv.v[e], uc.v[e], nbc) : op.relax_direct(t[e], fv.v[e], nbc);
+        }
+    }
+}
+
+// PRE: LINEAR selects the restriction (0: residual + 2x2 average here; 1: none, both colours stored)
+template <typename T, bool PRE, int LINEAR, bool ERR, bool CLZ>
+__global__ __launch_bounds__((YsShape<T, PRE>::NTL)) void k_ys(const T* __restrict__ src, const T* __restrict__ f,
+                                                               T* __restrict__ dst, const T* old, T* __restrict__ R,
+                                                               const T* __restrict__ V, double* __restrict__ partials,
+                                                               Geo g, Geo gc, Op<T, 2> op, T clc, int yc)
+{
+    using S = YsShape<T, PRE>;
+    constexpr int N = S::N, H = S::H, G = S::G, TX = S::TX, NTL = S::NTL, ES = S::ES;
+    constexpr bool RR = PRE && LINEAR == 0;
+    using VT = Vec<T, N>;
+    using PF = YsPrefetch<T>;
+    __shared__ __align__(16) T lds[S::lds_floats];
+    const int tid = threadIdx.x;
+    const int tiles_x = g.nx / TX;
+    const int b = xcd_remap(blockIdx.x, gridDim.x);
+    const int X0 = (b % tiles_x) * TX, Y0 = (b / tiles_x) * yc;
+    const int hw = g.hw, Hh = (int)g.H, ny = g.ny;
+    const bool on = tid < G;
+    const int gx = on ? tid : 0;
+    const int gm = (X0 - S::HX) / 2 + gx * N;  // global packed m of my first cell
+    const bool inx = on && gm >= 0 && gm < hw;
+    const bool xin = !inx || (gm > 0 && 2 * (gm + N) < g.nx);  // no cell of the group on an x face
+    const int cgm = gm < 0 ? 0 : (gm > hw - N ? hw - N : gm);
+    const bool tile_x = on && gx >= S::HXG && gx < G - S::HXG;
+    const int zlo = Y0 - H;
+    const int p_end = Y0 + yc + (PRE ? 4 : 3);
+    auto iny = [&](int q) { return q >= 0 && q < ny; };
+    auto rcl = [&](int q) { return q < 0 ? 0 : (q >= ny ? ny - 1 : q); };
+    auto nby = [&](int q) { return CLZ ? 0 : (q == 0) + (q == ny - 1); };
+    for (int i = tid; i < (int)S::lds_floats; i += NTL) lds[i] = (T)0;
+    __syncthreads();
+    // edge slot of stage base `off` with `ns` rows, row q
+    auto eslot = [&](int off, int ns, int q) { return lds + off + (q & (ns - 1)) * ES; };
+    auto put = [&](T* sl, const VT& v) {
+        if (inx) {
+            sl[2 * gx] = v.v[0];
+            sl[2 * gx + 1] = v.v[N - 1];
+        }
+    };
+    auto edges = [&](const T* sl, T& ep, T& en) {  // left group's last cell, right group's first
+        ep = gx > 0 ? sl[2 * gx - 1] : (T)0;
+        en = gx < G - 1 ? sl[2 * gx + 2] : (T)0;
+    };
+    auto prefetch = [&](PF& r, int p) {
+        r.u = vload<T, N>(src + Hh + (int64_t)rcl(p) * hw + cgm);
+        r.f1 = vload<T, N>(f + (int64_t)rcl(p - 1) * hw + cgm);
+        r.f2 = vload<T, N>(f + Hh + (int64_t)rcl(p - 2) * hw + cgm);
+        if (!PRE && ERR && tile_x) {
+            const int64_t ro = (int64_t)rcl(p - 4) * hw + cgm;
+            r.o0 = vload<T, N>(old + ro);
+            r.o1 = vload<T, N>(old + Hh + ro);
+        }
+    };
+    const VT vz = vzero<T, N>();
+    VT W0[4], W1[4], W2[4], W3[4], W4[4], FR[4], FB[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) W0[i] = W1[i] = W2[i] = W3[i] = W4[i] = FR[i] = FB[i] = vz;
+    T acc[N];
+#pragma unroll
+    for (int e = 0; e < N; ++e) acc[e] = (T)0;
+    double err = 0.0, err1 = 0.0;
+
+    auto step = [&](auto rt, const PF& cur, PF& nxt, int p) {
+        constexpr int RS = decltype(rt)::value;  // (p - zlo) & 3
+        auto sl = [](int k) constexpr { return (RS - k) & 3; };
+        constexpr int PP = (H + RS) & 1;  // parity of p (Y0 even)
+        auto par = [](int k) constexpr { return (PP + k) & 1; };  // parity of row p - k (mod 2)
+        zs_hold<T, N>(cur.u);
+        zs_hold<T, N>(cur.f1);
+        zs_hold<T, N>(cur.f2);
+        if (!PRE && ERR) {
+            zs_hold<T, N>(cur.o0);
+            zs_hold<T, N>(cur.o1);
+        }
+        asm volatile("" ::: "memory");
+        if (p + 1 <= p_end) prefetch(nxt, p + 1);
+
+        // ---- stage 0: black cells of row p (POST: + P V) ----
+        VT a0 = cur.u;
+        if (!iny(p) || !inx) {
+            a0 = vz;
+        } else if (!PRE) {
+            PvRow<T, N, 2, LINEAR> pv;
+            pv.load(V, gc, p, 0, cgm);
+            const int ob = 1 ^ par(0);  // x parity of row p's black cells
+#pragma unroll
+            for (int e = 0; e < N; ++e) a0.v[e] = a0.v[e] + pv.value(e, ob, clc);
+        }
+        W0[sl(0)] = a0;
+        // ---- stages 1..4: half-sweep k on row p - k (red, black, red, black) ----
+        T ep, en;
+        VT o1, o2, o3, o4;
+        edges(eslot(0, 2, p - 1), ep, en);
+        ys_cells<T, N, CLZ, false>(W0[sl(2)], W0[sl(1)], W0[sl(0)], ep, en, cur.f1, vz, par(1), nby(p - 1), gm, g.nx, xin,
+                                   op, o1.v);
+        if (!iny(p - 1) || !inx) o1 = vz;
+        W1[sl(1)] = o1;
+        edges(eslot(S::OFF1, 2, p - 2), ep, en);
+        ys_cells<T, N, CLZ, false>(W1[sl(3)], W1[sl(2)], W1[sl(1)], ep, en, cur.f2, vz, 1 ^ par(2), nby(p - 2), gm, g.nx,
+                                   xin, op, o2.v);
+        if (!iny(p - 2) || !inx) o2 = vz;
+        W2[sl(2)] = o2;
+        edges(eslot(S::OFF2, 2, p - 3), ep, en);
+        ys_cells<T, N, CLZ, false>(W2[sl(4)], W2[sl(3)], W2[sl(2)], ep, en, FR[sl(3)], vz, par(3), nby(p - 3), gm, g.nx,
+                                   xin, op, o3.v);
+        if (!iny(p - 3) || !inx) o3 = vz;
+        W3[sl(3)] = o3;
+        edges(eslot(S::OFF3, 4, p - 4), ep, en);
+        ys_cells<T, N, CLZ, false>(W3[sl(5)], W3[sl(4)], W3[sl(3)], ep, en, FB[sl(4)], vz, 1 ^ par(4), nby(p - 4), gm,
+                                   g.nx, xin, op, o4.v);
+        if (!iny(p - 4) || !inx) o4 = vz;
+        W4[sl(4)] = o4;
+        // ---- edge writes (slots no stage of this step reads) ----
+        put(eslot(0, 2, p), a0);
+        put(eslot(S::OFF1, 2, p - 1), o1);
+        put(eslot(S::OFF2, 2, p - 2), o2);
+        put(eslot(S::OFF3, 4, p - 3), o3);
+        if (RR) put(eslot(S::OFF4, 2, p - 4), o4);
+        // ---- the smoothed row p - 4: red final after stage 3, black after stage 4 ----
+        {
+            const int q = p - 4;
+            if (q >= Y0 && q < Y0 + yc && tile_x) {
+                if (!PRE && ERR) {
+#pragma unroll
+                    for (int e = 0; e < N; ++e) {
+                        const double d0 = (double)W3[sl(4)].v[e] - (double)cur.o0.v[e];
+                        const double d1 = (double)o4.v[e] - (double)cur.o1.v[e];
+                        err = __builtin_fma(d0, d0, err);
+                        err1 = __builtin_fma(d1, d1, err1);
+                    }
+                }
+                T* dp = dst + (int64_t)q * hw + gm;
+                if (!RR) vstore<T, N>(dp, W3[sl(4)]);  // PRE's red cells are read by no one (POST loads black)
+                vstore<T, N>(dp + Hh, o4);
+            }
+        }
+        // ---- PRE: residual of row p - 5 and the 2 x 2 restriction ----
+        if (RR) {
+            const int q = p - 5;
+            T rred[N], rblk[N];
+            T bep, ben, rep, ren;
+            edges(eslot(S::OFF4, 2, q), bep, ben);  // black (stage 4) cells of row q
+            edges(eslot(S::OFF3, 4, q), rep, ren);  // red (stage 3) cells of row q
+            ys_cells<T, N, CLZ, true>(W4[sl(6)], W4[sl(5)], W4[sl(4)], bep, ben, FR[sl(5)], W3[sl(5)], par(5), nby(q), gm,
+                                      g.nx, xin, op, rred);
+            ys_cells<T, N, CLZ, true>(W3[sl(6)], W3[sl(5)], W3[sl(4)], rep, ren, FB[sl(5)], W4[sl(5)], 1 ^ par(5), nby(q),
+                                      gm, g.nx, xin, op, rblk);
+            if (q >= Y0 && q < Y0 + yc && tile_x) {
+#pragma unroll
+                for (int e = 0; e < N; ++e) {
+                    const T r0 = par(5) == 0 ? rred[e] : rblk[e];  // x parity 0 (cell 2I) and 1 (2I + 1)
+                    const T r1 = par(5) == 0 ? rblk[e] : rred[e];
+                    if (par(5) == 0) {
+                        acc[e] = r0 + r1;
+                    } else {
+                        acc[e] = acc[e] + r0;
+                        acc[e] = acc[e] + r1;
+                    }
+                }
+                if (par(5) == 1) {  // coarse row q >> 1 complete
+                    const int J = q >> 1;
+                    T* rowc = R + (int64_t)J * gc.hw;
+#pragma unroll
+                    for (int e = 0; e < N; ++e) {
+                        const int I = gm + e;
+                        rowc[((I + J) & 1) * gc.H + (I >> 1)] = (T)0.25 * acc[e];
+                    }
+                }
+            }
+        }
+        FR[sl(1)] = cur.f1;
+        FB[sl(2)] = cur.f2;
+        lds_barrier();
+    };
+
+    const std::integral_constant<int, 0> R0;
+    const std::integral_constant<int, 1> R1;
+    const std::integral_constant<int, 2> R2;
+    const std::integral_constant<int, 3> R3;
+    PF pa, pb;
+    prefetch(pa, zlo);
+    for (int p = zlo; p <= p_end; p += 4) {
+        step(R0, pa, pb, p);
+        if (p + 1 <= p_end) step(R1, pb, pa, p + 1);
+        if (p + 2 <= p_end) step(R2, pa, pb, p + 2);
+        if (p + 3 <= p_end) step(R3, pb, pa, p + 3);
     }
     if (ERR) block_partial_t<NTL>(err + err1, partials);
 }
@@ -2963,6 +3240,47 @@ __global__ __launch_bounds__(blk_threads<DIM>()) void k_blk(const T* __restrict_
     }
 }
 
+// ---- copy-bandwidth probe ("a measured copy-kernel peak is also reported") --------
+
+// dst = src in 16-byte lanes.  kind 0: grid-stride, 4 independent loads in flight per thread per
+// iteration; kind 1: one pass, each thread 4 vectors a workgroup apart; kind 2: kind 1 with non-temporal
+// loads and stores.  The probe reports the fastest.
+template <int KIND>
+__global__ __launch_bounds__(kBlock) void k_copy16(const float4* __restrict__ src, float4* __restrict__ dst, int64_t n)
+{
+    if (KIND == 0) {
+        const int64_t stride = (int64_t)gridDim.x * kBlock;
+        int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+        for (; i + 3 * stride < n; i += 4 * stride) {
+            const float4 a = src[i], b = src[i + stride], c = src[i + 2 * stride], d = src[i + 3 * stride];
+            dst[i] = a;
+            dst[i + stride] = b;
+            dst[i + 2 * stride] = c;
+            dst[i + 3 * stride] = d;
+        }
+        for (; i < n; i += stride) dst[i] = src[i];
+        return;
+    }
+    typedef float f4v __attribute__((ext_vector_type(4)));
+    const f4v* s4 = reinterpret_cast<const f4v*>(src);
+    f4v* d4 = reinterpret_cast<f4v*>(dst);
+    const int64_t base = (int64_t)blockIdx.x * (4 * kBlock) + threadIdx.x;
+    f4v v[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int64_t i = base + k * kBlock;
+        if (i < n) v[k] = KIND == 2 ? __builtin_nontemporal_load(s4 + i) : s4[i];
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int64_t i = base + k * kBlock;
+        if (i < n) {
+            if (KIND == 2) __builtin_nontemporal_store(v[k], d4 + i);
+            else d4[i] = v[k];
+        }
+    }
+}
+
 // ---- reductions -----------------------------------------------------------------------------
 
 template <typename T>
@@ -3420,6 +3738,27 @@ static hipError_t zs_launch(const FusedArgs& a, hipStream_t s)
     return hipGetLastError();
 }
 
+template <typename T, bool PRE, int LINEAR, bool ERR, bool CLZ>
+static hipError_t ys_launch(const FusedArgs& a, hipStream_t s)
+{
+    using S = YsShape<T, PRE>;
+    const Op<T, 2> op = make_op<T, 2>(a.h, a.cl);
+    const unsigned nb = (unsigned)((a.g.nx / S::TX) * (a.g.ny / a.zc));
+    k_ys<T, PRE, LINEAR, ERR, CLZ><<<nb, S::NTL, 0, s>>>((const T*)a.src, (const T*)a.f, (T*)a.dst,
+                                                         (const T*)(a.old ? a.old : a.dst), (T*)a.R, (const T*)a.V,
+                                                         a.partials, a.g, a.gc, op, (T)a.clc, a.zc);
+    return hipGetLastError();
+}
+
+template <typename T, bool CLZ>
+static hipError_t fused_dispatch_2d(const FusedArgs& a, hipStream_t s)
+{
+    const bool err = a.partials != nullptr;
+    if (a.pre) return a.linear ? ys_launch<T, true, 1, false, CLZ>(a, s) : ys_launch<T, true, 0, false, CLZ>(a, s);
+    if (a.linear) return err ? ys_launch<T, false, 1, true, CLZ>(a, s) : ys_launch<T, false, 1, false, CLZ>(a, s);
+    return err ? ys_launch<T, false, 0, true, CLZ>(a, s) : ys_launch<T, false, 0, false, CLZ>(a, s);
+}
+
 template <typename T, bool CLZ>
 static hipError_t fused_dispatch(const FusedArgs& a, hipStream_t s)
 {
@@ -3440,8 +3779,24 @@ static void zs_tile(int rb, int& tx, int& ty, int pre = -1)
     ty = pre < 0 ? (a > b ? a : b) : (pre ? a : b);
 }
 
+// 2D (k_ys): rows per z-chunk of a workgroup (MGP_YS_ROWS, default 32; even)
+static int ys_rows(const Geo& g)
+{
+    static const int rows = [] {
+        const char* v = std::getenv("MGP_YS_ROWS");
+        const int r = v ? std::atoi(v) : 32;
+        return r >= 8 && (r & 1) == 0 ? r : 32;
+    }();
+    int r = rows;
+    while (r > 8 && g.ny % r != 0) r /= 2;
+    return r;
+}
+
+static int ys_tx(int rb) { return rb == 4 ? YsShape<float, true>::TX : YsShape<double, true>::TX; }
+
 bool fused_supported(int rb, int dim, int ns, const Geo& g)
 {
+    if (dim == 2) return ns == 2 && g.nz == 1 && g.nx % ys_tx(rb) == 0 && g.ny >= 16 && g.ny % ys_rows(g) == 0;
     if (dim != 3 || ns != 2) return false;
     int TX, TY;
     zs_tile(rb, TX, TY);
@@ -3452,6 +3807,7 @@ bool fused_supported(int rb, int dim, int ns, const Geo& g)
 // workgroups or a chunk would drop below 16 planes
 int fused_zc(int rb, const Geo& g, bool pre)
 {
+    if (g.gnz == 1 && g.nz == 1) return ys_rows(g);  // 2D: rows per chunk
     int TX, TY;
     zs_tile(rb, TX, TY, pre ? 1 : 0);
     static const int64_t target = [] {
@@ -3466,6 +3822,7 @@ int fused_zc(int rb, const Geo& g, bool pre)
 
 int fused_blocks(int rb, const Geo& g, int zc)  // POST's workgroups (one err partial each)
 {
+    if (g.gnz == 1 && g.nz == 1) return (g.nx / ys_tx(rb)) * (g.ny / zc);
     int TX, TY;
     zs_tile(rb, TX, TY, 0);
     return (int)((int64_t)(g.nx / TX) * (g.ny / TY) * (g.nz / zc));
@@ -3536,6 +3893,10 @@ hipError_t prepare_kernels(int rb)
 hipError_t launch_fused(int rb, const FusedArgs& a, hipStream_t s)
 {
     const bool clz = a.cl == 0.0;
+    if (a.g.gnz == 1 && a.g.nz == 1) {  // 2D level: k_ys
+        if (rb == 4) return clz ? fused_dispatch_2d<float, true>(a, s) : fused_dispatch_2d<float, false>(a, s);
+        return clz ? fused_dispatch_2d<double, true>(a, s) : fused_dispatch_2d<double, false>(a, s);
+    }
     if (rb == 4) return clz ? fused_dispatch<float, true>(a, s) : fused_dispatch<float, false>(a, s);
     return clz ? fused_dispatch<double, true>(a, s) : fused_dispatch<double, false>(a, s);
 }
@@ -3693,6 +4054,16 @@ hipError_t launch_block(int rb, int dim, const BlockArgs& a, hipStream_t s)
     }
     if (dim == 3) return a.ns == 1 ? blk_t<float, 3, 1>(a, s) : blk_t<float, 3, 2>(a, s);
     return a.ns == 1 ? blk_t<float, 2, 1>(a, s) : blk_t<float, 2, 2>(a, s);
+}
+
+hipError_t launch_copy16(int kind, const void* src, void* dst, int64_t bytes, hipStream_t s)
+{
+    const int64_t n = bytes / 16;
+    const unsigned one_pass = (unsigned)((n + 4 * kBlock - 1) / (4 * kBlock));
+    if (kind == 0) k_copy16<0><<<2048, kBlock, 0, s>>>((const float4*)src, (float4*)dst, n);
+    else if (kind == 1) k_copy16<1><<<one_pass, kBlock, 0, s>>>((const float4*)src, (float4*)dst, n);
+    else k_copy16<2><<<one_pass, kBlock, 0, s>>>((const float4*)src, (float4*)dst, n);
+    return hipGetLastError();
 }
 
 hipError_t launch_sqdiff_sum(int rb, const void* a, const void* b, int64_t n, double* partials, double* out,

@@ -114,6 +114,7 @@ SIGNATURES = {
     "mgp_set_coarse_handoff": (ctypes.c_int, [_vp, _i64, COARSE_FN, _vp]),
     "mgp_timing": (ctypes.c_int, [_vp, ctypes.c_int]),
     "mgp_timing_read": (ctypes.c_int, [_vp, ctypes.c_int, _P(_dbl), _P(_i64), _P(_dbl)]),
+    "mgp_copy_bandwidth": (ctypes.c_int, [ctypes.c_int, _i64, _i32, _P(_dbl)]),
     "mgp_group_create": (ctypes.c_int, [_P(_vp), _P(MGPOpts), ctypes.c_int, _P(ctypes.c_int)]),
     "mgp_group_destroy": (None, [_vp]),
     "mgp_group_last_error": (ctypes.c_char_p, [_vp]),
@@ -178,3 +179,10 @@ def plan(opts: MGPOpts, max_levels: int = 48):
     for l, d in enumerate(out):
         d["engine"] = ("piece", "tail", "zs", "blk")[rows[8 * l + 6]]
     return out
+
+
+def copy_bandwidth(device: int = -1, nbytes: int = 2 << 30, reps: int = 10) -> float:
+    """Measured 16-byte streaming copy bandwidth of the device in GB/s (read + write bytes, best of reps)."""
+    g = ctypes.c_double()
+    check(lib.mgp_copy_bandwidth(int(device), int(nbytes), int(reps), ctypes.byref(g)))
+    return g.value

@@ -100,11 +100,12 @@ def test_block_graph_replay_equals_eager(monkeypatch):
 
 
 def test_block_levels_of_the_2d_config():
-    """4096^2 RB-GS 2+2 (configs[1]): 1024^2 .. 128^2 tiled, 64^2 and below in the tail."""
+    """4096^2 RB-GS 2+2 (configs[1]): 4096^2 temporally blocked (k_ys), 2048^2 per piece, 1024^2 .. 128^2 tiled,
+    64^2 and below in the tail."""
     ctx = _ctx(dim=2, n=(4096, 4096, 1), real="float", smoother="rbgs", nu1=2, nu2=2, prolong="linear",
                coarse_bc="consistent")
     eng = [lv["engine"] for lv in ctx.levels]
-    assert eng[:6] == ["piece", "piece", "blk", "blk", "blk", "blk"] and eng[6] == "tail", eng
+    assert eng[:6] == ["zs", "piece", "blk", "blk", "blk", "blk"] and eng[6] == "tail", eng
 
 
 def test_block_levels_of_the_bench_config():

@@ -295,6 +295,48 @@ def test_fused_phases_match_oracle(cfg, monkeypatch):
         assert np.array_equal(a.get_psi(level), b.get_psi(level)), f"psi level {level}"
 
 
+YS_CONFIGS = [
+    dict(n=(1024, 1024, 1), real="float", prolong="linear", coarse_bc="consistent"),
+    dict(n=(2048, 1024, 1), real="double", prolong="linear", coarse_bc="consistent", cycle="F"),
+    dict(n=(1024, 2048, 1), real="float", prolong="pc", coarse_bc="zero", coarse_init="warm"),
+    dict(n=(2048, 2048, 1), real="float", prolong="linear", coarse_bc="consistent", cycle="F", rows="16"),
+    dict(n=(1024, 512, 1), real="double", prolong="linear", coarse_bc="zero", err_mode=0),
+]
+
+
+@pytest.mark.parametrize("cfg", YS_CONFIGS, ids=_cfg_id)
+def test_ys_phases_match_oracle(cfg, monkeypatch):
+    """2D temporally blocked RB-GS 2+2 phases (k_ys: rows streamed, forced down to 2^16 cells) vs one launch
+    per piece vs the C oracle: psi bit-identical on every level (the coarse 2D levels with cl != 0 included);
+    err to summation order."""
+    cfg = dict(cfg)
+    rows = cfg.pop("rows", None)
+    if rows:
+        monkeypatch.setenv("MGP_YS_ROWS", rows)
+    kw = dict(dim=2, smoother="rbgs", nu1=2, nu2=2, **cfg)
+    monkeypatch.setenv("MGP_YS_MIN_CELLS", "65536")
+    monkeypatch.setenv("MGP_FUSED", "1")
+    a = _ctx(**kw)
+    monkeypatch.setenv("MGP_FUSED", "0")
+    b = _ctx(**kw)
+    assert a.levels[0]["engine"] == "zs" and b.levels[0]["engine"] != "zs"
+    o = Oracle(threads=8, **{k: v for k, v in kw.items() if k != "err_mode"})
+    for x in (a, b, o):
+        x.init_point_charge()
+    for it in range(3):
+        old = o.get(0)
+        ea, eb, eo = a.cycle(), b.cycle(), o.step()
+        new = o.get(0)
+        assert np.array_equal(a.get_psi(), new), f"k_ys psi differs after cycle {it + 1}"
+        assert np.array_equal(b.get_psi(), new), f"per-piece psi differs after cycle {it + 1}"
+        if kw.get("err_mode", 1):
+            _check_err(ea, eo, new, old)
+            assert abs(ea - eb) <= 1e-12 * abs(eb)
+    for level in range(len(a.levels)):
+        assert np.array_equal(a.get_psi(level), b.get_psi(level)), f"psi level {level}"
+        assert np.array_equal(a.get_f(level), b.get_f(level)), f"f level {level}"
+
+
 def test_fused_timing_kinds(monkeypatch):
     """The bench's roofline window sees the fused level-0 kernels with their algorithmic bytes."""
     monkeypatch.setenv("MGP_FUSED_MIN_CELLS", "65536")
@@ -526,13 +568,15 @@ def test_metrics_match_reference_formulas(kw):
     assert abs(frob - r_frob) <= 1e-12 * r_frob and abs(frob - e) <= 1e-12 * e
 
 
-@pytest.mark.parametrize("real,cycle", [("float", "V"), ("double", "F")])
-def test_metrics_under_temporally_blocked_finest_level(real, cycle, monkeypatch):
+@pytest.mark.parametrize("real,cycle,dim", [("float", "V", 3), ("double", "F", 3), ("float", "V", 2)])
+def test_metrics_under_temporally_blocked_finest_level(real, cycle, dim, monkeypatch):
     """k_zs on level 0 (forced down to 128^3): POST writes a buffer of its own, so psiOld survives the cycle and
     the reference's metrics (gpu.lua:173-200, test-gpu-obj.lua:222-243) and the psiOld / errorBuf fields
     (cpu-raw.lua:148-153) work on the north-star path; psi equals MGP_KEEP_PSI_OLD=0 (in place) bit for bit."""
     monkeypatch.setenv("MGP_FUSED_MIN_CELLS", "65536")
-    kw = dict(dim=3, n=(128, 128, 128), real=real, cycle=cycle, smoother="rbgs", nu1=2, nu2=2, prolong="linear",
+    monkeypatch.setenv("MGP_YS_MIN_CELLS", "65536")
+    n = (128, 128, 128) if dim == 3 else (1024, 1024, 1)
+    kw = dict(dim=dim, n=n, real=real, cycle=cycle, smoother="rbgs", nu1=2, nu2=2, prolong="linear",
               coarse_bc="consistent")
     ctx = _ctx(**kw)
     monkeypatch.setenv("MGP_KEEP_PSI_OLD", "0")

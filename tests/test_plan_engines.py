@@ -22,8 +22,10 @@ def test_bench_config_512_cube():
 
 
 def test_2d_config_4096():
-    """configs[1]: 4096^2 and 2048^2 per piece, 1024^2 .. 128^2 tiled (32 x 32 tiles), 64^2 .. 1 in the tail."""
-    assert engines(dim=2, n=(4096, 4096, 1), real="float", **NS) == ["piece"] * 2 + ["blk"] * 4 + ["tail"] * 7
+    """configs[1]: 4096^2 temporally blocked (k_ys, rows streamed), 2048^2 per piece, 1024^2 .. 128^2 tiled (32 x 32
+    tiles), 64^2 .. 1 in the tail; fp64 too."""
+    for real in ("float", "double"):
+        assert engines(dim=2, n=(4096, 4096, 1), real=real, **NS) == ["zs", "piece"] + ["blk"] * 4 + ["tail"] * 7
 
 
 def test_config5_rank_slab_f_cycle():

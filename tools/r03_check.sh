@@ -14,7 +14,7 @@ step() {
   [ $rc -eq 0 ] || { echo "stopping after $name (rc=$rc)"; exit $rc; }
 }
 if [ -n "${FIRST:-}" ]; then
-  step tests_first 600 python3 -u -m pytest $FIRST -x -v --timeout 300 --timeout-method thread
+  step tests_first 600 python3 -u -m pytest $FIRST -x -v --timeout 300 --timeout-method thread ${FIRST_K:+-k "$FIRST_K"}
 fi
 if [ -z "${SKIP_ALL:-}" ]; then
   step tests_all 900 python3 -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread ${DESELECT:+--deselect $DESELECT}
