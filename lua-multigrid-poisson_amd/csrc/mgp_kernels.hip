@@ -1830,6 +1830,44 @@ __device__ __forceinline__ void zs_correct(Vec<T, N>& uv, const ZsCoarse<T, N>& 
     }
 }
 
+// The y-interpolated half of zs_correct for one coarse plane: b[e] = w0 a(J) + w1 a(Jn) with a = the
+// x-interpolation of coarse row c0 (J) / c1 (Jn) (zs_correct's b0, or b1 with oz = false: the same
+// expressions over the other plane).  A thread's rows J, Jn and its columns never change, so k_zs
+// evaluates it once per coarse plane and x parity and keeps it in registers for the four fine planes
+// that read the plane.
+template <typename T, int N>
+__device__ __forceinline__ void zs_bq(T (&b)[N], const T (&c0)[N + 2], const T (&c1)[N + 2], int o, int I0, int cx,
+                                      bool oy, T cl, bool fast)
+{
+    const T w0 = (T)0.75, w1 = (T)0.25;
+    if (fast) {
+#pragma unroll
+        for (int e = 0; e < N; ++e) {
+            const T nb0 = o ? c0[e + 2] : c0[e];
+            const T nb1 = o ? c1[e + 2] : c1[e];
+            const T a0 = w0 * c0[e + 1] + w1 * nb0;
+            const T a1 = w0 * c1[e + 1] + w1 * nb1;
+            b[e] = w0 * a0 + w1 * a1;
+        }
+        return;
+    }
+    auto sv = [&](T val, bool fx, bool fy) {
+        T s = (T)1;
+        if (fx) s = -cl * s;
+        if (fy) s = -cl * s;
+        return s == (T)1 ? val : s * val;
+    };
+#pragma unroll
+    for (int e = 0; e < N; ++e) {
+        const int pe = e + 1;
+        const bool ox = (o == 0 && I0 + e == 0) || (o == 1 && I0 + e == cx - 1);
+        auto col = [&](const T (&cc)[N + 2]) { return ox ? cc[pe] : (o ? cc[e + 2] : cc[e]); };
+        const T a0 = w0 * c0[pe] + w1 * sv(col(c0), ox, false);
+        const T a1 = w0 * sv(c1[pe], false, oy) + w1 * sv(col(c1), ox, oy);
+        b[e] = w0 * a0 + w1 * a1;
+    }
+}
+
 // Fixed-order workgroup sum of one double per thread (NTL threads, any count <= 1024).
 template <int NTL>
 __device__ __forceinline__ void block_partial_t(double acc, double* partials)
@@ -1852,6 +1890,9 @@ __device__ __forceinline__ void block_partial_t(double acc, double* partials)
 // current H planes).  CLZ: the level operator has no boundary modification (cl == 0, level 0).
 #ifndef ZS_WPE_PRE
 #define ZS_WPE_PRE 2
+#endif
+#ifndef ZS_BQ
+#define ZS_BQ 1  // POST: per-thread cache of the coarse planes' y-interpolation (zs_bq)
 #endif
 #ifndef ZS_WPE_POST
 #define ZS_WPE_POST 4
@@ -2034,6 +2075,24 @@ __attribute__((amdgpu_waves_per_eu(1, PRE ? ZS_WPE_PRE : ZS_WPE_POST))) void k_z
     const bool corr_lane = !PRE && (cgy >> 1) + ((cgy & 1) ? 1 : -1) >= 0 && (cgy >> 1) + ((cgy & 1) ? 1 : -1) < gc.ny &&
                            cgm > 0 && cgm + N < gc.nx;
     const bool corr_fast = __all(corr_lane);
+    // POST, linear P, steady steps: BQ[K & 1][q][e] = zs_bq of coarse plane K for the black cells of the
+    // fine planes of parity 1 ^ q (x parity q ^ (cgy & 1)).  Plane K + 1 is evaluated at odd step 2K + 1,
+    // its first reader; fine plane p reads planes K and Kn = K +- 1, the two slots.
+    T BQ[2][2][N];
+#pragma unroll
+    for (int i = 0; i < 2 * 2 * N; ++i) (&BQ[0][0][0])[i] = (T)0;
+    const int bq_J = cgy >> 1;
+    int bq_Jn = (cgy & 1) ? bq_J + 1 : bq_J - 1;
+    const bool bq_oy = !PRE && (bq_Jn < 0 || bq_Jn >= gc.ny);
+    if (bq_oy) bq_Jn = bq_J;
+    auto bq_fill = [&](T (&bq)[2][N], int K) {
+        T c0[N + 2], c1[N + 2];
+        crow(K, bq_J, c0);
+        crow(K, bq_Jn, c1);
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+            zs_bq<T, N>(bq[q], c0, c1, q ^ (cgy & 1), cgm, gc.nx, bq_oy, clc, corr_fast);
+    };
     auto step = [&](auto st, auto rt, const PF& cur, PF& nxt, int p) {
         constexpr bool ST = decltype(st)::value;
         constexpr int RS = decltype(rt)::value;  // (p - zlo) & 3
@@ -2065,7 +2124,14 @@ __attribute__((amdgpu_waves_per_eu(1, PRE ? ZS_WPE_PRE : ZS_WPE_POST))) void k_z
 
         // ---- stage 0: black cells of plane p ----
         VT a0 = cur.u;
-        if (!PRE && (ST || inz(p))) {
+        if constexpr (!PRE && ST && LINEAR == 1 && ZS_BQ) {
+            // (z0 + Z0) % 4 == 0 in steady steps: K & 1 and p & 1 are static
+            constexpr int KS = (RS >> 1) & 1, Q = 1 ^ (RS & 1);
+            if constexpr ((RS & 1) != 0) bq_fill(BQ[KS ^ 1], ((zz0 + p) >> 1) + 1);
+            const T w0 = (T)0.75, w1 = (T)0.25;
+#pragma unroll
+            for (int e = 0; e < N; ++e) a0.v[e] = a0.v[e] + (w0 * BQ[KS][Q][e] + w1 * BQ[KS ^ 1][Q][e]);
+        } else if (!PRE && (ST || inz(p))) {
             const int J = cgy >> 1, K = (zz0 + p) >> 1;
             int Jn = (cgy & 1) ? J + 1 : J - 1;
             int Kn = ((zz0 + p) & 1) ? K + 1 : K - 1;
@@ -2231,7 +2297,8 @@ __attribute__((amdgpu_waves_per_eu(1, PRE ? ZS_WPE_PRE : ZS_WPE_POST))) void k_z
     ps += (zlo - ps) & 3;              // whole groups of four steps in the prologue
     pe -= (pe - ps + 1) & 3;           // and in the steady part
     // no steady part (the epilogue takes all) without a whole group or with odd z0 / Z0 (static parity)
-    if (pe < ps || ((z0 | Z0) & 1)) ps = pe = zlo - 1;
+    // POST with the BQ cache: (z0 + Z0) % 4 == 0 as well (static parity of the coarse plane)
+    if (pe < ps || ((z0 | Z0) & 1) || (!PRE && LINEAR == 1 && ZS_BQ && ((z0 + Z0) & 3))) ps = pe = zlo - 1;
     int p = zlo;
     const std::integral_constant<int, 0> R0;
     const std::integral_constant<int, 1> R1;
@@ -2242,6 +2309,13 @@ __attribute__((amdgpu_waves_per_eu(1, PRE ? ZS_WPE_PRE : ZS_WPE_POST))) void k_z
         step(GEN, R1, pb, pa, p + 1);
         step(GEN, R2, pa, pb, p + 2);
         step(GEN, R3, pb, pa, p + 3);
+    }
+    if constexpr (!PRE && LINEAR == 1 && ZS_BQ) {
+        if (p <= pe) {  // the first steady step (even, K & 1 == 0) reads coarse planes K and K - 1
+            const int K = (z0 + p) >> 1;
+            bq_fill(BQ[0], K);
+            bq_fill(BQ[1], K - 1);
+        }
     }
     for (; p <= pe; p += 4) {
         step(STY, R0, pa, pb, p);
