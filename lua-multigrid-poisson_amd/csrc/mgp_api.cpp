@@ -17,6 +17,7 @@
 #include <condition_variable>
 #include <mutex>
 #include <functional>
+#include <optional>
 #include <thread>
 #include <cmath>
 #include <cstdarg>
@@ -25,6 +26,8 @@
 #include <cstring>
 #include <string>
 #include <vector>
+
+#include <dlfcn.h>
 
 #include "../../include/mgpoisson.h"
 
@@ -1001,14 +1004,63 @@ int run_tail(mgp_ctx* c, bool fcycle)
     return MGP_OK;
 }
 
+// ---- roctx ranges (SURVEY.md §5 tracing): MGP_ROCTX=1 names the cycle and every level's phases on the host
+// timeline of rocprofv3 --marker-trace.  The roctx library is opened at run time (no link dependency); graph
+// replay is off while ranges are on, so every cycle enqueues (and names) its launches.
+struct Roctx {
+    int (*push)(const char*) = nullptr;
+    int (*pop)() = nullptr;
+    Roctx()
+    {
+        const char* v = std::getenv("MGP_ROCTX");
+        if (!(v && std::atoi(v))) return;
+        void* h = dlopen("librocprofiler-sdk-roctx.so.1", RTLD_NOW | RTLD_LOCAL);
+        if (!h) h = dlopen("libroctx64.so.4", RTLD_NOW | RTLD_LOCAL);
+        if (!h) return;
+        push = reinterpret_cast<int (*)(const char*)>(dlsym(h, "roctxRangePushA"));
+        pop = reinterpret_cast<int (*)()>(dlsym(h, "roctxRangePop"));
+        if (!push || !pop) push = nullptr, pop = nullptr;
+    }
+};
+const Roctx& roctx()
+{
+    static const Roctx r;
+    return r;
+}
+bool roctx_on() { return roctx().push != nullptr; }
+struct Range {
+    bool on;
+    Range(const char* fmt, int l) : on(roctx_on())
+    {
+        if (!on) return;
+        char b[64];
+        std::snprintf(b, sizeof(b), fmt, l);
+        roctx().push(b);
+    }
+    ~Range()
+    {
+        if (on) roctx().pop();
+    }
+};
+
 int cycle_rec(mgp_ctx* c, int l, double h, bool fcycle)
 {
     const int last = (int)c->lev.size() - 1;
-    if (l == c->handoff_level && c->handoff_fn) return run_handoff(c, l, h);
-    if (l == c->tail_level && h == level_h(c, l)) return run_tail(c, fcycle);
-    if (l == last) return coarse_solve_at(c, l, h);
+    if (l == c->handoff_level && c->handoff_fn) {
+        Range r("L%d hand-off", l);
+        return run_handoff(c, l, h);
+    }
+    if (l == c->tail_level && h == level_h(c, l)) {
+        Range r("L%d+ coarse tail", l);
+        return run_tail(c, fcycle);
+    }
+    if (l == last) {
+        Range r("L%d coarse solve", l);
+        return coarse_solve_at(c, l, h);
+    }
     const bool fused = c->lev[l].fused && h == level_h(c, l);
     const bool blk = !fused && c->lev[l].blk && h == level_h(c, l);
+    std::optional<Range> pre_range(std::in_place, "L%d pre-smooth + restrict", l);
     if (fused) {
         TRY(fused_pre(c, l, h));
     } else if (blk) {
@@ -1018,9 +1070,11 @@ int cycle_rec(mgp_ctx* c, int l, double h, bool fcycle)
         TRY(residual_restrict(c, l, h));
     }
     if (c->o.coarse_init == MGP_COARSE_FRESH) TRY(zero_level(c, c->lev[l + 1]));
+    pre_range.reset();
     if (fcycle) TRY(cycle_rec(c, l + 1, 2 * h, true));
     TRY(cycle_rec(c, l + 1, 2 * h, false));
     const bool want_err = l == 0 && c->in_cycle && c->err_fuse;
+    Range post_range("L%d prolong + post-smooth", l);
     if (fused) {
         TRY(fused_post(c, l, h, want_err));
     } else if (blk && !want_err) {
@@ -1062,7 +1116,11 @@ int one_cycle(mgp_ctx* c, double* dst)
         HIP_TRY(c, hipMemcpyAsync(c->psi_old, c->ui(L, L.u), bytes, hipMemcpyDeviceToDevice, c->s));
     const double h = 1.0 / (double)L.p.nx;  // cpu.lua:197-198
     c->in_cycle = true;
-    int rc = cycle_rec(c, 0, h, c->o.cycle == MGP_CYCLE_F);
+    int rc;
+    {
+        Range r(c->o.cycle == MGP_CYCLE_F ? "F-cycle%.0d" : "V-cycle%.0d", 0);
+        rc = cycle_rec(c, 0, h, c->o.cycle == MGP_CYCLE_F);
+    }
     c->in_cycle = false;
     TRY(rc);
     if (fuse && !c->err_done) return c->fail(MGP_ERR_STATE, "internal: fused err launch did not run");
@@ -1528,7 +1586,7 @@ static int create_impl(mgp_ctx** out, const mgp_opts* o, mgp_loopback* lb, ncclC
     }
     {
         const char* v = std::getenv("MGP_GRAPH");
-        c->use_graph = c->o.world == 1 && !(v && std::atoi(v) == 0);
+        c->use_graph = c->o.world == 1 && !(v && std::atoi(v) == 0) && !roctx_on();
     }
     if (c->o.smoother == MGP_RBGS && c->o.coarse_init == MGP_COARSE_FRESH) {
         for (size_t l = 1; l < c->lev.size(); ++l)
@@ -2125,8 +2183,11 @@ int mgp_copy_bandwidth(int device, int64_t bytes, int32_t reps, double* gbps)
         g_create_error = "mgp_copy_bandwidth: allocation failed";
         rc = MGP_ERR_OOM;
     }
-    // every copy kernel shape, reps timed launches each after an untimed first touch; the best counts
-    for (int kind = 0; kind < mgp::kCopyKinds && rc == MGP_OK; ++kind)
+    // every copy kernel shape, reps timed launches each after an untimed first touch; the best counts.
+    // MGP_COPY_CALIB=1 adds the narrow-lane copies (FETCH_SIZE calibration, tools/fetch_calib.py).
+    const char* calib = std::getenv("MGP_COPY_CALIB");
+    const int kinds = calib && std::atoi(calib) ? mgp::kCopyCalibKinds : mgp::kCopyKinds;
+    for (int kind = 0; kind < kinds && rc == MGP_OK; ++kind)
         for (int r = -1; r < reps && rc == MGP_OK; ++r) {
             if (hipEventRecord(e0, s) != hipSuccess || mgp::launch_copy16(kind, a, b, bytes, s) != hipSuccess ||
                 hipEventRecord(e1, s) != hipSuccess || hipEventSynchronize(e1) != hipSuccess) {

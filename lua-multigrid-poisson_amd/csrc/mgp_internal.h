@@ -196,8 +196,8 @@ int cg_scratch_doubles();
 hipError_t launch_cg(int rb, int dim, CgArgs& a, hipStream_t s);
 
 // 16-byte streaming copy of `bytes` (a multiple of 16) for the copy-bandwidth probe; kind 0..2 (kCopyKinds):
-// grid-stride / one pass / one pass non-temporal
-constexpr int kCopyKinds = 3;
+// grid-stride / one pass / one pass non-temporal; kinds 3 and 4 (calibration only): 8- and 4-byte lanes
+constexpr int kCopyKinds = 3, kCopyCalibKinds = 5;
 hipError_t launch_copy16(int kind, const void* src, void* dst, int64_t bytes, hipStream_t s);
 
 constexpr int kSumBlocks = 1024;

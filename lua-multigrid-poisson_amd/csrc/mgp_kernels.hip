@@ -3316,6 +3316,30 @@ __global__ __launch_bounds__(blk_threads<DIM>()) void k_blk(const T* __restrict_
 
 // ---- copy-bandwidth probe ("a measured copy-kernel peak is also reported") --------
 
+// Narrow-lane copies (W = 8 or 4 bytes per lane, one pass, 4 elements per thread a workgroup apart): the
+// FETCH_SIZE calibration of loads narrower than 16 bytes (tools/fetch_calib.py; mgp_copy_bandwidth runs
+// them only under MGP_COPY_CALIB=1).
+template <int W>
+__global__ __launch_bounds__(kBlock) void k_copy_w(const void* __restrict__ src, void* __restrict__ dst, int64_t n)
+{
+    typedef float f2v __attribute__((ext_vector_type(2)));
+    using E = typename std::conditional<W == 8, f2v, float>::type;
+    const E* s = reinterpret_cast<const E*>(src);
+    E* d = reinterpret_cast<E*>(dst);
+    const int64_t base = (int64_t)blockIdx.x * (4 * kBlock) + threadIdx.x;
+    E v[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int64_t i = base + k * kBlock;
+        if (i < n) v[k] = s[i];
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int64_t i = base + k * kBlock;
+        if (i < n) d[i] = v[k];
+    }
+}
+
 // dst = src in 16-byte lanes.  kind 0: grid-stride, 4 independent loads in flight per thread per
 // iteration; kind 1: one pass, each thread 4 vectors a workgroup apart; kind 2: kind 1 with non-temporal
 // loads and stores.  The probe reports the fastest.
@@ -4136,7 +4160,9 @@ hipError_t launch_copy16(int kind, const void* src, void* dst, int64_t bytes, hi
     const unsigned one_pass = (unsigned)((n + 4 * kBlock - 1) / (4 * kBlock));
     if (kind == 0) k_copy16<0><<<2048, kBlock, 0, s>>>((const float4*)src, (float4*)dst, n);
     else if (kind == 1) k_copy16<1><<<one_pass, kBlock, 0, s>>>((const float4*)src, (float4*)dst, n);
-    else k_copy16<2><<<one_pass, kBlock, 0, s>>>((const float4*)src, (float4*)dst, n);
+    else if (kind == 2) k_copy16<2><<<one_pass, kBlock, 0, s>>>((const float4*)src, (float4*)dst, n);
+    else if (kind == 3) k_copy_w<8><<<one_pass * 2, kBlock, 0, s>>>(src, dst, n * 2);
+    else k_copy_w<4><<<one_pass * 4, kBlock, 0, s>>>(src, dst, n * 4);
     return hipGetLastError();
 }
 
