@@ -202,17 +202,19 @@ def main():
     tname = "float" if a.real == "float" else "double"
     lin = 1 if a.prolong == "linear" else 0
     fw = a.restriction == "full_weighting"
+    kz = "k_zs" if cfg["dim"] == 3 else "k_ys"  # the temporally blocked phases: planes / rows streamed
     kernels = {"half_sweep": f"k_half<{tname}, {cfg['dim']}, 1, false>",
-               "fused_pre": f"k_zs<{tname}, true, {1 if fw else 0}, false, true>",
-               "fused_post": f"k_zs<{tname}, false, {lin}, true, true>"}
+               "fused_pre": f"{kz}<{tname}, true, {1 if fw else 0}, false, true>",
+               "fused_post": f"{kz}<{tname}, false, {lin}, true, true>"}
     # Algorithmic bytes per level-0 cell of one launch (reals): what the launch must move
     # to and from HBM.  half_sweep: read the other colour and f, write this colour of half the cells.
-    # fused_pre (k_zs: 2 RB-GS sweeps + residual + restriction): read black u and f, write black u and R/8
-    # (its red cells are never read: the only reader, fused_post, loads black cells and its first red
-    # half-sweep replaces the red ones).
-    # fused_post (k_zs: prolongation + correction + 2 sweeps + err): read black u, V/8, f, psiOld; write u.
+    # fused_pre (k_zs / k_ys: 2 RB-GS sweeps + residual + restriction): read black u and f, write black u and
+    # R / 2^dim (its red cells are never read: the only reader, fused_post, loads black cells and its first
+    # red half-sweep replaces the red ones).
+    # fused_post (prolongation + correction + 2 sweeps + err): read black u, V / 2^dim, f, psiOld; write u.
     # (full weighting: PRE smooths only and stores both colours, 2.5 reals; the restriction runs after it)
-    algo_reals = {"half_sweep": 1.5, "fused_pre": 2.5 if fw else 2.125, "fused_post": 3.625}
+    coarse = 0.5 ** cfg["dim"]
+    algo_reals = {"half_sweep": 1.5, "fused_pre": 2.5 if fw else 2.0 + coarse, "fused_post": 3.5 + coarse}
     per_kind = {k: v for k, v in timed.items() if v[1] > 0}
     cells = cells_rank
     if per_kind:

@@ -1296,6 +1296,25 @@ struct PvRow {
     T c00[N + 2], c10[N + 2], c01[N + 2], c11[N + 2];  // [z: K / Kn][y: J / Jn]
     bool oy, oz, interior;
     int I0, cx;
+    // load()'s flags with rows J / Jn (2D, or plane K with oz = false) already in registers
+    __device__ __forceinline__ void set_rows(const Geo& gc, int j, int64_t k, int i0, const T (&r0)[N + 2],
+                                             const T (&r1)[N + 2])
+    {
+        static_assert(DIM == 2, "set_rows: 2D rows");
+        I0 = i0;
+        cx = gc.nx;
+        const int J = j >> 1;
+        const int Jn = (j & 1) ? J + 1 : J - 1;
+        oy = Jn < 0 || Jn >= gc.ny;
+        oz = false;
+        (void)k;
+#pragma unroll
+        for (int e = 0; e < N + 2; ++e) {
+            c00[e] = r0[e];
+            if (LINEAR) c10[e] = r1[e];
+        }
+        interior = !oy && I0 > 0 && I0 + N < cx;
+    }
     __device__ __forceinline__ void load(const T* __restrict__ V, const Geo& gc, int j, int64_t k, int i0)
     {
         I0 = i0;
@@ -2368,14 +2387,24 @@ struct YsShape {
     // its row p - 5 at step p), stage 4 two (PRE)
     static constexpr int ES = 2 * G;
     static constexpr int OFF1 = 2 * ES, OFF2 = 4 * ES, OFF3 = 6 * ES, OFF4 = 10 * ES;
-    static constexpr size_t lds_floats = 12 * ES;
+    // POST: ring of 4 coarse rows (cells I in [X0/2 - 8, X0/2 + TX/2 + 8), x order, both colours)
+    static constexpr int CI = PRE ? 0 : TX / 2 + 16, CPAIRS = CI / 2, OFFC = 12 * ES;
+    static constexpr size_t lds_floats = 12 * ES + 4 * CI;
+    static_assert(CPAIRS <= 2 * NTL, "coarse staging: two pairs per thread");
     static_assert(NTL <= 1024, "too many threads");
     static_assert(2 * N * HXG >= H, "x halo too small");
 };
 
+// Rows prefetched YS_PF steps ahead (a ring of 4 buffers, so every index stays static in the 4-step loop).
+#ifndef YS_PF
+#define YS_PF 2
+#endif
+static_assert(YS_PF >= 1 && YS_PF <= 3, "prefetch distance 1..3");
 template <typename T>
 struct YsPrefetch {
-    Vec<T, 16 / sizeof(T)> u, f1, f2, o0, o1;  // black u of row p; red f of p - 1; black f of p - 2; psiOld of p - 4
+    static constexpr int N = 16 / sizeof(T);
+    Vec<T, N> u, f1, f2, o0, o1;  // black u of row p; red f of p - 1; black f of p - 2; psiOld of p - 4
+    Vec<T, 2> cv[2];              // POST, even p: this thread's coarse pairs of coarse row p / 2 + 1
 };
 
 // relax of my N cells of x parity o: rows ym / yp above and below (other colour), cen my row's other
@@ -2462,6 +2491,41 @@ __global__ __launch_bounds__((YsShape<T, PRE>::NTL)) void k_ys(const T* __restri
         ep = gx > 0 ? sl[2 * gx - 1] : (T)0;
         en = gx < G - 1 ? sl[2 * gx + 2] : (T)0;
     };
+    // ---- POST: coarse staging ring, row J in slot J & 3 (rows clamped to the box) ----
+    const int Ia = X0 / 2 - 8;
+    auto cjl = [&](int J) { return J < 0 ? 0 : (J >= gc.ny ? gc.ny - 1 : J); };
+    auto cslot = [&](int J) { return lds + S::OFFC + (J & 3) * S::CI; };
+    auto cload = [&](PF& r, int J) {
+        J = cjl(J);
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int t = tid + i * NTL;
+            const int I = Ia + 2 * t;
+            r.cv[i].v[0] = r.cv[i].v[1] = (T)0;
+            if (t < S::CPAIRS && I >= 0 && I < gc.nx) {  // I even: cells I, I + 1 at m = I / 2 of the two halves
+                const T* row = V + (int64_t)J * gc.hw + (I >> 1);
+                const int ce = (I + J) & 1;
+                r.cv[i].v[0] = row[ce * gc.H];
+                r.cv[i].v[1] = row[(ce ^ 1) * gc.H];
+            }
+        }
+    };
+    auto cstore = [&](const PF& r, int J) {
+        T* const sl = cslot(cjl(J));
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int t = tid + i * NTL;
+            if (t < S::CPAIRS) vstore<T, 2>(sl + 2 * t, r.cv[i]);
+        }
+    };
+    auto crow = [&](int J, T (&c)[N + 2]) {  // cells cgm - 1 .. cgm + N of coarse row J
+        const T* const sl = cslot(cjl(J)) + (cgm - Ia);
+        const Vec<T, N> mid = vload<T, N>(sl);
+        c[0] = vload_lds_whole<T, N>(sl - N).v[N - 1];
+#pragma unroll
+        for (int e = 0; e < N; ++e) c[e + 1] = mid.v[e];
+        c[N + 1] = vload_lds_whole<T, N>(sl + N).v[0];
+    };
     auto prefetch = [&](PF& r, int p) {
         r.u = vload<T, N>(src + Hh + (int64_t)rcl(p) * hw + cgm);
         r.f1 = vload<T, N>(f + (int64_t)rcl(p - 1) * hw + cgm);
@@ -2471,6 +2535,9 @@ __global__ __launch_bounds__((YsShape<T, PRE>::NTL)) void k_ys(const T* __restri
             r.o0 = vload<T, N>(old + ro);
             r.o1 = vload<T, N>(old + Hh + ro);
         }
+        // POST: fine row 2m + 1 is the first to need coarse row m + 1; it is loaded with the prefetch of row
+        // 2m and put in the ring at the top of step 2m
+        if (!PRE && (p & 1) == 0) cload(r, (p >> 1) + 1);
     };
     const VT vz = vzero<T, N>();
     VT W0[4], W1[4], W2[4], W3[4], W4[4], FR[4], FB[4];
@@ -2481,8 +2548,10 @@ __global__ __launch_bounds__((YsShape<T, PRE>::NTL)) void k_ys(const T* __restri
     for (int e = 0; e < N; ++e) acc[e] = (T)0;
     double err = 0.0, err1 = 0.0;
 
-    auto step = [&](auto rt, const PF& cur, PF& nxt, int p) {
+    PF pf[4];
+    auto step = [&](auto rt, int p) {
         constexpr int RS = decltype(rt)::value;  // (p - zlo) & 3
+        const PF& cur = pf[RS];
         auto sl = [](int k) constexpr { return (RS - k) & 3; };
         constexpr int PP = (H + RS) & 1;  // parity of p (Y0 even)
         auto par = [](int k) constexpr { return (PP + k) & 1; };  // parity of row p - k (mod 2)
@@ -2493,8 +2562,15 @@ __global__ __launch_bounds__((YsShape<T, PRE>::NTL)) void k_ys(const T* __restri
             zs_hold<T, N>(cur.o0);
             zs_hold<T, N>(cur.o1);
         }
+        if (!PRE && PP == 0) {
+            zs_hold<T, 2>(cur.cv[0]);
+            zs_hold<T, 2>(cur.cv[1]);
+        }
         asm volatile("" ::: "memory");
-        if (p + 1 <= p_end) prefetch(nxt, p + 1);
+        // POST: the coarse row this row's prefetch loaded (first read one step on; the slot it replaces was
+        // last read three steps back)
+        if (!PRE && PP == 0) cstore(cur, (p >> 1) + 1);
+        if (p + YS_PF <= p_end) prefetch(pf[(RS + YS_PF) & 3], p + YS_PF);
 
         // ---- stage 0: black cells of row p (POST: + P V) ----
         VT a0 = cur.u;
@@ -2502,7 +2578,11 @@ __global__ __launch_bounds__((YsShape<T, PRE>::NTL)) void k_ys(const T* __restri
             a0 = vz;
         } else if (!PRE) {
             PvRow<T, N, 2, LINEAR> pv;
-            pv.load(V, gc, p, 0, cgm);
+            T c0[N + 2], c1[N + 2];
+            const int J = p >> 1;
+            crow(J, c0);
+            if (LINEAR) crow((p & 1) ? J + 1 : J - 1, c1);  // Jn (clamped: PvRow's oy factor applies)
+            pv.set_rows(gc, p, 0, cgm, c0, c1);
             const int ob = 1 ^ par(0);  // x parity of row p's black cells
 #pragma unroll
             for (int e = 0; e < N; ++e) a0.v[e] = a0.v[e] + pv.value(e, ob, clc);
@@ -2598,13 +2678,21 @@ __global__ __launch_bounds__((YsShape<T, PRE>::NTL)) void k_ys(const T* __restri
     const std::integral_constant<int, 1> R1;
     const std::integral_constant<int, 2> R2;
     const std::integral_constant<int, 3> R3;
-    PF pa, pb;
-    prefetch(pa, zlo);
+    if (!PRE) {  // the coarse rows the first fine row needs
+        const int J = zlo >> 1;
+        for (int k = J - 1; k <= J + 1; ++k) {
+            cload(pf[0], k);
+            cstore(pf[0], k);
+        }
+        __syncthreads();
+    }
+#pragma unroll
+    for (int d = 0; d < YS_PF; ++d) prefetch(pf[d], zlo + d);
     for (int p = zlo; p <= p_end; p += 4) {
-        step(R0, pa, pb, p);
-        if (p + 1 <= p_end) step(R1, pb, pa, p + 1);
-        if (p + 2 <= p_end) step(R2, pa, pb, p + 2);
-        if (p + 3 <= p_end) step(R3, pb, pa, p + 3);
+        step(R0, p);
+        if (p + 1 <= p_end) step(R1, p + 1);
+        if (p + 2 <= p_end) step(R2, p + 2);
+        if (p + 3 <= p_end) step(R3, p + 3);
     }
     if (ERR) block_partial_t<NTL>(err + err1, partials);
 }
