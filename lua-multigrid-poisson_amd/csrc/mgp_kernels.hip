@@ -776,6 +776,98 @@ __global__ __launch_bounds__(kBlock) void k_resnorm(const T* __restrict__ u, con
     }
 }
 
+// 3D levels streamed through z: a thread owns N cells of each colour in one row (j, packed m0 .. m0 + N - 1)
+// and walks kResZ planes, holding both colours of the row in planes k - 1, k, k + 1 in registers, so each
+// plane of u and f is read once (rows j +- 1 come from L2, where the neighbouring rows' threads read them as
+// their own).  The per-cell expressions are k_resnorm's; only the partial sums' grouping differs.
+constexpr int kResZ = 16;
+template <typename T>
+__global__ __launch_bounds__(kBlock) void k_resnorm_z(const T* __restrict__ u, const T* __restrict__ f, Geo g,
+                                                      Op<T, 3> op, double* __restrict__ partials, int fofs)
+{
+    constexpr int N = VN<T>::n;
+    const int groups = g.hw / N;
+    const int64_t cols = (int64_t)groups * g.ny;
+    const int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    double rr = 0.0, ff = 0.0;
+    if (t < cols * (g.nz / kResZ)) {
+        const int64_t col = t % cols;
+        const int64_t k0 = (t / cols) * kResZ;
+        const int grp = (int)(col % groups), j = (int)(col / groups), m0 = grp * N;
+        const int64_t roff = (int64_t)j * g.hw + m0;
+        Vec<T, N> A[2], B[2];
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+            A[c] = vload<T, N>(u + (k0 - 1) * g.P + c * g.H + roff);  // a ghost plane at the slab's ends
+            B[c] = vload<T, N>(u + k0 * g.P + c * g.H + roff);
+        }
+        for (int64_t k = k0; k < k0 + kResZ; ++k) {
+            const int64_t gk = g.z0 + k;
+            const T* const pk = u + k * g.P + roff;
+            Vec<T, N> C[2], YL[2], YR[2], F[2];
+            T edge[2];
+#pragma unroll
+            for (int c = 0; c < 2; ++c) {
+                C[c] = vload<T, N>(pk + g.P + c * g.H);
+                YL[c] = j > 0 ? vload<T, N>(pk + c * g.H - g.hw) : vzero<T, N>();
+                YR[c] = j < g.ny - 1 ? vload<T, N>(pk + c * g.H + g.hw) : vzero<T, N>();
+                F[c] = vload<T, N>(f + k * g.P + c * g.H + roff);
+                // x edge of colour c's cells, from the other colour's row: x - 1 of the first cell (x parity 0)
+                // or x + 1 of the last (parity 1)
+                const int o = c ^ (int)((j + gk) & 1);
+                const T* const oth = pk + (c ^ 1) * g.H;
+                if (o == 0)
+                    edge[c] = m0 > 0 ? oth[-1] : (T)0;
+                else
+                    edge[c] = m0 + N < g.hw ? oth[N] : (T)0;
+            }
+            const int nbyz = (j == 0) + (j == g.ny - 1) + (gk == 0) + (gk == g.gnz - 1);
+#pragma unroll
+            for (int c = 0; c < 2; ++c) {
+                const int oc = c ^ 1, o = c ^ (int)((j + gk) & 1);
+                const Vec<T, N>& cen = B[oc];
+#pragma unroll
+                for (int e = 0; e < N; ++e) {
+                    const int i = 2 * (m0 + e) + o;
+                    const T xl = o == 0 ? (e == 0 ? edge[c] : cen.v[e - 1]) : cen.v[e];
+                    const T xr = o == 0 ? cen.v[e] : (e == N - 1 ? edge[c] : cen.v[e + 1]);
+                    T sm = xl + xr;
+                    sm = sm + YL[oc].v[e];
+                    sm = sm + YR[oc].v[e];
+                    sm = sm + A[oc].v[e];
+                    sm = sm + C[oc].v[e];
+                    const T r = op.residual(sm, F[c].v[e], B[c].v[e], nbyz + (i == 0) + (i == g.nx - 1));
+                    rr = __builtin_fma((double)r, (double)r, rr);
+                    ff = __builtin_fma((double)F[c].v[e], (double)F[c].v[e], ff);
+                }
+            }
+#pragma unroll
+            for (int c = 0; c < 2; ++c) {
+                A[c] = B[c];
+                B[c] = C[c];
+            }
+        }
+    }
+    rr = wave_sum(rr);
+    ff = wave_sum(ff);
+    __shared__ double ws[2][kBlock / 64];
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) {
+        ws[0][w] = rr;
+        ws[1][w] = ff;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double a = 0.0, b = 0.0;
+        for (int q = 0; q < kBlock / 64; ++q) {
+            a += ws[0][q];
+            b += ws[1][q];
+        }
+        partials[blockIdx.x] = a;
+        partials[fofs + blockIdx.x] = b;
+    }
+}
+
 // Scalar form for small levels (hw < N, nx = 1 included): a thread per packed slot.
 template <typename T, int DIM>
 __global__ __launch_bounds__(kBlock) void k_resnorm_s(const T* __restrict__ u, const T* __restrict__ f, Geo g,
@@ -3597,9 +3689,17 @@ hipError_t launch_unpack(int rb, const void* packed, void* lex, Geo g, hipStream
     return hipGetLastError();
 }
 
+// k_resnorm_z: 3D levels whose rows hold whole vectors and whose planes split into kResZ-plane chunks
+static bool resnorm_z_ok(int rb, const Geo& g)
+{
+    const int n = 16 / rb;
+    return g.nz % kResZ == 0 && g.hw >= n && g.hw % n == 0 && g.nx >= 2;
+}
+
 int resnorm_blocks(int rb, Geo g)
 {
     const int n = 16 / rb;
+    if (resnorm_z_ok(rb, g)) return (int)nblk((int64_t)(g.hw / n) * g.ny * (g.nz / kResZ));
     return (g.hw >= n && g.nx >= 2) ? (int)nblk(2 * (g.H / n) * g.nz) : (int)nblk(g.P * g.nz);
 }
 
@@ -3611,7 +3711,9 @@ static void resnorm_t(const void* u, const void* f, Geo g, double h, double cl, 
     constexpr int n = VN<T>::n;
     const unsigned nb = (unsigned)resnorm_blocks(sizeof(T), g);
     const int fofs = (int)nb + sum_scratch((int)nb);
-    if (g.hw >= n && g.nx >= 2) {
+    if (D == 3 && resnorm_z_ok(sizeof(T), g)) {
+        k_resnorm_z<T><<<nb, kBlock, 0, s>>>((const T*)u, (const T*)f, g, make_op<T, 3>(h, cl), partials, fofs);
+    } else if (g.hw >= n && g.nx >= 2) {
         const int64_t items = (g.H / n) * g.nz;
         k_resnorm<T, D><<<nb, kBlock, 0, s>>>((const T*)u, (const T*)f, g, op, items, partials, fofs);
     } else {
