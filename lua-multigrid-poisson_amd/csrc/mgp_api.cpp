@@ -135,6 +135,7 @@ struct Level {
     bool zero_pending = false;  // u is logically 0: the next red half-sweep reads c->zbuf instead
     bool ghost_zero = false;    // u is 0 everywhere, so ghost planes of any depth are current
     int64_t exchanges = 0;      // halo exchanges of this level so far (mgp_level_info info[7])
+    bool early_u = false;       // POST's u halo was exchanged on the side stream after PRE (wait on x_ev1)
     int zc = 0, zc_pre = 0;  // k_zs z-chunks (planes per workgroup) of POST and PRE
 };
 
@@ -183,6 +184,11 @@ struct mgp_ctx {
     ncclComm_t comm = nullptr;
     mgp_loopback* lb = nullptr;  // loopback transport instead of RCCL (tests)
     hipEvent_t lb_ev = nullptr, lb_ev2 = nullptr;
+    // Slab levels: the u halo that a temporally blocked POST reads is final after PRE, so it is exchanged on
+    // the side stream xs right after PRE and overlaps the coarse levels (MGP_EARLY_X=0: before POST instead)
+    hipStream_t xs = nullptr;
+    hipEvent_t x_ev0 = nullptr, x_ev1 = nullptr;
+    bool early_x = true;
     char* lb_buf = nullptr;
     double* lb_red = nullptr;
     // psiOld of the last outer iteration (for mgp_metrics), nullptr when not kept
@@ -311,7 +317,7 @@ Geo make_geo(const LevelPlan& p, int dim)
 
 int lb_fail(mgp_ctx* c) { return c->fail(MGP_ERR_STATE, "loopback group barrier timed out or broken"); }
 
-int lb_exchange(mgp_ctx* c, int l, char* buf, int depth, int colour)
+int lb_exchange(mgp_ctx* c, int l, char* buf, int depth, int colour, hipStream_t st)
 {
     mgp_loopback* g = c->lb;
     const size_t rb = (size_t)c->rb;
@@ -320,25 +326,25 @@ int lb_exchange(mgp_ctx* c, int l, char* buf, int depth, int colour)
     const size_t coff = colour < 0 ? 0 : (size_t)(colour * L.g.H) * rb;  // one colour half per plane
     auto at = [&](char* b, int64_t k) { return b + (size_t)((k + c->G) * L.g.P) * rb + coff; };
     c->lb_buf = buf;
-    HIP_TRY(c, hipEventRecord(c->lb_ev, c->s));  // my boundary planes are final here
+    HIP_TRY(c, hipEventRecord(c->lb_ev, c->s));  // my boundary planes are final here (compute stream)
     if (!g->barrier()) return lb_fail(c);
     const int r = c->o.rank;
     for (int nb : {r - 1, r + 1}) {
         if (nb < 0 || nb >= c->o.world) continue;
         mgp_ctx* o = g->ranks[nb];
-        HIP_TRY(c, hipStreamWaitEvent(c->s, o->lb_ev, 0));
+        HIP_TRY(c, hipStreamWaitEvent(st, o->lb_ev, 0));
         const char* src = nb < r ? at(o->lb_buf, L.g.nz - depth) : at(o->lb_buf, 0);
         char* dst = nb < r ? at(buf, -depth) : at(buf, L.g.nz);
         if (colour < 0)
-            HIP_TRY(c, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, c->s));
+            HIP_TRY(c, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, st));
         else
             HIP_TRY(c, hipMemcpy2DAsync(dst, (size_t)L.g.P * rb, src, (size_t)L.g.P * rb, (size_t)L.g.H * rb,
-                                        (size_t)depth, hipMemcpyDeviceToDevice, c->s));
+                                        (size_t)depth, hipMemcpyDeviceToDevice, st));
     }
-    HIP_TRY(c, hipEventRecord(c->lb_ev2, c->s));  // my pulls are done here
+    HIP_TRY(c, hipEventRecord(c->lb_ev2, st));  // my pulls are done here
     if (!g->barrier()) return lb_fail(c);
     for (int nb : {r - 1, r + 1})  // neighbours may overwrite their planes only after my pull
-        if (nb >= 0 && nb < c->o.world) HIP_TRY(c, hipStreamWaitEvent(c->s, g->ranks[nb]->lb_ev2, 0));
+        if (nb >= 0 && nb < c->o.world) HIP_TRY(c, hipStreamWaitEvent(st, g->ranks[nb]->lb_ev2, 0));
     return MGP_OK;
 }
 
@@ -391,13 +397,16 @@ int lb_allreduce(mgp_ctx* c, double* v, int n = 1)
 // colour 0 / 1: only that colour's half of each plane (depth pairs of H reals), for readers that never
 // look at the other colour (a red/black sweep reads only black cells of its input: the red ones are
 // overwritten before they are read), halving the bytes.
-int exchange_buf(mgp_ctx* c, Level& L, char* buf, int depth = 1, int colour = -1)
+// st: the stream the exchange runs on (nullptr: the compute stream; the side stream xs must already wait
+// for the compute stream's last write of buf's boundary planes; the loopback transport records that itself)
+int exchange_buf(mgp_ctx* c, Level& L, char* buf, int depth = 1, int colour = -1, hipStream_t st = nullptr)
 {
+    if (!st) st = c->s;
     if (depth > c->G || depth > L.g.nz)
         return c->fail(MGP_ERR_STATE, "internal: exchange depth %d (ghost %d, slab %d)", depth, c->G, (int)L.g.nz);
     if (c->group_stop && c->group_stop->load()) return c->fail(MGP_ERR_STATE, "group aborted: another rank failed");
     ++L.exchanges;
-    if (c->lb) return lb_exchange(c, (int)(&L - c->lev.data()), buf, depth, colour);
+    if (c->lb) return lb_exchange(c, (int)(&L - c->lev.data()), buf, depth, colour, st);
     const size_t rb = (size_t)c->rb;
     const size_t coff = colour < 0 ? 0 : (size_t)(colour * L.g.H) * rb;
     auto at = [&](int64_t k) { return buf + (size_t)((k + c->G) * L.g.P) * rb + coff; };
@@ -407,12 +416,12 @@ int exchange_buf(mgp_ctx* c, Level& L, char* buf, int depth = 1, int colour = -1
     ncclResult_t r = ncclGroupStart();
     for (int i = 0; i < msgs && r == ncclSuccess; ++i) {
         if (c->o.rank > 0) {
-            r = ncclSend(at(i), cnt, c->nccl_real(), c->o.rank - 1, c->comm, c->s);
-            if (r == ncclSuccess) r = ncclRecv(at(i - depth), cnt, c->nccl_real(), c->o.rank - 1, c->comm, c->s);
+            r = ncclSend(at(i), cnt, c->nccl_real(), c->o.rank - 1, c->comm, st);
+            if (r == ncclSuccess) r = ncclRecv(at(i - depth), cnt, c->nccl_real(), c->o.rank - 1, c->comm, st);
         }
         if (c->o.rank < c->o.world - 1 && r == ncclSuccess) {
-            r = ncclSend(at(L.g.nz - depth + i), cnt, c->nccl_real(), c->o.rank + 1, c->comm, c->s);
-            if (r == ncclSuccess) r = ncclRecv(at(L.g.nz + i), cnt, c->nccl_real(), c->o.rank + 1, c->comm, c->s);
+            r = ncclSend(at(L.g.nz - depth + i), cnt, c->nccl_real(), c->o.rank + 1, c->comm, st);
+            if (r == ncclSuccess) r = ncclRecv(at(L.g.nz + i), cnt, c->nccl_real(), c->o.rank + 1, c->comm, st);
         }
     }
     const ncclResult_t e = ncclGroupEnd();  // always closes the group, also after a failed call
@@ -745,6 +754,24 @@ int materialize_zero(mgp_ctx* c, Level& L)
 
 double level_h(const mgp_ctx* c, int level) { return std::ldexp(1.0 / (double)c->lev[0].p.nx, level); }
 
+// The black u planes a temporally blocked POST on slab level l reads from its z-neighbours are final once
+// PRE has run (the coarse levels never touch them), so they go out on the side stream xs at once and the
+// transfer overlaps the coarse levels; fused_post then only waits for x_ev1.  Every rank issues it at the
+// same point of the cycle, so the RCCL (and loopback) call order is the same on all ranks.
+int early_exchange_post(mgp_ctx* c, int l)
+{
+    Level& L = c->lev[l];
+    if (!c->early_x || !c->xs || !L.p.dist) return MGP_OK;
+    if (!c->lb) {  // RCCL: xs waits for PRE (the loopback transport records the compute stream itself)
+        HIP_TRY(c, hipEventRecord(c->x_ev0, c->s));
+        HIP_TRY(c, hipStreamWaitEvent(c->xs, c->x_ev0, 0));
+    }
+    TRY(exchange_buf(c, L, L.u, mgp::kZsHaloPost, 1, c->xs));
+    HIP_TRY(c, hipEventRecord(c->x_ev1, c->xs));
+    L.early_u = true;
+    return MGP_OK;
+}
+
 // smooth(l, nu1) + residual_restrict(l) as one temporally blocked pass: u -> t, R -> f of l+1
 int fused_pre(mgp_ctx* c, int l, double h)
 {
@@ -792,7 +819,12 @@ int fused_post(mgp_ctx* c, int l, double h, bool want_err)
     Level& L = c->lev[l];
     Level& C = c->lev[l + 1];
     if (L.p.dist) {  // kZsHaloPost planes of u and f, kZsHaloCoarse coarse planes of V
-        TRY(exchange_buf(c, L, L.u, mgp::kZsHaloPost, 1));
+        if (L.early_u) {  // exchanged on xs after PRE (early_exchange_post)
+            HIP_TRY(c, hipStreamWaitEvent(c->s, c->x_ev1, 0));
+            L.early_u = false;
+        } else {
+            TRY(exchange_buf(c, L, L.u, mgp::kZsHaloPost, 1));
+        }
         if (!L.fghost_ok) TRY(exchange_buf(c, L, L.f, mgp::kZsHaloPost));
         L.fghost_ok = true;
         if (C.p.dist) TRY(exchange_buf(c, C, C.u, mgp::kZsHaloCoarse));
@@ -1063,6 +1095,7 @@ int cycle_rec(mgp_ctx* c, int l, double h, bool fcycle)
     std::optional<Range> pre_range(std::in_place, "L%d pre-smooth + restrict", l);
     if (fused) {
         TRY(fused_pre(c, l, h));
+        TRY(early_exchange_post(c, l));
     } else if (blk) {
         TRY(block_pre(c, l, h));
     } else {
@@ -1368,6 +1401,10 @@ static void destroy_impl(mgp_ctx* c)
     }
     if (c->lb_ev) (void)hipEventDestroy(c->lb_ev);
     if (c->lb_ev2) (void)hipEventDestroy(c->lb_ev2);
+    if (c->xs) (void)hipStreamSynchronize(c->xs);
+    if (c->x_ev0) (void)hipEventDestroy(c->x_ev0);
+    if (c->x_ev1) (void)hipEventDestroy(c->x_ev1);
+    if (c->xs) (void)hipStreamDestroy(c->xs);
     if (c->lb_red) (void)hipFree(c->lb_red);
     if (c->d_metrics) (void)hipFree(c->d_metrics);
     if (c->d_rn) (void)hipFree(c->d_rn);
@@ -1604,6 +1641,16 @@ static int create_impl(mgp_ctx** out, const mgp_opts* o, mgp_loopback* lb, ncclC
     if (he != hipSuccess) {
         c->err = std::string("hipFuncSetAttribute (dynamic LDS): ") + hipGetErrorString(he);
         return bail(MGP_ERR_HIP);
+    }
+    if (c->o.world > 1) {  // side stream of the early POST halo exchange
+        const char* v = std::getenv("MGP_EARLY_X");
+        if (v && std::atoi(v) == 0) c->early_x = false;
+        if (c->early_x && (hipStreamCreateWithFlags(&c->xs, hipStreamNonBlocking) != hipSuccess ||
+                           hipEventCreateWithFlags(&c->x_ev0, hipEventDisableTiming) != hipSuccess ||
+                           hipEventCreateWithFlags(&c->x_ev1, hipEventDisableTiming) != hipSuccess)) {
+            c->err = "exchange stream setup failed";
+            return bail(MGP_ERR_HIP);
+        }
     }
     if (c->o.world > 1 && lb) {
         c->lb = lb;

@@ -26,6 +26,7 @@
 
 #include <cstdlib>
 #include <type_traits>
+#include <utility>
 
 namespace mgp {
 namespace {
@@ -1636,6 +1637,21 @@ __device__ __forceinline__ void lds_barrier()
 #ifndef ZS_NPRE_F32
 #define ZS_NPRE_F32 4
 #endif
+// Row-parity-uniform waves (ZS_PSPLIT, see ZsShape) and x-edge operands read raw at the extended tile's
+// outer groups (ZS_XRAW: those cells lie in the halo that every stage shrinks by one cell, so their
+// values never reach an owned cell and need no zeroing select)
+#ifndef ZS_PSPLIT
+#define ZS_PSPLIT 0
+#endif
+#ifndef ZS_PSPLIT_PRE
+#define ZS_PSPLIT_PRE ZS_PSPLIT
+#endif
+#ifndef ZS_PSPLIT_POST
+#define ZS_PSPLIT_POST ZS_PSPLIT
+#endif
+#ifndef ZS_XRAW
+#define ZS_XRAW 1
+#endif
 #ifndef ZS_NPOST_F32
 #define ZS_NPOST_F32 2
 #endif
@@ -1707,7 +1723,12 @@ struct ZsShape {
     static constexpr int HXG = HX / 2 / N;             // halo groups per side
     static constexpr int YE = TY + 2 * H;
     static constexpr int NT = G * YE;                  // threads with a column
-    static constexpr int NTL = (NT + 63) / 64 * 64;    // launched threads
+    // ZS_PSPLIT: the even extended rows in waves [0, NPAR / 64), the odd ones in the waves after them, so
+    // that a wave's row parity is uniform and steady steps know every cell's colour at compile time
+    static constexpr int YEV = (YE + 1) / 2;           // even extended rows
+    static constexpr int NPAR = (G * YEV + 63) / 64 * 64;
+    static constexpr bool PS = PRE ? ZS_PSPLIT_PRE != 0 : ZS_PSPLIT_POST != 0;
+    static constexpr int NTL = PS ? 2 * NPAR : (NT + 63) / 64 * 64;  // launched threads
     static constexpr int SLOT = YE * HWE;              // reals per LDS slot (one colour of a plane)
     // stage-3 slots: PRE's residual reads 2 back (3 needed; 4 while LDS allows: power-of-2 ring)
     static constexpr int NS3 = PRE ? (TY > 32 ? 3 : 4) : 2;
@@ -1775,8 +1796,8 @@ __device__ __forceinline__ void zs_nb_load(ZsNb<T, N>& nb, const T* s_in, const 
     nb.yr = vload<T, N>(s_in + c.lyp);
     // whole neighbouring groups (conflict-free), of which one cell each is used
     const Vec<T, N> l = vload_lds_whole<T, N>(s_in + c.lxm), r = vload_lds_whole<T, N>(s_in + c.lxp);
-    nb.ep = c.x_first ? (T)0 : l.v[N - 1];
-    nb.en = c.x_last ? (T)0 : r.v[0];
+    nb.ep = (c.x_first && !ZS_XRAW) ? (T)0 : l.v[N - 1];
+    nb.en = (c.x_last && !ZS_XRAW) ? (T)0 : r.v[0];
 }
 
 // xl + xr of my N cells of x parity o (IEEE addition commutes, so the pair sums are shared
@@ -2002,6 +2023,25 @@ __device__ __forceinline__ void block_partial_t(double acc, double* partials)
 #ifndef ZS_WPE_PRE
 #define ZS_WPE_PRE 2
 #endif
+// Prefetch distance in planes: step p issues the loads of plane p + PFD into one of PFD + 1 register
+// buffers (the loop unrolls lcm(PFD + 1, 4) steps, so every buffer and ring index is static)
+#ifndef ZS_PFD_PRE
+#define ZS_PFD_PRE 1
+#endif
+#ifndef ZS_PFD_POST
+#define ZS_PFD_POST 1
+#endif
+template <typename F, int... K>
+__device__ __forceinline__ void zs_unroll_impl(F& f, std::integer_sequence<int, K...>)
+{
+    (f(std::integral_constant<int, K>()), ...);
+}
+// f(integral_constant<int, k>) for k = 0 .. U - 1, in order
+template <int U, typename F>
+__device__ __forceinline__ void zs_unroll(F&& f)
+{
+    zs_unroll_impl(f, std::make_integer_sequence<int, U>());
+}
 #ifndef ZS_BQ
 #define ZS_BQ 1  // POST: per-thread cache of the coarse planes' y-interpolation (zs_bq)
 #endif
@@ -2023,6 +2063,8 @@ __attribute__((amdgpu_waves_per_eu(1, PRE ? ZS_WPE_PRE : ZS_WPE_POST))) void k_z
     constexpr bool RR = PRE && LINEAR == 0;
     using VT = Vec<T, N>;
     using PF = ZsPrefetch<T, N>;
+    constexpr int PFD = PRE ? ZS_PFD_PRE : ZS_PFD_POST, NPF = PFD + 1, UNR = NPF == 3 ? 12 : 4;
+    static_assert(PFD >= 1 && PFD <= 3, "prefetch distance 1..3");
     extern __shared__ __align__(16) unsigned char zs_smem[];
     T* const lds = reinterpret_cast<T*>(zs_smem);
     const int tid = threadIdx.x;
@@ -2037,15 +2079,20 @@ __attribute__((amdgpu_waves_per_eu(1, PRE ? ZS_WPE_PRE : ZS_WPE_POST))) void k_z
     const int64_t P = g.P;
     const int qlo = -gz, qhi = (int)g.nz - 1 + gz;  // readable local planes
 
-    // my column of the extended tile
-    const bool on = tid < S::NT;
-    const int gx = on ? tid % G : 0, ye = on ? tid / G : 0;
+    // my column of the extended tile; ZS_PSPLIT: wcls = my wave's row parity (even / odd extended rows)
+    const int wcls = S::PS ? __builtin_amdgcn_readfirstlane(tid >= S::NPAR ? 1 : 0) : 0;
+    const int rt_ = S::PS ? tid - wcls * S::NPAR : tid;
+    const bool on = S::PS ? rt_ < G * (wcls ? YE / 2 : S::YEV) : tid < S::NT;
+    const int gx = on ? rt_ % G : 0, ye = S::PS ? (on ? 2 * (rt_ / G) + wcls : wcls) : (on ? tid / G : 0);
     const int gy = Y0 - H + ye;
     const int m0 = gx * N;
     ZsCol col;
-    col.lrow = ye * HWE + m0;
-    col.lym = (ye > 0 ? ye - 1 : ye) * HWE + m0;
-    col.lyp = (ye < YE - 1 ? ye + 1 : ye) * HWE + m0;
+    // LDS row of extended row y: ZS_PSPLIT stores the even rows first, then the odd ones, so that the rows
+    // of one wave stay contiguous in LDS (conflict-free vector reads)
+    auto lr = [&](int y) { return S::PS ? (y & 1) * S::YEV + (y >> 1) : y; };
+    col.lrow = lr(ye) * HWE + m0;
+    col.lym = lr(ye > 0 ? ye - 1 : ye) * HWE + m0;
+    col.lyp = lr(ye < YE - 1 ? ye + 1 : ye) * HWE + m0;
     col.gm = (X0 - S::HX) / 2 + m0;  // global packed m of my first cell
     col.x_first = gx == 0;
     col.x_last = gx == G - 1;
@@ -2082,7 +2129,6 @@ __attribute__((amdgpu_waves_per_eu(1, PRE ? ZS_WPE_PRE : ZS_WPE_POST))) void k_z
         return CLZ ? 0 : (gy == 0) + (gy == g.ny - 1) + (z0 + q == 0) + (z0 + q == gnz - 1);
     };
     const int rowpar = (gy + z0) & 1;
-    auto par = [&](int q) { return rowpar ^ (q & 1); };
     const T* const src_black = src + Hh;
 
     for (int i = tid; i < (int)(S::lds_bytes / sizeof(T)); i += NTL) lds[i] = (T)0;
@@ -2177,7 +2223,7 @@ __attribute__((amdgpu_waves_per_eu(1, PRE ? ZS_WPE_PRE : ZS_WPE_POST))) void k_z
 #pragma unroll
     for (int e = 0; e < N; ++e) acc[e] = (T)0;
     double err = 0.0, err1 = 0.0;
-    const bool even_row = (gy & 1) == 0;
+    const bool even_row_l = (gy & 1) == 0;
     T* const xbase = lds + S::OFFX + (((ye + (H & 1)) >> 1) * G + gx) * 2 * N;
     auto xs = [&](int q) { return xbase + (q & 1) * (S::XPAIRS * G * 2 * N); };
 
@@ -2196,17 +2242,25 @@ __attribute__((amdgpu_waves_per_eu(1, PRE ? ZS_WPE_PRE : ZS_WPE_POST))) void k_z
     int bq_Jn = (cgy & 1) ? bq_J + 1 : bq_J - 1;
     const bool bq_oy = !PRE && (bq_Jn < 0 || bq_Jn >= gc.ny);
     if (bq_oy) bq_Jn = bq_J;
-    auto bq_fill = [&](T (&bq)[2][N], int K) {
+    auto bq_fill = [&](auto rp, T (&bq)[2][N], int K) {
+        constexpr int RP = decltype(rp)::value;  // static row parity (>= 0) or runtime (-1)
+        const int cp = RP >= 0 ? RP : (cgy & 1);
         T c0[N + 2], c1[N + 2];
         crow(K, bq_J, c0);
         crow(K, bq_Jn, c1);
 #pragma unroll
         for (int q = 0; q < 2; ++q)
-            zs_bq<T, N>(bq[q], c0, c1, q ^ (cgy & 1), cgm, gc.nx, bq_oy, clc, corr_fast);
+            zs_bq<T, N>(bq[q], c0, c1, q ^ cp, cgm, gc.nx, bq_oy, clc, corr_fast);
     };
-    auto step = [&](auto st, auto rt, const PF& cur, PF& nxt, int p) {
+    auto step = [&](auto st, auto rt, auto rp, const PF& cur, PF& nxt, int p) __attribute__((always_inline)) {
         constexpr bool ST = decltype(st)::value;
         constexpr int RS = decltype(rt)::value;  // (p - zlo) & 3
+        // RP >= 0: my wave's row parity rowpar, known statically (ZS_PSPLIT steady steps: z0 and Y0 even, so
+        // it is also the parity of gy); -1: per lane
+        constexpr int RP = decltype(rp)::value;
+        static_assert(RP < 0 || ST, "static row parity in steady steps only");
+        auto par = [&](int q) { return RP >= 0 ? ((RP ^ q) & 1) : (rowpar ^ (q & 1)); };
+        const bool even_row = RP >= 0 ? RP == 0 : even_row_l;
         // ring slot of plane p - k
         auto sl = [](int k) constexpr { return (RS - k) & 3; };
         // steady: Z0 even, so p's parity is zlo's plus RS
@@ -2227,7 +2281,7 @@ __attribute__((amdgpu_waves_per_eu(1, PRE ? ZS_WPE_PRE : ZS_WPE_POST))) void k_z
         // POST: the coarse plane cur's prefetch loaded (first read one step on; the slot it replaces
         // was last read three steps back)
         if (!PRE && ((zz0 + p) & 1) == 0) cstore(cur, ((zz0 + p) >> 1) + 1);
-        if (ST || p + 1 <= p_end) prefetch(st, nxt, p + 1);
+        if (ST || p + PFD <= p_end) prefetch(st, nxt, p + PFD);
 
         // Every LDS read of a step hits a slot filled in the previous step (the writes come after
         // the stages), so the compiler may schedule them as early as registers allow.
@@ -2238,7 +2292,7 @@ __attribute__((amdgpu_waves_per_eu(1, PRE ? ZS_WPE_PRE : ZS_WPE_POST))) void k_z
         if constexpr (!PRE && ST && LINEAR == 1 && ZS_BQ) {
             // (z0 + Z0) % 4 == 0 in steady steps: K & 1 and p & 1 are static
             constexpr int KS = (RS >> 1) & 1, Q = 1 ^ (RS & 1);
-            if constexpr ((RS & 1) != 0) bq_fill(BQ[KS ^ 1], ((zz0 + p) >> 1) + 1);
+            if constexpr ((RS & 1) != 0) bq_fill(rp, BQ[KS ^ 1], ((zz0 + p) >> 1) + 1);
             const T w0 = (T)0.75, w1 = (T)0.25;
 #pragma unroll
             for (int e = 0; e < N; ++e) a0.v[e] = a0.v[e] + (w0 * BQ[KS][Q][e] + w1 * BQ[KS ^ 1][Q][e]);
@@ -2387,59 +2441,61 @@ __attribute__((amdgpu_waves_per_eu(1, PRE ? ZS_WPE_PRE : ZS_WPE_POST))) void k_z
 
     const std::false_type GEN;
     const std::true_type STY;
-    PF pa, pb;
+    PF pb[NPF];
     if (!PRE) {  // the coarse planes the first fine plane needs
         const int K = (z0 + zlo) >> 1;
         for (int k = K - 1; k <= K + 1; ++k) {
-            cload(pa, k);
-            cstore(pa, k);
+            cload(pb[0], k);
+            cstore(pb[0], k);
         }
         __syncthreads();
     }
-    prefetch(GEN, pa, zlo);
+#pragma unroll
+    for (int k = 0; k < PFD; ++k) prefetch(GEN, pb[k], zlo + k);
     // steady steps [ps, pe]: stages inside the box (z0 + p - 5 >= 0, z0 + p < gnz), the stored plane
     // and PRE's residual plane inside the chunk, the prefetched planes (p + 1 .. p - 3) readable
     int ps = Z0 + 6, pe = Z0 + zc + 3;
     ps = ps > 5 - z0 ? ps : 5 - z0;
     ps = ps > qlo + 3 ? ps : qlo + 3;
     pe = pe < gnz - (PRE ? 1 : 2) - z0 ? pe : gnz - (PRE ? 1 : 2) - z0;  // POST: Kn inside the coarse box
-    pe = pe < qhi - 1 ? pe : qhi - 1;
-    pe = pe < p_end - 1 ? pe : p_end - 1;
-    ps += (zlo - ps) & 3;              // whole groups of four steps in the prologue
-    pe -= (pe - ps + 1) & 3;           // and in the steady part
+    pe = pe < qhi - PFD ? pe : qhi - PFD;
+    pe = pe < p_end - PFD ? pe : p_end - PFD;
+    ps += (UNR - (ps - zlo) % UNR) % UNR;  // whole groups of UNR steps in the prologue
+    pe -= (pe - ps + 1) % UNR;             // and in the steady part
     // no steady part (the epilogue takes all) without a whole group or with odd z0 / Z0 (static parity)
     // POST with the BQ cache: (z0 + Z0) % 4 == 0 as well (static parity of the coarse plane)
     if (pe < ps || ((z0 | Z0) & 1) || (!PRE && LINEAR == 1 && ZS_BQ && ((z0 + Z0) & 3))) ps = pe = zlo - 1;
     int p = zlo;
-    const std::integral_constant<int, 0> R0;
-    const std::integral_constant<int, 1> R1;
-    const std::integral_constant<int, 2> R2;
-    const std::integral_constant<int, 3> R3;
-    for (; p < ps; p += 4) {
-        step(GEN, R0, pa, pb, p);
-        step(GEN, R1, pb, pa, p + 1);
-        step(GEN, R2, pa, pb, p + 2);
-        step(GEN, R3, pb, pa, p + 3);
-    }
-    if constexpr (!PRE && LINEAR == 1 && ZS_BQ) {
-        if (p <= pe) {  // the first steady step (even, K & 1 == 0) reads coarse planes K and K - 1
-            const int K = (z0 + p) >> 1;
-            bq_fill(BQ[0], K);
-            bq_fill(BQ[1], K - 1);
+    const std::integral_constant<int, -1> RPL;
+    // UNR steps from p0 (p0 - zlo a multiple of UNR): ring slot k & 3, buffers k % NPF and (k + PFD) % NPF;
+    // steps past plim are skipped (epilogue)
+    auto group = [&](auto st, auto rp, int p0, int plim) __attribute__((always_inline)) {
+        zs_unroll<UNR>([&](auto kk) __attribute__((always_inline)) {
+            constexpr int k = decltype(kk)::value;
+            if (k == 0 || p0 + k <= plim)
+                step(st, std::integral_constant<int, (k & 3)>(), rp, pb[k % NPF], pb[(k + PFD) % NPF], p0 + k);
+        });
+    };
+    for (; p < ps; p += UNR) group(GEN, RPL, p, p + UNR);
+    auto steady = [&](auto rp) __attribute__((always_inline)) {
+        if constexpr (!PRE && LINEAR == 1 && ZS_BQ) {
+            if (p <= pe) {  // the first steady step (even, K & 1 == 0) reads coarse planes K and K - 1
+                const int K = (z0 + p) >> 1;
+                bq_fill(rp, BQ[0], K);
+                bq_fill(rp, BQ[1], K - 1);
+            }
         }
+        for (; p <= pe; p += UNR) group(STY, rp, p, p + UNR);
+    };
+    if constexpr (S::PS) {  // wave-uniform: one copy of the steady loop per row parity
+        if (((H + wcls) & 1) == 0)
+            steady(std::integral_constant<int, 0>());
+        else
+            steady(std::integral_constant<int, 1>());
+    } else {
+        steady(RPL);
     }
-    for (; p <= pe; p += 4) {
-        step(STY, R0, pa, pb, p);
-        step(STY, R1, pb, pa, p + 1);
-        step(STY, R2, pa, pb, p + 2);
-        step(STY, R3, pb, pa, p + 3);
-    }
-    for (; p <= p_end; p += 4) {
-        step(GEN, R0, pa, pb, p);
-        if (p + 1 <= p_end) step(GEN, R1, pb, pa, p + 1);
-        if (p + 2 <= p_end) step(GEN, R2, pa, pb, p + 2);
-        if (p + 3 <= p_end) step(GEN, R3, pb, pa, p + 3);
-    }
+    for (; p <= p_end; p += UNR) group(GEN, RPL, p, p_end);
     if (ERR) block_partial_t<NTL>(err + err1, partials);
 }
 

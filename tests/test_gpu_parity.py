@@ -466,6 +466,28 @@ def _loopback_run(box, world, gather, cfg, cycles=2):
     return np.concatenate([out[r][0] for r in range(world)], axis=0), [out[r][1] for r in range(world)], out[0][2]
 
 
+@pytest.mark.parametrize("world,real,cycle", [(2, "float", "V"), (4, "double", "F"), (8, "float", "V")])
+def test_early_post_exchange_loopback(world, real, cycle, monkeypatch):
+    """The u halo of a temporally blocked POST on slab levels goes out on the side stream right after PRE
+    (overlapping the coarse levels) instead of just before POST.  Same exchanges, same psi bit for bit as the
+    exchange-before-POST schedule (MGP_EARLY_X=0) and as the single domain."""
+    box, gather = (64, 64, 256), 4096
+    cfg = dict(real=real, smoother="rbgs", nu1=2, nu2=2, prolong="linear", coarse_bc="consistent", cycle=cycle)
+    monkeypatch.setenv("MGP_FUSED", "1")
+    monkeypatch.setenv("MGP_FUSED_MIN_CELLS", "65536")
+    monkeypatch.setenv("MGP_EARLY_X", "1")
+    psi_e, ex_e, dist = _loopback_run(box, world, gather, cfg, cycles=3)
+    monkeypatch.setenv("MGP_EARLY_X", "0")
+    psi_l, ex_l, _ = _loopback_run(box, world, gather, cfg, cycles=3)
+    assert dist[0]
+    assert np.array_equal(psi_e, psi_l)
+    assert ex_e == ex_l
+    ref = _ctx(dim=3, n=box, gather_cells=gather, **cfg)
+    ref.init_point_charge()
+    ref.cycles(3)
+    assert np.array_equal(psi_e, ref.get_psi())
+
+
 @pytest.mark.parametrize("world,real", [(2, "float"), (4, "double")])
 def test_deep_halo_smoothing_loopback(world, real, monkeypatch):
     """Deep-halo RB-GS on distributed levels below the finest (smooth_deep): one exchange of 2 nu + 1
