@@ -190,6 +190,23 @@ struct Op {
         const T a_u = askew + dg[nb] * uc;
         return fc - a_u;
     }
+    // The diagonals of a row whose cells have nbyz y/z faces on the box boundary: off (d0, y0 = RN(1/d0)) and on
+    // (d1, y1) an x face, one table walk per row; relax(s, f, nbyz + xface) == div_rn(f - s/h^2, xface ? d1 : d0,
+    // xface ? y1 : y0) (dg[0] = adiag, ydg[0] = yadiag, and with cl = 0 every entry equals those)
+    __device__ __forceinline__ void row_diag(int nbyz, T& d0, T& y0, T& d1, T& y1) const
+    {
+        d0 = dg[0];
+        y0 = ydg[0];
+        d1 = dg[1];
+        y1 = ydg[1];
+#pragma unroll
+        for (int q = 1; q < 2 * DIM; ++q) {
+            d0 = nbyz == q ? dg[q] : d0;
+            y0 = nbyz == q ? ydg[q] : y0;
+            d1 = nbyz == q ? dg[q + 1] : d1;
+            y1 = nbyz == q ? ydg[q + 1] : y1;
+        }
+    }
     // The same two with the diagonal computed and divided by directly (the oracle's expressions):
     // the temporally blocked phases' rare boundary path, where the table selects cost registers.
     __device__ __forceinline__ T diag_direct(int nb) const
@@ -480,6 +497,8 @@ __device__ __forceinline__ void half_store(const HalfIn<T, VN<T>::n>& in, T* __r
 {
     constexpr int N = VN<T>::n;
     const int o = in.o;
+    T d0, y0, d1, y1;
+    op.row_diag(in.nbyz, d0, y0, d1, y1);
     Vec<T, N> out;
 #pragma unroll
     for (int e = 0; e < N; ++e) {
@@ -493,8 +512,8 @@ __device__ __forceinline__ void half_store(const HalfIn<T, VN<T>::n>& in, T* __r
             s = s + in.zl.v[e];
             s = s + in.zr.v[e];
         }
-        const int nb = in.nbyz + (i == 0) + (i == g.nx - 1);
-        out.v[e] = op.relax(s, in.fv.v[e], nb);
+        const bool xf = i == 0 || i == g.nx - 1;
+        out.v[e] = div_rn(in.fv.v[e] - s * op.inv_hSq, xf ? d1 : d0, xf ? y1 : y0);  // op.relax(s, f, nbyz + xf)
     }
     if (NT)
         vstore_nt<T, N>(dst + in.own, out);
@@ -630,6 +649,16 @@ __global__ __launch_bounds__(kBlock) void k_fresh(const T* __restrict__ f, T* __
     const int m0 = grp * N;
     const int64_t gk = g.z0 + k;
     const int ob = 1 ^ (int)((j + gk) & 1);  // x parity of this row's black cells (red: ob ^ 1)
+    // A row's diagonals are looked up once per row (Op::row_diag), so a cell's relax is div_rn with a select
+    // between two of them.  relax(+0, f, nb) = div_rn(f - (+0), ..) = div_rn(f, ..) exactly (f - (+0) == f).
+    struct RowDiag {
+        T d0, y0, d1, y1;
+    };
+    auto row_diag = [&](int nbyz) {
+        RowDiag r;
+        op.row_diag(nbyz, r.d0, r.y0, r.d1, r.y1);
+        return r;
+    };
     // red values of row (jj, kk) at m0 .. m0+N-1 (0 outside the box)
     auto red_row = [&](int jj, int64_t kk, Vec<T, N>& r) {
         const int64_t gkk = g.z0 + kk;
@@ -640,10 +669,12 @@ __global__ __launch_bounds__(kBlock) void k_fresh(const T* __restrict__ f, T* __
         const int orr = (int)((jj + gkk) & 1);  // x parity of red cells in that row
         const Vec<T, N> fv = vload<T, N>(f + kk * g.P + (int64_t)jj * g.hw + m0);
         const int nbyz = (jj == 0) + (jj == g.ny - 1) + (DIM == 3 ? (gkk == 0) + (gkk == g.gnz - 1) : 0);
+        const RowDiag rd = row_diag(nbyz);
 #pragma unroll
         for (int e = 0; e < N; ++e) {
             const int i = 2 * (m0 + e) + orr;
-            r.v[e] = op.relax((T)0, fv.v[e], nbyz + (i == 0) + (i == g.nx - 1));
+            const bool xf = i == 0 || i == g.nx - 1;
+            r.v[e] = div_rn(fv.v[e], xf ? rd.d1 : rd.d0, xf ? rd.y1 : rd.y0);
         }
     };
     Vec<T, N> rc, ryl, ryr, rzl, rzr;
@@ -656,15 +687,15 @@ __global__ __launch_bounds__(kBlock) void k_fresh(const T* __restrict__ f, T* __
     }
     // the red x-neighbour outside the segment: m0 - 1 (black cells at even x) or m0 + N (odd x)
     const int me = ob == 0 ? m0 - 1 : m0 + N;
+    const int nbyz = (j == 0) + (j == g.ny - 1) + (DIM == 3 ? (gk == 0) + (gk == g.gnz - 1) : 0);
     T edge = (T)0;
     if (me >= 0 && me < g.hw) {
         const int i = 2 * me + (ob ^ 1);
-        const int nbyz = (j == 0) + (j == g.ny - 1) + (DIM == 3 ? (gk == 0) + (gk == g.gnz - 1) : 0);
         edge = op.relax((T)0, f[k * g.P + (int64_t)j * g.hw + me], nbyz + (i == 0) + (i == g.nx - 1));
     }
     const int64_t own = k * g.P + (int64_t)j * g.hw + m0;
     const Vec<T, N> fb = vload<T, N>(f + own + g.H);
-    const int nbyz = (j == 0) + (j == g.ny - 1) + (DIM == 3 ? (gk == 0) + (gk == g.gnz - 1) : 0);
+    const RowDiag bd = row_diag(nbyz);
     Vec<T, N> out;
 #pragma unroll
     for (int e = 0; e < N; ++e) {
@@ -678,7 +709,8 @@ __global__ __launch_bounds__(kBlock) void k_fresh(const T* __restrict__ f, T* __
             s = s + rzl.v[e];
             s = s + rzr.v[e];
         }
-        out.v[e] = op.relax(s, fb.v[e], nbyz + (i == 0) + (i == g.nx - 1));
+        const bool xf = i == 0 || i == g.nx - 1;
+        out.v[e] = div_rn(fb.v[e] - s * op.inv_hSq, xf ? bd.d1 : bd.d0, xf ? bd.y1 : bd.y0);  // Op::relax
     }
     if (RED) vstore<T, N>(u + own, rc);
     vstore<T, N>(u + own + g.H, out);
@@ -1454,6 +1486,23 @@ struct PvRow {
             const T b1 = w0 * a01 + w1 * a11;
             return w0 * b0 + w1 * b1;
         }
+        const bool ox = (o == 0 && I0 + e == 0) || (o == 1 && I0 + e == cx - 1);
+        if (!oy && !oz) {
+            // only the x neighbour can leave the box: the general form below with fy = fz = false, i.e. the
+            // neighbour column replaced by the parent times the factor -cl (sv's s == 1 test kept)
+            const T sx = -cl;
+            auto nx_ = [&](const T (&cc)[N + 2]) {
+                return ox ? (sx == (T)1 ? cc[pe] : sx * cc[pe]) : (o ? cc[e + 2] : cc[e]);
+            };
+            const T a00 = w0 * c00[pe] + w1 * nx_(c00);
+            const T a10 = w0 * c10[pe] + w1 * nx_(c10);
+            if (DIM == 2) return w0 * a00 + w1 * a10;
+            const T a01 = w0 * c01[pe] + w1 * nx_(c01);
+            const T a11 = w0 * c11[pe] + w1 * nx_(c11);
+            const T b0 = w0 * a00 + w1 * a10;
+            const T b1 = w0 * a01 + w1 * a11;
+            return w0 * b0 + w1 * b1;
+        }
         auto sv = [&](T val, bool fx, bool fy, bool fz) {
             T s = (T)1;
             if (fx) s = -cl * s;
@@ -1461,7 +1510,6 @@ struct PvRow {
             if (fz) s = -cl * s;
             return s == (T)1 ? val : s * val;
         };
-        const bool ox = (o == 0 && I0 + e == 0) || (o == 1 && I0 + e == cx - 1);
         // neighbour column: e (o = 0) or e + 2 (o = 1); the parent when out of the box
         auto col = [&](const T (&cc)[N + 2]) { return ox ? cc[pe] : (o ? cc[e + 2] : cc[e]); };
         const T a00 = w0 * c00[pe] + w1 * sv(col(c00), ox, false, false);
@@ -1700,7 +1748,8 @@ struct ZsTile<double> {
 #ifndef ZS_NT
 #define ZS_NT 0
 #endif
-constexpr bool kZsNTL = (ZS_NT & 1) != 0, kZsNTS = (ZS_NT & 2) != 0;
+// bit 2: psiOld loads only (read once per launch: nothing else in the launch reads them)
+constexpr bool kZsNTL = (ZS_NT & 1) != 0, kZsNTS = (ZS_NT & 2) != 0, kZsNTO = (ZS_NT & 5) != 0;
 #ifndef ZS_PRE_RED_STORE  // timing experiment: PRE stores its (unread) red cells too
 #define ZS_PRE_RED_STORE 0
 #endif
@@ -2026,7 +2075,7 @@ __device__ __forceinline__ void block_partial_t(double acc, double* partials)
 // Prefetch distance in planes: step p issues the loads of plane p + PFD into one of PFD + 1 register
 // buffers (the loop unrolls lcm(PFD + 1, 4) steps, so every buffer and ring index is static)
 #ifndef ZS_PFD_PRE
-#define ZS_PFD_PRE 1
+#define ZS_PFD_PRE 2
 #endif
 #ifndef ZS_PFD_POST
 #define ZS_PFD_POST 1
@@ -2194,8 +2243,8 @@ __attribute__((amdgpu_waves_per_eu(1, PRE ? ZS_WPE_PRE : ZS_WPE_POST))) void k_z
             r.f2 = gload<T, N, kZsNTL>(f + (pP - 2 * Pz) + Hh + goff);
             if (!PRE && ERR && tile_xy) {  // psiOld of plane p - 4, for the tile's own columns only
                 const T* dp = old + (pP - 4 * Pz);
-                r.o0 = gload<T, N, kZsNTL>(dp + goff);
-                r.o1 = gload<T, N, kZsNTL>(dp + Hh + goff);
+                r.o0 = gload<T, N, kZsNTO>(dp + goff);
+                r.o1 = gload<T, N, kZsNTO>(dp + Hh + goff);
             }
         } else {
             r.u = gload<T, N, kZsNTL>(src_black + (int64_t)ZS_PLANE(pcl(p)) * P + goff);
@@ -2203,8 +2252,8 @@ __attribute__((amdgpu_waves_per_eu(1, PRE ? ZS_WPE_PRE : ZS_WPE_POST))) void k_z
             r.f2 = gload<T, N, kZsNTL>(f + (int64_t)ZS_PLANE(pcl(p - 2)) * P + Hh + goff);
             if (!PRE && ERR && tile_xy) {
                 const T* dp = old + (int64_t)pcl(p - 4) * P;
-                r.o0 = gload<T, N, kZsNTL>(dp + goff);
-                r.o1 = gload<T, N, kZsNTL>(dp + Hh + goff);
+                r.o0 = gload<T, N, kZsNTO>(dp + goff);
+                r.o1 = gload<T, N, kZsNTO>(dp + Hh + goff);
             }
         }
     };

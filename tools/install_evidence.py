@@ -1,41 +1,72 @@
 #!/usr/bin/env python3
-"""Copy the end-of-round evidence (tools/r02_final_all.sh output in gpurun_out/) into profiles/ and print
-the bench lines.  usage: tools/install_evidence.py <gpurun log of that call>"""
+"""Copy the end-of-round evidence in gpurun_out/ (tools/r03_final_tests.sh + tools/r03_final.sh) into profiles/
+under a round prefix and print the bench lines.
+
+usage: tools/install_evidence.py [prefix]   (default r03)
+
+Files: <p>_pytest_gpu.txt, <p>_pmc_traffic.json (+ pmc_traffic_current.json, read by bench.py when its source
+hash matches the build), <p>_pmc_traffic_summary.txt, <p>_kernel_stats.csv / <p>_trace_summary.txt /
+<p>_cycle_breakdown.txt (rocprofv3 --kernel-trace --stats of the default bench command), <p>_2d_* (the same for
+BASELINE configs[1]), <p>_bench.json (default bench line with PMC traffic) and one <p>_bench_*.json per config line.
+"""
 import json
+import os
 import shutil
 import subprocess
 import sys
 
 P = "profiles/"
 G = "gpurun_out/"
-shutil.copy(G + "pmc_traffic.json", P + "r02_pmc_traffic.json")
-shutil.copy(G + "pmc_traffic.json", P + "pmc_traffic_current.json")
-shutil.copy(G + "pmc_traffic.txt", P + "r02_pmc_traffic_summary.txt")
-shutil.copy(G + "prof/run_kernel_stats.csv", P + "r02_kernel_stats.csv")
+pre = sys.argv[1] if len(sys.argv) > 1 else "r03"
 
 
 def last(p):
     return [l for l in open(p) if l.startswith("{")][-1]
 
 
-open(P + "r02_bench.json", "w").write(last(G + "bench.log"))
-names = {1: "r02_bench_default20.json", 2: "r02_bench_4096x4096.json", 3: "r02_bench_f64_4096x4096.json",
-         4: "r02_bench_f64_512x512x512.json", 5: "r02_bench_2048x2048x256.json", 6: "r02_bench_4096x4096x512_F.json"}
-for i, n in names.items():
-    open(P + n, "w").write(last(G + f"bench_{i}.log"))
-log = open(sys.argv[1]).read().splitlines()
-start = [i for i, l in enumerate(log) if l.startswith("== ") and "grid=" in l][0]
-end = [i for i, l in enumerate(log) if l.startswith("[gpurun] status")][0]
-open(P + "r02_sq_counters_summary.txt", "w").write("\n".join(l for l in log[start:end] if not l.startswith("smoke")) + "\n")
-with open(P + "r02_trace_summary.txt", "w") as fh:
-    subprocess.run([sys.executable, "tools/trace_summary.py", G + "prof/run_kernel_trace.csv"], stdout=fh, check=True)
-with open(P + "r02_cycle_breakdown.txt", "w") as fh:
-    subprocess.run([sys.executable, "tools/cycle_breakdown.py", G + "prof/run_kernel_trace.csv", "8"], stdout=fh, check=True)
-for f in ["r02_bench.json"] + list(names.values()):
+def tool(args, out):
+    with open(P + out, "w") as fh:
+        subprocess.run([sys.executable] + args, stdout=fh, check=True)
+
+
+shutil.copy(G + "pmc_traffic.json", P + f"{pre}_pmc_traffic.json")
+shutil.copy(G + "pmc_traffic.json", P + "pmc_traffic_current.json")
+shutil.copy(G + "pmc_traffic.txt", P + f"{pre}_pmc_traffic_summary.txt")
+shutil.copy(G + "prof/run_kernel_stats.csv", P + f"{pre}_kernel_stats.csv")
+if os.path.exists(G + "fetch_calib.json"):
+    shutil.copy(G + "fetch_calib.json", P + f"{pre}_fetch_calib.json")
+tail = [l for l in open(G + "pytest_gpu.log").read().splitlines() if l.strip()][-1:]
+smoke = [l for l in open(G + "smoke.log").read().splitlines() if l.startswith("smoke")]
+open(P + f"{pre}_pytest_gpu.txt", "w").write("\n".join(tail + smoke) + "\n")
+tool(["tools/trace_summary.py", G + "prof/run_kernel_trace.csv"], f"{pre}_trace_summary.txt")
+tool(["tools/cycle_breakdown.py", G + "prof/run_kernel_trace.csv", "8"], f"{pre}_cycle_breakdown.txt")
+if os.path.exists(G + "prof2d/run_kernel_stats.csv"):
+    shutil.copy(G + "prof2d/run_kernel_stats.csv", P + f"{pre}_2d_kernel_stats.csv")
+    tool(["tools/trace_summary.py", G + "prof2d/run_kernel_trace.csv"], f"{pre}_2d_trace_summary.txt")
+    tool(["tools/cycle_breakdown.py", G + "prof2d/run_kernel_trace.csv", "8"], f"{pre}_2d_cycle_breakdown.txt")
+
+open(P + f"{pre}_bench.json", "w").write(last(G + "bench.log"))
+files = [f"{pre}_bench.json"]
+i = 1
+while os.path.exists(G + f"bench_{i}.log"):
+    d = json.loads(last(G + f"bench_{i}.log"))
+    c = d["config"]
+    box = "x".join(str(v) for v in c["global_box"] if v > 1)
+    tag = f"{pre}_bench_{i}_{d['dtype']}_{box}" + ("_F" if d["unit"].startswith("F") else "")
+    if "configs[0]" in c["workload"]:
+        tag += "_config0"
+    if "full-weighting" in c["workload"]:
+        tag += "_fw"
+    if d["steps"] == 20 and d["warmup"] == 5:
+        tag += "_driver20x5"
+    open(P + tag + ".json", "w").write(json.dumps(d) + "\n")
+    files.append(tag + ".json")
+    i += 1
+for f in files:
     d = json.loads(open(P + f).read())
-    r, c = d["roofline"], d["cpu_baseline"]
-    print(f, round(d["value"], 1), round(d["ms_per_step"], 3), r["kernel"][:30], round(r["achieved"]), round(r["frac"], 3),
-          r.get("traffic"), round(c["value"], 3))
-d = json.loads(open(P + "r02_bench.json").read())
-for k, v in d["level0_kernels"].items():
+    r, c = d.get("roofline", {}), d.get("cpu_baseline", {})
+    print(f, round(d["value"], 1), round(d["ms_per_step"], 4), r.get("kernel", "")[:32], round(r.get("achieved", 0)),
+          round(r.get("frac", 0), 3), r.get("traffic"), round(c.get("value", 0), 3))
+d = json.loads(open(P + f"{pre}_bench.json").read())
+for k, v in d.get("level0_kernels", {}).items():
     print(k, round(v["avg_us"], 1), round(v["achieved_GBps"]))
