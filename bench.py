@@ -57,6 +57,9 @@ def parse():
     p.add_argument("--copy-probe-mb", type=int, default=2048,
                    help="buffer size of the measured copy-bandwidth probe reported beside the roofline (0 = skip)")
     p.add_argument("--no-timing", action="store_true", help="skip the per-launch smoother events")
+    p.add_argument("--plan-only", action="store_true",
+                   help="no GPU: run the launch plumbing (process group, comm id broadcast, options) and print every "
+                        "rank's level plan (mgp_plan, host logic) after checking that the ranks' slabs tile the box")
     p.add_argument("--cpu-cycles", type=int, default=4, help="oracle cycles timed for cpu_baseline (0 = skip)")
     p.add_argument("--cpu-threads", type=int, default=0,
                    help="threads of the OpenMP cpu_baseline (0 = OMP_NUM_THREADS or all host cores)")
@@ -104,6 +107,9 @@ def main():
     cfg = dict(dim=a.dim if not a.box else 3, n=box, real=a.real, smoother=a.smoother, nu1=a.nu, nu2=a.nu, cycle=a.cycle,
                prolong=a.prolong, coarse_bc=a.coarse_bc, coarse_init="fresh", err_mode=1, device=local,
                rank=rank, world=world, comm_id=comm_id, restriction=a.restriction)
+    if a.plan_only:
+        plan_only(a, cfg, box, rank, world, dist)
+        return
     ctx = mgpoisson.Context(mgpoisson.make_opts(**cfg))
     ctx.init_point_charge()
     rb = 4 if a.real == "float" else 8
@@ -264,6 +270,43 @@ def main():
         print(json.dumps(line), flush=True)
     ctx.close()
     if world > 1:
+        dist.destroy_process_group()
+
+
+def plan_only(a, cfg, box, rank, world, dist):
+    """--plan-only: every rank computes its level plan exactly as mgp_create would (mgp_plan: slab, ghost
+    depth rules, engines), the plans are gathered over the process group, and rank 0 checks that the ranks
+    agree on the hierarchy and that the distributed levels' slabs tile the box in rank order, then prints one
+    JSON line.  Exercises the N > 1 launch path of this script without a GPU (tests/test_bench_launch.py)."""
+    import mgpoisson
+
+    mine = mgpoisson.plan(mgpoisson.make_opts(**cfg))
+    plans = [mine]
+    if world > 1:
+        plans = [None] * world
+        dist.all_gather_object(plans, mine)
+    if rank == 0:
+        nl = len(plans[0])
+        assert all(len(p) == nl for p in plans), "ranks disagree on the number of levels"
+        for l in range(nl):
+            rows = [p[l] for p in plans]
+            for key in ("nx", "ny", "nz_global", "distributed", "engine"):
+                assert len({r[key] for r in rows}) == 1, f"level {l}: ranks disagree on {key}"
+            if rows[0]["distributed"]:
+                z = 0
+                for r in rows:
+                    assert r["z0"] == z, f"level {l}: slab of rank {rows.index(r)} starts at {r['z0']}, expected {z}"
+                    z += r["nz_local"]
+                assert z == rows[0]["nz_global"], f"level {l}: slabs cover {z} of {rows[0]['nz_global']} planes"
+            else:
+                assert all(r["z0"] == 0 and r["nz_local"] == r["nz_global"] for r in rows), f"level {l}: replicated"
+        print(json.dumps({"plan_only": True, "n_gpus": world, "global_box": list(box), "levels": nl,
+                          "distributed_levels": sum(1 for r in plans[0] if r["distributed"]),
+                          "engines": [r["engine"] for r in plans[0]],
+                          "rank_slabs_level0": [[r[0]["z0"], r[0]["nz_local"]] for r in plans],
+                          "comm_id_bytes": len(cfg["comm_id"] or b"")}), flush=True)
+    if world > 1:
+        dist.barrier()
         dist.destroy_process_group()
 
 
