@@ -1009,12 +1009,13 @@ __global__ __launch_bounds__(kBlock) void k_resrestrict_s(const T* __restrict__ 
 // each fine (plane, row, colour) vector it needs exactly once into registers — planes 2K, 2K+1
 // with rows 2J-1 .. 2J+2, planes 2K-1, 2K+2 with rows 2J, 2J+1 — and keeps the reference order
 //   R = 1/8 (((((((r000 + r100) + r010) + r110) + r001) + r101) + r011) + r111).
-template <typename T, int DIM>
+// NV: coarse cells per thread (default: one 16-byte vector; 2 gives mid-size levels more threads)
+template <typename T, int DIM, int NV = VN<T>::n>
 __global__ __launch_bounds__(kBlock) void k_resrestrict(const T* __restrict__ u, const T* __restrict__ f,
                                                         T* __restrict__ R, Geo g, Geo gc, Op<T, DIM> op)
 {
-    constexpr int N = VN<T>::n;
-    constexpr int LN = N == 4 ? 2 : 1;
+    constexpr int N = NV;
+    constexpr int LN = N == 4 ? 2 : (N == 2 ? 1 : 0);
     constexpr int NZ = DIM == 3 ? 2 : 1;  // fine planes per coarse plane
     const int cy = g.ny >> 1;
     const int lgpr = (g.lx - 1) - LN;  // log2 groups of N per coarse row
@@ -1539,8 +1540,10 @@ __global__ __launch_bounds__(kBlock) void k_prolong_v(T* __restrict__ u, const T
     const int64_t it = (int64_t)b * kBlock + threadIdx.x;
     const int grp = (int)(it & ((1 << lgpr) - 1));
     const int j = (int)((it >> lgpr) & (g.ny - 1));
-    const int64_t k = DIM == 3 ? it >> (lgpr + g.ly) : 0;
-    if (k >= g.nz) return;
+    // the threads past the last item (the grid is whole workgroups) leave here in 2D as well: their j would
+    // wrap onto rows that other threads update (u += P V twice, a cross-wave race)
+    const int64_t k = it >> (lgpr + g.ly);
+    if (k >= (DIM == 3 ? (int64_t)g.nz : 1)) return;
     const int I0 = grp * N;
     PvRow<T, N, DIM, LINEAR> pv;
     pv.load(V, gc, j, k, I0);
@@ -4005,9 +4008,18 @@ static void rr_t(const void* u, const void* f, void* R, Geo g, Geo gc, double h,
         const char* v = std::getenv("MGP_RR_SCALAR_CELLS");
         return v ? std::atoll(v) : (int64_t)1 << 22;
     }();
-    if (cx >= n && (int64_t)cx * (g.ny / 2) * ncz >= scalar_below) {
+    // from MGP_RR_PAIR_CELLS coarse cells up to scalar_below: two coarse cells per thread (default off)
+    static const int64_t pair_from = [] {
+        const char* v = std::getenv("MGP_RR_PAIR_CELLS");
+        return v ? std::atoll(v) : INT64_MAX;
+    }();
+    const int64_t ccells = (int64_t)cx * (g.ny / 2) * ncz;
+    if (cx >= n && ccells >= scalar_below) {
         const int64_t items = (int64_t)(cx / n) * (g.ny / 2) * ncz;
         k_resrestrict<T, D><<<nblk(items), kBlock, 0, s>>>((const T*)u, (const T*)f, (T*)R, g, gc, op);
+    } else if (n > 2 && cx >= 2 && ccells >= pair_from) {
+        const int64_t items = (int64_t)(cx / 2) * (g.ny / 2) * ncz;
+        k_resrestrict<T, D, 2><<<nblk(items), kBlock, 0, s>>>((const T*)u, (const T*)f, (T*)R, g, gc, op);
     } else {
         const int64_t items = (int64_t)cx * (g.ny / 2) * ncz;
         k_resrestrict_s<T, D><<<nblk(items), kBlock, 0, s>>>((const T*)u, (const T*)f, (T*)R, g, gc, op);

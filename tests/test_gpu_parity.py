@@ -112,18 +112,23 @@ def test_residual_restrict_kernel(dim, n, real, level, bc):
 
 
 @pytest.mark.parametrize("prolong", ["pc", "linear"])
-@pytest.mark.parametrize("dim,n", [(2, 32), (2, 128), (3, 16), (3, 32)])
+@pytest.mark.parametrize("dim,n", [(2, 8), (2, 16), (2, 32), (2, 128), (3, 16), (3, 32)])
 @pytest.mark.parametrize("real", ["double", "float"])
 @pytest.mark.parametrize("bc", ["zero", "consistent"])
 def test_prolong_correct_kernel(prolong, dim, n, real, bc):
+    """u += P V on level 0 == the oracle.  The small 2D levels launch fewer items than one workgroup of
+    threads: the surplus threads must not repeat a row (round 3 fix: k_prolong_v let them through in 2D, and
+    a repeat in another wave adds P V twice).  Applied three times, so a repeat is seen once it happens."""
     ctx = _ctx(dim=dim, n=_n3(dim, n), real=real, prolong=prolong, coarse_bc=bc)
     u = _rand(ctx.shape(0), REAL[real], 5)
     V = _rand(ctx.shape(1), REAL[real], 6)
     ctx.set_psi(u, 0)
     ctx.set_psi(V, 1)
-    ctx.prolong_correct(0)
-    ref = prolong_correct_arr(dim, u, V, prolong, coarse_coef(bc, 1))
-    assert np.array_equal(ctx.get_psi(0), ref)
+    ref = u
+    for _ in range(3):
+        ctx.prolong_correct(0)
+        ref = prolong_correct_arr(dim, ref, V, prolong, coarse_coef(bc, 1))
+        assert np.array_equal(ctx.get_psi(0), ref)
 
 
 CYCLE_CONFIGS = [
@@ -694,6 +699,29 @@ def test_coarse_level_switch_is_exact(kw):
         runs.append((ctx.cycles(3), ctx.get_psi()))
     for e, p in runs[1:]:
         assert np.array_equal(p, runs[0][1]) and np.array_equal(e, runs[0][0])
+
+
+@pytest.mark.parametrize("real", ["double", "float"])
+def test_every_level_per_piece_matches_oracle_on_reused_memory(real):
+    """The reference cpu.lua configuration (2D 256^2 Jacobi 7+7, fresh coarse guess, err every cycle) with no
+    coarse tail (set_coarse_level(0): every level down to 1x1 one launch per piece), on device memory a previous
+    context of the same shape has just released: psi bit-identical to the oracle after every cycle.  (Round 3:
+    the 2D prolongation's surplus threads repeated rows of the 4^2 .. 16^2 levels and added P V twice.)"""
+    kw = dict(dim=2, n=(256, 256, 1), real=real)
+    warm = _ctx(**kw)
+    warm.init_point_charge()
+    warm.cycles(3)
+    warm.close()
+    ctx = _ctx(**kw)
+    ctx.set_coarse_level(0)
+    assert not any(lv["tail"] for lv in ctx.levels)
+    o = Oracle(**kw)
+    ctx.init_point_charge()
+    o.init_point_charge()
+    for it in range(4):
+        ctx.cycle()
+        o.step()
+        assert np.array_equal(ctx.get_psi(), o.get(0)), f"psi differs after cycle {it + 1}"
 
 
 @pytest.mark.parametrize("init", ["fresh", "warm"])

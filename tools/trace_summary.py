@@ -21,10 +21,10 @@ tot = sum(sum(v) for v in d.values())
 for k, v in sorted(d.items(), key=lambda kv: -sum(kv[1]))[:int(sys.argv[2]) if len(sys.argv) > 2 else 30]:
     print(f"{k[0][:46]:46s} {k[1]:>10d} {len(v):>5d} {sum(v)/len(v):9.1f} us {100*sum(v)/tot:5.1f}%")
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-# Cycles start at the finest level's PRE phase (the temporally blocked k_zs PRE); without it, at the
+# Cycles start at the finest level's PRE phase (the temporally blocked k_zs / k_ys PRE); without it, at the
 # finest-level plain half-sweep that follows a coarse-tail launch.  (Round 2 delimited by k_sum_n, which
 # k_resnorm's reduction launches too: its "per cycle" line mixed cycles and norm evaluations.)
-delim = sys.argv[3] if len(sys.argv) > 3 else r"k_zs<\w+, true"
+delim = sys.argv[3] if len(sys.argv) > 3 else r"k_(zs|ys)<\w+, true"
 starts = [i for i, r in enumerate(rows) if re.search(delim, r["Kernel_Name"])]
 if len(starts) > 6:
     a, b = starts[-6], starts[-1]
