@@ -9,18 +9,52 @@
 #include <stdlib.h>
 #include <string.h>
 
+/* gpu.lua's real = float (every operation in float) and real = double */
 #define MGO_T float
+#define MGO_C float
 #define MGO_S f
+#define MGO_ROUND_ERR 0
 #include "mgp_oracle_impl.h"
 #undef MGO_T
+#undef MGO_C
 #undef MGO_S
 #define MGO_T double
+#define MGO_C double
 #define MGO_S d
 #include "mgp_oracle_impl.h"
 #undef MGO_T
+#undef MGO_C
 #undef MGO_S
+#undef MGO_ROUND_ERR
+/* cpu-raw.lua's real = 'float': float buffers, double expressions, float errorBuf */
+#define MGO_T float
+#define MGO_C double
+#define MGO_S fd
+#define MGO_ROUND_ERR 1
+#include "mgp_oracle_impl.h"
+#undef MGO_T
+#undef MGO_C
+#undef MGO_S
+#undef MGO_ROUND_ERR
 
 #define MGO_MAX_LEVELS 40
+
+static int kind_of(int real_bytes, int arith)
+{
+    return real_bytes == 4 && arith == MGO_ARITH_DOUBLE ? MGO_REAL_F32_ARITH_F64 : real_bytes;
+}
+static size_t kind_bytes(int kind) { return kind == 8 ? 8 : 4; }
+
+#define MGO_DISPATCH(kind, CALL_D, CALL_F, CALL_FD) \
+    do {                                            \
+        if ((kind) == 8)                            \
+            CALL_D;                                 \
+        else if ((kind) == MGO_REAL_F32_ARITH_F64)  \
+            CALL_FD;                                \
+        else                                        \
+            CALL_F;                                 \
+    } while (0)
+
 
 typedef struct {
     int64_t nx, ny, nz;
@@ -32,6 +66,7 @@ typedef struct {
 
 struct mgo_ctx {
     mgo_opts o;
+    int kind; /* kind_of(real_bytes, arith) */
     int nlev;
     mgo_level lev[MGO_MAX_LEVELS];
     void* psi_old;
@@ -53,6 +88,7 @@ void mgo_opts_default(mgo_opts* o)
     o->coarse_bc = MGO_BC_ZERO;       /* ghost 0 on every level, cpu.lua:28-31 */
     o->threads = 1;
     o->restriction = MGO_RESTRICT_AVERAGE; /* cpu.lua:127-135 */
+    o->arith = MGO_ARITH_REAL;
 }
 
 static int64_t ncell(const mgo_level* L) { return L->nx * L->ny * L->nz; }
@@ -61,7 +97,8 @@ static int is_pow2(int64_t v) { return v > 0 && (v & (v - 1)) == 0; }
 
 mgo_ctx* mgo_create(const mgo_opts* o)
 {
-    if (!o || (o->dim != 2 && o->dim != 3) || (o->real_bytes != 4 && o->real_bytes != 8))
+    if (!o || (o->dim != 2 && o->dim != 3) || (o->real_bytes != 4 && o->real_bytes != 8) ||
+        (o->arith != MGO_ARITH_REAL && o->arith != MGO_ARITH_DOUBLE))
         return NULL;
     int64_t nz = o->dim == 2 ? 1 : o->nz;
     if (!is_pow2(o->nx) || !is_pow2(o->ny) || !is_pow2(nz)) return NULL;
@@ -69,6 +106,7 @@ mgo_ctx* mgo_create(const mgo_opts* o)
     c->o = *o;
     c->o.nz = nz;
     if (c->o.threads < 1) c->o.threads = 1;
+    c->kind = kind_of(o->real_bytes, o->arith);
     int64_t nx = o->nx, ny = o->ny;
     const size_t rb = (size_t)o->real_bytes;
     for (;;) {
@@ -153,51 +191,49 @@ int mgo_get_field(const mgo_ctx* c, int which, void* dst, int64_t count)
     return 0;
 }
 
-/* ---- dispatch helpers on (dims, real_bytes) ---- */
+/* ---- dispatch helpers on (dims, kind) ----
+ * kind = 8 (double), 4 (float, gpu.lua's float arithmetic) or MGO_REAL_F32_ARITH_F64 (float buffers,
+ * double arithmetic: cpu-raw.lua's real = 'float'); buffers are float for both float kinds. */
 
-static void smooth_any(int dim, int64_t nx, int64_t ny, int64_t nz, int rb, int smoother, int sweeps,
+static void smooth_any(int dim, int64_t nx, int64_t ny, int64_t nz, int kind, int smoother, int sweeps,
                        double h, double cl, void* u, const void* f, void* tmp, int threads)
 {
-    if (rb == 8)
-        smooth_d(dim, nx, ny, nz, smoother, sweeps, h, cl, (double*)u, (const double*)f, (double*)tmp, threads);
-    else
-        smooth_f(dim, nx, ny, nz, smoother, sweeps, h, cl, (float*)u, (const float*)f, (float*)tmp, threads);
+    MGO_DISPATCH(kind,
+                 smooth_d(dim, nx, ny, nz, smoother, sweeps, h, cl, (double*)u, (const double*)f, (double*)tmp, threads),
+                 smooth_f(dim, nx, ny, nz, smoother, sweeps, h, cl, (float*)u, (const float*)f, (float*)tmp, threads),
+                 smooth_fd(dim, nx, ny, nz, smoother, sweeps, h, cl, (float*)u, (const float*)f, (float*)tmp, threads));
 }
 
-static void residual_any(int dim, int64_t nx, int64_t ny, int64_t nz, int rb, double h, double cl,
+static void residual_any(int dim, int64_t nx, int64_t ny, int64_t nz, int kind, double h, double cl,
                          const void* u, const void* f, void* r, int threads)
 {
-    if (rb == 8)
-        residual_d(dim, nx, ny, nz, h, cl, (const double*)u, (const double*)f, (double*)r, threads);
-    else
-        residual_f(dim, nx, ny, nz, h, cl, (const float*)u, (const float*)f, (float*)r, threads);
+    MGO_DISPATCH(kind, residual_d(dim, nx, ny, nz, h, cl, (const double*)u, (const double*)f, (double*)r, threads),
+                 residual_f(dim, nx, ny, nz, h, cl, (const float*)u, (const float*)f, (float*)r, threads),
+                 residual_fd(dim, nx, ny, nz, h, cl, (const float*)u, (const float*)f, (float*)r, threads));
 }
 
-static void restrict_any(int dim, int64_t nx, int64_t ny, int64_t nz, int rb, const void* r, void* R,
+static void restrict_any(int dim, int64_t nx, int64_t ny, int64_t nz, int kind, const void* r, void* R,
                          int threads)
 {
-    if (rb == 8)
-        restrict__d(dim, nx, ny, nz, (const double*)r, (double*)R, threads);
-    else
-        restrict__f(dim, nx, ny, nz, (const float*)r, (float*)R, threads);
+    MGO_DISPATCH(kind, restrict__d(dim, nx, ny, nz, (const double*)r, (double*)R, threads),
+                 restrict__f(dim, nx, ny, nz, (const float*)r, (float*)R, threads),
+                 restrict__fd(dim, nx, ny, nz, (const float*)r, (float*)R, threads));
 }
 
-static void restrict_fw_any(int dim, int64_t nx, int64_t ny, int64_t nz, int rb, double clc, const void* r,
+static void restrict_fw_any(int dim, int64_t nx, int64_t ny, int64_t nz, int kind, double clc, const void* r,
                             void* R, int threads)
 {
-    if (rb == 8)
-        restrict_fw_d(dim, nx, ny, nz, clc, (const double*)r, (double*)R, threads);
-    else
-        restrict_fw_f(dim, nx, ny, nz, clc, (const float*)r, (float*)R, threads);
+    MGO_DISPATCH(kind, restrict_fw_d(dim, nx, ny, nz, clc, (const double*)r, (double*)R, threads),
+                 restrict_fw_f(dim, nx, ny, nz, clc, (const float*)r, (float*)R, threads),
+                 restrict_fw_fd(dim, nx, ny, nz, clc, (const float*)r, (float*)R, threads));
 }
 
-static void prolong_any(int dim, int64_t nx, int64_t ny, int64_t nz, int rb, int prolong, double clc,
+static void prolong_any(int dim, int64_t nx, int64_t ny, int64_t nz, int kind, int prolong, double clc,
                         void* u, const void* V, int threads)
 {
-    if (rb == 8)
-        prolong_correct_d(dim, nx, ny, nz, prolong, clc, (double*)u, (const double*)V, threads);
-    else
-        prolong_correct_f(dim, nx, ny, nz, prolong, clc, (float*)u, (const float*)V, threads);
+    MGO_DISPATCH(kind, prolong_correct_d(dim, nx, ny, nz, prolong, clc, (double*)u, (const double*)V, threads),
+                 prolong_correct_f(dim, nx, ny, nz, prolong, clc, (float*)u, (const float*)V, threads),
+                 prolong_correct_fd(dim, nx, ny, nz, prolong, clc, (float*)u, (const float*)V, threads));
 }
 
 double mgo_coarse_coef(int coarse_bc, int level)
@@ -217,7 +253,7 @@ static void coarse_solve(mgo_ctx* c, int l, double h)
     /* 1 cell: one sweep == u = (f - 0)/adiag exactly (cpu.lua:76-93, cpu-raw.lua:190-196).
      * A coarsest line/plane (non-cubic boxes, build-defined) gets coarse_sweeps sweeps. */
     int sweeps = ncell(L) == 1 ? 1 : c->o.coarse_sweeps;
-    smooth_any(c->o.dim, L->nx, L->ny, L->nz, c->o.real_bytes, c->o.smoother, sweeps, h,
+    smooth_any(c->o.dim, L->nx, L->ny, L->nz, c->kind, c->o.smoother, sweeps, h,
                mgo_coarse_coef(c->o.coarse_bc, l), L->u, L->f, L->tmp, c->o.threads);
 }
 
@@ -231,13 +267,13 @@ static void cycle_rec(mgo_ctx* c, int l, double h, int fcycle)
     }
     mgo_level* C = &c->lev[l + 1];
     const double cl = mgo_coarse_coef(o->coarse_bc, l), clc = mgo_coarse_coef(o->coarse_bc, l + 1);
-    smooth_any(o->dim, L->nx, L->ny, L->nz, o->real_bytes, o->smoother, o->nu1, h, cl, L->u, L->f,
+    smooth_any(o->dim, L->nx, L->ny, L->nz, c->kind, o->smoother, o->nu1, h, cl, L->u, L->f,
                L->tmp, o->threads);
-    residual_any(o->dim, L->nx, L->ny, L->nz, o->real_bytes, h, cl, L->u, L->f, L->r, o->threads);
+    residual_any(o->dim, L->nx, L->ny, L->nz, c->kind, h, cl, L->u, L->f, L->r, o->threads);
     if (o->restriction == MGO_RESTRICT_FULL_WEIGHTING)
-        restrict_fw_any(o->dim, L->nx, L->ny, L->nz, o->real_bytes, clc, L->r, C->f, o->threads);
+        restrict_fw_any(o->dim, L->nx, L->ny, L->nz, c->kind, clc, L->r, C->f, o->threads);
     else
-        restrict_any(o->dim, L->nx, L->ny, L->nz, o->real_bytes, L->r, C->f, o->threads);
+        restrict_any(o->dim, L->nx, L->ny, L->nz, c->kind, L->r, C->f, o->threads);
     if (o->coarse_init == MGO_COARSE_FRESH) /* V = matrix.zeros (cpu.lua:138) */
         memset(C->u, 0, (size_t)ncell(C) * (size_t)o->real_bytes);
     if (fcycle) {
@@ -246,15 +282,17 @@ static void cycle_rec(mgo_ctx* c, int l, double h, int fcycle)
     } else {
         cycle_rec(c, l + 1, 2 * h, 0); /* twoGrid(2*h, V, R) (cpu.lua:139) */
     }
-    prolong_any(o->dim, L->nx, L->ny, L->nz, o->real_bytes, o->prolong, clc, L->u, C->u, o->threads);
-    smooth_any(o->dim, L->nx, L->ny, L->nz, o->real_bytes, o->smoother, o->nu2, h, cl, L->u, L->f,
+    prolong_any(o->dim, L->nx, L->ny, L->nz, c->kind, o->prolong, clc, L->u, C->u, o->threads);
+    smooth_any(o->dim, L->nx, L->ny, L->nz, c->kind, o->smoother, o->nu2, h, cl, L->u, L->f,
                L->tmp, o->threads);
 }
 
 double mgo_err_arr(int64_t n, int real_bytes, const void* psi, const void* psi_old)
 {
-    double s = real_bytes == 8 ? sqdiff_d(n, (const double*)psi, (const double*)psi_old)
-                               : sqdiff_f(n, (const float*)psi, (const float*)psi_old);
+    double s = 0.0;
+    MGO_DISPATCH(real_bytes, s = sqdiff_d(n, (const double*)psi, (const double*)psi_old),
+                 s = sqdiff_f(n, (const float*)psi, (const float*)psi_old),
+                 s = sqdiff_fd(n, (const float*)psi, (const float*)psi_old));
     return sqrt(s / (double)n);
 }
 
@@ -265,7 +303,7 @@ double mgo_step(mgo_ctx* c)
     const size_t bytes = (size_t)ncell(L) * (size_t)c->o.real_bytes;
     memcpy(c->psi_old, L->u, bytes); /* psiOld = matrix(self.psi) (cpu.lua:200) */
     cycle_rec(c, 0, h, c->o.cycle == MGO_CYCLE_F);
-    return mgo_err_arr(ncell(L), c->o.real_bytes, L->u, c->psi_old); /* cpu.lua:203 */
+    return mgo_err_arr(ncell(L), c->kind, L->u, c->psi_old); /* cpu.lua:203, cpu-raw.lua:249-254 */
 }
 
 int mgo_solve(mgo_ctx* c, int maxiter, double epsilon, double* errs)
@@ -301,7 +339,7 @@ void mgo_smooth_arr(int dim, int64_t nx, int64_t ny, int64_t nz, int real_bytes,
                     int sweeps, double h, double cl, void* u, const void* f)
 {
     if (dim == 2) nz = 1;
-    void* tmp = malloc((size_t)(nx * ny * nz) * (size_t)real_bytes);
+    void* tmp = malloc((size_t)(nx * ny * nz) * kind_bytes(real_bytes));
     smooth_any(dim, nx, ny, nz, real_bytes, smoother, sweeps, h, cl, u, f, tmp, 1);
     free(tmp);
 }
@@ -322,8 +360,11 @@ double mgo_residual_sumsq_arr(int dim, int64_t nx, int64_t ny, int64_t nz, int r
                               const void* u, const void* f, int64_t z_lo, int64_t z_hi, int threads)
 {
     if (dim == 2) nz = 1;
-    return real_bytes == 8 ? residual_sumsq_d(dim, nx, ny, nz, h, cl, (const double*)u, (const double*)f, z_lo, z_hi, threads)
-                           : residual_sumsq_f(dim, nx, ny, nz, h, cl, (const float*)u, (const float*)f, z_lo, z_hi, threads);
+    double s = 0.0;
+    MGO_DISPATCH(real_bytes, s = residual_sumsq_d(dim, nx, ny, nz, h, cl, (const double*)u, (const double*)f, z_lo, z_hi, threads),
+                 s = residual_sumsq_f(dim, nx, ny, nz, h, cl, (const float*)u, (const float*)f, z_lo, z_hi, threads),
+                 s = residual_sumsq_fd(dim, nx, ny, nz, h, cl, (const float*)u, (const float*)f, z_lo, z_hi, threads));
+    return s;
 }
 
 void mgo_restrict_fw_arr(int dim, int64_t nx, int64_t ny, int64_t nz, int real_bytes, double cl_coarse,

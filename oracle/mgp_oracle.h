@@ -41,6 +41,14 @@ enum { MGO_PROLONG_PC = 0, MGO_PROLONG_LINEAR = 1 };
 enum { MGO_COARSE_FRESH = 0, MGO_COARSE_WARM = 1 };
 enum { MGO_BC_ZERO = 0, MGO_BC_CONSISTENT = 1 };
 enum { MGO_RESTRICT_AVERAGE = 0, MGO_RESTRICT_FULL_WEIGHTING = 1 };
+/* Arithmetic of real = float (no effect on double):
+ *   MGO_ARITH_REAL   every operation rounded to float: gpu.lua's OpenCL `real` (gpu.lua:32)
+ *   MGO_ARITH_DOUBLE float buffers, every expression in double, rounded once at the store into a
+ *                    buffer: cpu-raw.lua under real = 'float' (cpu-raw.lua:142-153; LuaJIT numbers are
+ *                    doubles), the errorBuf squares included (cpu-raw.lua:96-100, 249-254) */
+enum { MGO_ARITH_REAL = 0, MGO_ARITH_DOUBLE = 1 };
+/* real_bytes argument of the stateless *_arr kernels for float arrays with MGO_ARITH_DOUBLE */
+#define MGO_REAL_F32_ARITH_F64 12
 
 typedef struct mgo_opts {
     int dim;            /* 2 or 3 */
@@ -60,6 +68,7 @@ typedef struct mgo_opts {
     int restriction;    /* MGO_RESTRICT_AVERAGE: 2^d cell average (reference, cpu.lua:127-135)
                            MGO_RESTRICT_FULL_WEIGHTING: cell-centred full weighting, the adjoint of
                            the linear prolongation (build-defined; restrict_fw in mgp_oracle_impl.h) */
+    int arith;          /* MGO_ARITH_REAL (default) / MGO_ARITH_DOUBLE (cpu-raw.lua's real = 'float') */
 } mgo_opts;
 
 typedef struct mgo_ctx mgo_ctx;
@@ -81,7 +90,8 @@ int      mgo_solve(mgo_ctx* c, int maxiter, double epsilon, double* errs);
  * (L must be one of the hierarchy's level sizes; u is updated in place). */
 int      mgo_two_grid(mgo_ctx* c, double h, void* u, const void* f, int64_t L);
 
-/* Stateless per-level kernels on caller arrays (x fastest, dims nx,ny,nz; nz=1 in 2D). */
+/* Stateless per-level kernels on caller arrays (x fastest, dims nx,ny,nz; nz=1 in 2D).
+ * real_bytes: 8, 4, or MGO_REAL_F32_ARITH_F64 (float arrays, cpu-raw.lua's double arithmetic). */
 /* cl = the level's coarse-boundary coefficient (0 for the reference operator). */
 void mgo_smooth_arr(int dim, int64_t nx, int64_t ny, int64_t nz, int real_bytes, int smoother,
                     int sweeps, double h, double cl, void* u, const void* f);

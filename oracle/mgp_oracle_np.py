@@ -10,6 +10,11 @@ independent restatements must agree bit-for-bit in fp64 (and fp32) before either
   ``cpu.lua:76-93`` 1-cell coarse solve, ``cpu.lua:180-206`` init / step / err,
   ``cpu-raw.lua:221`` warm (persistent) coarse buffers.
 * Build-defined: 3D 7-point form, red/black GS, F-cycle, cell-centred linear prolongation.
+* ``arith="double"`` with float32 arrays: ``cpu-raw.lua`` under ``real = 'float'`` (cpu-raw.lua:142-153) —
+  float buffers read into LuaJIT numbers, so every expression is evaluated in float64 and rounded to
+  float32 once, where the reference stores into a buffer (Jacobi :34-44, calcResidual :46-57,
+  reduceResidual :59-63, expandResidual / addTo :65-85, calcFrobErr's errorBuf :96-100).  The default
+  ``arith="real"`` rounds every operation to the array type (gpu.lua's OpenCL ``real``, gpu.lua:32).
 
 Parity status: "parity unpinned" against the reference itself (no Lua runtime here, no
 reference golden vectors); pinned by known-answer tests in tests/test_oracle.py.
@@ -88,40 +93,56 @@ def color_mask(shape, z0: int = 0) -> np.ndarray:
     return ((i + j + k) & 1) == 0  # red
 
 
-def smooth(u, f, h, dim, smoother, sweeps, cl=0.0, z0=0, gnz=None):
+def _cdt(dt, arith):
+    """Type the expressions are evaluated in: float64 for float32 buffers under arith="double"."""
+    return np.dtype(np.float64) if arith == "double" else np.dtype(dt)
+
+
+def smooth(u, f, h, dim, smoother, sweeps, cl=0.0, z0=0, gnz=None, arith="real"):
     u = u.copy()
+    dt, cdt = u.dtype, _cdt(u.dtype, arith)
+    fc = f.astype(cdt)
+
+    def relax(v):  # computed in cdt, stored (rounded) in the buffer type
+        return _relax(v.astype(cdt), fc, h, dim, cl, z0, gnz).astype(dt)
+
     for _ in range(sweeps):
         if smoother == JACOBI:
-            u = _relax(u, f, h, dim, cl, z0, gnz)
+            u = relax(u)
         elif smoother == RBGS:
             red = color_mask(u.shape, z0)
-            u = np.where(red, _relax(u, f, h, dim, cl, z0, gnz), u)
-            u = np.where(~red, _relax(u, f, h, dim, cl, z0, gnz), u)
+            u = np.where(red, relax(u), u)
+            u = np.where(~red, relax(u), u)
         else:  # lexicographic, cpu.lua:26-27 order (x outer, y, z inner)
-            hsq, _ = _consts(h, dim, u.dtype)
-            dg = diag(u.shape, h, dim, u.dtype, cl, z0, gnz)
+            hsq, _ = _consts(h, dim, cdt)
+            dg = diag(u.shape, h, dim, cdt, cl, z0, gnz)
             nz, ny, nx = u.shape
-            z = u.dtype.type(0)
+            z = cdt.type(0)
+            U = lambda k, j, i: cdt.type(u[k, j, i])  # noqa: E731
             for i in range(nx):
                 for j in range(ny):
                     for k in range(nz):
-                        s = (u[k, j, i - 1] if i > 0 else z) + (u[k, j, i + 1] if i < nx - 1 else z)
-                        s = s + (u[k, j - 1, i] if j > 0 else z)
-                        s = s + (u[k, j + 1, i] if j < ny - 1 else z)
+                        s = (U(k, j, i - 1) if i > 0 else z) + (U(k, j, i + 1) if i < nx - 1 else z)
+                        s = s + (U(k, j - 1, i) if j > 0 else z)
+                        s = s + (U(k, j + 1, i) if j < ny - 1 else z)
                         if dim == 3:
-                            s = s + (u[k - 1, j, i] if k > 0 else z)
-                            s = s + (u[k + 1, j, i] if k < nz - 1 else z)
-                        u[k, j, i] = (f[k, j, i] - s / hsq) / dg[k, j, i]
+                            s = s + (U(k - 1, j, i) if k > 0 else z)
+                            s = s + (U(k + 1, j, i) if k < nz - 1 else z)
+                        u[k, j, i] = (fc[k, j, i] - s / hsq) / dg[k, j, i]
     return u
 
 
-def residual(u, f, h, dim, cl=0.0, z0=0, gnz=None):
-    hsq, _ = _consts(h, dim, u.dtype)
-    askew = _nbsum(u, dim) / hsq
-    return f - (askew + diag(u.shape, h, dim, u.dtype, cl, z0, gnz) * u)
+def residual(u, f, h, dim, cl=0.0, z0=0, gnz=None, arith="real"):
+    dt, cdt = u.dtype, _cdt(u.dtype, arith)
+    uc = u.astype(cdt)
+    hsq, _ = _consts(h, dim, cdt)
+    askew = _nbsum(uc, dim) / hsq
+    return (f.astype(cdt) - (askew + diag(u.shape, h, dim, cdt, cl, z0, gnz) * uc)).astype(dt)
 
 
-def restrict(r, dim):
+def restrict(r, dim, arith="real"):
+    if arith == "double" and r.dtype != np.float64:
+        return restrict(r.astype(np.float64), dim).astype(r.dtype)
     if dim == 2:
         s = r[:, 0::2, 0::2] + r[:, 0::2, 1::2]
         s = s + r[:, 1::2, 0::2]
@@ -137,13 +158,15 @@ def restrict(r, dim):
     return r.dtype.type(0.125) * s
 
 
-def restrict_fw(r, dim, clc=0.0):
+def restrict_fw(r, dim, clc=0.0, arith="real"):
     """Full weighting (build-defined option): the cell-centred adjoint of the linear prolongation.
 
     Per axis, coarse cell I gets fine cells 2I-1 .. 2I+2 as ((r_a + w_b r_b) + w_c r_c) + r_d with
     w = 3, or 3 - clc next to a box face (I = 0 for 2I, I = m-1 for 2I+1); fine cells outside the box
     are +0.  x, then y, then z; finally times 1/8^d (mgp_oracle_impl.h restrict_fw()).
     """
+    if arith == "double" and r.dtype != np.float64:
+        return restrict_fw(r.astype(np.float64), dim, clc).astype(r.dtype)
     dt = r.dtype.type
     w3, wf = dt(3), dt(3) - dt(clc)
     axes = (2, 1, 0) if dim == 3 else (2, 1)
@@ -174,13 +197,16 @@ def _axis_idx(n_fine, n_coarse):
     return parent, np.clip(nb, 0, n_coarse - 1), out
 
 
-def prolong(V, fine_shape, dim, kind, cl=0.0):
+def prolong(V, fine_shape, dim, kind, cl=0.0, arith="real"):
     """PC injection (cpu.lua:142-150) or cell-centred separable linear (build-defined).
 
     Linear: each coarse sample outside the box is -cl times the nearest inside value, with
     the factor built per axis in x, y, z order (mgp_oracle_impl.h cval()); then x-, y-, z-
-    interpolation with weights 3/4 (parent) and 1/4 (neighbour).
+    interpolation with weights 3/4 (parent) and 1/4 (neighbour).  The result is in V's type (the
+    reference's real buffer vs[L], cpu-raw.lua:226).
     """
+    if arith == "double" and V.dtype != np.float64:
+        return prolong(V.astype(np.float64), fine_shape, dim, kind, cl).astype(V.dtype)
     nz, ny, nx = fine_shape
     if kind == PROLONG_PC:
         v = np.repeat(np.repeat(V, 2, axis=2), 2, axis=1)
@@ -220,6 +246,22 @@ def prolong(V, fine_shape, dim, kind, cl=0.0):
     return w0 * b0 + w1 * b1
 
 
+def add_to(u, v, arith="real"):
+    """addTo u + v (cpu-raw.lua:83-85), evaluated in the compute type and stored in u's type."""
+    cdt = _cdt(u.dtype, arith)
+    return (u.astype(cdt) + v.astype(cdt)).astype(u.dtype)
+
+
+def err_sum(psi, old, arith="real"):
+    """sum (psi - psiOld)^2 in float64 (cpu.lua:203); arith="double": each square first stored in the
+    float errorBuf (cpu-raw.lua:96-100, 249-253)."""
+    d = psi.astype(np.float64) - old.astype(np.float64)
+    sq = d * d
+    if arith == "double" and psi.dtype != np.float64:
+        sq = sq.astype(psi.dtype).astype(np.float64)
+    return float(np.sum(sq))
+
+
 def coarse_coef(coarse_bc: int, level: int) -> float:
     """c_l of MGO_BC_CONSISTENT: (2^l - 1)/(2^l + 1); 0 on level 0 and for the reference."""
     if coarse_bc != BC_CONSISTENT or level <= 0:
@@ -233,7 +275,7 @@ class Multigrid:
 
     def __init__(self, dim=2, n=(8, 8, 1), dtype=np.float64, nu1=7, nu2=7, smoother=JACOBI,
                  cycle=CYCLE_V, prolong_kind=PROLONG_PC, coarse_init=COARSE_FRESH,
-                 coarse_sweeps=48, coarse_bc=BC_ZERO, restriction=RESTRICT_AVERAGE):
+                 coarse_sweeps=48, coarse_bc=BC_ZERO, restriction=RESTRICT_AVERAGE, arith="real"):
         nx, ny, nz = n
         if dim == 2:
             nz = 1
@@ -242,6 +284,7 @@ class Multigrid:
         self.prolong_kind, self.coarse_init, self.coarse_sweeps = prolong_kind, coarse_init, coarse_sweeps
         self.coarse_bc = coarse_bc
         self.restriction = restriction
+        self.arith = arith
         shapes = []
         s = (nz, ny, nx)
         while True:
@@ -264,29 +307,30 @@ class Multigrid:
 
     def _cycle(self, l, u, f, h, fcycle):
         cl = coarse_coef(self.coarse_bc, l)
+        ar = self.arith
         if l == len(self.shapes) - 1:
             sweeps = 1 if u.size == 1 else self.coarse_sweeps
-            return smooth(u, f, h, self.dim, self.smoother, sweeps, cl)
-        u = smooth(u, f, h, self.dim, self.smoother, self.nu1, cl)
-        r = residual(u, f, h, self.dim, cl)
+            return smooth(u, f, h, self.dim, self.smoother, sweeps, cl, arith=ar)
+        u = smooth(u, f, h, self.dim, self.smoother, self.nu1, cl, arith=ar)
+        r = residual(u, f, h, self.dim, cl, arith=ar)
         if self.restriction == RESTRICT_FULL_WEIGHTING:
-            R = restrict_fw(r, self.dim, coarse_coef(self.coarse_bc, l + 1))
+            R = restrict_fw(r, self.dim, coarse_coef(self.coarse_bc, l + 1), arith=ar)
         else:
-            R = restrict(r, self.dim)
+            R = restrict(r, self.dim, arith=ar)
         V = np.zeros_like(R) if self.coarse_init == COARSE_FRESH else self.V[l + 1]
         if fcycle:
             V = self._cycle(l + 1, V, R, 2 * h, True)
         V = self._cycle(l + 1, V, R, 2 * h, False)
         self.V[l + 1] = V
-        u = u + prolong(V, u.shape, self.dim, self.prolong_kind, coarse_coef(self.coarse_bc, l + 1))
-        return smooth(u, f, h, self.dim, self.smoother, self.nu2, cl)
+        u = add_to(u, prolong(V, u.shape, self.dim, self.prolong_kind, coarse_coef(self.coarse_bc, l + 1), arith=ar),
+                   arith=ar)
+        return smooth(u, f, h, self.dim, self.smoother, self.nu2, cl, arith=ar)
 
     def step(self) -> float:
         h = 1.0 / self.shapes[0][2]
         old = self.psi.copy()
         self.psi = self._cycle(0, self.psi, self.f, h, self.cycle == CYCLE_F)
-        d = self.psi.astype(np.float64) - old.astype(np.float64)
-        return float(np.sqrt(np.sum(d * d) / d.size))
+        return float(np.sqrt(err_sum(self.psi, old, self.arith) / self.psi.size))
 
 
 def dst_exact(f: np.ndarray, h: float, dim: int) -> np.ndarray:

@@ -4,7 +4,7 @@
  *
  * Every option of mgo_opts on small boxes (2D / 3D, cubic and non-cubic, fp32 / fp64, Jacobi / red-black /
  * lexicographic GS, V / F, injection / linear prolongation, fresh / warm coarse guess, both coarse boundary
- * conditions, both restrictions, 1 and 2 OpenMP threads) for a few outer iterations, plus the stateless
+ * conditions, both restrictions, 1 and 2 OpenMP threads, fp32 with cpu-raw.lua's double arithmetic) for a few outer iterations, plus the stateless
  * per-level functions and cpu-raw's twoGrid entry (mgo_two_grid).  Any out-of-bounds access, leak-free
  * misuse or undefined arithmetic aborts the run with a sanitizer report; success prints "sanitize ok".
  */
@@ -24,7 +24,8 @@ static int run_case(int dim, int64_t nx, int64_t ny, int64_t nz, int rb, int smo
     o.nx = nx;
     o.ny = ny;
     o.nz = dim == 3 ? nz : 1;
-    o.real_bytes = rb;
+    o.real_bytes = rb == MGO_REAL_F32_ARITH_F64 ? 4 : rb;
+    o.arith = rb == MGO_REAL_F32_ARITH_F64 ? MGO_ARITH_DOUBLE : MGO_ARITH_REAL;
     o.nu1 = o.nu2 = 2;
     o.smoother = smoother;
     o.cycle = cycle;
@@ -42,7 +43,7 @@ static int run_case(int dim, int64_t nx, int64_t ny, int64_t nz, int rb, int smo
     double errs[3];
     mgo_solve(c, 3, 0.0, errs);
     const int64_t n = nx * ny * o.nz;
-    void* psi = malloc((size_t)n * rb);
+    void* psi = malloc((size_t)n * o.real_bytes);
     mgo_get_field(c, 0, psi, n);
     mgo_set_field(c, 0, psi, n);
     const double e = mgo_step(c);
@@ -54,10 +55,11 @@ static int run_case(int dim, int64_t nx, int64_t ny, int64_t nz, int rb, int smo
 static int run_arrays(int dim, int64_t n, int rb)
 {
     const int64_t nz = dim == 3 ? n : 1, cells = n * n * nz, coarse = cells >> dim;
-    void* u = calloc((size_t)cells, rb);
-    void* f = calloc((size_t)cells, rb);
-    void* r = calloc((size_t)cells, rb);
-    void* R = calloc((size_t)coarse, rb);
+    const size_t eb = rb == 8 ? 8 : 4;
+    void* u = calloc((size_t)cells, eb);
+    void* f = calloc((size_t)cells, eb);
+    void* r = calloc((size_t)cells, eb);
+    void* R = calloc((size_t)coarse, eb);
     for (int64_t i = 0; i < cells; ++i) {
         const double v = sin(0.37 * (double)i);
         if (rb == 8) ((double*)f)[i] = v, ((double*)u)[i] = 0.5 * v;
@@ -82,12 +84,13 @@ static int run_two_grid(int rb)
     o.dim = 2;
     o.nx = o.ny = 32;
     o.nz = 1;
-    o.real_bytes = rb;
+    o.real_bytes = rb == 8 ? 8 : 4;
+    o.arith = rb == MGO_REAL_F32_ARITH_F64 ? MGO_ARITH_DOUBLE : MGO_ARITH_REAL;
     mgo_ctx* c = mgo_create(&o);
     if (!c) return 4;
     const int64_t L = 16, n = L * L;
-    void* u = calloc((size_t)n, rb);
-    void* f = calloc((size_t)n, rb);
+    void* u = calloc((size_t)n, o.real_bytes);
+    void* f = calloc((size_t)n, o.real_bytes);
     if (rb == 8) ((double*)f)[n / 2 + L / 2] = -1e6;
     else ((float*)f)[n / 2 + L / 2] = -1e6f;
     const int rc = mgo_two_grid(c, 1.0 / (double)L, u, f, L);
@@ -103,7 +106,7 @@ int main(void)
     };
     int fails = 0, cases = 0;
     for (size_t b = 0; b < sizeof(boxes) / sizeof(boxes[0]); ++b)
-        for (int rb = 4; rb <= 8; rb += 4)
+        for (int rb = 4; rb <= MGO_REAL_F32_ARITH_F64; rb += 4)
             for (int sm = 0; sm < 3; ++sm)
                 for (int v = 0; v < 16; ++v) {
                     const int cycle = v & 1, prolong = (v >> 1) & 1, init = (v >> 2) & 1, bc = (v >> 3) & 1;
@@ -114,7 +117,7 @@ int main(void)
                     fails += rc != 0;
                     ++cases;
                 }
-    for (int rb = 4; rb <= 8; rb += 4) {
+    for (int rb = 4; rb <= MGO_REAL_F32_ARITH_F64; rb += 4) {
         fails += run_arrays(2, 16, rb) != 0;
         fails += run_arrays(3, 8, rb) != 0;
         fails += run_two_grid(rb) != 0;

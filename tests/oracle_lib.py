@@ -21,6 +21,10 @@ PROLONGS = {"pc": 0, "linear": 1}
 INITS = {"fresh": 0, "warm": 1}
 BCS = {"zero": 0, "consistent": 1}
 RESTRICTIONS = {"average": 0, "full_weighting": 1}
+# real = float arithmetic: "real" = every operation in float (gpu.lua:32), "double" = float buffers with
+# every expression in double (cpu-raw.lua's real = 'float', LuaJIT numbers)
+ARITHS = {"real": 0, "double": 1}
+F32_ARITH_F64 = 12  # real_bytes code of the stateless *_arr kernels for float arrays + double arithmetic
 
 
 class Opts(ctypes.Structure):
@@ -28,7 +32,7 @@ class Opts(ctypes.Structure):
                 ("real_bytes", ctypes.c_int), ("nu1", ctypes.c_int), ("nu2", ctypes.c_int),
                 ("smoother", ctypes.c_int), ("cycle", ctypes.c_int), ("prolong", ctypes.c_int),
                 ("coarse_init", ctypes.c_int), ("coarse_sweeps", ctypes.c_int), ("coarse_bc", ctypes.c_int),
-                ("threads", ctypes.c_int), ("restriction", ctypes.c_int)]
+                ("threads", ctypes.c_int), ("restriction", ctypes.c_int), ("arith", ctypes.c_int)]
 
 
 def _load():
@@ -70,7 +74,7 @@ class Oracle:
 
     def __init__(self, dim=2, n=(8, 8, 1), real="double", nu1=7, nu2=7, smoother="jacobi", cycle="V",
                  prolong="pc", coarse_init="fresh", coarse_bc="zero", coarse_sweeps=48, threads=1,
-                 restriction="average"):
+                 restriction="average", arith="real"):
         o = Opts()
         lib.mgo_opts_default(ctypes.byref(o))
         nn = tuple(n) + (1,) * (3 - len(n))
@@ -80,6 +84,7 @@ class Oracle:
         o.smoother, o.cycle, o.prolong = SMOOTHERS[smoother], CYCLES[cycle], PROLONGS[prolong]
         o.coarse_init, o.coarse_bc, o.coarse_sweeps, o.threads = INITS[coarse_init], BCS[coarse_bc], coarse_sweeps, threads
         o.restriction = RESTRICTIONS[restriction]
+        o.arith = ARITHS[arith]
         self.o = o
         self.dtype = np.dtype(np.float64 if o.real_bytes == 8 else np.float32)
         self.shape = (o.nz, o.ny, o.nx) if dim == 3 else (o.ny, o.nx)
@@ -107,43 +112,56 @@ class Oracle:
     def step(self):
         return lib.mgo_step(self.h)
 
+    def two_grid(self, h, u, f, size):
+        """cpu-raw.lua:186 twoGrid(h, u, f, L) on host arrays of one level's size; u updated in place."""
+        assert u.flags.c_contiguous and u.dtype == self.dtype
+        fc = np.ascontiguousarray(f, self.dtype)
+        assert lib.mgo_two_grid(self.h, h, u.ctypes.data, fc.ctypes.data, int(size)) == 0
+
     def levels(self):
         return lib.mgo_num_levels(self.h)
 
 
-def smooth_arr(dim, u, f, smoother, sweeps, h, cl=0.0):
+def _kind(a, arith):
+    """real_bytes code of the stateless kernels: the element size, or F32_ARITH_F64 for float arrays with
+    cpu-raw.lua's double arithmetic."""
+    return F32_ARITH_F64 if (arith == "double" and a.itemsize == 4) else a.itemsize
+
+
+def smooth_arr(dim, u, f, smoother, sweeps, h, cl=0.0, arith="real"):
     u = np.ascontiguousarray(u).copy()
     f = np.ascontiguousarray(f, u.dtype)
     nz, ny, nx = (u.shape if dim == 3 else (1,) + u.shape)
-    lib.mgo_smooth_arr(dim, nx, ny, nz, u.itemsize, SMOOTHERS[smoother], sweeps, h, cl, u.ctypes.data, f.ctypes.data)
+    lib.mgo_smooth_arr(dim, nx, ny, nz, _kind(u, arith), SMOOTHERS[smoother], sweeps, h, cl, u.ctypes.data,
+                       f.ctypes.data)
     return u
 
 
-def residual_arr(dim, u, f, h, cl=0.0):
+def residual_arr(dim, u, f, h, cl=0.0, arith="real"):
     u = np.ascontiguousarray(u)
     f = np.ascontiguousarray(f, u.dtype)
     r = np.empty_like(u)
     nz, ny, nx = (u.shape if dim == 3 else (1,) + u.shape)
-    lib.mgo_residual_arr(dim, nx, ny, nz, u.itemsize, h, cl, u.ctypes.data, f.ctypes.data, r.ctypes.data)
+    lib.mgo_residual_arr(dim, nx, ny, nz, _kind(u, arith), h, cl, u.ctypes.data, f.ctypes.data, r.ctypes.data)
     return r
 
 
-def residual_sumsq_arr(dim, u, f, h, cl=0.0, z_lo=0, z_hi=None, threads=1):
+def residual_sumsq_arr(dim, u, f, h, cl=0.0, z_lo=0, z_hi=None, threads=1, arith="real"):
     """sum of (f - A u)^2 (fp64) over planes [z_lo, z_hi) of a 3D (nz, ny, nx) array; its ends are the ghost."""
     u = np.ascontiguousarray(u)
     f = np.ascontiguousarray(f, u.dtype)
     nz, ny, nx = (u.shape if dim == 3 else (1,) + u.shape)
     z_hi = nz if z_hi is None else z_hi
-    return lib.mgo_residual_sumsq_arr(dim, nx, ny, nz, u.itemsize, h, cl, u.ctypes.data, f.ctypes.data, z_lo, z_hi,
-                                      threads)
+    return lib.mgo_residual_sumsq_arr(dim, nx, ny, nz, _kind(u, arith), h, cl, u.ctypes.data, f.ctypes.data, z_lo,
+                                      z_hi, threads)
 
 
-def restrict_arr(dim, r):
+def restrict_arr(dim, r, arith="real"):
     r = np.ascontiguousarray(r)
     shp = tuple(s // 2 for s in r.shape)
     R = np.empty(shp, r.dtype)
     nz, ny, nx = (r.shape if dim == 3 else (1,) + r.shape)
-    lib.mgo_restrict_arr(dim, nx, ny, nz, r.itemsize, r.ctypes.data, R.ctypes.data)
+    lib.mgo_restrict_arr(dim, nx, ny, nz, _kind(r, arith), r.ctypes.data, R.ctypes.data)
     return R
 
 
@@ -157,12 +175,20 @@ def restrict_fw_arr(dim, r, cl_coarse=0.0):
     return R
 
 
-def prolong_correct_arr(dim, u, V, prolong, cl_coarse=0.0):
+def prolong_correct_arr(dim, u, V, prolong, cl_coarse=0.0, arith="real"):
     u = np.ascontiguousarray(u).copy()
     V = np.ascontiguousarray(V, u.dtype)
     nz, ny, nx = (u.shape if dim == 3 else (1,) + u.shape)
-    lib.mgo_prolong_correct_arr(dim, nx, ny, nz, u.itemsize, PROLONGS[prolong], cl_coarse, u.ctypes.data, V.ctypes.data)
+    lib.mgo_prolong_correct_arr(dim, nx, ny, nz, _kind(u, arith), PROLONGS[prolong], cl_coarse, u.ctypes.data,
+                                V.ctypes.data)
     return u
+
+
+def err_arr(psi, old, arith="real"):
+    """sqrt(sum (psi - psiOld)^2 / N) as the oracle's step() computes it (cpu.lua:203, cpu-raw.lua:249-254)."""
+    a = np.ascontiguousarray(psi)
+    b = np.ascontiguousarray(old, a.dtype)
+    return lib.mgo_err_arr(a.size, _kind(a, arith), a.ctypes.data, b.ctypes.data)
 
 
 def coarse_coef(bc, level):

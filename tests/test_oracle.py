@@ -26,7 +26,8 @@ def _np_model(cfg):
                        codes["smoother"][cfg.get("smoother", "jacobi")], codes["cycle"][cfg.get("cycle", "V")],
                        codes["prolong"][cfg.get("prolong", "pc")], codes["coarse_init"][cfg.get("coarse_init", "fresh")],
                        coarse_bc=codes["coarse_bc"][cfg.get("coarse_bc", "zero")],
-                       restriction={"average": 0, "full_weighting": 1}[cfg.get("restriction", "average")])
+                       restriction={"average": 0, "full_weighting": 1}[cfg.get("restriction", "average")],
+                       arith=cfg.get("arith", "real"))
 
 
 CROSS = [
@@ -46,6 +47,15 @@ CROSS = [
     dict(dim=3, n=(8, 8, 16), smoother="rbgs", nu1=2, nu2=2, cycle="F", prolong="linear", coarse_bc="consistent",
          restriction="full_weighting"),
     dict(dim=3, n=(8, 8, 8), smoother="rbgs", nu1=2, nu2=2, prolong="linear", real="float", restriction="full_weighting"),
+    # cpu-raw.lua's real = 'float' (float buffers, double expressions, float errorBuf)
+    dict(dim=2, n=(16, 16, 1), real="float", arith="double", coarse_init="warm"),
+    dict(dim=2, n=(32, 32, 1), real="float", arith="double"),
+    dict(dim=2, n=(16, 8, 1), real="float", arith="double", smoother="rbgs", nu1=2, nu2=2, prolong="linear",
+         coarse_bc="consistent", cycle="F"),
+    dict(dim=2, n=(8, 8, 1), real="float", arith="double", smoother="gs_lex", nu1=2, nu2=2),
+    dict(dim=3, n=(8, 8, 16), real="float", arith="double", smoother="rbgs", nu1=2, nu2=2, prolong="linear",
+         coarse_bc="consistent", restriction="full_weighting"),
+    dict(dim=3, n=(8, 8, 8), real="float", arith="double", smoother="jacobi", prolong="pc"),
 ]
 
 
@@ -286,3 +296,53 @@ def test_full_weighting_rescues_the_zero_boundary_v_cycle():
     ef = [f.step() for _ in range(14)]
     assert ea[-1] > ea[-2]
     assert ef[-1] < 0.9 * ef[-2] and ef[-1] < 1e-2 * ef[0]
+
+
+# ---- cpu-raw.lua's real = 'float' (arith="double"): float buffers, double expressions ----
+
+def test_cpu_raw_float_differs_from_gpu_lua_float():
+    """The two reference fp32 semantics disagree: gpu.lua rounds every operation to float (gpu.lua:32),
+    cpu-raw.lua evaluates in LuaJIT doubles and rounds at each store (cpu-raw.lua:34-63).  Both stay within
+    fp32 accuracy of the fp64 run."""
+    kw = dict(dim=2, n=(64, 64, 1), coarse_init="warm")
+    a, b, d = Oracle(real="float", **kw), Oracle(real="float", arith="double", **kw), Oracle(real="double", **kw)
+    for o in (a, b, d):
+        o.init_point_charge()
+        o.step()
+        o.step()
+    pa, pb, pd = a.get(0).astype(np.float64), b.get(0).astype(np.float64), d.get(0)
+    assert not np.array_equal(pa, pb)
+    for p in (pa, pb):
+        assert np.linalg.norm(p - pd) <= 1e-5 * np.linalg.norm(pd)
+
+
+def test_cpu_raw_float_pieces_round_once():
+    """Per piece, arith="double" equals the fp64 expression rounded once to float (cpu-raw.lua:34-85)."""
+    from oracle_lib import err_arr
+    rng = np.random.default_rng(11)
+    u = rng.standard_normal((16, 16)).astype(np.float32)
+    f = rng.standard_normal((16, 16)).astype(np.float32)
+    h = 1 / 16
+    assert np.array_equal(smooth_arr(2, u, f, "jacobi", 1, h, arith="double"),
+                          smooth_arr(2, u.astype(np.float64), f.astype(np.float64), "jacobi", 1, h).astype(np.float32))
+    r = residual_arr(2, u, f, h, arith="double")
+    assert np.array_equal(r, residual_arr(2, u.astype(np.float64), f.astype(np.float64), h).astype(np.float32))
+    assert np.array_equal(restrict_arr(2, r, arith="double"),
+                          restrict_arr(2, r.astype(np.float64)).astype(np.float32))
+    V = rng.standard_normal((8, 8)).astype(np.float32)
+    assert np.array_equal(prolong_correct_arr(2, u, V, "pc", arith="double"), prolong_correct_arr(2, u, V, "pc"))
+    # errorBuf is a float image: each square rounded to float before the double sum (cpu-raw.lua:249-253)
+    d = u.astype(np.float64) - f.astype(np.float64)
+    ref = np.sqrt(sum(float(np.float32(x)) for x in (d * d).ravel()) / d.size)
+    assert err_arr(u, f, arith="double") == pytest.approx(ref, rel=1e-15)
+    assert err_arr(u, f, arith="double") != err_arr(u, f)
+
+
+def test_cpu_raw_float_first_sweep_closed_form():
+    """SURVEY §8c KAT 2 holds for cpu-raw's float run too: the first Jacobi sweep values are exact floats."""
+    n, h = 8, 1.0 / 8
+    o = Oracle(dim=2, n=(n, n, 1), real="float", arith="double")
+    o.init_point_charge()
+    u = smooth_arr(2, o.get(0), o.get(1), "jacobi", 1, h, arith="double")
+    c = n // 2
+    assert u[c, c] == np.float32(3906.25) and u[c, c + 1] == np.float32(2.5e5)
