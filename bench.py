@@ -21,6 +21,16 @@ and --box 4096,4096,512 run one rank's slab of those configs.  value = cycles/s 
 ghost-0 coarse levels), with the CPU port timed over the same cycles (1 thread and OpenMP) beside the GPU.
 --restriction full_weighting: the build's full-weighting option instead of the 2^d cell average.
 
+With N >= 4 ranks the default (weak) run adds the north-star workloads to the same JSON line
+(`north_star_lines`): BASELINE configs[3] (2048^3 V-cycle) and configs[4] (4096^3 F-cycle) as one box split
+into N z-slabs, each run after the previous context is closed, with per-rank halo-exchange and collective
+time from HIP events (--no-north-star skips them; configs[4] is skipped where it does not fit the ranks' HBM).
+
+Roofline fields: `roofline.frac` is the dominant level-0 kernel's algorithmic (compulsory) bytes over its
+event-timed duration against 8 TB/s; `roofline.cycle_frac` the compulsory bytes of every level of one cycle
+ over ms_per_step against 8 TB/s; `finest_smoother_GBps` BASELINE.md's definition
+3 sizeof(real) cells_per_rank sweeps / summed finest-level smoothing kernel time.
+
 Launch: python bench.py [--gpus N --steps K --warmup W]  (N>1 under torch.distributed.run).
 """
 from __future__ import annotations
@@ -59,7 +69,13 @@ def parse():
     p.add_argument("--no-timing", action="store_true", help="skip the per-launch smoother events")
     p.add_argument("--plan-only", action="store_true",
                    help="no GPU: run the launch plumbing (process group, comm id broadcast, options) and print every "
-                        "rank's level plan (mgp_plan, host logic) after checking that the ranks' slabs tile the box")
+                        "rank's level plan (mgp_plan, host logic) after checking that the ranks' slabs tile the box, "
+                        "with each workload's per-cycle RCCL calls and bytes per rank (mgp_plan_comm)")
+    p.add_argument("--no-north-star", action="store_true",
+                   help="with N >= 4: skip the configs[3] / configs[4] lines after the weak-scaling line")
+    p.add_argument("--ns-steps", type=int, default=5, help="timed cycles of each north-star line")
+    p.add_argument("--ns-warmup", type=int, default=2, help="untimed cycles of each north-star line")
+    p.add_argument("--cpu-reps", type=int, default=3, help="cpu_baseline: best of this many timed samples")
     p.add_argument("--cpu-cycles", type=int, default=4, help="oracle cycles timed for cpu_baseline (0 = skip)")
     p.add_argument("--cpu-threads", type=int, default=0,
                    help="threads of the OpenMP cpu_baseline (0 = OMP_NUM_THREADS or all host cores)")
@@ -72,6 +88,10 @@ def parse():
     return a
 
 
+NORTH_STAR = [("configs[3]", (2048, 2048, 2048), "V", "BASELINE configs[3]: 3D Poisson 2048^3"),
+              ("configs[4]", (4096, 4096, 4096), "F", "BASELINE configs[4]: 3D Poisson 4096^3 fp32 F-cycle")]
+
+
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -80,36 +100,121 @@ def main():
     if world != a.gpus:
         if world == 1 and a.gpus > 1:
             raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run (one rank per GPU)")
-    import torch
     import torch.distributed as dist
 
-    import mgpoisson
-
-    comm_id = None
     if world > 1:
         dist.init_process_group(backend="gloo")
-        obj = [mgpoisson.comm_unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(obj, src=0)
-        comm_id = obj[0]
 
+    box, strong = workload_box(a, world)
+    cfg = make_cfg(a, box, rank, world, local, new_comm_id(dist, rank, world))
+    if a.plan_only:
+        plan_only(a, cfg, box, rank, world, dist)
+        return
+    line = run_workload(a, cfg, box, strong, rank, world, local, dist, a.steps, a.warmup, primary=True)
+    if want_north_star(a, world):
+        extra = {}
+        for name, nbox, cyc, _ in NORTH_STAR:
+            if nbox[2] % world or nbox[2] // world < 2:
+                continue
+            ns = argparse.Namespace(**vars(a))
+            ns.cycle, ns.box = cyc, ",".join(map(str, nbox))
+            ncfg = make_cfg(ns, nbox, rank, world, local, new_comm_id(dist, rank, world))
+            fit = fits_hbm(ncfg, world, local)
+            if fit is None:
+                extra[name] = {"skipped": f"does not fit {world} x HBM (u, f, t and the hierarchy)"}
+                continue
+            with env_override(fit):
+                sub = run_workload(ns, ncfg, nbox, True, rank, world, local, dist, a.ns_steps, a.ns_warmup)
+            if rank == 0:
+                extra[name] = {k: sub.get(k) for k in ("value", "unit", "ms_per_step", "steps", "warmup", "config",
+                                                       "final_err", "relative_residual", "hbm_used_GB_rank0",
+                                                       "roofline", "comm_per_rank", "finest_smoother_GBps")}
+                if fit:
+                    extra[name]["env"] = fit
+        if rank == 0:
+            line["north_star_lines"] = extra
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def want_north_star(a, world):
+    return world >= 4 and not a.box and a.dim == 3 and not a.config0 and not a.no_north_star
+
+
+def new_comm_id(dist, rank, world):
+    """A fresh RCCL unique id from rank 0 for every context (an id serves one communicator)."""
+    if world == 1:
+        return None
+    import mgpoisson
+
+    obj = [mgpoisson.comm_unique_id() if rank == 0 else None]
+    dist.broadcast_object_list(obj, src=0)
+    return obj[0]
+
+
+def workload_box(a, world):
     n = a.n
     if a.box:
         box = tuple(int(x) for x in a.box.split(","))
         if len(box) != 3:
             raise SystemExit("--box takes NX,NY,NZ")
-        strong = True
-    elif a.dim == 2:
+        return box, True
+    if a.dim == 2:
         if world != 1:
             raise SystemExit("2D runs are single-GPU (the slab decomposition is 3D)")
-        box, strong = (n, n, 1), False
-    else:
-        box, strong = (n, n, n * world), False
-    cfg = dict(dim=a.dim if not a.box else 3, n=box, real=a.real, smoother=a.smoother, nu1=a.nu, nu2=a.nu, cycle=a.cycle,
-               prolong=a.prolong, coarse_bc=a.coarse_bc, coarse_init="fresh", err_mode=1, device=local,
-               rank=rank, world=world, comm_id=comm_id, restriction=a.restriction)
-    if a.plan_only:
-        plan_only(a, cfg, box, rank, world, dist)
-        return
+        return (n, n, 1), False
+    return (n, n, n * world), False
+
+
+def make_cfg(a, box, rank, world, local, comm_id):
+    return dict(dim=a.dim if not a.box else 3, n=box, real=a.real, smoother=a.smoother, nu1=a.nu, nu2=a.nu,
+                cycle=a.cycle, prolong=a.prolong, coarse_bc=a.coarse_bc, coarse_init="fresh", err_mode=1, device=local,
+                rank=rank, world=world, comm_id=comm_id, restriction=a.restriction)
+
+
+def fits_hbm(cfg, world, local):
+    """{} if the context fits this GPU's HBM as built, {"MGP_KEEP_PSI_OLD": "0"} if it fits only without the
+    psiOld-keeping output buffer (u, f, t and the hierarchy), None if not even then."""
+    import torch
+
+    rb = 4 if cfg["real"] == "float" else 8
+    cells = cfg["n"][0] * cfg["n"][1] * cfg["n"][2] / world
+    total = torch.cuda.get_device_properties(local).total_memory
+    est = lambda arrays: cells * rb * arrays * 8 / 7 + (2 << 30)  # noqa: E731
+    if est(4) < 0.92 * total:
+        return {}
+    if est(3) < 0.92 * total:
+        return {"MGP_KEEP_PSI_OLD": "0"}
+    return None
+
+
+class env_override:
+    def __init__(self, env):
+        self.env, self.old = env or {}, {}
+
+    def __enter__(self):
+        for k, v in self.env.items():
+            self.old[k] = os.environ.get(k)
+            os.environ[k] = v
+
+    def __exit__(self, *exc):
+        for k, v in self.old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
+def run_workload(a, cfg, box, strong, rank, world, local, dist, steps, warmup, primary=False):
+    """One workload: K timed cycles (hipGraph replay on one GPU), then the same K again with event timing; returns
+    the bench line (meaningful on rank 0)."""
+    import torch
+
+    import mgpoisson
+
+    n = a.n
     ctx = mgpoisson.Context(mgpoisson.make_opts(**cfg))
     ctx.init_point_charge()
     rb = 4 if a.real == "float" else 8
@@ -124,34 +229,39 @@ def main():
             dist.barrier()
 
     # warmup (untimed; also captures the hipGraphs of the cycle)
-    if a.warmup:
-        ctx.cycles(a.warmup)
+    if warmup:
+        ctx.cycles(warmup)
     barrier_sync()
     t0 = time.perf_counter()
-    errs = ctx.cycles(a.steps)
+    errs = ctx.cycles(steps)
     barrier_sync()
     dt = time.perf_counter() - t0
 
     # roofline window: the same K cycles again, launched eagerly with a HIP event pair around
-    # every timed level-0 launch on the context's stream (graph replay cannot bracket single
-    # launches); the kernels are identical, only the host launch path differs
+    # every timed level-0 launch and every exchange / collective on the stream it runs on (graph replay cannot
+    # bracket single launches); the kernels are identical, only the host launch path differs
     timed = {}
     if not a.no_timing:
         ctx.timing(True)
-        ctx.cycles(a.steps)
+        ctx.cycles(steps)
         timed = ctx.timing_read()
         ctx.timing(False)
         barrier_sync()
 
     copy_peak = None
-    if a.copy_probe_mb > 0 and local == 0 and rank == 0:
+    if primary and a.copy_probe_mb > 0 and local == 0 and rank == 0:
         copy_peak = mgpoisson.copy_bandwidth(local, a.copy_probe_mb << 20, 10)
     if world > 1:
         t = torch.tensor([dt], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
+    comm = {k: timed.get(k, (0.0, 0, 0.0)) for k in ("exchange", "collective")}
+    comm_all = [comm]
+    if world > 1:
+        comm_all = [None] * world
+        dist.all_gather_object(comm_all, comm)
 
-    value = (1 if strong else world) * a.steps / dt
+    value = (1 if strong else world) * steps / dt
     kind = "V" if a.cycle == "V" else "F"
     gcells = box[0] * box[1] * box[2]
     sm = "RB-GS" if a.smoother == "rbgs" else "Jacobi"
@@ -161,8 +271,7 @@ def main():
     bc = "consistent coarse boundary" if a.coarse_bc == "consistent" else "ghost-0 coarse boundary"
     algo = f"{sm} {a.nu}+{a.nu}, {kind}-cycle, {pr}, {rs}, {bc}, per-cycle RMS-update err"
     if strong:
-        named = {(2048, 2048, 2048): "BASELINE configs[3]: 3D Poisson 2048^3",
-                 (4096, 4096, 4096): "BASELINE configs[4]: 3D Poisson 4096^3 fp32 F-cycle"}
+        named = {nb: label for _, nb, _, label in NORTH_STAR}
         slab = {(2048, 2048, 256): "one rank's slab of BASELINE configs[3] (2048^3 / 8 ranks)",
                 (4096, 4096, 512): "one rank's slab of BASELINE configs[4] (4096^3 / 8 ranks)"}
         wl = named.get(box) or (slab.get(box) if world == 1 else None) or f"3D Poisson {box[0]}x{box[1]}x{box[2]}"
@@ -181,14 +290,15 @@ def main():
         workload = f"{tag}3D Poisson {n}^3 per GPU, 7-point, {algo}"
         unit = f"{kind}-cycles/s ({n}^3-cell slabs, whole job)"
     rnorm, fnorm = ctx.residual_norm()
+    ms_step = 1e3 * dt / steps
     line = {
         "metric": "V-cycles/sec + finest-smoother achieved HBM GB/s, 3D Poisson",
         "value": value,
         "unit": unit,
         "n_gpus": world,
-        "steps": a.steps,
-        "warmup": a.warmup,
-        "ms_per_step": 1e3 * dt / a.steps,
+        "steps": steps,
+        "warmup": warmup,
+        "ms_per_step": ms_step,
         "higher_is_better": True,
         "scaling": "strong" if strong else "weak",
         "vs_baseline": None,
@@ -205,6 +315,14 @@ def main():
         "relative_residual": rnorm / fnorm,
         "hbm_used_GB_rank0": (total_b - free_b) / 1e9,
     }
+    if world > 1:
+        # per rank and cycle: halo exchanges (grouped send/recv, either stream) and the all-gather / err all-reduce,
+        # HIP-event time on the stream they run on (includes waiting for the neighbour), and what the rank sends
+        line["comm_per_rank"] = [
+            {"exchange_ms_per_cycle": r["exchange"][0] / steps, "exchanges_per_cycle": r["exchange"][1] / steps,
+             "exchange_MB_sent_per_cycle": r["exchange"][2] / steps / 1e6,
+             "collective_ms_per_cycle": r["collective"][0] / steps,
+             "collectives_per_cycle": r["collective"][1] / steps} for r in comm_all]
     tname = "float" if a.real == "float" else "double"
     lin = 1 if a.prolong == "linear" else 0
     fw = a.restriction == "full_weighting"
@@ -212,34 +330,35 @@ def main():
     kernels = {"half_sweep": f"k_half<{tname}, {cfg['dim']}, 1, false>",
                "fused_pre": f"{kz}<{tname}, true, {1 if fw else 0}, false, true>",
                "fused_post": f"{kz}<{tname}, false, {lin}, true, true>"}
-    # Algorithmic bytes per level-0 cell of one launch (reals): what the launch must move
-    # to and from HBM.  half_sweep: read the other colour and f, write this colour of half the cells.
-    # fused_pre (k_zs / k_ys: 2 RB-GS sweeps + residual + restriction): read black u and f, write black u and
-    # R / 2^dim (its red cells are never read: the only reader, fused_post, loads black cells and its first
-    # red half-sweep replaces the red ones).
-    # fused_post (prolongation + correction + 2 sweeps + err): read black u, V / 2^dim, f, psiOld; write u.
-    # (full weighting: PRE smooths only and stores both colours, 2.5 reals; the restriction runs after it)
     coarse = 0.5 ** cfg["dim"]
-    algo_reals = {"half_sweep": 1.5, "fused_pre": 2.5 if fw else 2.0 + coarse, "fused_post": 3.5 + coarse}
-    per_kind = {k: v for k, v in timed.items() if v[1] > 0}
+    # SURVEY.md §8(d) per-sweep accounting (what one launch per half-sweep would move) of the fused phases
+    per_sweep = {"half_sweep": 1.5, "fused_pre": 3.0 * a.nu + 2.0 + coarse, "fused_post": 3.0 * a.nu + 2.0 + coarse + 2.0}
+    per_kind = {k: v for k, v in timed.items() if k in kernels and v[1] > 0}
     cells = cells_rank
     if per_kind:
-        # per kind: (ms, launches, algorithmic bytes, reference-path bytes as the library counts them:
-        # SURVEY.md §8(d) per-sweep accounting, i.e. what one launch per half-sweep would move)
-        kinds = {k: (ms, cnt, algo_reals[k] * rb * cells * cnt, by) for k, (ms, cnt, by) in per_kind.items()}
+        # per kind: (ms, launches, algorithmic bytes as the library counts them: include/mgpoisson.h
+        # MGP_TIMING_*, DESIGN.md §4 — read black u and f, write black u and R / 2^dim for PRE; read black u,
+        # V / 2^dim, f, psiOld, write u for POST)
+        kinds = {k: (ms, cnt, by) for k, (ms, cnt, by) in per_kind.items()}
         line["level0_kernels"] = {
             k: {"kernel": kernels[k], "launches": cnt, "avg_us": 1e3 * ms / cnt,
-                "algorithmic_bytes_per_launch": ab / cnt, "achieved_GBps": ab / (ms * 1e-3) / 1e9,
-                "per_sweep_accounting_bytes_per_launch": by / cnt,
-                "effective_GBps_per_sweep_accounting": by / (ms * 1e-3) / 1e9}
-            for k, (ms, cnt, ab, by) in kinds.items()}
+                "algorithmic_bytes_per_launch": by / cnt, "achieved_GBps": by / (ms * 1e-3) / 1e9,
+                "per_sweep_accounting_bytes_per_launch": per_sweep[k] * rb * cells,
+                "effective_GBps_per_sweep_accounting": per_sweep[k] * rb * cells * cnt / (ms * 1e-3) / 1e9}
+            for k, (ms, cnt, by) in kinds.items()}
         dom = max(kinds, key=lambda k: kinds[k][0])  # the kernel with the most level-0 time
-        ms, cnt, ab, by = kinds[dom]
-        achieved = ab / (ms * 1e-3) / 1e9
+        ms, cnt, by = kinds[dom]
+        achieved = by / (ms * 1e-3) / 1e9
         roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBPS, "traffic": None, "kernel": kernels[dom],
-                "algorithmic_bytes_per_launch": ab / cnt, "avg_launch_us": 1e3 * ms / cnt,
-                "window": f"{a.steps} cycles after the timed region, HIP events around each launch"}
+                "algorithmic_bytes_per_launch": by / cnt, "avg_launch_us": 1e3 * ms / cnt,
+                "window": f"{steps} cycles after the timed region, HIP events around each launch"}
+        cyc_bytes = cycle_compulsory_bytes(ctx.levels, cfg, a, rb)
+        roof["cycle_compulsory_bytes"] = cyc_bytes
+        roof["cycle_frac"] = cyc_bytes / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBPS
+        roof["cycle_frac_definition"] = ("compulsory bytes of every level of one cycle (fused / tiled levels: their "
+                                         "phases' algorithmic bytes; per-piece levels: SURVEY §8(d) W; F-cycle: level "
+                                         "l visited l+1 times) / ms_per_step / 8 TB/s")
         # PMC traffic is measured by a separate rocprofv3 pass (tools/gpu_round.sh), never in this run; it
         # is used only when it was measured on this exact kernel source and workload
         if copy_peak:
@@ -259,18 +378,49 @@ def main():
             if ent and src_ok and wl_ok:
                 roof["traffic"] = ent.get("bytes_per_launch")
         line["roofline"] = roof
+        # finest-smoother GB/s = 3 sizeof(real) cells_per_rank sweeps / summed smoother kernel time
+        # (the level-0 smoothing launches; a fused phase is counted with its nu sweeps)
+        sweeps = sum(cnt * (1 if k == "half_sweep" else a.nu) / (2 if k == "half_sweep" else 1)
+                     for k, (ms_, cnt, _) in kinds.items())
+        tsum = sum(ms_ for ms_, _, _ in kinds.values()) * 1e-3
+        line["finest_smoother_GBps"] = {
+            "value": 3 * rb * cells * sweeps / tsum / 1e9, "sweeps_timed": sweeps, "kernel_s": tsum,
+            "definition": "BASELINE.md: 3 sizeof(real) cells_per_rank sweeps / summed finest-level smoothing kernel "
+                          "time; the temporally blocked phases do nu sweeps per launch from one read of the level, so "
+                          "this per-sweep figure is bounded by 8 TB/s x (sweeps per compulsory pass), not 8 TB/s"}
 
-    if rank == 0 and world == 1 and a.cpu_cycles > 0:
+    if primary and rank == 0 and world == 1 and a.cpu_cycles > 0:
         thr = a.cpu_threads or int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
         # configs[0] is small: the CPU port runs the same cycles the GPU timed, in full
-        c_omp, c_one = (a.steps, a.steps) if a.config0 else (a.cpu_cycles * 2, a.cpu_cycles)
-        line["cpu_baseline"] = cpu_baseline(cfg, c_omp, thr, gcells)
-        line["cpu_baseline_1thread"] = cpu_baseline(cfg, c_one, 1, gcells)
-    if rank == 0:
-        print(json.dumps(line), flush=True)
+        c_omp, c_one = (steps, steps) if a.config0 else (a.cpu_cycles, max(1, a.cpu_cycles // 2))
+        line["cpu_baseline"] = cpu_baseline(cfg, c_omp, thr, gcells, a.cpu_reps)
+        line["cpu_baseline_1thread"] = cpu_baseline(cfg, c_one, 1, gcells, a.cpu_reps)
     ctx.close()
-    if world > 1:
-        dist.destroy_process_group()
+    return line
+
+
+def cycle_compulsory_bytes(levels, cfg, a, rb):
+    """Compulsory HBM bytes of one cycle: per level the cells x reals a level must move — fused
+    (k_zs / k_ys) and tiled (k_blk, tail) levels their phases' algorithmic reals (PRE 2 + 2^-d, POST 2.5 + 2^-d,
+    + 1 psiOld with the err on level 0), per-piece levels SURVEY §8(d)'s W = (nu1 + nu2) 3 + 2 (2 + 2^-d)
+    (+ 1 psiOld on level 0); F-cycle: level l is visited l + 1 times."""
+    d = cfg["dim"]
+    coarse = 0.5 ** d
+    total = 0.0
+    for l, lv in enumerate(levels):
+        cells = lv["nx"] * lv["ny"] * (lv["nz_local"] if d == 3 else 1)
+        last = l == len(levels) - 1
+        if last:
+            reals = 2.0  # coarse solve: read f, write u
+        elif lv["engine"] == "piece":
+            reals = 3.0 * 2 * a.nu + 2 * (2 + coarse)
+        else:
+            reals = (2 + coarse) + (2.5 + coarse)
+        if l == 0:
+            reals += 1.0  # psiOld of the err
+        visits = (l + 1) if a.cycle == "F" else 1
+        total += visits * reals * rb * cells
+    return total
 
 
 def plan_only(a, cfg, box, rank, world, dist):
@@ -300,14 +450,46 @@ def plan_only(a, cfg, box, rank, world, dist):
                 assert z == rows[0]["nz_global"], f"level {l}: slabs cover {z} of {rows[0]['nz_global']} planes"
             else:
                 assert all(r["z0"] == 0 and r["nz_local"] == r["nz_global"] for r in rows), f"level {l}: replicated"
-        print(json.dumps({"plan_only": True, "n_gpus": world, "global_box": list(box), "levels": nl,
-                          "distributed_levels": sum(1 for r in plans[0] if r["distributed"]),
-                          "engines": [r["engine"] for r in plans[0]],
-                          "rank_slabs_level0": [[r[0]["z0"], r[0]["nz_local"]] for r in plans],
-                          "comm_id_bytes": len(cfg["comm_id"] or b"")}), flush=True)
+        out = {"plan_only": True, "n_gpus": world, "global_box": list(box), "levels": nl,
+               "distributed_levels": sum(1 for r in plans[0] if r["distributed"]),
+               "engines": [r["engine"] for r in plans[0]],
+               "rank_slabs_level0": [[r[0]["z0"], r[0]["nz_local"]] for r in plans],
+               "comm_id_bytes": len(cfg["comm_id"] or b""),
+               "comm_per_cycle": comm_schedule(cfg)}
+        if want_north_star(a, world):
+            out["north_star_lines"] = {}
+            for name, nbox, cyc, _ in NORTH_STAR:
+                if nbox[2] % world or nbox[2] // world < 2:
+                    continue
+                ns = argparse.Namespace(**vars(a))
+                ns.cycle, ns.box = cyc, ",".join(map(str, nbox))
+                ncfg = make_cfg(ns, nbox, 0, world, 0, cfg["comm_id"])
+                out["north_star_lines"][name] = {"global_box": list(nbox), "cycle": cyc,
+                                                 "comm_per_cycle": comm_schedule(ncfg)}
+        print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def comm_schedule(cfg):
+    """Rank 0's RCCL calls of one steady cycle (the second: the first also exchanges f once), from the library's
+    host-only dry run of the cycle (mgp_plan_comm): calls per kind and bytes this rank sends."""
+    import mgpoisson
+
+    if cfg["world"] == 1:
+        return {"calls": 0}
+    one = len(mgpoisson.plan_comm(mgpoisson.make_opts(**cfg), 1))
+    log = mgpoisson.plan_comm(mgpoisson.make_opts(**cfg), 2)[one:]
+    nb = 1  # rank 0 has one neighbour; interior ranks send the same to each of their two
+    out = {"calls": len(log), "halo_exchanges": sum(1 for r in log if r[0] == "exchange"),
+           "side_stream_exchanges": sum(1 for r in log if r[0] == "exchange" and r[1]),
+           "allgathers": sum(1 for r in log if r[0] == "allgather"),
+           "allreduces": sum(1 for r in log if r[0] == "allreduce"),
+           "halo_MB_per_neighbour": sum(r[4] for r in log if r[0] == "exchange") * nb / 1e6,
+           "allgather_MB": sum(r[4] for r in log if r[0] == "allgather") / 1e6,
+           "sequence": [list(r) for r in log]}
+    return out
 
 
 def source_hash():
@@ -321,8 +503,9 @@ def source_hash():
     return h.hexdigest()[:16]
 
 
-def cpu_baseline(cfg, cycles, threads, gcells):
-    """The C oracle (the build's restatement of the reference CPU path) on this host.
+def cpu_baseline(cfg, cycles, threads, gcells, reps=3):
+    """The C oracle (the build's restatement of the reference CPU path) on this host, best of `reps` samples of
+    `cycles` cycles each (best of 3).
 
     Bounded sample: the workload itself when it has <= 512^3 cells, else a 512^3 (3D) box of the same
     algorithm, scaled to the workload by cells (labelled extrapolated)."""
@@ -337,14 +520,19 @@ def cpu_baseline(cfg, cycles, threads, gcells):
         scale = 512 ** 3 / gcells
     o = Oracle(threads=threads, **kw)
     o.init_point_charge()
-    t0 = time.perf_counter()
-    for _ in range(cycles):
-        o.step()
-    dt = time.perf_counter() - t0
+    samples = []
+    for _ in range(max(1, reps)):
+        t0 = time.perf_counter()
+        for _ in range(cycles):
+            o.step()
+        samples.append(time.perf_counter() - t0)
+    dt = min(samples)
     n = kw["n"]
     kind = "V" if cfg["cycle"] == "V" else "F"
-    sample = (f"{cycles} full {kind}-cycles of {n[0]}x{n[1]}x{n[2] if cfg['dim'] == 3 else 1} with the same "
-              f"algorithm, oracle/mgp_oracle.c (gcc -O2, -ffp-contract=off), {threads} thread(s), {dt:.1f} s")
+    sample = (f"best of {len(samples)} samples of {cycles} full {kind}-cycles of {n[0]}x{n[1]}x"
+              f"{n[2] if cfg['dim'] == 3 else 1} with the same algorithm, oracle/mgp_oracle.c (gcc -O2, "
+              f"-ffp-contract=off), {threads} thread(s), {dt:.1f} s each (all: "
+              + ", ".join(f"{s:.1f}" for s in samples) + " s)")
     if scale != 1.0:
         sample += "; EXTRAPOLATED to the workload's cells (x %.3g)" % scale
     return {"value": scale * cycles / dt, "unit": f"{kind}-cycles/s (same workload)", "cores": threads,

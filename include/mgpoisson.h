@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define MGP_API_VERSION 2  /* 2: mgp_opts.restriction (in the former padding after world) */
+#define MGP_API_VERSION 3  /* 2: mgp_opts.restriction; 3: mgp_opts.arith and .api_version appended (232 bytes) */
 #define MGP_COMM_ID_BYTES 128 /* == NCCL_UNIQUE_ID_BYTES */
 
 typedef enum mgp_status {
@@ -47,6 +47,15 @@ enum { MGP_BC_ZERO = 0, MGP_BC_CONSISTENT = 1 };       /* coarse ghost: 0 (ref) 
  * weighting (north_star "full-weighting restriction"): the adjoint of the linear prolongation, per axis
  * (1, 3, 3, 1) / 8 over fine cells 2I-1 .. 2I+2, face weight (3 - c) next to the box boundary */
 enum { MGP_RESTRICT_AVERAGE = 0, MGP_RESTRICT_FULL_WEIGHTING = 1 };
+/* arith: the arithmetic of real = float (no effect on double).  The reference's two float paths disagree:
+ *   MGP_ARITH_REAL   every operation rounded to float, gpu.lua's OpenCL `real` (gpu.lua:32) — the default,
+ *                    and the arithmetic of the north-star configurations
+ *   MGP_ARITH_DOUBLE float buffers, every expression evaluated in double and rounded once where the
+ *                    reference stores into a buffer: cpu-raw.lua under real = 'float' (cpu-raw.lua:142-153,
+ *                    LuaJIT numbers are doubles; Jacobi :34-44, calcResidual :46-57, reduceResidual :59-63,
+ *                    addTo :83-85), err from the float errorBuf (calcFrobErr :96-100, summed in double
+ *                    :249-254).  Every level then runs one launch per piece (no fused / tiled / tail engines). */
+enum { MGP_ARITH_REAL = 0, MGP_ARITH_DOUBLE = 1 };
 /* Fields of a level, by cpu-raw.lua's names (cpu-raw.lua:148-171).  U and F are the stored, writable
  * state; the others are read-only views computed on request from it:
  *   MGP_FIELD_U          psi on level 0, Vs[L] below (the coarse correction)
@@ -81,12 +90,16 @@ typedef struct mgp_opts {
     int32_t restriction;   /* MGP_RESTRICT_AVERAGE (reference) | MGP_RESTRICT_FULL_WEIGHTING */
     int64_t gather_cells;  /* a level with <= this many cells is replicated on every rank */
     uint8_t comm_id[MGP_COMM_ID_BYTES]; /* from mgp_comm_unique_id() on rank 0 (world > 1) */
+    int32_t arith;         /* MGP_ARITH_REAL (gpu.lua) | MGP_ARITH_DOUBLE (cpu-raw.lua's real = 'float') */
+    int32_t api_version;   /* MGP_API_VERSION of the header the caller was built with (mgp_opts_default sets it) */
 } mgp_opts;
-/* The layout is part of the ABI (LuaJIT cdef, ctypes mirror): a change must bump MGP_API_VERSION. */
+/* The layout is part of the ABI (LuaJIT cdef, ctypes mirror): a change must bump MGP_API_VERSION and append
+ * fields, so that struct_size changes with it.  mgp_create rejects a struct_size or api_version that is not
+ * this library's: fill the struct with the library's own mgp_opts_default before setting fields. */
 #ifdef __cplusplus
-static_assert(sizeof(mgp_opts) == 224, "mgp_opts layout changed");
+static_assert(sizeof(mgp_opts) == 232, "mgp_opts layout changed");
 #else
-_Static_assert(sizeof(mgp_opts) == 224, "mgp_opts layout changed");
+_Static_assert(sizeof(mgp_opts) == 232, "mgp_opts layout changed");
 #endif
 
 typedef struct mgp_ctx mgp_ctx;
@@ -217,20 +230,37 @@ int         mgp_group_get_field(mgp_group* g, int level, int which, void* dst, i
 int         mgp_group_residual_norm(mgp_group* g, int level, double* rnorm, double* fnorm);
 int         mgp_group_field_stats(mgp_group* g, int level, int which, uint64_t* hash, double stats[3]);
 
-/* Finest-level kernel timing with HIP events on the context's stream.  mgp_timing(c, 1) resets and
- * enables (cycles then run eagerly, without hipGraph replay, so each launch can be bracketed).
- * Timed kinds, level 0 only:
+/* Kernel and communication timing with HIP events on the stream the work runs on.  mgp_timing(c, 1) resets
+ * and enables (cycles then run eagerly, without hipGraph replay, so each launch can be bracketed).
+ * Timed kinds; the first three on level 0 only:
  *   MGP_TIMING_HALF_SWEEP  plain red/black (or Jacobi) half-sweeps (not the err-fused last ones);
  *                          1.5 reals per cell per launch
- *   MGP_TIMING_FUSED_PRE   temporally blocked nu1 sweeps + residual + restriction;
- *                          (3 nu1 + 2 + 1/8) reals per cell
- *   MGP_TIMING_FUSED_POST  temporally blocked prolongation + correction + nu2 sweeps (+ err);
- *                          (3 nu2 + 2 + 1/8 [+ 2]) reals per cell
- * mgp_timing_read returns, for one kind, the summed kernel milliseconds, the number of launches
- * and their ALGORITHMIC bytes (SURVEY.md §8d accounting, not measured traffic). */
-enum { MGP_TIMING_HALF_SWEEP = 0, MGP_TIMING_FUSED_PRE = 1, MGP_TIMING_FUSED_POST = 2, MGP_TIMING_KINDS = 3 };
+ *   MGP_TIMING_FUSED_PRE   temporally blocked nu1 sweeps + residual + restriction: ALGORITHMIC bytes
+ *                          (2 + 2^-dim) reals per cell (read black u and f, write black u and R / 2^dim;
+ *                          2.5 with the full weighting, which restricts after the phase)
+ *   MGP_TIMING_FUSED_POST  temporally blocked prolongation + correction + nu2 sweeps (+ err): (2.5 + 2^-dim
+ *                          [+ 1 psiOld]) reals per cell
+ *   MGP_TIMING_EXCHANGE    every halo exchange of any level (grouped send/recv with the z-neighbours, on the
+ *                          compute or the side stream); bytes = what this rank sends
+ *   MGP_TIMING_COLLECTIVE  the agglomeration all-gather and the err all-reduce; bytes = what this rank sends
+ * mgp_timing_read returns, for one kind, the summed milliseconds, the number of timed launches / calls and
+ * their bytes (algorithmic for the kernels: SURVEY.md §8d, not measured traffic). */
+enum { MGP_TIMING_HALF_SWEEP = 0, MGP_TIMING_FUSED_PRE = 1, MGP_TIMING_FUSED_POST = 2, MGP_TIMING_EXCHANGE = 3,
+       MGP_TIMING_COLLECTIVE = 4, MGP_TIMING_KINDS = 5 };
 int         mgp_timing(mgp_ctx* c, int enable);
 int         mgp_timing_read(mgp_ctx* c, int kind, double* ms_total, int64_t* launches, double* bytes);
+
+/* The exchanges and collectives this rank has issued since creation or the last reset (reset != 0 clears after
+ * reading), in issue order: up to max_rows rows of 5 int64 {op, side, level, msgs, bytes}, op 0 = halo exchange
+ * (msgs per neighbour and direction, bytes sent per neighbour), 1 = agglomeration all-gather (bytes of this
+ * rank's part), 2 = err all-reduce (8 bytes); side 1 = issued on the side stream's communicator.  Returns the
+ * number of rows recorded (which may exceed max_rows).  Every rank of a decomposition must issue the same
+ * sequence per communicator (RCCL matches calls in order); tests compare the ranks' logs. */
+int         mgp_comm_log(mgp_ctx* c, int64_t* rows, int max_rows, int reset);
+/* The same log for `cycles` outer iterations of a context mgp_create(o) would build, computed on the host
+ * without a device (the cycle's host logic runs with every device and RCCL call skipped): what each rank of a
+ * world > 1 decomposition will issue per cycle.  GPU tests check it against the executed mgp_comm_log. */
+int         mgp_plan_comm(const mgp_opts* o, int32_t cycles, int64_t* rows, int max_rows);
 
 /* Measurement helper (BASELINE.md "a measured copy-kernel peak"): the best of `reps` 16-byte streaming copies
  * of `bytes` between two fresh device buffers on `device` (-1: current), over three copy-kernel shapes

@@ -68,9 +68,16 @@ int plan_levels(const mgp_opts& o, std::vector<LevelPlan>& out, std::string& err
 {
     out.clear();
     if (o.struct_size != (int32_t)sizeof(mgp_opts)) {
-        err = "mgp_opts.struct_size mismatch (header/library version skew)";
+        err = "mgp_opts.struct_size mismatch (header/library version skew): fill the struct with this library's "
+              "mgp_opts_default";
         return MGP_ERR_ARG;
     }
+    if (o.api_version != MGP_API_VERSION) {
+        err = "mgp_opts.api_version " + std::to_string(o.api_version) + " != library " + std::to_string(MGP_API_VERSION) +
+              " (header/library version skew)";
+        return MGP_ERR_ARG;
+    }
+    if (o.arith != MGP_ARITH_REAL && o.arith != MGP_ARITH_DOUBLE) { err = "unknown arith"; return MGP_ERR_ARG; }
     if (o.dim != 2 && o.dim != 3) { err = "dim must be 2 or 3"; return MGP_ERR_ARG; }
     int64_t nx = o.n[0], ny = o.n[1], nz = o.dim == 3 ? o.n[2] : 1;
     if (!is_pow2(nx) || !is_pow2(ny) || !is_pow2(nz)) { err = "n[] must be powers of two"; return MGP_ERR_ARG; }
@@ -110,6 +117,12 @@ int plan_levels(const mgp_opts& o, std::vector<LevelPlan>& out, std::string& err
         dist = dist && next_more && nz % o.world == 0 && nz / o.world >= 2 && nx * ny * nz > o.gather_cells;
     }
     return MGP_OK;
+}
+
+// the launchers' real kind (mgp_internal.h): float buffers with cpu-raw.lua's double arithmetic, or sizeof(real)
+int real_kind(const mgp_opts& o)
+{
+    return o.real_bytes == 4 && o.arith == MGP_ARITH_DOUBLE ? mgp::kRealF32D : o.real_bytes;
 }
 
 double coarse_coef(int coarse_bc, int level)
@@ -170,6 +183,9 @@ struct mgp_loopback {
 struct mgp_ctx {
     mgp_opts o{};
     int rb = 8;
+    // real kind of the per-piece launchers: rb, or mgp::kRealF32D for float buffers with cpu-raw.lua's double
+    // arithmetic (mgp_opts.arith = MGP_ARITH_DOUBLE), which runs every level one launch per piece
+    int rk = 8;
     int G = 0;  // ghost planes per side (kGhost3D in 3D, 0 in 2D; kGhostZs for distributed 3D)
     bool deep_halo = true;  // smooth_deep on distributed levels below the finest
     bool fresh_sweep = true;        // k_fresh for the first sweep of a lazily zeroed level (MGP_FRESH=0: off)
@@ -182,6 +198,19 @@ struct mgp_ctx {
     hipStream_t s = nullptr;
     int device = 0;
     ncclComm_t comm = nullptr;
+    // the side stream's own communicator (ncclCommSplit of comm): RCCL runs one communicator's operations in
+    // issue order, so the early POST exchange on xs would otherwise hold back every exchange the compute
+    // stream issues for the coarse levels until it has finished
+    ncclComm_t xcomm = nullptr;
+    // host-only dry run (mgp_plan_comm): the cycle's host logic runs, every device and RCCL call is skipped and
+    // only the exchange / collective log is kept
+    bool dry = false;
+    bool nb_comm = false;  // non-blocking communicators (mgp_group_create): every call is polled to completion
+    // RCCL API calls of this rank in flight (group_abort waits for them to return before it aborts the
+    // communicators) and whether the rank waits on its peers (a halo exchange, collective or the stream
+    // synchronisation after one): the group aborts only when a surviving rank is blocked that way
+    std::atomic<int> in_nccl{0};
+    std::atomic<int> waiting{0};
     mgp_loopback* lb = nullptr;  // loopback transport instead of RCCL (tests)
     hipEvent_t lb_ev = nullptr, lb_ev2 = nullptr;
     // Slab levels: the u halo that a temporally blocked POST reads is final after PRE, so it is exchanged on
@@ -222,6 +251,7 @@ struct mgp_ctx {
     // set by the owning group when another rank failed: no new exchange / collective is issued, and the
     // communicator (aborted by the group) is not touched again
     const std::atomic<bool>* group_stop = nullptr;
+    bool stopped() const { return group_stop && group_stop->load(); }
     bool first_done = false;
     bool err_done = false;
     // hipGraph replay of whole cycles (single GPU): one instantiated graph per pointer state of
@@ -251,6 +281,12 @@ struct mgp_ctx {
     std::vector<hipEvent_t> ev;
     std::vector<std::pair<int, double>> ev_meta;  // (kind, algorithmic bytes) per pair
     size_t ev_used = 0;
+    struct CommRec {
+        int op, side, level;
+        int64_t msgs, bytes;
+    };
+    static constexpr size_t kCommLogCap = 1 << 16;
+    std::vector<CommRec> clog;
     double t_ms[MGP_TIMING_KINDS] = {};
     int64_t t_launch[MGP_TIMING_KINDS] = {};
     double t_bytes[MGP_TIMING_KINDS] = {};
@@ -272,6 +308,7 @@ struct mgp_ctx {
 
 #define HIP_TRY(c, expr)                                                                         \
     do {                                                                                        \
+        if ((c)->dry) break;                                                                    \
         hipError_t e_ = (expr);                                                                 \
         if (e_ != hipSuccess)                                                                   \
             return (c)->fail(MGP_ERR_HIP, "%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_), \
@@ -280,6 +317,7 @@ struct mgp_ctx {
 
 #define NCCL_TRY(c, expr)                                                                           \
     do {                                                                                           \
+        if ((c)->dry) break;                                                                       \
         ncclResult_t r_ = (expr);                                                                  \
         if (r_ != ncclSuccess)                                                                     \
             return (c)->fail(MGP_ERR_RCCL, "%s failed: %s (%s:%d)", #expr, ncclGetErrorString(r_), \
@@ -391,6 +429,56 @@ int lb_allreduce(mgp_ctx* c, double* v, int n = 1)
     return MGP_OK;
 }
 
+// One RCCL call sequence on communicator `comm`: counted in in_nccl for its whole duration (group_abort
+// waits for it), refused once the group was stopped, and, on a non-blocking communicator, polled until it
+// has left ncclInProgress (returning early when the group is stopped meanwhile).
+struct NcclScope {
+    mgp_ctx* c;
+    explicit NcclScope(mgp_ctx* cc) : c(cc)
+    {
+        c->in_nccl.fetch_add(1);
+        c->waiting.fetch_add(1);
+    }
+    ~NcclScope()
+    {
+        c->waiting.fetch_sub(1);
+        c->in_nccl.fetch_sub(1);
+    }
+};
+
+struct WaitScope {
+    mgp_ctx* c;
+    explicit WaitScope(mgp_ctx* cc) : c(cc) { c->waiting.fetch_add(1); }
+    ~WaitScope() { c->waiting.fetch_sub(1); }
+};
+
+int nccl_done(mgp_ctx* c, ncclComm_t comm, ncclResult_t r, const char* what)
+{
+    if (r == ncclInProgress || (r == ncclSuccess && c->nb_comm)) {
+        for (;;) {
+            ncclResult_t st = ncclSuccess;
+            r = ncclCommGetAsyncError(comm, &st);
+            if (r != ncclSuccess) break;
+            if (st != ncclInProgress) {
+                r = st;
+                break;
+            }
+            if (c->stopped()) return c->fail(MGP_ERR_STATE, "group aborted during %s", what);
+            std::this_thread::yield();
+        }
+    }
+    if (r != ncclSuccess) return c->fail(MGP_ERR_RCCL, "%s: %s", what, ncclGetErrorString(r));
+    return MGP_OK;
+}
+
+#define NCCL_CALL(c, comm, expr, what)                                                                    \
+    do {                                                                                                 \
+        if ((c)->dry) break;                                                                             \
+        NcclScope scope_(c);                                                                             \
+        if ((c)->stopped()) return (c)->fail(MGP_ERR_STATE, "group aborted: another rank failed");       \
+        TRY(nccl_done((c), (comm), (expr), (what)));                                                     \
+    } while (0)
+
 // Exchange `depth` boundary planes of `buf` with each z-neighbour: my first interior planes go to
 // rank-1's upper ghosts, my last to rank+1's lower ghosts.  Planes are contiguous in the packed
 // layout, so each direction is one ncclSend/ncclRecv pair on that neighbour's xGMI link.
@@ -399,13 +487,12 @@ int lb_allreduce(mgp_ctx* c, double* v, int n = 1)
 // overwritten before they are read), halving the bytes.
 // st: the stream the exchange runs on (nullptr: the compute stream; the side stream xs must already wait
 // for the compute stream's last write of buf's boundary planes; the loopback transport records that itself)
-int exchange_buf(mgp_ctx* c, Level& L, char* buf, int depth = 1, int colour = -1, hipStream_t st = nullptr)
+int timed_begin_on(mgp_ctx* c, hipStream_t st, hipEvent_t* e1);
+int timed_end_on(mgp_ctx* c, hipStream_t st, hipEvent_t e1, int kind, double bytes);
+void comm_log(mgp_ctx* c, int op, int side, int level, int64_t msgs, int64_t bytes);
+
+int exchange_buf_impl(mgp_ctx* c, Level& L, char* buf, int depth, int colour, hipStream_t st)
 {
-    if (!st) st = c->s;
-    if (depth > c->G || depth > L.g.nz)
-        return c->fail(MGP_ERR_STATE, "internal: exchange depth %d (ghost %d, slab %d)", depth, c->G, (int)L.g.nz);
-    if (c->group_stop && c->group_stop->load()) return c->fail(MGP_ERR_STATE, "group aborted: another rank failed");
-    ++L.exchanges;
     if (c->lb) return lb_exchange(c, (int)(&L - c->lev.data()), buf, depth, colour, st);
     const size_t rb = (size_t)c->rb;
     const size_t coff = colour < 0 ? 0 : (size_t)(colour * L.g.H) * rb;
@@ -413,22 +500,46 @@ int exchange_buf(mgp_ctx* c, Level& L, char* buf, int depth = 1, int colour = -1
     // one message per direction (whole planes) or one per plane (a colour half of each)
     const int msgs = colour < 0 ? 1 : depth;
     const size_t cnt = colour < 0 ? (size_t)(depth * L.g.P) : (size_t)L.g.H;
+    ncclComm_t comm = st == c->xs && c->xcomm ? c->xcomm : c->comm;
+    NcclScope scope(c);
+    if (c->stopped()) return c->fail(MGP_ERR_STATE, "group aborted: another rank failed");
     ncclResult_t r = ncclGroupStart();
     for (int i = 0; i < msgs && r == ncclSuccess; ++i) {
         if (c->o.rank > 0) {
-            r = ncclSend(at(i), cnt, c->nccl_real(), c->o.rank - 1, c->comm, st);
-            if (r == ncclSuccess) r = ncclRecv(at(i - depth), cnt, c->nccl_real(), c->o.rank - 1, c->comm, st);
+            r = ncclSend(at(i), cnt, c->nccl_real(), c->o.rank - 1, comm, st);
+            if (r == ncclSuccess) r = ncclRecv(at(i - depth), cnt, c->nccl_real(), c->o.rank - 1, comm, st);
         }
         if (c->o.rank < c->o.world - 1 && r == ncclSuccess) {
-            r = ncclSend(at(L.g.nz - depth + i), cnt, c->nccl_real(), c->o.rank + 1, c->comm, st);
-            if (r == ncclSuccess) r = ncclRecv(at(L.g.nz + i), cnt, c->nccl_real(), c->o.rank + 1, c->comm, st);
+            r = ncclSend(at(L.g.nz - depth + i), cnt, c->nccl_real(), c->o.rank + 1, comm, st);
+            if (r == ncclSuccess) r = ncclRecv(at(L.g.nz + i), cnt, c->nccl_real(), c->o.rank + 1, comm, st);
         }
     }
     const ncclResult_t e = ncclGroupEnd();  // always closes the group, also after a failed call
     if (r == ncclSuccess) r = e;
-    if (r != ncclSuccess) return c->fail(MGP_ERR_RCCL, "halo exchange (level %d): %s", (int)(&L - c->lev.data()),
-                                         ncclGetErrorString(r));
-    return MGP_OK;
+    char what[64];
+    std::snprintf(what, sizeof what, "halo exchange (level %d)", (int)(&L - c->lev.data()));
+    return nccl_done(c, comm, r, what);
+}
+
+int exchange_buf(mgp_ctx* c, Level& L, char* buf, int depth = 1, int colour = -1, hipStream_t st = nullptr)
+{
+    if (!st) st = c->s;
+    if (depth > c->G || depth > L.g.nz)
+        return c->fail(MGP_ERR_STATE, "internal: exchange depth %d (ghost %d, slab %d)", depth, c->G, (int)L.g.nz);
+    if (c->stopped()) return c->fail(MGP_ERR_STATE, "group aborted: another rank failed");
+    ++L.exchanges;
+    // bytes this rank sends per neighbour: depth planes, or the colour half of each
+    const int64_t per_nb = (int64_t)depth * (colour < 0 ? L.g.P : L.g.H) * c->rb;
+    const int nbs = (c->o.rank > 0) + (c->o.rank < c->o.world - 1);
+    comm_log(c, 0, st == c->xs, (int)(&L - c->lev.data()), colour < 0 ? 1 : depth, per_nb);
+    if (c->dry) return MGP_OK;
+    hipEvent_t e;
+    TRY(timed_begin_on(c, st, &e));
+    {
+        WaitScope w(c);  // the loopback barrier waits for the peers too
+        TRY(exchange_buf_impl(c, L, buf, depth, colour, st));
+    }
+    return timed_end_on(c, st, e, MGP_TIMING_EXCHANGE, (double)(per_nb * nbs));
 }
 
 int exchange(mgp_ctx* c, Level& L)
@@ -454,26 +565,46 @@ void timing_collect(mgp_ctx* c)
     c->ev_used = 0;
 }
 
-int timed_begin(mgp_ctx* c, int l, hipEvent_t* e1)
+// An event pair around work on stream st (any level): the exchange and collective kinds
+int timed_begin_on(mgp_ctx* c, hipStream_t st, hipEvent_t* e1)
 {
     *e1 = nullptr;
-    if (!c->timing || l != 0) return MGP_OK;
+    if (!c->timing) return MGP_OK;
     if (c->ev_used + 2 > c->ev.size()) {
         HIP_TRY(c, hipStreamSynchronize(c->s));
+        if (c->xs) HIP_TRY(c, hipStreamSynchronize(c->xs));
         timing_collect(c);
     }
     *e1 = c->ev[c->ev_used];
-    HIP_TRY(c, hipEventRecord(*e1, c->s));
+    HIP_TRY(c, hipEventRecord(*e1, st));
     return MGP_OK;
 }
 
-int timed_end(mgp_ctx* c, hipEvent_t e1, int kind, double bytes)
+int timed_end_on(mgp_ctx* c, hipStream_t st, hipEvent_t e1, int kind, double bytes)
 {
     if (!e1) return MGP_OK;
-    HIP_TRY(c, hipEventRecord(c->ev[c->ev_used + 1], c->s));
+    HIP_TRY(c, hipEventRecord(c->ev[c->ev_used + 1], st));
     c->ev_meta[c->ev_used / 2] = {kind, bytes};
     c->ev_used += 2;
     return MGP_OK;
+}
+
+// Level-0 launches on the compute stream: the finest-smoother kinds
+int timed_begin(mgp_ctx* c, int l, hipEvent_t* e1)
+{
+    *e1 = nullptr;
+    if (l != 0) return MGP_OK;
+    return timed_begin_on(c, c->s, e1);
+}
+
+int timed_end(mgp_ctx* c, hipEvent_t e1, int kind, double bytes) { return timed_end_on(c, c->s, e1, kind, bytes); }
+
+// Record of the exchanges and collectives a rank issues (mgp_comm_log): op 0 halo exchange (msgs per
+// neighbour and direction, bytes per neighbour), 1 all-gather (bytes of this rank's slab), 2 all-reduce;
+// side = issued on the side stream / its communicator.  Bounded: the first kCommLogCap calls after a reset.
+void comm_log(mgp_ctx* c, int op, int side, int level, int64_t msgs, int64_t bytes)
+{
+    if (c->clog.size() < mgp_ctx::kCommLogCap) c->clog.push_back({op, side, level, msgs, bytes});
 }
 
 int64_t level_cells(const Level& L) { return L.p.nx * L.p.ny * L.p.nz; }
@@ -500,7 +631,7 @@ int half(mgp_ctx* c, int l, int color, char* other, char* dst, const char* old, 
     // matches that kernel's rocprofv3 row; the err-fused variant reads psiOld as well
     hipEvent_t e;
     TRY(timed_begin(c, old ? -1 : l, &e));
-    HIP_TRY(c, mgp::launch_half_sweep(c->rb, c->o.dim, l == 0, color, c->ui(L, other) - back, c->ui(L, L.f) - back,
+    HIP_TRY(c, mgp::launch_half_sweep(c->rk, c->o.dim, l == 0, color, c->ui(L, other) - back, c->ui(L, L.f) - back,
                                       c->ui(L, dst) - back, old ? c->ui(L, (char*)old) : nullptr, c->d_part + part_off,
                                       g, h, cl, c->use_gs, c->s));
     TRY(timed_end(c, e, MGP_TIMING_HALF_SWEEP, 1.5 * c->rb * (double)level_cells(L)));
@@ -576,7 +707,7 @@ int smooth(mgp_ctx* c, int l, int sweeps, double h, bool want_err = false, bool 
             continue;
         }
         const char* old = last_err ? L.t : nullptr;
-        const int nb = mgp::half_blocks(c->rb, L.g, c->use_gs);
+        const int nb = mgp::half_blocks(c->rk, L.g, c->use_gs);
         char* dst = oop ? L.t : L.u;
         if (!(red_done && sw == 0)) {
             TRY(exchange(c, L));
@@ -614,9 +745,16 @@ Geo coarse_view(const Level& L, const Level& C, int64_t* zc_local)
 int gather_coarse_rhs(mgp_ctx* c, Level& L, Level& C, char* R)
 {
     const size_t count = (size_t)((L.g.nz / 2) * C.g.P);
-    if (c->lb) return lb_allgather(c, c->ui(C, C.f), count);
-    NCCL_TRY(c, ncclAllGather(R, c->ui(C, C.f), count, c->nccl_real(), c->comm, c->s));
-    return MGP_OK;
+    comm_log(c, 1, 0, (int)(&C - c->lev.data()), 1, (int64_t)(count * c->rb));
+    if (c->dry) return MGP_OK;
+    hipEvent_t e;
+    TRY(timed_begin_on(c, c->s, &e));
+    WaitScope w(c);
+    if (c->lb)
+        TRY(lb_allgather(c, c->ui(C, C.f), count));
+    else
+        NCCL_CALL(c, c->comm, ncclAllGather(R, c->ui(C, C.f), count, c->nccl_real(), c->comm, c->s), "all-gather");
+    return timed_end_on(c, c->s, e, MGP_TIMING_COLLECTIVE, (double)(count * c->rb * (c->o.world - 1)));
 }
 
 // calcResidual + the full-weighting restriction (MGP_RESTRICT_FULL_WEIGHTING): r of the level's own planes
@@ -627,13 +765,13 @@ int residual_restrict_fw(mgp_ctx* c, int l, double h)
     Level& C = c->lev[l + 1];
     TRY(materialize_zero(c, L));
     TRY(exchange(c, L));
-    HIP_TRY(c, mgp::launch_residual_field_v(c->rb, c->o.dim, c->ui(L, L.u), c->ui(L, L.f), c->ui(L, c->rscratch), L.g,
+    HIP_TRY(c, mgp::launch_residual_field_v(c->rk, c->o.dim, c->ui(L, L.u), c->ui(L, L.f), c->ui(L, c->rscratch), L.g,
                                             h, coarse_coef(c->o.coarse_bc, l), c->s));
     if (L.p.dist) TRY(exchange_buf(c, L, c->rscratch, 1));
     int64_t zc = 0;
     const Geo gc = coarse_view(L, C, &zc);
     char* R = c->ui(C, C.f) + (size_t)(zc * C.g.P) * c->rb;
-    HIP_TRY(c, mgp::launch_fw_restrict(c->rb, c->o.dim, c->ui(L, c->rscratch), R, L.g, gc,
+    HIP_TRY(c, mgp::launch_fw_restrict(c->rk, c->o.dim, c->ui(L, c->rscratch), R, L.g, gc,
                                        coarse_coef(c->o.coarse_bc, l + 1), c->s));
     C.fghost_ok = !C.p.dist;
     if (L.p.dist && !C.p.dist) TRY(gather_coarse_rhs(c, L, C, R));
@@ -650,7 +788,7 @@ int residual_restrict(mgp_ctx* c, int l, double h)
     int64_t zc = 0;
     const Geo gc = coarse_view(L, C, &zc);
     char* R = c->ui(C, C.f) + (size_t)(zc * C.g.P) * c->rb;
-    HIP_TRY(c, mgp::launch_residual_restrict(c->rb, c->o.dim, c->ui(L, L.u), c->ui(L, L.f), R, L.g, gc, h,
+    HIP_TRY(c, mgp::launch_residual_restrict(c->rk, c->o.dim, c->ui(L, L.u), c->ui(L, L.f), R, L.g, gc, h,
                                              coarse_coef(c->o.coarse_bc, l), c->s));
     C.fghost_ok = !C.p.dist;
     if (L.p.dist && !C.p.dist) TRY(gather_coarse_rhs(c, L, C, R));
@@ -670,7 +808,7 @@ int prolong_correct(mgp_ctx* c, int l, bool black_only = false)
     int64_t zc = 0;
     const Geo gc = coarse_view(L, C, &zc);
     char* V = c->ui(C, C.u) + (size_t)(zc * C.g.P) * c->rb;
-    HIP_TRY(c, mgp::launch_prolong_correct(c->rb, c->o.dim, linear, c->ui(L, L.u), V, L.g, gc,
+    HIP_TRY(c, mgp::launch_prolong_correct(c->rk, c->o.dim, linear, c->ui(L, L.u), V, L.g, gc,
                                            coarse_coef(c->o.coarse_bc, l + 1), c->s, black_only));
     L.ghost_ok = !L.p.dist;
     L.ghost_zero = false;
@@ -762,10 +900,10 @@ int early_exchange_post(mgp_ctx* c, int l)
 {
     Level& L = c->lev[l];
     if (!c->early_x || !c->xs || !L.p.dist) return MGP_OK;
-    if (!c->lb) {  // RCCL: xs waits for PRE (the loopback transport records the compute stream itself)
-        HIP_TRY(c, hipEventRecord(c->x_ev0, c->s));
-        HIP_TRY(c, hipStreamWaitEvent(c->xs, c->x_ev0, 0));
-    }
+    // xs waits for PRE on both transports: the ghost planes it writes are read by the compute stream's kernels
+    // (the loopback copies additionally wait for the neighbours' events)
+    HIP_TRY(c, hipEventRecord(c->x_ev0, c->s));
+    HIP_TRY(c, hipStreamWaitEvent(c->xs, c->x_ev0, 0));
     TRY(exchange_buf(c, L, L.u, mgp::kZsHaloPost, 1, c->xs));
     HIP_TRY(c, hipEventRecord(c->x_ev1, c->xs));
     L.early_u = true;
@@ -801,8 +939,10 @@ int fused_pre(mgp_ctx* c, int l, double h)
     hipEvent_t e;
     TRY(timed_begin(c, l, &e));
     HIP_TRY(c, mgp::launch_fused(c->rb, a, c->s));
-    // algorithmic bytes: nu1 sweeps x 3 reals + (2 + 1/8) reals of residual/restriction
-    TRY(timed_end(c, e, MGP_TIMING_FUSED_PRE, (3.0 * c->o.nu1 + (fw ? 0.0 : 2.125)) * c->rb * (double)level_cells(L)));
+    // algorithmic bytes (include/mgpoisson.h): read black u and f, write black u and R / 2^dim
+    // (full weighting: both colours of u, the restriction runs after the phase)
+    const double coarse = std::ldexp(1.0, -c->o.dim);
+    TRY(timed_end(c, e, MGP_TIMING_FUSED_PRE, (fw ? 2.5 : 2.0 + coarse) * c->rb * (double)level_cells(L)));
     std::swap(L.u, L.t);  // u = smoothed; t = the previous iterate (psiOld on level 0)
     L.ghost_ok = !L.p.dist;
     L.ghost_zero = false;
@@ -852,8 +992,9 @@ int fused_post(mgp_ctx* c, int l, double h, bool want_err)
     hipEvent_t e;
     TRY(timed_begin(c, l, &e));
     HIP_TRY(c, mgp::launch_fused(c->rb, a, c->s));
+    // read black u, V / 2^dim, f (and psiOld with err), write u
     TRY(timed_end(c, e, MGP_TIMING_FUSED_POST,
-                  (3.0 * c->o.nu2 + 2.125 + (want_err ? 2.0 : 0.0)) * c->rb * (double)level_cells(L)));
+                  (2.5 + std::ldexp(1.0, -c->o.dim) + (want_err ? 1.0 : 0.0)) * c->rb * (double)level_cells(L)));
     if (keep)
         std::swap(L.u, c->xbuf);  // u = new iterate, t = psiOld (kept), xbuf = the smoothed PRE output (scratch)
     else
@@ -955,6 +1096,7 @@ bool try_tail(mgp_ctx* c, int T)
 {
     const int last = (int)c->lev.size() - 1;
     if (T < 1 || T > last || c->lev[T].p.dist) return false;
+    if (c->rk == mgp::kRealF32D) return false;  // the tail evaluates in the real type
     const int nlev = last - T + 1;
     if (nlev > mgp::kTailMaxLevels) return false;
     std::vector<Geo> g;
@@ -1159,14 +1301,20 @@ int one_cycle(mgp_ctx* c, double* dst)
     if (fuse && !c->err_done) return c->fail(MGP_ERR_STATE, "internal: fused err launch did not run");
     if (c->o.err_mode && !fuse) {
         Level& L0 = c->lev[0];
-        HIP_TRY(c, mgp::launch_sqdiff_sum(c->rb, c->ui(L0, L0.u), c->psi_old, L0.g.P * L0.g.nz, c->d_part, dst, c->s,
+        HIP_TRY(c, mgp::launch_sqdiff_sum(c->rk, c->ui(L0, L0.u), c->psi_old, L0.g.P * L0.g.nz, c->d_part, dst, c->s,
                                           c->err_ctr));
     }
     if (c->o.err_mode && c->o.world > 1) {
+        comm_log(c, 2, 0, 0, 1, (int64_t)sizeof(double));
+        if (c->dry) return MGP_OK;
+        hipEvent_t e;
+        TRY(timed_begin_on(c, c->s, &e));
+        WaitScope w(c);
         if (c->lb)
             TRY(lb_allreduce(c, dst));
         else
-            NCCL_TRY(c, ncclAllReduce(dst, dst, 1, ncclDouble, ncclSum, c->comm, c->s));
+            NCCL_CALL(c, c->comm, ncclAllReduce(dst, dst, 1, ncclDouble, ncclSum, c->comm, c->s), "err all-reduce");
+        TRY(timed_end_on(c, c->s, e, MGP_TIMING_COLLECTIVE, (double)sizeof(double)));
     }
     update_metrics_old(c);
     return MGP_OK;
@@ -1277,12 +1425,29 @@ int check_level(const mgp_ctx* c, int level)
 
 int sync_and_check(mgp_ctx* c)
 {
-    HIP_TRY(c, hipStreamSynchronize(c->s));
-    if (c->group_stop && c->group_stop->load()) return c->fail(MGP_ERR_STATE, "group aborted: another rank failed");
-    if (c->comm) {
+    {
+        // with peers, the stream may hold an exchange a failed rank never joins: the group may abort under it
+        struct Wait {
+            mgp_ctx* c;
+            bool on;
+            ~Wait()
+            {
+                if (on) c->waiting.fetch_sub(1);
+            }
+        } w{c, c->o.world > 1};
+        if (w.on) c->waiting.fetch_add(1);
+        HIP_TRY(c, hipStreamSynchronize(c->s));
+        if (c->xs) HIP_TRY(c, hipStreamSynchronize(c->xs));
+    }
+    if (c->stopped()) return c->fail(MGP_ERR_STATE, "group aborted: another rank failed");
+    for (ncclComm_t comm : {c->comm, c->xcomm}) {
+        if (!comm) continue;
+        NcclScope scope(c);
+        if (c->stopped()) return c->fail(MGP_ERR_STATE, "group aborted: another rank failed");
         ncclResult_t ar = ncclSuccess;
-        NCCL_TRY(c, ncclCommGetAsyncError(c->comm, &ar));
-        if (ar != ncclSuccess) return c->fail(MGP_ERR_RCCL, "RCCL async error: %s", ncclGetErrorString(ar));
+        NCCL_TRY(c, ncclCommGetAsyncError(comm, &ar));
+        if (ar != ncclSuccess && ar != ncclInProgress)
+            return c->fail(MGP_ERR_RCCL, "RCCL async error: %s", ncclGetErrorString(ar));
     }
     return MGP_OK;
 }
@@ -1318,6 +1483,8 @@ void mgp_opts_default(mgp_opts* o)
     o->world = 1;
     o->gather_cells = 32768;
     o->restriction = MGP_RESTRICT_AVERAGE;  // cpu.lua:127-135
+    o->arith = MGP_ARITH_REAL;              // gpu.lua:32 (real-typed OpenCL arithmetic)
+    o->api_version = MGP_API_VERSION;
 }
 
 int mgp_comm_unique_id(void* out, int64_t nbytes)
@@ -1339,6 +1506,49 @@ int mgp_comm_unique_id(void* out, int64_t nbytes)
 static void select_engines(mgp_ctx* c);
 static int level_engine(const mgp_ctx* c, int l);
 
+// Everything mgp_create decides on the host before touching a device: options, the environment switches,
+// ghost depth, the level hierarchy and each level's engine (shared with mgp_plan and mgp_plan_comm, so that
+// those describe exactly what mgp_create would run).
+static void host_setup(mgp_ctx* c, const mgp_opts& o, const std::vector<LevelPlan>& plan)
+{
+    c->o = o;
+    if (c->o.dim == 2) c->o.n[2] = 1;
+    c->rb = o.real_bytes;
+    c->rk = real_kind(o);
+    c->G = o.dim == 3 ? mgp::kGhost3D : 0;  // widened below when a distributed level is fused
+    {
+        const char* v = std::getenv("MGP_FRESH");
+        c->fresh_sweep = !(v && std::atoi(v) == 0);
+        const char* vb = std::getenv("MGP_POST_BLACK");
+        c->post_black = !(vb && std::atoi(vb) == 0);
+        const char* vp = std::getenv("MGP_POST1");
+        c->post1 = vp && std::atoi(vp) != 0;
+        const char* vd = std::getenv("MGP_DEEP_HALO");  // 0: exchange before every half-sweep instead
+        c->deep_halo = !(vd && std::atoi(vd) == 0);
+        const char* ve = std::getenv("MGP_EARLY_X");
+        c->early_x = !(ve && std::atoi(ve) == 0);
+    }
+    // distributed 3D levels sweep with deep halos (smooth_deep): kGhostZs ghost planes per side
+    if (c->deep_halo && o.dim == 3 && o.world > 1) c->G = mgp::kGhostZs;
+    for (auto& p : plan) {
+        Level L;
+        L.p = p;
+        L.g = make_geo(p, c->o.dim);
+        c->lev.push_back(L);
+    }
+    select_engines(c);
+    for (auto& L : c->lev) L.alloc = L.g.P * (L.g.nz + 2 * c->G);
+}
+
+// the zero buffer of the lazily zeroed fresh coarse guesses: the largest such level's layout
+static int64_t zbuf_reals_of(const mgp_ctx* c)
+{
+    int64_t z = 0;
+    for (size_t l = 1; l < c->lev.size(); ++l)
+        if (!c->lev[l].fused && (c->tail_level < 0 || (int)l < c->tail_level)) z = std::max(z, c->lev[l].alloc);
+    return z;
+}
+
 int mgp_plan(const mgp_opts* o, int64_t* rows, int max_levels)
 {
     if (!o) return MGP_ERR_ARG;
@@ -1347,16 +1557,7 @@ int mgp_plan(const mgp_opts* o, int64_t* rows, int max_levels)
     if (rc != MGP_OK) return rc;
     // the engines mgp_create would pick, on a device-free context
     mgp_ctx c;
-    c.o = *o;
-    if (c.o.dim == 2) c.o.n[2] = 1;
-    c.rb = o->real_bytes;
-    for (auto& p : plan) {
-        Level L;
-        L.p = p;
-        L.g = make_geo(p, c.o.dim);
-        c.lev.push_back(L);
-    }
-    select_engines(&c);
+    host_setup(&c, *o, plan);
     for (int l = 0; l < (int)plan.size() && l < max_levels && rows; ++l) {
         int64_t* r = rows + 8 * l;
         r[0] = plan[l].nx;
@@ -1371,6 +1572,45 @@ int mgp_plan(const mgp_opts* o, int64_t* rows, int max_levels)
     return (int)plan.size();
 }
 
+
+// level 0's u and f were just written (init or host I/O): their ghost planes are stale on a slab level
+static void fields_written(mgp_ctx* c)
+{
+    Level& L = c->lev[0];
+    L.ghost_ok = !L.p.dist;
+    L.ghost_zero = false;
+    L.fghost_ok = !L.p.dist;
+}
+
+int mgp_plan_comm(const mgp_opts* o, int32_t cycles, int64_t* rows, int max_rows)
+{
+    if (!o || cycles < 0 || max_rows < 0 || (max_rows > 0 && !rows)) return MGP_ERR_ARG;
+    std::vector<LevelPlan> plan;
+    int rc = plan_levels(*o, plan, g_create_error);
+    if (rc != MGP_OK) return rc;
+    mgp_ctx c;
+    host_setup(&c, *o, plan);
+    c.dry = true;
+    // stand-ins for the device objects whose presence steers the host logic (never dereferenced: every device
+    // call is skipped): the side stream of the early exchange and the zero buffer of lazily zeroed levels
+    static char stand_in[16];
+    if (c.o.world > 1 && c.early_x) c.xs = reinterpret_cast<hipStream_t>(stand_in);
+    if (c.o.smoother == MGP_RBGS && c.o.coarse_init == MGP_COARSE_FRESH) {
+        c.zbuf_reals = zbuf_reals_of(&c);
+        if (c.zbuf_reals) c.zbuf = stand_in;
+    }
+    fields_written(&c);  // after mgp_init_point_charge (or mgp_set_field) of psi and f
+    for (int k = 0; k < cycles; ++k) {
+        rc = one_cycle(&c, nullptr);
+        if (rc != MGP_OK) {
+            g_create_error = c.err;
+            return rc;
+        }
+    }
+    c.xs = nullptr;
+    c.zbuf = nullptr;
+    return mgp_comm_log(&c, rows, max_rows, 0);
+}
 
 static void destroy_impl(mgp_ctx* c)
 {
@@ -1393,6 +1633,7 @@ static void destroy_impl(mgp_ctx* c)
     if (c->d_slot) (void)hipFree(c->d_slot);
     for (auto& g : c->graphs) (void)hipGraphExecDestroy(g.exec);
     for (auto e : c->ev) (void)hipEventDestroy(e);
+    if (c->xcomm) (void)ncclCommDestroy(c->xcomm);
     if (c->comm) (void)ncclCommDestroy(c->comm);
     if (c->lb) {
         std::lock_guard<std::mutex> lk(c->lb->m);
@@ -1412,7 +1653,8 @@ static void destroy_impl(mgp_ctx* c)
     delete c;
 }
 
-static int create_impl(mgp_ctx** out, const mgp_opts* o, mgp_loopback* lb, ncclComm_t comm = nullptr);
+static int create_impl(mgp_ctx** out, const mgp_opts* o, mgp_loopback* lb, ncclComm_t comm = nullptr,
+                       ncclComm_t xcomm = nullptr);
 
 int mgp_create(mgp_ctx** out, const mgp_opts* o) { return create_impl(out, o, nullptr); }
 
@@ -1441,6 +1683,17 @@ int mgp_create_loopback(mgp_ctx** out, const mgp_opts* o, mgp_loopback* lb)
 // the tiled one-launch phases (k_blk) and the one-launch coarse tail; shared by mgp_create and mgp_plan.
 static void select_engines(mgp_ctx* c)
 {
+    if (c->rk == mgp::kRealF32D) {
+        // cpu-raw.lua's float arithmetic (cpu-raw.lua:142-153, 186-237): every level one launch per piece through
+        // the scalar double-evaluating kernels; the err is calcFrobErr's float errorBuf summed after the cycle
+        // (cpu-raw.lua:249-254); the fused, tiled and tail engines evaluate in the real type and stay off
+        c->err_fuse = false;
+        c->fresh_sweep = false;
+        c->post1 = false;
+        for (auto& L : c->lev) L.fused = L.blk = false;
+        c->tail_level = -1;
+        return;
+    }
     c->err_fuse = c->o.err_mode && c->o.smoother == MGP_RBGS && c->o.nu1 >= 1 && c->o.nu2 >= 1 && c->lev.size() > 1;
     {
         // temporally blocked phases: RB-GS 2+2 on 3D levels of >= MGP_FUSED_MIN_CELLS cells per rank (k_zs,
@@ -1487,7 +1740,7 @@ static int level_engine(const mgp_ctx* c, int l)
     return c->tail_level >= 0 && l >= c->tail_level ? 1 : L.fused ? 2 : L.blk ? 3 : 0;
 }
 
-static int create_impl(mgp_ctx** out, const mgp_opts* o, mgp_loopback* lb, ncclComm_t ext_comm)
+static int create_impl(mgp_ctx** out, const mgp_opts* o, mgp_loopback* lb, ncclComm_t ext_comm, ncclComm_t ext_xcomm)
 {
     if (!out || !o) {
         g_create_error = "mgp_create: null argument";
@@ -1499,25 +1752,12 @@ static int create_impl(mgp_ctx** out, const mgp_opts* o, mgp_loopback* lb, ncclC
     if (rc != MGP_OK) return rc;
 
     mgp_ctx* c = new mgp_ctx();
-    c->o = *o;
-    if (ext_comm && o->world > 1) c->comm = ext_comm;  // from ncclCommInitAll (mgp_group_create); owned from here
-    if (c->o.dim == 2) c->o.n[2] = 1;
-    c->rb = o->real_bytes;
-    c->G = o->dim == 3 ? mgp::kGhost3D : 0;  // widened below when a distributed level is fused
-    {
-        const char* v = std::getenv("MGP_FRESH");
-        c->fresh_sweep = !(v && std::atoi(v) == 0);
-        const char* vb = std::getenv("MGP_POST_BLACK");
-        c->post_black = !(vb && std::atoi(vb) == 0);
-        const char* vp = std::getenv("MGP_POST1");
-        c->post1 = vp && std::atoi(vp) != 0;
+    if (ext_comm && o->world > 1) {  // from mgp_group_create (non-blocking communicators); owned from here
+        c->comm = ext_comm;
+        c->xcomm = ext_xcomm;
+        c->nb_comm = true;
     }
-    {
-        const char* v = std::getenv("MGP_DEEP_HALO");  // 0: exchange before every half-sweep instead
-        c->deep_halo = !(v && std::atoi(v) == 0);
-    }
-    // distributed 3D levels sweep with deep halos (smooth_deep): kGhostZs ghost planes per side
-    if (c->deep_halo && o->dim == 3 && o->world > 1) c->G = mgp::kGhostZs;
+    host_setup(c, *o, plan);
     auto bail = [&](int code) {
         g_create_error = c->err;
         destroy_impl(c);
@@ -1547,14 +1787,6 @@ static int create_impl(mgp_ctx** out, const mgp_opts* o, mgp_loopback* lb, ncclC
         return bail(MGP_ERR_HIP);
     }
     const size_t rb = (size_t)c->rb;
-    for (auto& p : plan) {
-        Level L;
-        L.p = p;
-        L.g = make_geo(p, c->o.dim);
-        c->lev.push_back(L);
-    }
-    select_engines(c);
-    for (auto& L : c->lev) L.alloc = L.g.P * (L.g.nz + 2 * c->G);
     for (size_t l = 0; l < c->lev.size(); ++l) {
         Level& L = c->lev[l];
         const size_t bytes = (size_t)L.alloc * rb;
@@ -1609,7 +1841,7 @@ static int create_impl(mgp_ctx** out, const mgp_opts* o, mgp_loopback* lb, ncclC
         const char* v = std::getenv("MGP_GS");
         c->use_gs = v && std::atoi(v) != 0;
     }
-    int nb2 = 2 * mgp::half_blocks(c->rb, L0.g, c->use_gs);
+    int nb2 = 2 * mgp::half_blocks(c->rk, L0.g, c->use_gs);
     if (L0.fused) nb2 = std::max(nb2, mgp::fused_blocks(c->rb, L0.g, L0.zc));
     c->part_cap = std::max<int64_t>(mgp::kSumBlocks, nb2 + mgp::sum_scratch(nb2));
     if (hipMalloc(&c->d_part, sizeof(double) * c->part_cap) != hipSuccess) {
@@ -1626,9 +1858,7 @@ static int create_impl(mgp_ctx** out, const mgp_opts* o, mgp_loopback* lb, ncclC
         c->use_graph = c->o.world == 1 && !(v && std::atoi(v) == 0) && !roctx_on();
     }
     if (c->o.smoother == MGP_RBGS && c->o.coarse_init == MGP_COARSE_FRESH) {
-        for (size_t l = 1; l < c->lev.size(); ++l)
-            if (!c->lev[l].fused && (c->tail_level < 0 || (int)l < c->tail_level))
-                c->zbuf_reals = std::max(c->zbuf_reals, c->lev[l].alloc);
+        c->zbuf_reals = zbuf_reals_of(c);
         const size_t zb = (size_t)c->zbuf_reals * rb;
         if (zb && (hipMalloc(&c->zbuf, zb) != hipSuccess || hipMemsetAsync(c->zbuf, 0, zb, c->s) != hipSuccess)) {
             c->err = "hipMalloc failed for the zero buffer";
@@ -1643,8 +1873,6 @@ static int create_impl(mgp_ctx** out, const mgp_opts* o, mgp_loopback* lb, ncclC
         return bail(MGP_ERR_HIP);
     }
     if (c->o.world > 1) {  // side stream of the early POST halo exchange
-        const char* v = std::getenv("MGP_EARLY_X");
-        if (v && std::atoi(v) == 0) c->early_x = false;
         if (c->early_x && (hipStreamCreateWithFlags(&c->xs, hipStreamNonBlocking) != hipSuccess ||
                            hipEventCreateWithFlags(&c->x_ev0, hipEventDisableTiming) != hipSuccess ||
                            hipEventCreateWithFlags(&c->x_ev1, hipEventDisableTiming) != hipSuccess)) {
@@ -1678,6 +1906,17 @@ static int create_impl(mgp_ctx** out, const mgp_opts* o, mgp_loopback* lb, ncclC
             c->err = std::string("ncclCommInitRank: ") + ncclGetErrorString(r);
             c->comm = nullptr;
             return bail(MGP_ERR_RCCL);
+        }
+        // the side stream's communicator: a collective split every rank makes at the same point (all or none:
+        // MGP_EARLY_X is the same on every rank), so that the early POST exchange does not serialise with the
+        // compute stream's exchanges of the coarse levels
+        if (c->early_x) {
+            r = ncclCommSplit(c->comm, 0, c->o.rank, &c->xcomm, nullptr);
+            if (r != ncclSuccess) {
+                c->err = std::string("ncclCommSplit (side-stream communicator): ") + ncclGetErrorString(r);
+                c->xcomm = nullptr;
+                return bail(MGP_ERR_RCCL);
+            }
         }
     }
     if (hipStreamSynchronize(c->s) != hipSuccess) {
@@ -1717,9 +1956,7 @@ int mgp_init_point_charge(mgp_ctx* c)
     const int64_t cz = c->o.dim == 3 ? L.p.gnz / 2 : 0;
     HIP_TRY(c, mgp::launch_init_point_charge(c->rb, c->o.dim, c->ui(L, L.u), c->ui(L, L.f), L.g, L.p.nx / 2,
                                              L.p.ny / 2, cz, c->s));
-    L.ghost_ok = !L.p.dist;
-    L.ghost_zero = false;
-    L.fghost_ok = !L.p.dist;
+    fields_written(c);
     return sync_and_check(c);
 }
 
@@ -1759,10 +1996,10 @@ static int field_source(mgp_ctx* c, int level, int which, char** src, char** scr
     if (which == MGP_FIELD_PSI_OLD) {
         HIP_TRY(c, hipMemcpyAsync(sc, c->metrics_old, (size_t)n * c->rb, hipMemcpyDeviceToDevice, c->s));
     } else if (which == MGP_FIELD_ERROR) {
-        HIP_TRY(c, mgp::launch_sqdiff_field(c->rb, c->ui(L, L.u), c->metrics_old, sc, n, c->s));
+        HIP_TRY(c, mgp::launch_sqdiff_field(c->rk, c->ui(L, L.u), c->metrics_old, sc, n, c->s));
     } else if (which == MGP_FIELD_RESIDUAL) {
         TRY(exchange(c, L));
-        HIP_TRY(c, mgp::launch_residual_field(c->rb, c->o.dim, c->ui(L, L.u), c->ui(L, L.f), sc, L.g, level_h(c, level),
+        HIP_TRY(c, mgp::launch_residual_field(c->rk, c->o.dim, c->ui(L, L.u), c->ui(L, L.f), sc, L.g, level_h(c, level),
                                               coarse_coef(c->o.coarse_bc, level), c->s));
     } else {  // MGP_FIELD_CORRECTION: P V onto zeros
         Level& C = c->lev[(size_t)level + 1];
@@ -1772,7 +2009,7 @@ static int field_source(mgp_ctx* c, int level, int which, char** src, char** scr
         int64_t zc = 0;
         const Geo gc = coarse_view(L, C, &zc);
         char* V = c->ui(C, C.u) + (size_t)(zc * C.g.P) * c->rb;
-        HIP_TRY(c, mgp::launch_prolong_correct(c->rb, c->o.dim, linear, sc, V, L.g, gc,
+        HIP_TRY(c, mgp::launch_prolong_correct(c->rk, c->o.dim, linear, sc, V, L.g, gc,
                                                coarse_coef(c->o.coarse_bc, level + 1), c->s));
     }
     *src = *scratch;
@@ -2031,6 +2268,9 @@ int mgp_set_coarse_level(mgp_ctx* c, int64_t size)
     }
     const int l = level_of_size(c, size);
     if (l < 0) return c->fail(MGP_ERR_ARG, "mgp_set_coarse_level: no level >= 1 with nx = %lld", (long long)size);
+    if (c->rk == mgp::kRealF32D)
+        return c->fail(MGP_ERR_ARG, "mgp_set_coarse_level: the coarse engine evaluates in the real type; arith = "
+                                    "MGP_ARITH_DOUBLE runs every level per piece");
     const int prev = c->tail_level;
     if (!try_tail(c, l)) {
         c->tail_level = prev;
@@ -2076,7 +2316,7 @@ int mgp_metrics(mgp_ctx* c, double* rel_err, int64_t* count, double* frob)
         if (c->lb)
             TRY(lb_allreduce(c, out, 3));
         else
-            NCCL_TRY(c, ncclAllReduce(out, out, 3, ncclDouble, ncclSum, c->comm, c->s));
+            NCCL_CALL(c, c->comm, ncclAllReduce(out, out, 3, ncclDouble, ncclSum, c->comm, c->s), "metrics all-reduce");
     }
     double h[3];
     HIP_TRY(c, hipMemcpyAsync(h, out, sizeof h, hipMemcpyDeviceToHost, c->s));
@@ -2095,7 +2335,7 @@ int mgp_residual_norm(mgp_ctx* c, int level, double* rnorm, double* fnorm)
     Level& L = c->lev[level];
     TRY(materialize_zero(c, L));
     TRY(exchange(c, L));
-    const int nb = mgp::resnorm_blocks(c->rb, L.g);
+    const int nb = mgp::resnorm_blocks(c->rk, L.g);
     const int64_t need = 2 * (int64_t)(nb + mgp::sum_scratch(nb)) + 2;
     if (need > c->d_rn_cap) {
         if (c->d_rn) HIP_TRY(c, hipFree(c->d_rn));
@@ -2105,13 +2345,13 @@ int mgp_residual_norm(mgp_ctx* c, int level, double* rnorm, double* fnorm)
         c->d_rn_cap = need;
     }
     double* out = c->d_rn + need - 2;
-    HIP_TRY(c, mgp::launch_residual_norm(c->rb, c->o.dim, c->ui(L, L.u), c->ui(L, L.f), L.g, level_h(c, level),
+    HIP_TRY(c, mgp::launch_residual_norm(c->rk, c->o.dim, c->ui(L, L.u), c->ui(L, L.f), L.g, level_h(c, level),
                                          coarse_coef(c->o.coarse_bc, level), c->d_rn, out, c->s));
     if (L.p.dist) {
         if (c->lb)
             TRY(lb_allreduce(c, out, 2));
         else
-            NCCL_TRY(c, ncclAllReduce(out, out, 2, ncclDouble, ncclSum, c->comm, c->s));
+            NCCL_CALL(c, c->comm, ncclAllReduce(out, out, 2, ncclDouble, ncclSum, c->comm, c->s), "norm all-reduce");
     }
     double h[2];
     HIP_TRY(c, hipMemcpyAsync(h, out, sizeof h, hipMemcpyDeviceToHost, c->s));
@@ -2196,6 +2436,23 @@ int mgp_timing(mgp_ctx* c, int enable)
     return MGP_OK;
 }
 
+int mgp_comm_log(mgp_ctx* c, int64_t* rows, int max_rows, int reset)
+{
+    if (!c || max_rows < 0 || (max_rows > 0 && !rows)) return MGP_ERR_ARG;
+    const int n = (int)c->clog.size();
+    for (int i = 0; i < n && i < max_rows; ++i) {
+        const auto& r = c->clog[(size_t)i];
+        int64_t* o = rows + 5 * i;
+        o[0] = r.op;
+        o[1] = r.side;
+        o[2] = r.level;
+        o[3] = r.msgs;
+        o[4] = r.bytes;
+    }
+    if (reset) c->clog.clear();
+    return n;
+}
+
 int mgp_timing_read(mgp_ctx* c, int kind, double* ms_total, int64_t* launches, double* bytes)
 {
     if (!c || kind < 0 || kind >= MGP_TIMING_KINDS) return MGP_ERR_ARG;
@@ -2271,8 +2528,12 @@ struct mgp_group {
 static thread_local std::string g_group_error;
 
 // Wake the ranks still blocked on a failed rank: they would otherwise wait forever in a halo exchange or
-// collective that rank never joined.  Loopback: break the host barrier.  RCCL: ncclCommAbort every
-// communicator (its outstanding kernels exit); the ranks see `stop` before touching their comm again.
+// collective that rank never joined.  Loopback: break the host barrier.  RCCL: the group's communicators are
+// non-blocking, so no rank thread sits inside an RCCL call for long (every call is polled to completion and
+// the poll checks `stop`); once `stop` is set, no rank starts another call (NcclScope counts a call before
+// it checks `stop`, so either the rank sees `stop` or this thread sees the call and waits for it), and when
+// every rank's in-flight calls have returned, each communicator is aborted from here: its outstanding
+// kernels exit, so a rank blocked in hipStreamSynchronize returns, sees `stop` and never touches it again.
 static void group_abort(mgp_group* g)
 {
     g->stop.store(true);
@@ -2282,11 +2543,15 @@ static void group_abort(mgp_group* g)
         g->lb->cv.notify_all();
         return;
     }
-    for (size_t r = 0; r < g->ranks.size(); ++r)
-        if (g->ranks[r] && g->ranks[r]->comm) {
-            (void)hipSetDevice(g->dev[r]);
-            (void)ncclCommAbort(g->ranks[r]->comm);
-        }
+    for (auto* c : g->ranks)
+        while (c && c->in_nccl.load() > 0) std::this_thread::yield();
+    for (size_t r = 0; r < g->ranks.size(); ++r) {
+        mgp_ctx* c = g->ranks[r];
+        if (!c) continue;
+        (void)hipSetDevice(g->dev[r]);
+        if (c->xcomm) (void)ncclCommAbort(c->xcomm);
+        if (c->comm) (void)ncclCommAbort(c->comm);
+    }
 }
 
 // Run fn(rank context, r) on every rank, each in its own host thread with its device current (the
@@ -2307,7 +2572,8 @@ static int group_run(mgp_group* g, const std::function<int(mgp_ctx*, int)>& fn)
     int done = 0;
     bool failed = false;
     int first = -1;  // the rank that failed first: the root cause (the others may fail because of it)
-    // test hook: this rank fails at once, before any exchange (tests/test_gpu_group.py)
+    // test hook: this rank fails at once, before any exchange (tests/test_gpu_group.py); read per call so that
+    // a test can set it for one group only
     const char* fr = std::getenv("MGP_TEST_FAIL_RANK");
     const int fail_rank = fr ? std::atoi(fr) : -1;
     std::vector<std::thread> th;
@@ -2331,16 +2597,25 @@ static int group_run(mgp_group* g, const std::function<int(mgp_ctx*, int)>& fn)
             cv.notify_all();
         });
     {
+        // after a failure, the others either finish (work that needs no peer) or block on the failed rank in an
+        // exchange or collective (or in the stream synchronisation after one): abort only in that case, checked
+        // every 2 s (a healthy rank doing long local work is not cut off)
         std::unique_lock<std::mutex> lk(m);
         cv.wait(lk, [&] { return done == n || failed; });
-        if (done < n && !cv.wait_for(lk, std::chrono::seconds(2), [&] { return done == n; })) {
-            lk.unlock();
-            group_abort(g);
+        while (done < n && !cv.wait_for(lk, std::chrono::seconds(2), [&] { return done == n; })) {
+            bool blocked = false;
+            for (int r = 0; r < n; ++r)
+                blocked = blocked || (r != first && g->ranks[(size_t)r]->waiting.load() > 0);
+            if (blocked) {
+                lk.unlock();
+                group_abort(g);
+                break;
+            }
         }
     }
     for (auto& t : th) t.join();
     if (g->stop.load() && !g->lb)
-        for (auto* c : g->ranks) c->comm = nullptr;  // freed by ncclCommAbort
+        for (auto* c : g->ranks) c->comm = c->xcomm = nullptr;  // freed by ncclCommAbort
     if (first >= 0) {
         g->err = "rank " + std::to_string(first) + ": " + g->ranks[(size_t)first]->err;
         return rc[(size_t)first];
@@ -2359,6 +2634,59 @@ void mgp_group_destroy(mgp_group* g)
         }
     delete g->lb;
     delete g;
+}
+
+// The group's communicators: one rank per device, created by this one thread as NON-BLOCKING communicators
+// (ncclConfig_t.blocking = 0; group_abort may then abort them from another thread), plus each rank's side-stream
+// communicator (a grouped ncclCommSplit).  Returns nullptr or an error message.
+static const char* group_comms(const std::vector<int>& dev, std::vector<ncclComm_t>& comms, std::vector<ncclComm_t>& xcomms)
+{
+    static thread_local std::string msg;
+    const int n = (int)dev.size();
+    auto wait_all = [&](std::vector<ncclComm_t>& cs, const char* what) -> const char* {
+        for (auto cm : cs) {
+            ncclResult_t st = ncclInProgress;
+            while (st == ncclInProgress)
+                if (ncclCommGetAsyncError(cm, &st) != ncclSuccess) st = ncclInternalError;
+            if (st != ncclSuccess) {
+                msg = std::string(what) + ": " + ncclGetErrorString(st);
+                return msg.c_str();
+            }
+        }
+        return nullptr;
+    };
+    ncclUniqueId id;
+    ncclResult_t r = ncclGetUniqueId(&id);
+    if (r != ncclSuccess) {
+        msg = std::string("ncclGetUniqueId: ") + ncclGetErrorString(r);
+        return msg.c_str();
+    }
+    ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+    cfg.blocking = 0;
+    r = ncclGroupStart();
+    for (int q = 0; q < n && (r == ncclSuccess || r == ncclInProgress); ++q) {
+        (void)hipSetDevice(dev[(size_t)q]);
+        r = ncclCommInitRankConfig(&comms[(size_t)q], n, id, q, &cfg);
+    }
+    const ncclResult_t e = ncclGroupEnd();
+    if (r == ncclSuccess) r = e;
+    if (r != ncclSuccess && r != ncclInProgress) {
+        msg = std::string("ncclCommInitRankConfig (non-blocking): ") + ncclGetErrorString(r);
+        return msg.c_str();
+    }
+    if (const char* m = wait_all(comms, "communicator init")) return m;
+    r = ncclGroupStart();
+    for (int q = 0; q < n && (r == ncclSuccess || r == ncclInProgress); ++q) {
+        (void)hipSetDevice(dev[(size_t)q]);
+        r = ncclCommSplit(comms[(size_t)q], 0, q, &xcomms[(size_t)q], &cfg);
+    }
+    const ncclResult_t e2 = ncclGroupEnd();
+    if (r == ncclSuccess) r = e2;
+    if (r != ncclSuccess && r != ncclInProgress) {
+        msg = std::string("ncclCommSplit (side-stream communicators): ") + ncclGetErrorString(r);
+        return msg.c_str();
+    }
+    return wait_all(xcomms, "side-stream communicator split");
 }
 
 int mgp_group_create(mgp_group** out, const mgp_opts* o, int ngpu, const int* devices)
@@ -2384,13 +2712,13 @@ int mgp_group_create(mgp_group** out, const mgp_opts* o, int ngpu, const int* de
             return rc;
         }
     }
-    std::vector<ncclComm_t> comms((size_t)ngpu, nullptr);
+    std::vector<ncclComm_t> comms((size_t)ngpu, nullptr), xcomms((size_t)ngpu, nullptr);
     if (ngpu > 1 && same) {
         mgp_loopback_create(&g->lb, ngpu);
     } else if (ngpu > 1) {
-        const ncclResult_t r = ncclCommInitAll(comms.data(), ngpu, g->dev.data());
-        if (r != ncclSuccess) {
-            g_create_error = std::string("ncclCommInitAll: ") + ncclGetErrorString(r);
+        const char* rc_msg = group_comms(g->dev, comms, xcomms);
+        if (rc_msg) {
+            g_create_error = rc_msg;
             delete g;
             return MGP_ERR_RCCL;
         }
@@ -2399,11 +2727,13 @@ int mgp_group_create(mgp_group** out, const mgp_opts* o, int ngpu, const int* de
     for (int r = 0; r < ngpu; ++r) {
         ro.rank = r;
         ro.device = g->dev[(size_t)r];
-        const int rc = create_impl(&g->ranks[(size_t)r], &ro, g->lb, comms[(size_t)r]);
+        const int rc = create_impl(&g->ranks[(size_t)r], &ro, g->lb, comms[(size_t)r], xcomms[(size_t)r]);
         if (rc == MGP_OK) g->ranks[(size_t)r]->group_stop = &g->stop;
         if (rc != MGP_OK) {
-            for (int q = r + 1; q < ngpu; ++q)
+            for (int q = r + 1; q < ngpu; ++q) {
+                if (xcomms[(size_t)q]) (void)ncclCommDestroy(xcomms[(size_t)q]);
                 if (comms[(size_t)q]) (void)ncclCommDestroy(comms[(size_t)q]);
+            }
             const std::string e = g_create_error;
             mgp_group_destroy(g);
             g_create_error = "rank " + std::to_string(r) + ": " + e;

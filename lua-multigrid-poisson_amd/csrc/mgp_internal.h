@@ -34,6 +34,13 @@ struct Geo {
 // Launchers enqueue on `s` and return the launch's hipGetLastError().  rb = sizeof(real),
 // dim = 2 or 3.  `fine` selects the finest-level instantiation (a distinct symbol, so rocprofv3
 // reports the finest smoother on its own line).
+//
+// The launchers of the per-piece cycle (half-sweep, residual + restriction, full weighting, prolongation +
+// correction, err sum, the residual / errorBuf views and the residual norm) also take rb = kRealF32D:
+// float buffers with every expression evaluated in double and rounded once at the store — cpu-raw.lua
+// under real = 'float' (cpu-raw.lua:142-153: LuaJIT numbers are doubles; mgp_opts.arith =
+// MGP_ARITH_DOUBLE).  Those run the scalar kernels templated on the compute type (C = double).
+constexpr int kRealF32D = 12;
 
 // f = -1e6 at global (cx, cy, cz), 0 elsewhere; u = -f (cpu.lua:180-193).
 hipError_t launch_init_point_charge(int rb, int dim, void* u, void* f, Geo g, int64_t cx, int64_t cy,

@@ -576,9 +576,11 @@ __global__ __launch_bounds__(kBlock) void k_half_gs(const T* __restrict__ other,
 
 // One colour-c slot of a half-sweep (scalar; any level size, nx = 1 included).  Returns the
 // packed index written, or -1 for the empty slot of an nx = 1 row; *v = the new value.
-template <typename T, int DIM>
+// C: the type the expression is evaluated in (C = double with T = float: cpu-raw.lua's real = 'float',
+// LuaJIT doubles rounded once at the store, cpu-raw.lua:34-44); with C = T every cast is the identity.
+template <typename T, int DIM, typename C = T>
 __device__ __forceinline__ int64_t half_item(const T* other, const T* __restrict__ f, T* dst, const Geo& g,
-                                             int color, const Op<T, DIM>& op, int64_t it, T* v)
+                                             int color, const Op<C, DIM>& op, int64_t it, T* v)
 {
     const int m = (int)(it & (g.hw - 1));
     const int j = (int)((it >> g.lhw) & (g.ny - 1));
@@ -589,34 +591,35 @@ __device__ __forceinline__ int64_t half_item(const T* other, const T* __restrict
     if (i >= g.nx) return -1;
     const int64_t own = k * g.P + color * g.H + (int64_t)j * g.hw + m;
     const int64_t oth = k * g.P + (color ^ 1) * g.H + (int64_t)j * g.hw + m;
-    const T xl = i > 0 ? other[oth - 1 + o] : (T)0;
-    const T xr = i < g.nx - 1 ? other[oth + o] : (T)0;
-    T s = xl + xr;
-    s = s + (j > 0 ? other[oth - g.hw] : (T)0);
-    s = s + (j < g.ny - 1 ? other[oth + g.hw] : (T)0);
+    const C xl = i > 0 ? (C)other[oth - 1 + o] : (C)0;
+    const C xr = i < g.nx - 1 ? (C)other[oth + o] : (C)0;
+    C s = xl + xr;
+    s = s + (j > 0 ? (C)other[oth - g.hw] : (C)0);
+    s = s + (j < g.ny - 1 ? (C)other[oth + g.hw] : (C)0);
     if (DIM == 3) {
-        s = s + other[oth - g.P];
-        s = s + other[oth + g.P];
+        s = s + (C)other[oth - g.P];
+        s = s + (C)other[oth + g.P];
     }
     const int nb = (i == 0) + (i == g.nx - 1) + (j == 0) + (j == g.ny - 1) +
                    (DIM == 3 ? (gk == 0) + (gk == g.gnz - 1) : 0);
-    *v = op.relax(s, f[own], nb);
+    *v = (T)op.relax(s, (C)f[own], nb);
     dst[own] = *v;
     return own;
 }
 
-// Scalar form for small levels (hw < N, nx = 1 included): a thread per colour-c slot.
-template <typename T, int DIM, bool ERR>
+// Scalar form for small levels (hw < N, nx = 1 included) and for the cpu-raw float arithmetic
+// (C = double, every level): a thread per colour-c slot.
+template <typename T, int DIM, bool ERR, typename C = T>
 __global__ __launch_bounds__(kBlock) void k_half_s(const T* __restrict__ other, const T* __restrict__ f,
                                                    T* __restrict__ dst, const T* __restrict__ old,
                                                    double* __restrict__ partials, Geo g, int color,
-                                                   Op<T, DIM> op)
+                                                   Op<C, DIM> op)
 {
     const int64_t it = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     double acc = 0.0;
     if (it < g.H * g.nz) {
         T v;
-        const int64_t own = half_item<T, DIM>(other, f, dst, g, color, op, it, &v);
+        const int64_t own = half_item<T, DIM, C>(other, f, dst, g, color, op, it, &v);
         if (ERR && own >= 0) {
             const double d = (double)v - (double)old[own];
             acc += d * d;
@@ -718,27 +721,27 @@ __global__ __launch_bounds__(kBlock) void k_fresh(const T* __restrict__ f, T* __
 
 // ---- fused residual + restriction -----------------------------------------------------------
 
-// Residual of one fine cell from packed u (generic, scalar loads).
-template <typename T, int DIM>
-__device__ __forceinline__ T residual_at(const T* __restrict__ u, const T* __restrict__ f, const Geo& g,
-                                         const Op<T, DIM>& op, int i, int j, int64_t k)
+// Residual of one fine cell from packed u (generic, scalar loads), evaluated in C (half_item's C).
+template <typename T, int DIM, typename C = T>
+__device__ __forceinline__ C residual_at(const T* __restrict__ u, const T* __restrict__ f, const Geo& g,
+                                         const Op<C, DIM>& op, int i, int j, int64_t k)
 {
     const int64_t c = pidx(g, i, j, k);
     const int o = i & 1;
     // neighbours: other colour, same row at m-1+o / m+o; rows j+-1 and planes k+-1 at m
     const int64_t oth = c + ((c - k * g.P) >= g.H ? -g.H : g.H);
-    const T xl = i > 0 ? u[oth - 1 + o] : (T)0;
-    const T xr = i < g.nx - 1 ? u[oth + o] : (T)0;
-    T s = xl + xr;
-    s = s + (j > 0 ? u[oth - g.hw] : (T)0);
-    s = s + (j < g.ny - 1 ? u[oth + g.hw] : (T)0);
+    const C xl = i > 0 ? (C)u[oth - 1 + o] : (C)0;
+    const C xr = i < g.nx - 1 ? (C)u[oth + o] : (C)0;
+    C s = xl + xr;
+    s = s + (j > 0 ? (C)u[oth - g.hw] : (C)0);
+    s = s + (j < g.ny - 1 ? (C)u[oth + g.hw] : (C)0);
     const int64_t gk = g.z0 + k;
     if (DIM == 3) {
-        s = s + u[oth - g.P];
-        s = s + u[oth + g.P];
+        s = s + (C)u[oth - g.P];
+        s = s + (C)u[oth + g.P];
     }
     const int nb = (i == 0) + (i == g.nx - 1) + (j == 0) + (j == g.ny - 1) + (DIM == 3 ? (gk == 0) + (gk == g.gnz - 1) : 0);
-    return op.residual(s, f[c], u[c], nb);
+    return op.residual(s, (C)f[c], (C)u[c], nb);
 }
 
 // ---- residual norm (north star: wavefront-level reductions for the residual norm) -------------
@@ -901,10 +904,11 @@ __global__ __launch_bounds__(kBlock) void k_resnorm_z(const T* __restrict__ u, c
     }
 }
 
-// Scalar form for small levels (hw < N, nx = 1 included): a thread per packed slot.
-template <typename T, int DIM>
+// Scalar form for small levels (hw < N, nx = 1 included), and for the cpu-raw float arithmetic (C = double:
+// r evaluated in double and rounded to the real type, as rs[L] would hold it): a thread per packed slot.
+template <typename T, int DIM, typename C = T>
 __global__ __launch_bounds__(kBlock) void k_resnorm_s(const T* __restrict__ u, const T* __restrict__ f, Geo g,
-                                                      Op<T, DIM> op, double* __restrict__ partials, int fofs)
+                                                      Op<C, DIM> op, double* __restrict__ partials, int fofs)
 {
     const int64_t s = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     double rr = 0.0, ff = 0.0;
@@ -912,7 +916,7 @@ __global__ __launch_bounds__(kBlock) void k_resnorm_s(const T* __restrict__ u, c
         int i, j;
         int64_t k;
         if (slot_cell(s, g, i, j, k)) {
-            const T r = residual_at<T, DIM>(u, f, g, op, i, j, k);
+            const T r = (T)residual_at<T, DIM, C>(u, f, g, op, i, j, k);
             rr = (double)r * (double)r;
             ff = (double)f[s] * (double)f[s];
         }
@@ -939,33 +943,36 @@ __global__ __launch_bounds__(kBlock) void k_resnorm_s(const T* __restrict__ u, c
 
 // rs[L] of cpu-raw.lua:155-171 (calcResidual, cpu.lua:108-123) materialised on request (mgp_get_field
 // MGP_FIELD_RESIDUAL): r at every packed slot, grid-stride.
-template <typename T, int DIM>
+template <typename T, int DIM, typename C = T>
 __global__ __launch_bounds__(kBlock) void k_residual_field(const T* __restrict__ u, const T* __restrict__ f,
-                                                           T* __restrict__ r, Geo g, Op<T, DIM> op)
+                                                           T* __restrict__ r, Geo g, Op<C, DIM> op)
 {
     const int64_t n = g.P * g.nz;
     for (int64_t s = (int64_t)blockIdx.x * kBlock + threadIdx.x; s < n; s += (int64_t)gridDim.x * kBlock) {
         int i, j;
         int64_t k;
-        r[s] = slot_cell(s, g, i, j, k) ? residual_at<T, DIM>(u, f, g, op, i, j, k) : (T)0;
+        r[s] = slot_cell(s, g, i, j, k) ? (T)residual_at<T, DIM, C>(u, f, g, op, i, j, k) : (T)0;
     }
 }
 
-// errorBuf of cpu-raw.lua:96-100 / gpu.lua:189-200 (calcFrobErr): (psi - psiOld)^2 per cell, in real.
-template <typename T>
+// errorBuf of cpu-raw.lua:96-100 / gpu.lua:189-200 (calcFrobErr): (psi - psiOld)^2 per cell, evaluated in C
+// (gpu.lua: real; cpu-raw.lua: LuaJIT double) and stored in real.
+template <typename T, typename C = T>
 __global__ __launch_bounds__(kBlock) void k_sqdiff_field(const T* __restrict__ a, const T* __restrict__ b,
                                                          T* __restrict__ out, int64_t n)
 {
     for (int64_t s = (int64_t)blockIdx.x * kBlock + threadIdx.x; s < n; s += (int64_t)gridDim.x * kBlock) {
-        const T d = a[s] - b[s];
-        out[s] = d * d;
+        const C d = (C)a[s] - (C)b[s];
+        out[s] = (T)(d * d);
     }
 }
 
-// One coarse cell of the fused residual + restriction (scalar; any sizes).
-template <typename T, int DIM>
+// One coarse cell of the fused residual + restriction (scalar; any sizes).  C = double (cpu-raw.lua's float):
+// each child residual is rounded to the real type first (calcResidual stores it in rs[L], cpu-raw.lua:211),
+// then summed and scaled in double and rounded once (reduceResidual, cpu-raw.lua:59-63).
+template <typename T, int DIM, typename C = T>
 __device__ __forceinline__ void resrestrict_item(const T* u, const T* f, T* R, const Geo& g, const Geo& gc,
-                                                 const Op<T, DIM>& op, int64_t it)
+                                                 const Op<C, DIM>& op, int64_t it)
 {
     const int cx = g.nx >> 1, cy = g.ny >> 1;
     const int lcx = g.lx - 1, lcy = g.ly - 1;
@@ -974,17 +981,18 @@ __device__ __forceinline__ void resrestrict_item(const T* u, const T* f, T* R, c
     const int64_t K = it >> (lcx + lcy);
     const int i = 2 * I, j = 2 * J;
     const int64_t k = DIM == 3 ? 2 * K : 0;
-    T s = residual_at<T, DIM>(u, f, g, op, i, j, k) + residual_at<T, DIM>(u, f, g, op, i + 1, j, k);
-    s = s + residual_at<T, DIM>(u, f, g, op, i, j + 1, k);
-    s = s + residual_at<T, DIM>(u, f, g, op, i + 1, j + 1, k);
+    auto r = [&](int a, int b, int64_t c) { return (C)(T)residual_at<T, DIM, C>(u, f, g, op, a, b, c); };
+    C s = r(i, j, k) + r(i + 1, j, k);
+    s = s + r(i, j + 1, k);
+    s = s + r(i + 1, j + 1, k);
     if (DIM == 3) {
-        s = s + residual_at<T, DIM>(u, f, g, op, i, j, k + 1);
-        s = s + residual_at<T, DIM>(u, f, g, op, i + 1, j, k + 1);
-        s = s + residual_at<T, DIM>(u, f, g, op, i, j + 1, k + 1);
-        s = s + residual_at<T, DIM>(u, f, g, op, i + 1, j + 1, k + 1);
-        R[pidx(gc, I, J, K)] = (T)0.125 * s;
+        s = s + r(i, j, k + 1);
+        s = s + r(i + 1, j, k + 1);
+        s = s + r(i, j + 1, k + 1);
+        s = s + r(i + 1, j + 1, k + 1);
+        R[pidx(gc, I, J, K)] = (T)((C)0.125 * s);
     } else {
-        R[pidx(gc, I, J, 0)] = (T)0.25 * s;
+        R[pidx(gc, I, J, 0)] = (T)((C)0.25 * s);
     }
 }
 
@@ -994,14 +1002,14 @@ __device__ __forceinline__ int64_t resrestrict_items(const Geo& g)
     return (int64_t)(g.nx >> 1) * (g.ny >> 1) * (DIM == 3 ? (g.nz >> 1) : 1);
 }
 
-// Scalar form: a thread per coarse cell (any sizes).
-template <typename T, int DIM>
+// Scalar form: a thread per coarse cell (any sizes; every level under the cpu-raw float arithmetic).
+template <typename T, int DIM, typename C = T>
 __global__ __launch_bounds__(kBlock) void k_resrestrict_s(const T* __restrict__ u, const T* __restrict__ f,
-                                                          T* __restrict__ R, Geo g, Geo gc, Op<T, DIM> op)
+                                                          T* __restrict__ R, Geo g, Geo gc, Op<C, DIM> op)
 {
     const int64_t it = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (it >= resrestrict_items<T, DIM>(g)) return;
-    resrestrict_item<T, DIM>(u, f, R, g, gc, op, it);
+    resrestrict_item<T, DIM, C>(u, f, R, g, gc, op, it);
 }
 
 // Vector form: a thread owns N consecutive coarse cells I0 .. I0+N-1 of one coarse row.  Their
@@ -1212,17 +1220,18 @@ __global__ __launch_bounds__(kBlock) void k_resfield_v(const T* __restrict__ u, 
     vstore<T, N>(r + in.own, out);
 }
 
-// Scalar form: a thread per coarse cell (any sizes), r packed with readable planes -1 and g.nz
-template <typename T, int DIM>
-__global__ __launch_bounds__(kBlock) void k_fw_s(const T* __restrict__ r, T* __restrict__ R, Geo g, Geo gc, T wf)
+// Scalar form: a thread per coarse cell (any sizes), r packed with readable planes -1 and g.nz; evaluated in
+// C (double under the cpu-raw float arithmetic) and rounded once
+template <typename T, int DIM, typename C = T>
+__global__ __launch_bounds__(kBlock) void k_fw_s(const T* __restrict__ r, T* __restrict__ R, Geo g, Geo gc, C wf)
 {
     const int64_t it = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (it >= resrestrict_items<T, DIM>(g)) return;
     const int cx = g.nx >> 1, cy = g.ny >> 1;
     const int I = (int)(it % cx), J = (int)((it / cx) % cy);
     const int64_t K = it / ((int64_t)cx * cy);
-    auto get = [&](int i, int j, int64_t k) { return r[pidx(g, i, j, k)]; };
-    R[pidx(gc, I, J, K)] = fw_eval<T, DIM>(get, g, gc, wf, I, J, K);
+    auto get = [&](int i, int j, int64_t k) { return (C)r[pidx(g, i, j, k)]; };
+    R[pidx(gc, I, J, K)] = (T)fw_eval<C, DIM>(get, g, gc, wf, I, J, K);
 }
 
 // Vector form (coarse nx >= N): a thread owns N consecutive coarse cells I0 .. of one coarse row; each
@@ -1360,9 +1369,11 @@ __device__ __forceinline__ T prolong_value(const T* V, const Geo& g, const Geo& 
     return prolong_eval<T, DIM, LINEAR>(get, gc, cl, i, j, k);
 }
 
-// One fine slot of colour `color` of the prolongation + correction (scalar; any sizes).
-template <typename T, int DIM, int LINEAR>
-__device__ __forceinline__ void prolong_item(T* u, const T* V, const Geo& g, const Geo& gc, T cl, int color,
+// One fine slot of colour `color` of the prolongation + correction (scalar; any sizes).  C = double
+// (cpu-raw.lua's float): P V evaluated in double and rounded into the real type (the vs[L] buffer,
+// cpu-raw.lua:226), then addTo's u + v in double, rounded once (cpu-raw.lua:83-85).
+template <typename T, int DIM, int LINEAR, typename C = T>
+__device__ __forceinline__ void prolong_item(T* u, const T* V, const Geo& g, const Geo& gc, C cl, int color,
                                              int64_t it)
 {
     const int m = (int)(it & (g.hw - 1));
@@ -1372,18 +1383,19 @@ __device__ __forceinline__ void prolong_item(T* u, const T* V, const Geo& g, con
     const int i = 2 * m + o;
     if (i >= g.nx) return;
     const int64_t own = k * g.P + color * g.H + (int64_t)j * g.hw + m;
-    const T v = prolong_value<T, DIM, LINEAR>(V, g, gc, cl, i, j, k);
-    u[own] = u[own] + v;
+    auto get = [&](int I, int J, int64_t K) { return (C)V[pidx(gc, I, J, K)]; };
+    const T v = (T)prolong_eval<C, DIM, LINEAR>(get, gc, cl, i, j, k);
+    u[own] = (T)((C)u[own] + (C)v);
 }
 
 // a thread per fine slot of colour `color` (any sizes)
-template <typename T, int DIM, int LINEAR>
+template <typename T, int DIM, int LINEAR, typename C = T>
 __global__ __launch_bounds__(kBlock) void k_prolong(T* __restrict__ u, const T* __restrict__ V, Geo g, Geo gc,
                                                     double clc, int color)
 {
     const int64_t it = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (it >= g.H * g.nz) return;
-    prolong_item<T, DIM, LINEAR>(u, V, g, gc, (T)clc, color, it);
+    prolong_item<T, DIM, LINEAR, C>(u, V, g, gc, (C)clc, color, it);
 }
 
 // Coarse samples x = I0-1 .. I0+N of coarse row (Jr, Kr) (Kr relative to the V pointer) into
@@ -3669,14 +3681,15 @@ __global__ __launch_bounds__(kBlock) void k_copy16(const float4* __restrict__ sr
 
 // ---- reductions -----------------------------------------------------------------------------
 
-template <typename T>
+// ROUND: each square is first stored into the real-typed errorBuf (cpu-raw.lua:96-100, 249-253)
+template <typename T, bool ROUND = false>
 __global__ __launch_bounds__(kBlock) void k_sqdiff_partial(const T* __restrict__ a, const T* __restrict__ b,
                                                            int64_t n, double* __restrict__ partials)
 {
     double acc = 0.0;
     for (int64_t c = (int64_t)blockIdx.x * kBlock + threadIdx.x; c < n; c += (int64_t)gridDim.x * kBlock) {
         const double d = (double)a[c] - (double)b[c];
-        acc += d * d;
+        acc += ROUND ? (double)(T)(d * d) : d * d;
     }
     block_partial<T>(acc, partials);
 }
@@ -3806,6 +3819,7 @@ static bool resnorm_z_ok(int rb, const Geo& g)
 
 int resnorm_blocks(int rb, Geo g)
 {
+    if (rb == kRealF32D) return (int)nblk(g.P * g.nz);
     const int n = 16 / rb;
     if (resnorm_z_ok(rb, g)) return (int)nblk((int64_t)(g.hw / n) * g.ny * (g.nz / kResZ));
     return (g.hw >= n && g.nx >= 2) ? (int)nblk(2 * (g.H / n) * g.nz) : (int)nblk(g.P * g.nz);
@@ -3835,6 +3849,19 @@ static void resnorm_t(const void* u, const void* f, Geo g, double h, double cl, 
 hipError_t launch_residual_norm(int rb, int dim, const void* u, const void* f, Geo g, double h, double cl,
                                 double* partials, double* out, hipStream_t s)
 {
+    if (rb == kRealF32D) {  // the scalar form, r evaluated in double (resnorm_blocks(kRealF32D) counts it)
+        const unsigned nb = (unsigned)resnorm_blocks(rb, g);
+        const int fofs = (int)nb + sum_scratch((int)nb);
+        if (dim == 3)
+            k_resnorm_s<float, 3, double><<<nb, kBlock, 0, s>>>((const float*)u, (const float*)f, g,
+                                                                make_op<double, 3>(h, cl), partials, fofs);
+        else
+            k_resnorm_s<float, 2, double><<<nb, kBlock, 0, s>>>((const float*)u, (const float*)f, g,
+                                                                make_op<double, 2>(h, cl), partials, fofs);
+        (void)launch_sum_partials(partials, (int)nb, out, s);
+        (void)launch_sum_partials(partials + fofs, (int)nb, out + 1, s);
+        return hipGetLastError();
+    }
     if (rb == 8) {
         if (dim == 3) resnorm_t<double, 3>(u, f, g, h, cl, partials, out, s);
         else resnorm_t<double, 2>(u, f, g, h, cl, partials, out, s);
@@ -3849,6 +3876,11 @@ hipError_t launch_residual_field(int rb, int dim, const void* u, const void* f, 
                                  hipStream_t s)
 {
     const unsigned nb = nblk_gs(g.P * g.nz);
+    if (rb == kRealF32D) {
+        if (dim == 3) k_residual_field<float, 3, double><<<nb, kBlock, 0, s>>>((const float*)u, (const float*)f, (float*)r, g, make_op<double, 3>(h, cl));
+        else k_residual_field<float, 2, double><<<nb, kBlock, 0, s>>>((const float*)u, (const float*)f, (float*)r, g, make_op<double, 2>(h, cl));
+        return hipGetLastError();
+    }
     if (rb == 8) {
         if (dim == 3) k_residual_field<double, 3><<<nb, kBlock, 0, s>>>((const double*)u, (const double*)f, (double*)r, g, make_op<double, 3>(h, cl));
         else k_residual_field<double, 2><<<nb, kBlock, 0, s>>>((const double*)u, (const double*)f, (double*)r, g, make_op<double, 2>(h, cl));
@@ -3861,6 +3893,10 @@ hipError_t launch_residual_field(int rb, int dim, const void* u, const void* f, 
 
 hipError_t launch_sqdiff_field(int rb, const void* a, const void* b, void* out, int64_t n, hipStream_t s)
 {
+    if (rb == kRealF32D) {
+        k_sqdiff_field<float, double><<<nblk_gs(n), kBlock, 0, s>>>((const float*)a, (const float*)b, (float*)out, n);
+        return hipGetLastError();
+    }
     MGP_REAL(rb, (k_sqdiff_field<T><<<nblk_gs(n), kBlock, 0, s>>>((const T*)a, (const T*)b, (T*)out, n)));
     return hipGetLastError();
 }
@@ -3889,6 +3925,7 @@ static bool half_gs(int rb, const Geo& g, bool gs)
 
 int half_blocks(int rb, Geo g, bool gs)
 {
+    if (rb == kRealF32D) return (int)nblk(g.H * g.nz);  // scalar k_half_s
     return half_gs(rb, g, gs) ? kGsBlocks : (int)nblk(half_items(rb, g));
 }
 
@@ -3931,10 +3968,26 @@ static void half_t(bool fine, bool err, bool vec, bool gs, unsigned nb, int colo
     }
 }
 
+// cpu-raw.lua's float arithmetic: a thread per slot, evaluated in double, stored as float
+template <int D>
+static void half_f32d(bool err, unsigned nb, int color, const void* other, const void* f, void* dst, const void* old,
+                      double* partials, Geo g, double h, double cl, hipStream_t s)
+{
+    const Op<double, D> op = make_op<double, D>(h, cl);
+    const float *o_ = (const float*)other, *f_ = (const float*)f, *w_ = (const float*)old;
+    if (err) k_half_s<float, D, true, double><<<nb, kBlock, 0, s>>>(o_, f_, (float*)dst, w_, partials, g, color, op);
+    else k_half_s<float, D, false, double><<<nb, kBlock, 0, s>>>(o_, f_, (float*)dst, w_, partials, g, color, op);
+}
+
 hipError_t launch_half_sweep(int rb, int dim, bool fine, int color, const void* other, const void* f, void* dst,
                              const void* old, double* partials, Geo g, double h, double cl, bool gs, hipStream_t s)
 {
     const unsigned nb = (unsigned)half_blocks(rb, g, gs);
+    if (rb == kRealF32D) {
+        if (dim == 3) half_f32d<3>(old != nullptr, nb, color, other, f, dst, old, partials, g, h, cl, s);
+        else half_f32d<2>(old != nullptr, nb, color, other, f, dst, old, partials, g, h, cl, s);
+        return hipGetLastError();
+    }
     const bool err = old != nullptr, vec = half_vector(rb, g);
     if (rb == 8) {
         if (dim == 3) half_t<double, 3>(fine, err, vec, gs, nb, color, other, f, dst, old, partials, g, h, cl, s);
@@ -4029,6 +4082,16 @@ static void rr_t(const void* u, const void* f, void* R, Geo g, Geo gc, double h,
 hipError_t launch_residual_restrict(int rb, int dim, const void* u, const void* f, void* R, Geo g, Geo gc, double h,
                                     double cl, hipStream_t s)
 {
+    if (rb == kRealF32D) {
+        const int64_t items = (int64_t)(g.nx / 2) * (g.ny / 2) * (dim == 3 ? g.nz / 2 : 1);
+        if (dim == 3)
+            k_resrestrict_s<float, 3, double><<<nblk(items), kBlock, 0, s>>>((const float*)u, (const float*)f, (float*)R, g,
+                                                                            gc, make_op<double, 3>(h, cl));
+        else
+            k_resrestrict_s<float, 2, double><<<nblk(items), kBlock, 0, s>>>((const float*)u, (const float*)f, (float*)R, g,
+                                                                            gc, make_op<double, 2>(h, cl));
+        return hipGetLastError();
+    }
     if (rb == 8) {
         if (dim == 3) rr_t<double, 3>(u, f, R, g, gc, h, cl, s);
         else rr_t<double, 2>(u, f, R, g, gc, h, cl, s);
@@ -4054,6 +4117,7 @@ static void resfield_t(const void* u, const void* f, void* r, Geo g, double h, d
 hipError_t launch_residual_field_v(int rb, int dim, const void* u, const void* f, void* r, Geo g, double h, double cl,
                                    hipStream_t s)
 {
+    if (rb == kRealF32D) return launch_residual_field(rb, dim, u, f, r, g, h, cl, s);
     if (rb == 8) {
         if (dim == 3) resfield_t<double, 3>(u, f, r, g, h, cl, s);
         else resfield_t<double, 2>(u, f, r, g, h, cl, s);
@@ -4082,6 +4146,13 @@ static void fw_t(const void* r, void* R, Geo g, Geo gc, double clc, hipStream_t 
 
 hipError_t launch_fw_restrict(int rb, int dim, const void* r, void* R, Geo g, Geo gc, double clc, hipStream_t s)
 {
+    if (rb == kRealF32D) {
+        const int64_t items = (int64_t)(g.nx / 2) * (g.ny / 2) * (dim == 3 ? g.nz / 2 : 1);
+        const double wf = 3.0 - clc;
+        if (dim == 3) k_fw_s<float, 3, double><<<nblk(items), kBlock, 0, s>>>((const float*)r, (float*)R, g, gc, wf);
+        else k_fw_s<float, 2, double><<<nblk(items), kBlock, 0, s>>>((const float*)r, (float*)R, g, gc, wf);
+        return hipGetLastError();
+    }
     if (rb == 8) {
         if (dim == 3) fw_t<double, 3>(r, R, g, gc, clc, s);
         else fw_t<double, 2>(r, R, g, gc, clc, s);
@@ -4118,9 +4189,24 @@ static hipError_t pr_t(int linear, void* u, const void* V, Geo g, Geo gc, double
     return hipSuccess;
 }
 
+template <int D>
+static hipError_t pr_f32d(int linear, void* u, const void* V, Geo g, Geo gc, double clc, bool black, hipStream_t s)
+{
+    for (int color = black ? 1 : 0; color < 2; ++color) {
+        const unsigned nb = nblk(g.H * g.nz);
+        if (linear) k_prolong<float, D, 1, double><<<nb, kBlock, 0, s>>>((float*)u, (const float*)V, g, gc, clc, color);
+        else k_prolong<float, D, 0, double><<<nb, kBlock, 0, s>>>((float*)u, (const float*)V, g, gc, clc, color);
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+
 hipError_t launch_prolong_correct(int rb, int dim, int linear, void* u, const void* V, Geo g, Geo gc, double clc,
                                   hipStream_t s, bool black_only)
 {
+    if (rb == kRealF32D)
+        return dim == 3 ? pr_f32d<3>(linear, u, V, g, gc, clc, black_only, s) : pr_f32d<2>(linear, u, V, g, gc, clc, black_only, s);
     if (rb == 8)
         return dim == 3 ? pr_t<double, 3>(linear, u, V, g, gc, clc, black_only, s)
                         : pr_t<double, 2>(linear, u, V, g, gc, clc, black_only, s);
@@ -4476,7 +4562,9 @@ hipError_t launch_copy16(int kind, const void* src, void* dst, int64_t bytes, hi
 hipError_t launch_sqdiff_sum(int rb, const void* a, const void* b, int64_t n, double* partials, double* out,
                              hipStream_t s, int* ctr)
 {
-    MGP_REAL(rb, (k_sqdiff_partial<T><<<kSumBlocks, kBlock, 0, s>>>((const T*)a, (const T*)b, n, partials)));
+    if (rb == kRealF32D)  // cpu-raw.lua's float errorBuf: each square rounded to float before the sum
+        k_sqdiff_partial<float, true><<<kSumBlocks, kBlock, 0, s>>>((const float*)a, (const float*)b, n, partials);
+    else MGP_REAL(rb, (k_sqdiff_partial<T><<<kSumBlocks, kBlock, 0, s>>>((const T*)a, (const T*)b, n, partials)));
     k_sum_n<<<1, 1024, 0, s>>>(partials, kSumBlocks, out, ctr);
     return hipGetLastError();
 }

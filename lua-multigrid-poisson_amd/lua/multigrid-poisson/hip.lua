@@ -13,6 +13,9 @@ It accepts the constructor protocols of the reference:
     with psi and f kept.
   * cpu-raw.lua / gpu.lua positional protocol (cpu-raw.lua:142, 239; gpu.lua:26, 348):
         local mg = MG(size, real)    -- real = 'double' (default) or 'float'
+        -- real = 'float' computes as cpu-raw.lua does (float images read into LuaJIT doubles: every
+        -- expression in double, rounded at each store; arith = 'double'); MG{size=n, real='float',
+        -- arith='real'} gives gpu.lua's float OpenCL arithmetic (gpu.lua:32), the table protocol's default
         mg:run()              -- two outer iterations, prints '#iter err'
         mg:twoGrid(h, uPtr, fPtr, L) -- raw real* host buffers of an L x L grid (cpu-raw.lua:186)
     Fields as cpu-raw.lua:148-171 names them, each an image-like {buffer=real*, width, height}
@@ -30,7 +33,8 @@ mg:metrics() returns relErr, count, frobErr of the last outer iteration (gpu.lua
 mg:residualNorm() returns ||f - A psi||, ||f|| (device reduction).
 Extra table fields select the build's configurations: dim (2|3), real, smoother ('jacobi'|'rbgs'),
 cycle ('V'|'F'), prolong ('pc'|'linear'), coarse_init ('fresh'|'warm'), coarse_bc
-('zero'|'consistent'), restriction ('average'|'full_weighting'), device.  Defaults reproduce cpu.lua
+('zero'|'consistent'), restriction ('average'|'full_weighting'), arith ('real'|'double'), device.
+Defaults reproduce cpu.lua
 (2D, double, Jacobi 7+7, V-cycle, injection, 2x2 average, fresh zero coarse guess, ghost value 0).
 Errors from the library raise Lua errors (error()), as the reference's own failures do.
 
@@ -62,6 +66,8 @@ typedef struct mgp_opts {
     int32_t restriction;
     int64_t gather_cells;
     uint8_t comm_id[128];
+    int32_t arith;
+    int32_t api_version;
 } mgp_opts;
 int         mgp_version(void);
 void        mgp_opts_default(mgp_opts* o);
@@ -103,6 +109,7 @@ local CODES = {
 	coarse_init = {fresh = 0, warm = 1},
 	coarse_bc = {zero = 0, consistent = 1},
 	restriction = {average = 0, full_weighting = 1},
+	arith = {real = 0, double = 1},
 }
 -- include/mgpoisson.h MGP_FIELD_*; names of cpu-raw.lua:148-171
 local FIELD = {psi = 0, f = 1, rs = 2, vs = 3, psiOld = 4, errorBuf = 5, tmpU = 6, Vs = 0, Rs = 1}
@@ -239,8 +246,9 @@ function MultigridHIP:init(a, real, cpuDepth, engine)
 		rawset(self, 'errorCallback', args.errorCallback)
 		if args.debug ~= nil then rawset(self, 'debug', args.debug) end
 	else
-		-- cpu-raw.lua positional protocol: persistent coarse buffers (cpu-raw.lua:221)
-		args = {size = a, real = real, coarse_init = 'warm'}
+		-- cpu-raw.lua positional protocol: persistent coarse buffers (cpu-raw.lua:221) and, for
+		-- real = 'float', its LuaJIT-double arithmetic over float images (cpu-raw.lua:142-153)
+		args = {size = a, real = real, coarse_init = 'warm', arith = 'double'}
 		rawset(self, 'cpuDepth', cpuDepth)
 		rawset(self, 'engine', engine)
 	end
@@ -260,7 +268,7 @@ function MultigridHIP:init(a, real, cpuDepth, engine)
 	rawset(self, 'build', {real = rawget(self, 'real'), smooth = args.smooth or MultigridHIP.smooth,
 		smoother = smoother or 'jacobi', cycle = args.cycle, prolong = args.prolong,
 		coarse_init = args.coarse_init, coarse_bc = args.coarse_bc, restriction = args.restriction,
-		device = args.device})
+		arith = args.arith, device = args.device})
 	local cells = n * n * (dim == 3 and n or 1)
 	rawset(self, 'count', cells)
 	rawset(self, 'ctype', (rawget(self, 'real') == 'float') and 'float[?]' or 'double[?]')

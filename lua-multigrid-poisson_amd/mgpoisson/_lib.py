@@ -39,6 +39,8 @@ PROLONG_PC, PROLONG_LINEAR = 0, 1
 COARSE_FRESH, COARSE_WARM = 0, 1
 BC_ZERO, BC_CONSISTENT = 0, 1
 RESTRICT_AVERAGE, RESTRICT_FULL_WEIGHTING = 0, 1
+ARITH_REAL, ARITH_DOUBLE = 0, 1
+API_VERSION = 3
 FIELD_U, FIELD_F = 0, 1
 FIELD_RESIDUAL, FIELD_CORRECTION, FIELD_PSI_OLD, FIELD_ERROR, FIELD_TMP = 2, 3, 4, 5, 6
 # cpu-raw.lua:148-171 names of the level fields (Vs/Rs are U/F below the finest level)
@@ -48,8 +50,10 @@ MEM_HOST, MEM_DEVICE = 0, 1
 # int fn(void* user, double h, void* u, const void* f, int64_t size)
 COARSE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_double, ctypes.c_void_p, ctypes.c_void_p,
                              ctypes.c_int64)
-TIMING_HALF_SWEEP, TIMING_FUSED_PRE, TIMING_FUSED_POST = 0, 1, 2
-TIMING_KINDS = {TIMING_HALF_SWEEP: "half_sweep", TIMING_FUSED_PRE: "fused_pre", TIMING_FUSED_POST: "fused_post"}
+TIMING_HALF_SWEEP, TIMING_FUSED_PRE, TIMING_FUSED_POST, TIMING_EXCHANGE, TIMING_COLLECTIVE = 0, 1, 2, 3, 4
+TIMING_KINDS = {TIMING_HALF_SWEEP: "half_sweep", TIMING_FUSED_PRE: "fused_pre", TIMING_FUSED_POST: "fused_post",
+                TIMING_EXCHANGE: "exchange", TIMING_COLLECTIVE: "collective"}
+COMM_OPS = {0: "exchange", 1: "allgather", 2: "allreduce"}
 COMM_ID_BYTES = 128
 
 
@@ -74,6 +78,8 @@ class MGPOpts(ctypes.Structure):
         ("restriction", ctypes.c_int32),
         ("gather_cells", ctypes.c_int64),
         ("comm_id", ctypes.c_uint8 * COMM_ID_BYTES),
+        ("arith", ctypes.c_int32),
+        ("api_version", ctypes.c_int32),
     ]
 
 
@@ -114,6 +120,8 @@ SIGNATURES = {
     "mgp_set_coarse_handoff": (ctypes.c_int, [_vp, _i64, COARSE_FN, _vp]),
     "mgp_timing": (ctypes.c_int, [_vp, ctypes.c_int]),
     "mgp_timing_read": (ctypes.c_int, [_vp, ctypes.c_int, _P(_dbl), _P(_i64), _P(_dbl)]),
+    "mgp_comm_log": (ctypes.c_int, [_vp, _P(_i64), ctypes.c_int, ctypes.c_int]),
+    "mgp_plan_comm": (ctypes.c_int, [_P(MGPOpts), _i32, _P(_i64), ctypes.c_int]),
     "mgp_copy_bandwidth": (ctypes.c_int, [ctypes.c_int, _i64, _i32, _P(_dbl)]),
     "mgp_group_create": (ctypes.c_int, [_P(_vp), _P(MGPOpts), ctypes.c_int, _P(ctypes.c_int)]),
     "mgp_group_destroy": (None, [_vp]),
@@ -179,6 +187,14 @@ def plan(opts: MGPOpts, max_levels: int = 48):
     for l, d in enumerate(out):
         d["engine"] = ("piece", "tail", "zs", "blk")[rows[8 * l + 6]]
     return out
+
+
+def plan_comm(opts: MGPOpts, cycles: int = 1, max_rows: int = 1 << 14):
+    """Host-only schedule of the exchanges / collectives a rank with these options issues in `cycles` outer
+    iterations (mgp_plan_comm): [(op, side, level, msgs, bytes)], as Context.comm_log reports them."""
+    rows = (ctypes.c_int64 * (5 * max_rows))()
+    n = check(lib.mgp_plan_comm(ctypes.byref(opts), int(cycles), rows, max_rows))
+    return [(COMM_OPS[rows[5 * i]],) + tuple(rows[5 * i + k] for k in range(1, 5)) for i in range(min(n, max_rows))]
 
 
 def copy_bandwidth(device: int = -1, nbytes: int = 2 << 30, reps: int = 10) -> float:

@@ -19,12 +19,15 @@ COARSE_INITS = {"fresh": L.COARSE_FRESH, "warm": L.COARSE_WARM}
 COARSE_BCS = {"zero": L.BC_ZERO, "consistent": L.BC_CONSISTENT}
 RESTRICTIONS = {"average": L.RESTRICT_AVERAGE, "full_weighting": L.RESTRICT_FULL_WEIGHTING}
 REALS = {"double": 8, "float": 4}
+# real = float arithmetic: "real" = every operation in float (gpu.lua:32), "double" = float buffers with every
+# expression in double, rounded at each store (cpu-raw.lua's real = 'float', cpu-raw.lua:142-153)
+ARITHS = {"real": L.ARITH_REAL, "double": L.ARITH_DOUBLE}
 
 
 def make_opts(dim=2, n=(8, 8, 1), real="double", nu1=7, nu2=7, smoother="jacobi", cycle="V",
               prolong="pc", coarse_init="fresh", coarse_bc="zero", coarse_sweeps=48, err_mode=1,
               device=-1, rank=0, world=1, gather_cells=32768, comm_id: bytes | None = None,
-              restriction="average") -> L.MGPOpts:
+              restriction="average", arith="real") -> L.MGPOpts:
     """Build mgp_opts from keyword names (defaults = the reference cpu.lua configuration)."""
     o = L.default_opts()
     o.dim = dim
@@ -43,6 +46,7 @@ def make_opts(dim=2, n=(8, 8, 1), real="double", nu1=7, nu2=7, smoother="jacobi"
     o.rank, o.world = rank, world
     o.gather_cells = gather_cells
     o.restriction = RESTRICTIONS[restriction] if isinstance(restriction, str) else restriction
+    o.arith = ARITHS[arith] if isinstance(arith, str) else arith
     if comm_id is not None:
         ctypes.memmove(o.comm_id, comm_id, L.COMM_ID_BYTES)
     return o
@@ -266,8 +270,17 @@ class Context:
     def timing(self, enable=True):
         self._chk(L.lib.mgp_timing(self._h, 1 if enable else 0))
 
+    def comm_log(self, reset=False, max_rows=1 << 16):
+        """The exchanges / collectives this rank issued, in order: [(op, side, level, msgs, bytes)] with op one of
+        "exchange" (msgs per neighbour and direction, bytes sent per neighbour), "allgather", "allreduce"; side 1 =
+        the side stream's communicator (mgp_comm_log)."""
+        rows = (ctypes.c_int64 * (5 * max_rows))()
+        n = self._chk(L.lib.mgp_comm_log(self._h, rows, max_rows, 1 if reset else 0))
+        return [(L.COMM_OPS[rows[5 * i]],) + tuple(rows[5 * i + k] for k in range(1, 5)) for i in range(min(n, max_rows))]
+
     def timing_read(self):
-        """{kind name: (kernel ms, launches, algorithmic bytes)} of the level-0 launches timed so far."""
+        """{kind name: (ms, launches / calls, bytes)} timed so far: the level-0 smoothing launches (algorithmic
+        bytes) and every halo exchange / collective (bytes this rank sends)."""
         out = {}
         for kind, name in L.TIMING_KINDS.items():
             ms, n, by = ctypes.c_double(), ctypes.c_int64(), ctypes.c_double()

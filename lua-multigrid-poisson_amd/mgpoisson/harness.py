@@ -8,17 +8,26 @@ writes ``#size<TAB>col...`` rows to ``cpu-vs-gpu.txt``.  The reference times wit
 on the GPU.  The reference's harness calls ``run`` on ``multigrid-poisson.cpu``, which only has
 ``solve``.  Here every column is a solver whose class has ``run``.
 
+The reference's table is cpu against gpu (its column list, test/test.lua:8-14, is 'cpu', 'cpu-raw', 'gpu',
+...).  The GPU columns are built in (``COLUMNS``); CPU columns are plugged in by the caller, because this
+package holds no CPU solver (there is deliberately no CPU fallback): ``register_column(name, factory)`` or
+``--plugin module`` (a module whose ``columns()`` returns ``{name: factory}``), where
+``factory(size, real, cpudepth)`` returns an object with ``run()``.  The reference's own Lua classes
+bound from Python, or the test suite's C restatement of cpu-raw.lua (tests/harness_columns.py: column
+``cpu-raw``), fit that slot.
+
 ``python -m mgpoisson.harness converge`` reproduces the multigrid half of
 test/converge-multigrid-vs-krylov.lua:15-89.  For sizes 4 .. 128 it runs ``solve()`` with
 ``epsilon = 1e-20`` and records ``|psi|_inf`` per iteration from the ``errorCallback``.  It adds a
 conjugate-gradient column on the same system (the reference's ``solver.conjgrad`` with
-``x0 = -f``, ``b = f``, ``A`` = the 5-point operator with zero ghosts), computed with SciPy on the
-host as the cross-check.  Both columns are shifted by their common minimum and written to
-``converge/<size>.txt``.
+``x0 = -f``, ``b = f``, ``A`` = the 5-point operator with zero ghosts), computed on the device by
+``mgp_cg_solve`` (matrix-free CG, fp64 dot products) as the cross-check.  Both columns are shifted by
+their common minimum and written to ``converge/<size>.txt``.
 """
 from __future__ import annotations
 
 import argparse
+import importlib
 import os
 import sys
 import time
@@ -31,12 +40,26 @@ COLUMNS = {
     "hip-f32": ("float", {}),
     "hip-rbgs": ("double", dict(smoother="rbgs", nu1=2, nu2=2, prolong="linear", coarse_bc="consistent")),
 }
+# caller-supplied columns: name -> factory(size, real, cpudepth) returning an object with run()
+EXTRA_COLUMNS = {}
+
+
+def register_column(name, factory):
+    """Add a column (e.g. a CPU solver of the positional protocol, test/test.lua:8-14's 'cpu' / 'cpu-raw')."""
+    EXTRA_COLUMNS[name] = factory
+
+
+def _make(col, size, cpudepth):
+    if col in EXTRA_COLUMNS:
+        return EXTRA_COLUMNS[col](size, None, cpudepth)  # test/test.lua:54: cl(size, nil, cpudepth)
+    from .solver import MultigridHIPRaw
+
+    real, build = COLUMNS[col]
+    return MultigridHIPRaw(size, real, cpudepth, **build)
 
 
 def bench(lo=5, hi=10, tries=1, cols=("hip",), cpudepth=3, out="cpu-vs-gpu.txt", quiet=False):
     """test/test.lua: best-of-tries wall time of MG(size, real, cpudepth):run() per size and column."""
-    from .solver import MultigridHIPRaw
-
     rows = []
     with open(out, "w") as fh:
         def write(s):
@@ -52,16 +75,18 @@ def bench(lo=5, hi=10, tries=1, cols=("hip",), cpudepth=3, out="cpu-vs-gpu.txt",
             write(str(size))
             row = [size]
             for col in cols:
-                real, build = COLUMNS[col]
                 best = float("inf")
                 for _ in range(tries):
-                    mg = MultigridHIPRaw(size, real, cpudepth, **build)
+                    mg = _make(col, size, cpudepth)
                     mg.quiet = True
                     t0 = time.perf_counter()
                     mg.run()
-                    mg.ctx.sync()
+                    ctx = getattr(mg, "ctx", None)
+                    if ctx is not None:
+                        ctx.sync()
                     best = min(best, time.perf_counter() - t0)
-                    mg.ctx.close()
+                    if ctx is not None:
+                        ctx.close()
                 write(f"\t{best}")
                 row.append(best)
             write("\n")
@@ -108,7 +133,9 @@ def main(argv=None):
     b.add_argument("--lo", type=int, default=5)
     b.add_argument("--hi", type=int, default=10)
     b.add_argument("--tries", type=int, default=1)
-    b.add_argument("--cols", default="hip", help="comma list of " + ",".join(COLUMNS))
+    b.add_argument("--cols", default="hip", help="comma list of " + ",".join(COLUMNS) + " and plugged-in columns")
+    b.add_argument("--plugin", action="append", default=[],
+                   help="module whose columns() returns {name: factory(size, real, cpudepth)} (e.g. a CPU solver)")
     b.add_argument("--cpudepth", type=int, default=3)
     b.add_argument("--out", default="cpu-vs-gpu.txt")
     c = sub.add_parser("converge", help="converge-multigrid-vs-krylov.lua: |psi|_inf histories")
@@ -117,6 +144,9 @@ def main(argv=None):
     c.add_argument("--outdir", default="converge")
     a = p.parse_args(argv)
     if a.cmd == "bench":
+        for mod in a.plugin:
+            for name, factory in importlib.import_module(mod).columns().items():
+                register_column(name, factory)
         bench(a.lo, a.hi, a.tries, tuple(a.cols.split(",")), a.cpudepth, a.out)
     else:
         converge(tuple(int(s) for s in a.sizes.split(",")), a.epsilon, a.outdir)

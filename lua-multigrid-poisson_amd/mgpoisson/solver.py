@@ -10,6 +10,8 @@ the LuaJIT-FFI module a Lua user would load is lua/multigrid-poisson/hip.lua (IN
 * :class:`MultigridHIPRaw` — the ``cpu-raw.lua`` / ``gpu.lua`` positional protocol:
   ``MultigridCPURaw(size, real)`` then ``:run()`` (2 outer iterations) and
   ``:twoGrid(h, uPtr, fPtr, L)`` (cpu-raw.lua:142, 186, 239-258; gpu.lua:26, 296, 348).
+  ``real='float'`` follows cpu-raw.lua's arithmetic by default (float buffers, every expression in
+  double: ``arith='double'``); ``arith='real'`` gives gpu.lua's float-rounded OpenCL arithmetic.
 """
 from __future__ import annotations
 
@@ -234,7 +236,9 @@ class MultigridHIPRaw(_RawFields):
 
     ``MultigridHIPRaw(size, real='double')``; ``run()`` does the reference's two hard-coded
     outer iterations (cpu-raw.lua:245) printing ``#iter err`` lines; ``twoGrid(h, u, f, L)``
-    takes host numpy arrays or integer device pointers (``mem=MEM_DEVICE``).
+    takes host numpy arrays or integer device pointers (``mem=MEM_DEVICE``).  With ``real='float'`` the
+    arithmetic is cpu-raw.lua's (LuaJIT doubles over float images: ``arith='double'``, the default of this
+    protocol); ``arith='real'`` selects gpu.lua's (every operation rounded to float, gpu.lua:32).
     """
 
     debugging = False
@@ -247,8 +251,10 @@ class MultigridHIPRaw(_RawFields):
         self.cpuDepth = cpuDepth
         dim = int(build.pop("dim", 2))
         n = self.size
+        self.arith = build.pop("arith", "double")  # cpu-raw.lua's LuaJIT arithmetic (no effect on double)
         opts = make_opts(dim=dim, n=(n, n, n if dim == 3 else 1), real=self.real, nu1=build.pop("nu1", self.smooth),
-                         nu2=build.pop("nu2", self.smooth), coarse_init=build.pop("coarse_init", "warm"), **build)
+                         nu2=build.pop("nu2", self.smooth), coarse_init=build.pop("coarse_init", "warm"),
+                         arith=self.arith, **build)
         self._ctx = Context(opts)
         if cpuDepth:  # cpu-gpu.lua:61: switch to the coarse engine at size 2^cpuDepth when it fits
             try:

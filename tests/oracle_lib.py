@@ -165,13 +165,13 @@ def restrict_arr(dim, r, arith="real"):
     return R
 
 
-def restrict_fw_arr(dim, r, cl_coarse=0.0):
+def restrict_fw_arr(dim, r, cl_coarse=0.0, arith="real"):
     """Full-weighting restriction (the adjoint of the linear prolongation), mgp_oracle_impl.h restrict_fw."""
     r = np.ascontiguousarray(r)
     shp = tuple(s // 2 for s in r.shape)
     R = np.empty(shp, r.dtype)
     nz, ny, nx = (r.shape if dim == 3 else (1,) + r.shape)
-    lib.mgo_restrict_fw_arr(dim, nx, ny, nz, r.itemsize, cl_coarse, r.ctypes.data, R.ctypes.data)
+    lib.mgo_restrict_fw_arr(dim, nx, ny, nz, _kind(r, arith), cl_coarse, r.ctypes.data, R.ctypes.data)
     return R
 
 

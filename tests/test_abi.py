@@ -57,13 +57,16 @@ def _mg():
 def test_opts_struct_layout_matches_header():
     mg = _mg()
     o = mg.default_opts()
-    assert o.struct_size == ctypes.sizeof(mg._lib.MGPOpts) == 224
+    assert o.struct_size == ctypes.sizeof(mg._lib.MGPOpts) == 232
     # defaults = the reference cpu.lua configuration
     assert (o.dim, o.real_bytes, o.nu1, o.nu2) == (2, 8, 7, 7)
     assert (o.smoother, o.cycle, o.prolong, o.coarse_init, o.coarse_bc, o.restriction) == (0, 0, 0, 0, 0, 0)
-    assert mg._lib.lib.mgp_version() == 2
-    # restriction sits in the former padding after world, before the 8-byte gather_cells
+    assert mg._lib.lib.mgp_version() == 3 == o.api_version
+    # restriction sits in the former padding after world, before the 8-byte gather_cells; version 3 appends
+    # arith and api_version, so a caller built against an older header fails the struct_size check
     assert mg._lib.MGPOpts.restriction.offset == 84 and mg._lib.MGPOpts.gather_cells.offset == 88
+    assert mg._lib.MGPOpts.arith.offset == 224 and mg._lib.MGPOpts.api_version.offset == 228
+    assert o.arith == 0
 
 
 def test_plan_single_cube():
@@ -114,12 +117,39 @@ def test_plan_slab_decomposition(world):
     (dict(dim=2, n=(8, 8, 1), world=2, rank=0), "3D"),
     (dict(dim=3, n=(8, 8, 8), world=8, rank=0), "planes per rank"),
     (dict(dim=3, n=(8, 8, 8), rank=2, world=2), "rank"),
+    (dict(dim=2, n=(8, 8, 1), arith=5), "arith"),
 ])
 def test_plan_rejects_bad_options(kw, msg):
     mg = _mg()
     with pytest.raises(mg.MGPError) as ei:
         mg.plan(mg.make_opts(**kw))
     assert msg in str(ei.value)
+
+
+def test_version_skew_is_rejected():
+    """a caller built against another header revision fails loudly instead of reading garbage."""
+    mg = _mg()
+    o = mg.make_opts(dim=2, n=(8, 8, 1))
+    o.struct_size = 224  # an API-version-2 caller
+    with pytest.raises(mg.MGPError) as ei:
+        mg.plan(o)
+    assert "struct_size" in str(ei.value)
+    o = mg.make_opts(dim=2, n=(8, 8, 1))
+    o.api_version = 2
+    with pytest.raises(mg.MGPError) as ei:
+        mg.plan(o)
+    assert "api_version" in str(ei.value)
+
+
+def test_plan_cpu_raw_float_runs_every_level_per_piece():
+    """arith = double (cpu-raw.lua's float) evaluates in double on the per-piece kernels only: no temporally
+    blocked, tiled or tail engine, even where the real-typed build would pick them."""
+    mg = _mg()
+    kw = dict(dim=3, n=(512, 512, 512), real="float", smoother="rbgs", nu1=2, nu2=2, prolong="linear",
+              coarse_bc="consistent")
+    assert {r["engine"] for r in mg.plan(mg.make_opts(**kw))} >= {"zs", "blk", "tail"}
+    assert {r["engine"] for r in mg.plan(mg.make_opts(arith="double", **kw))} == {"piece"}
+    assert {r["engine"] for r in mg.plan(mg.make_opts(dim=2, n=(256, 256, 1), real="float", arith="double"))} == {"piece"}
 
 
 def test_create_without_gpu_fails_loudly():

@@ -52,3 +52,36 @@ def test_strong_scaling_launch_plan_config3():
     assert d["global_box"] == [2048, 2048, 2048]
     assert d["rank_slabs_level0"] == [[256 * r, 256] for r in range(8)]
     assert d["engines"][0] == "zs"
+
+
+def test_north_star_lines_planned_at_8_ranks():
+    """With N >= 4 the default run adds BASELINE configs[3] (2048^3 V) and configs[4] (4096^3 F) to the line;
+    --plan-only lists each workload's per-cycle RCCL calls and bytes per rank (mgp_plan_comm: the library's own
+    cycle logic, run on the host with every device call skipped)."""
+    d = _launch(8)
+    assert set(d["north_star_lines"]) == {"configs[3]", "configs[4]"}
+    weak = d["comm_per_cycle"]
+    # weak scaling: level 0 (k_zs): u before PRE, u on the side stream after PRE; levels 1-4 (deep halos): f before
+    # pre-smoothing, u before post-smoothing; the coarse V planes level 0's POST reads; one all-gather, one all-reduce
+    assert weak["allreduces"] == 1 and weak["allgathers"] == 1 and weak["side_stream_exchanges"] == 1
+    assert weak["calls"] == len(weak["sequence"]) == 13
+    c3, c4 = (d["north_star_lines"][k]["comm_per_cycle"] for k in ("configs[3]", "configs[4]"))
+    assert d["north_star_lines"]["configs[4]"]["cycle"] == "F"
+    assert c3["side_stream_exchanges"] == 2  # levels 0 and 1 run k_zs on 2048 x 2048 x 256 slabs
+    assert c4["allgathers"] > 1 and c4["calls"] > c3["calls"]  # the F-cycle revisits the agglomerated levels
+    assert c4["halo_MB_per_neighbour"] > c3["halo_MB_per_neighbour"] > weak["halo_MB_per_neighbour"]
+
+
+def test_plan_comm_is_identical_on_every_rank():
+    """RCCL matches calls per communicator in issue order: every rank of a slab decomposition must issue the same
+    sequence (a rank at the end of the stack exchanges with one neighbour, but calls in the same order)."""
+    sys.path.insert(0, os.path.join(ROOT, "lua-multigrid-poisson_amd"))
+    import mgpoisson as mg
+
+    for box, cyc, w in [((512, 512, 4096), "V", 8), ((2048, 2048, 2048), "V", 8), ((4096, 4096, 4096), "F", 8),
+                        ((256, 256, 512), "F", 2)]:
+        logs = [mg.plan_comm(mg.make_opts(dim=3, n=box, real="float", smoother="rbgs", nu1=2, nu2=2, prolong="linear",
+                                          coarse_bc="consistent", cycle=cyc, rank=r, world=w, comm_id=b"\0" * 128), 2)
+                for r in range(w)]
+        assert all(l == logs[0] for l in logs), (box, cyc, w)
+        assert logs[0][-1] == ("allreduce", 0, 0, 1, 8)

@@ -653,6 +653,19 @@ def test_harness_bench_tsv(tmp_path):
     assert all(len(r) == 3 and all(t > 0 for t in r[1:]) for r in rows)
 
 
+def test_harness_cpu_vs_gpu_columns(tmp_path):
+    """test/test.lua's cpu-vs-gpu table: the C port of cpu-raw.lua plugged in as the 'cpu-raw' column beside the
+    GPU's, both of the positional protocol's run() (two outer iterations)."""
+    import harness_columns
+    from mgpoisson import harness
+
+    harness.register_column("cpu-raw", harness_columns.CpuRaw)
+    out = tmp_path / "cpu-vs-gpu.txt"
+    rows = harness.bench(5, 6, tries=1, cols=("cpu-raw", "hip"), out=str(out), quiet=True)
+    assert out.read_text().splitlines()[0] == "#size\tcpu-raw\thip"
+    assert all(len(r) == 3 and all(t > 0 for t in r[1:]) for r in rows)
+
+
 def test_harness_converge_matches_cg(tmp_path):
     """converge-multigrid-vs-krylov.lua: multigrid and CG histories of |psi|_inf end at the same
     discrete solution (the converged values agree to 1e-8 relative)."""

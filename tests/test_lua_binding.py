@@ -83,8 +83,8 @@ def test_header_asserts_opts_size(tmp_path):
     """The header pins sizeof(mgp_opts) itself; a changed struct fails every C/C++ consumer's build."""
     out = _gcc('#include <stdio.h>\n#include <stddef.h>\n#include "mgpoisson.h"\nint main(void){printf("%zu\\n", '
                'sizeof(mgp_opts));return 0;}\n', tmp_path, run=True)
-    assert int(out) == 224
-    assert "_Static_assert(sizeof(mgp_opts) == 224" in open(os.path.join(HEADER_DIR, "mgpoisson.h")).read()
+    assert int(out) == 232
+    assert "_Static_assert(sizeof(mgp_opts) == 232" in open(os.path.join(HEADER_DIR, "mgpoisson.h")).read()
 
 
 def test_ctypes_mirror_offsets(tmp_path):

@@ -346,3 +346,22 @@ def test_cpu_raw_float_first_sweep_closed_form():
     u = smooth_arr(2, o.get(0), o.get(1), "jacobi", 1, h, arith="double")
     c = n // 2
     assert u[c, c] == np.float32(3906.25) and u[c, c + 1] == np.float32(2.5e5)
+
+
+def test_harness_cpu_column_runs_without_gpu(tmp_path):
+    """The TSV harness (test/test.lua:8-63) with only the plugged-in CPU column needs no device."""
+    import harness_columns
+    from mgpoisson import harness
+
+    harness.register_column("cpu-raw", harness_columns.CpuRaw)
+    out = tmp_path / "cpu-vs-gpu.txt"
+    rows = harness.bench(4, 5, tries=2, cols=("cpu-raw",), out=str(out), quiet=True)
+    lines = out.read_text().splitlines()
+    assert lines[0] == "#size\tcpu-raw" and [int(l.split("\t")[0]) for l in lines[1:]] == [16, 32]
+    assert all(r[1] > 0 for r in rows)
+    # the column is cpu-raw.lua's run(): 2 outer iterations from the warm-start semantics
+    s = harness_columns.CpuRaw(8)
+    s.quiet = True
+    e = s.run()
+    assert len(e) == 2 and e[0] == pytest.approx(122091.06275197188, rel=1e-14)
+    assert e[1] == pytest.approx(6828.1698388918103, rel=1e-14)
