@@ -1710,7 +1710,7 @@ static void select_engines(mgp_ctx* c)
             L.fused = on && level_cells(L) >= min_cells && mgp::fused_supported(c->rb, c->o.dim, 2, L.g);
             if (L.fused) {
                 L.zc = mgp::fused_zc(c->rb, L.g, false);
-                L.zc_pre = mgp::fused_zc(c->rb, L.g, true);
+                L.zc_pre = mgp::fused_zc(c->rb, L.g, true, coarse_coef(c->o.coarse_bc, (int)l) == 0.0);
             }
             if (L.fused && L.p.dist) c->G = mgp::kGhostZs;
         }

@@ -137,7 +137,8 @@ struct FusedArgs {
 bool fused_supported(int rb, int dim, int ns, const Geo& g);
 // Raise the dynamic-LDS limit of the fused and tail kernels (once per context, before any capture).
 hipError_t prepare_kernels(int rb);
-int fused_zc(int rb, const Geo& g, bool pre);
+// clz: the level's operator has no boundary modification (cl == 0): PRE's tile may differ otherwise
+int fused_zc(int rb, const Geo& g, bool pre, bool clz = true);
 int fused_blocks(int rb, const Geo& g, int zc);
 hipError_t launch_fused(int rb, const FusedArgs& a, hipStream_t s);
 

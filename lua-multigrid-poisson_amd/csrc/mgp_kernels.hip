@@ -1734,12 +1734,24 @@ __device__ __forceinline__ void lds_barrier()
 #ifndef ZS_TXPOST_F32
 #define ZS_TXPOST_F32 64
 #endif
+// PRE on a level with a boundary-modified operator (cl != 0): its own tile (the boundary diagonals cost
+// registers: at the level-0 shape the variant spills)
+#ifndef ZS_TXPRE_CL_F32
+#define ZS_TXPRE_CL_F32 ZS_TXPRE_F32
+#endif
+#ifndef ZS_TYPRE_CL_F32
+#define ZS_TYPRE_CL_F32 ZS_TYPRE_F32
+#endif
+#ifndef ZS_NPRE_CL_F32
+#define ZS_NPRE_CL_F32 ZS_NPRE_F32
+#endif
 template <typename T>
 struct ZsTile;
 template <>
 struct ZsTile<float> {
     static constexpr int TXPRE = ZS_TXPRE_F32, TXPOST = ZS_TXPOST_F32, TYPRE = ZS_TYPRE_F32, TYPOST = ZS_TYPOST_F32,
                          NPRE = ZS_NPRE_F32, NPOST = ZS_NPOST_F32;
+    static constexpr int TXPRE_CL = ZS_TXPRE_CL_F32, TYPRE_CL = ZS_TYPRE_CL_F32, NPRE_CL = ZS_NPRE_CL_F32;
 };
 #ifndef ZS_TXPRE_F64
 #define ZS_TXPRE_F64 32
@@ -1757,6 +1769,7 @@ template <>
 struct ZsTile<double> {
     static constexpr int TXPRE = ZS_TXPRE_F64, TXPOST = ZS_TXPOST_F64, TYPRE = ZS_TYPRE_F64, TYPOST = ZS_TYPOST_F64,
                          NPRE = 2, NPOST = 2;
+    static constexpr int TXPRE_CL = TXPRE, TYPRE_CL = TYPRE, NPRE_CL = NPRE;
 };
 // Streaming (non-temporal) level-0 loads / stores of the phases: timing experiments (ZS_NT bit 0:
 // loads, bit 1: stores), so that the level-0 stream does not evict the coarse level it writes
@@ -1770,11 +1783,11 @@ constexpr bool kZsNTL = (ZS_NT & 1) != 0, kZsNTS = (ZS_NT & 2) != 0, kZsNTO = (Z
 #endif
 constexpr bool kZsPreRed = ZS_PRE_RED_STORE != 0;
 
-template <typename T, bool PRE>
+template <typename T, bool PRE, bool CLZ = true>
 struct ZsShape {
-    static constexpr int N = PRE ? ZsTile<T>::NPRE : ZsTile<T>::NPOST;
-    static constexpr int TX = PRE ? ZsTile<T>::TXPRE : ZsTile<T>::TXPOST;
-    static constexpr int TY = PRE ? ZsTile<T>::TYPRE : ZsTile<T>::TYPOST;
+    static constexpr int N = PRE ? (CLZ ? ZsTile<T>::NPRE : ZsTile<T>::NPRE_CL) : ZsTile<T>::NPOST;
+    static constexpr int TX = PRE ? (CLZ ? ZsTile<T>::TXPRE : ZsTile<T>::TXPRE_CL) : ZsTile<T>::TXPOST;
+    static constexpr int TY = PRE ? (CLZ ? ZsTile<T>::TYPRE : ZsTile<T>::TYPRE_CL) : ZsTile<T>::TYPOST;
     static constexpr int H = PRE ? 5 : 4;              // y/z halo = stages that read neighbours
     // x halo cells per side: the trapezoid depth H in whole column groups (2 N cells of x each)
 #ifdef ZS_HX_FIXED  // timing experiment: the round-1 fixed 8-cell x halo
@@ -2095,6 +2108,11 @@ __device__ __forceinline__ void block_partial_t(double acc, double* partials)
 #ifndef ZS_PFD_POST
 #define ZS_PFD_POST 1
 #endif
+// PRE on a level with a boundary-modified operator (cl != 0, the coarser fused levels): distance 1 — at 2 the
+// variant needed 54 (fp64: 33) VGPRs beyond the 256 of two waves per SIMD and spilled to scratch
+#ifndef ZS_PFD_PRE_CL
+#define ZS_PFD_PRE_CL 1
+#endif
 template <typename F, int... K>
 __device__ __forceinline__ void zs_unroll_impl(F& f, std::integer_sequence<int, K...>)
 {
@@ -2113,13 +2131,13 @@ __device__ __forceinline__ void zs_unroll(F&& f)
 #define ZS_WPE_POST 4
 #endif
 template <typename T, bool PRE, int LINEAR, bool ERR, bool CLZ>
-__global__ __launch_bounds__((ZsShape<T, PRE>::NTL))
+__global__ __launch_bounds__((ZsShape<T, PRE, CLZ>::NTL))
 __attribute__((amdgpu_waves_per_eu(1, PRE ? ZS_WPE_PRE : ZS_WPE_POST))) void k_zs(const T* __restrict__ src, const T* __restrict__ f,
                                                                 T* __restrict__ dst, const T* old, T* __restrict__ R,
                                                                 const T* __restrict__ V, double* __restrict__ partials,
                                                                 Geo g, Geo gc, Op<T, 3> op, T clc, int zc, int gz)
 {
-    using S = ZsShape<T, PRE>;
+    using S = ZsShape<T, PRE, CLZ>;
     constexpr int N = S::N, H = S::H, HWE = S::HWE, G = S::G, YE = S::YE, SLOT = S::SLOT, TX = S::TX,
                   TY = S::TY, NS3 = S::NS3, NTL = S::NTL;
     // PRE: LINEAR selects the restriction: 0 = residual + 2^3 average here; 1 = none (both colours of the
@@ -2127,7 +2145,7 @@ __attribute__((amdgpu_waves_per_eu(1, PRE ? ZS_WPE_PRE : ZS_WPE_POST))) void k_z
     constexpr bool RR = PRE && LINEAR == 0;
     using VT = Vec<T, N>;
     using PF = ZsPrefetch<T, N>;
-    constexpr int PFD = PRE ? ZS_PFD_PRE : ZS_PFD_POST, NPF = PFD + 1, UNR = NPF == 3 ? 12 : 4;
+    constexpr int PFD = PRE ? (CLZ ? ZS_PFD_PRE : ZS_PFD_PRE_CL) : ZS_PFD_POST, NPF = PFD + 1, UNR = NPF == 3 ? 12 : 4;
     static_assert(PFD >= 1 && PFD <= 3, "prefetch distance 1..3");
     extern __shared__ __align__(16) unsigned char zs_smem[];
     T* const lds = reinterpret_cast<T*>(zs_smem);
@@ -2411,9 +2429,11 @@ __attribute__((amdgpu_waves_per_eu(1, PRE ? ZS_WPE_PRE : ZS_WPE_POST))) void k_z
         }
 
         // ---- the smoothed plane p - 4: red final after stage 3, black after stage 4 ----
+        // (the chunk test is wave-uniform: steady steps also run the trapezoid's warm-up before the chunk and
+        // its drain after it, which store nothing)
         {
             const int q = p - 4;
-            if ((ST || (q >= Z0 && q < Z0 + zc)) && tile_xy) {
+            if (q >= Z0 && q < Z0 + zc && tile_xy) {
                 if (!PRE && ERR) {
 #pragma unroll
                     for (int e = 0; e < N; ++e) {
@@ -2457,9 +2477,9 @@ __attribute__((amdgpu_waves_per_eu(1, PRE ? ZS_WPE_PRE : ZS_WPE_POST))) void k_z
                 rr[1][e] = pq == 0 ? rblk[e] : rred[e];
             }
             const int dq = q - (ST ? (Z0 & ~1) : Z0);
-            if ((ST || (dq >= 0 && dq <= zc)) && tile_xy) {
+            if (dq >= 0 && dq <= zc && tile_xy) {
                 if (!even_row) {
-                    if (ST || dq < zc) {
+                    if (dq < zc) {
                         T* x = xs(q);
 #pragma unroll
                         for (int e = 0; e < N; ++e) {
@@ -2468,7 +2488,7 @@ __attribute__((amdgpu_waves_per_eu(1, PRE ? ZS_WPE_PRE : ZS_WPE_POST))) void k_z
                         }
                     }
                 } else {
-                    if (ST || dq >= 1) {  // the odd row's children of plane q - 1
+                    if (dq >= 1) {  // the odd row's children of plane q - 1
 #pragma unroll
                         for (int e = 0; e < N; ++e) {
                             acc[e] = acc[e] + xr[e];
@@ -2484,7 +2504,7 @@ __attribute__((amdgpu_waves_per_eu(1, PRE ? ZS_WPE_PRE : ZS_WPE_POST))) void k_z
                             }
                         }
                     }
-                    if (ST || dq < zc) {
+                    if (dq < zc) {
 #pragma unroll
                         for (int e = 0; e < N; ++e) {
                             if ((dq & 1) == 0) {
@@ -2516,14 +2536,15 @@ __attribute__((amdgpu_waves_per_eu(1, PRE ? ZS_WPE_PRE : ZS_WPE_POST))) void k_z
     }
 #pragma unroll
     for (int k = 0; k < PFD; ++k) prefetch(GEN, pb[k], zlo + k);
-    // steady steps [ps, pe]: stages inside the box (z0 + p - 5 >= 0, z0 + p < gnz), the stored plane
-    // and PRE's residual plane inside the chunk, the prefetched planes (p + 1 .. p - 3) readable
-    int ps = Z0 + 6, pe = Z0 + zc + 3;
-    ps = ps > 5 - z0 ? ps : 5 - z0;
-    ps = ps > qlo + 3 ? ps : qlo + 3;
+    // steady steps [ps, pe]: stages inside the box (z0 + p - 5 >= 1, z0 + p < gnz) and the prefetched planes
+    // (p + PFD .. p - 4) readable; the chunk's warm-up and drain steps are steady too (their stores are skipped
+    // by the uniform chunk test), so a chunk away from the box faces runs no generic step at all (the short
+    // chunks of the coarser fused levels were ~45 % generic steps before)
+    int ps = zlo, pe = p_end;
+    ps = ps > 6 - z0 ? ps : 6 - z0;  // PRE's residual plane p - 5 off the z face (steady diagonals have no z face)
+    ps = ps > qlo + 4 ? ps : qlo + 4;
     pe = pe < gnz - (PRE ? 1 : 2) - z0 ? pe : gnz - (PRE ? 1 : 2) - z0;  // POST: Kn inside the coarse box
     pe = pe < qhi - PFD ? pe : qhi - PFD;
-    pe = pe < p_end - PFD ? pe : p_end - PFD;
     ps += (UNR - (ps - zlo) % UNR) % UNR;  // whole groups of UNR steps in the prologue
     pe -= (pe - ps + 1) % UNR;             // and in the steady part
     // no steady part (the epilogue takes all) without a whole group or with odd z0 / Z0 (static parity)
@@ -4219,7 +4240,7 @@ hipError_t launch_prolong_correct(int rb, int dim, int linear, void* u, const vo
 template <typename T, bool PRE, int LINEAR, bool ERR, bool CLZ>
 static hipError_t zs_launch(const FusedArgs& a, hipStream_t s)
 {
-    using S = ZsShape<T, PRE>;
+    using S = ZsShape<T, PRE, CLZ>;
     const Op<T, 3> op = make_op<T, 3>(a.h, a.cl);
     const unsigned nb = (unsigned)((a.g.nx / S::TX) * (a.g.ny / S::TY) * (a.g.nz / a.zc));
     k_zs<T, PRE, LINEAR, ERR, CLZ><<<nb, S::NTL, S::lds_bytes, s>>>((const T*)a.src, (const T*)a.f, (T*)a.dst,
@@ -4259,15 +4280,19 @@ static hipError_t fused_dispatch(const FusedArgs& a, hipStream_t s)
     return err ? zs_launch<T, false, 0, true, CLZ>(a, s) : zs_launch<T, false, 0, false, CLZ>(a, s);
 }
 
-// tile of a phase (pre) or the tallest of both (pre < 0)
-static void zs_tile(int rb, int& tx, int& ty, int pre = -1)
+// tile of a phase (pre) or the largest of all (pre < 0); clz: the level operator has no boundary modification
+static void zs_tile(int rb, int& tx, int& ty, int pre = -1, bool clz = true)
 {
     const int xa = rb == 4 ? ZsTile<float>::TXPRE : ZsTile<double>::TXPRE;
+    const int xc = rb == 4 ? ZsTile<float>::TXPRE_CL : ZsTile<double>::TXPRE_CL;
     const int xb = rb == 4 ? ZsTile<float>::TXPOST : ZsTile<double>::TXPOST;
     const int a = rb == 4 ? ZsTile<float>::TYPRE : ZsTile<double>::TYPRE;
+    const int ac = rb == 4 ? ZsTile<float>::TYPRE_CL : ZsTile<double>::TYPRE_CL;
     const int b = rb == 4 ? ZsTile<float>::TYPOST : ZsTile<double>::TYPOST;
-    tx = pre < 0 ? (xa > xb ? xa : xb) : (pre ? xa : xb);
-    ty = pre < 0 ? (a > b ? a : b) : (pre ? a : b);
+    const int xp = clz ? xa : xc, yp = clz ? a : ac;
+    auto mx = [](int u, int v, int w) { return u > v ? (u > w ? u : w) : (v > w ? v : w); };
+    tx = pre < 0 ? mx(xa, xb, xc) : (pre ? xp : xb);
+    ty = pre < 0 ? mx(a, b, ac) : (pre ? yp : b);
 }
 
 // 2D (k_ys): rows per z-chunk of a workgroup (MGP_YS_ROWS, default 32; even)
@@ -4296,11 +4321,11 @@ bool fused_supported(int rb, int dim, int ns, const Geo& g)
 
 // planes per workgroup: halve the z-chunk until there are >= MGP_ZS_WGS (default 256, one per CU)
 // workgroups or a chunk would drop below 16 planes
-int fused_zc(int rb, const Geo& g, bool pre)
+int fused_zc(int rb, const Geo& g, bool pre, bool clz)
 {
     if (g.gnz == 1 && g.nz == 1) return ys_rows(g);  // 2D: rows per chunk
     int TX, TY;
-    zs_tile(rb, TX, TY, pre ? 1 : 0);
+    zs_tile(rb, TX, TY, pre ? 1 : 0, clz);
     static const int64_t target = [] {
         const char* v = std::getenv("MGP_ZS_WGS");
         return v ? std::atoll(v) : (int64_t)256;
@@ -4324,7 +4349,7 @@ int fused_halo(bool pre) { return pre ? 5 : 4; }
 template <typename T, bool CLZ>
 static hipError_t fused_attr()
 {
-    const int pre = (int)ZsShape<T, true>::lds_bytes, post = (int)ZsShape<T, false>::lds_bytes;
+    const int pre = (int)ZsShape<T, true, CLZ>::lds_bytes, post = (int)ZsShape<T, false, CLZ>::lds_bytes;
     const auto A = hipFuncAttributeMaxDynamicSharedMemorySize;
     hipError_t e = hipFuncSetAttribute((const void*)k_zs<T, true, 0, false, CLZ>, A, pre);
     if (e == hipSuccess) e = hipFuncSetAttribute((const void*)k_zs<T, true, 1, false, CLZ>, A, pre);

@@ -300,6 +300,29 @@ def test_fused_phases_match_oracle(cfg, monkeypatch):
         assert np.array_equal(a.get_psi(level), b.get_psi(level)), f"psi level {level}"
 
 
+@pytest.mark.parametrize("real", ["float", "double"])
+def test_fused_level1_chunks_match_per_piece(real, monkeypatch):
+    """k_zs on the 256^3 level of a 512^3 box (cl != 0, 32-plane z-chunks whose warm-up and drain steps run the
+    steady path): psi of every level bit-identical to one launch per piece after 2 cycles."""
+    kw = dict(dim=3, n=(512, 512, 512), real=real, smoother="rbgs", nu1=2, nu2=2, prolong="linear",
+              coarse_bc="consistent")
+    monkeypatch.setenv("MGP_FUSED_MIN_CELLS", str(1 << 24))
+    a = _ctx(**kw)
+    assert [lv["engine"] for lv in a.levels[:2]] == ["zs", "zs"]
+    a.init_point_charge()
+    ea = a.cycles(2)
+    pa = [a.get_psi(l) for l in range(3)]
+    a.close()
+    monkeypatch.setenv("MGP_FUSED_MIN_CELLS", str(1 << 25))
+    b = _ctx(**kw)
+    assert [lv["engine"] for lv in b.levels[:2]] == ["zs", "piece"]
+    b.init_point_charge()
+    eb = b.cycles(2)
+    for l in range(3):
+        assert np.array_equal(pa[l], b.get_psi(l)), f"level {l}"
+    assert np.allclose(ea, eb, rtol=1e-12, atol=0)
+
+
 YS_CONFIGS = [
     dict(n=(1024, 1024, 1), real="float", prolong="linear", coarse_bc="consistent"),
     dict(n=(2048, 1024, 1), real="double", prolong="linear", coarse_bc="consistent", cycle="F"),
