@@ -2186,7 +2186,14 @@ __attribute__((amdgpu_waves_per_eu(1, PRE ? ZS_WPE_PRE : ZS_WPE_POST))) void k_z
     // LDS or HBM
     const int cgy = gy < 0 ? 0 : (gy >= g.ny ? g.ny - 1 : gy);
     const int cgm = col.gm < 0 ? 0 : (col.gm > hw - N ? hw - N : col.gm);
+#if defined(ZS_HALO_ALIAS)  // timing experiment only (wrong results): the halo's loads read the tile's own lines
+    // bit 0: x-halo column groups load from owned columns; bit 1: y-halo rows load from owned rows
+    const int agm = (ZS_HALO_ALIAS & 1) ? (gx < S::HXG ? cgm + S::HXG * N : (gx >= G - S::HXG ? cgm - S::HXG * N : cgm)) : cgm;
+    const int agy = (ZS_HALO_ALIAS & 2) ? (ye < H ? cgy + H : (ye >= H + TY ? cgy - H : cgy)) : cgy;
+    const int goff = agy * hw + agm;
+#else
     const int goff = cgy * hw + cgm;  // in-plane offset (nx * ny < 2^31)
+#endif
     const bool tile_xy = on && ye >= H && ye < H + TY && gx >= S::HXG && gx < G - S::HXG;
     const int zlo = Z0 - H;
     ZsDiag<T> dz;
