@@ -2613,10 +2613,13 @@ __attribute__((amdgpu_waves_per_eu(1, PRE ? ZS_WPE_PRE : ZS_WPE_POST))) void k_z
 #ifndef YS_TX_F64
 #define YS_TX_F64 512
 #endif
-template <typename T, bool PRE>
+template <typename T>
+constexpr int ys_tx_full() { return sizeof(T) == 4 ? YS_TX_F32 : YS_TX_F64; }
+// TXV: segment width (ys_tx_full, or half of it on levels whose full-width segments make too few workgroups)
+template <typename T, bool PRE, int TXV = ys_tx_full<T>()>
 struct YsShape {
     static constexpr int N = 16 / sizeof(T);
-    static constexpr int TX = sizeof(T) == 4 ? YS_TX_F32 : YS_TX_F64;
+    static constexpr int TX = TXV;
     static constexpr int H = PRE ? 5 : 4;
     static constexpr int HX = 2 * N * ((H + 2 * N - 1) / (2 * N));  // whole column groups
     static constexpr int HWE = TX / 2 + HX;                          // packed cells per colour of a row
@@ -2688,13 +2691,13 @@ __device__ __forceinline__ void ys_cells(const Vec<T, N>& ym, const Vec<T, N>& c
 }
 
 // PRE: LINEAR selects the restriction (0: residual + 2x2 average here; 1: none, both colours stored)
-template <typename T, bool PRE, int LINEAR, bool ERR, bool CLZ>
-__global__ __launch_bounds__((YsShape<T, PRE>::NTL)) void k_ys(const T* __restrict__ src, const T* __restrict__ f,
+template <typename T, bool PRE, int LINEAR, bool ERR, bool CLZ, int TXV>
+__global__ __launch_bounds__((YsShape<T, PRE, TXV>::NTL)) void k_ys(const T* __restrict__ src, const T* __restrict__ f,
                                                                T* __restrict__ dst, const T* old, T* __restrict__ R,
                                                                const T* __restrict__ V, double* __restrict__ partials,
                                                                Geo g, Geo gc, Op<T, 2> op, T clc, int yc)
 {
-    using S = YsShape<T, PRE>;
+    using S = YsShape<T, PRE, TXV>;
     constexpr int N = S::N, H = S::H, G = S::G, TX = S::TX, NTL = S::NTL, ES = S::ES;
     constexpr bool RR = PRE && LINEAR == 0;
     using VT = Vec<T, N>;
@@ -4257,16 +4260,26 @@ static hipError_t zs_launch(const FusedArgs& a, hipStream_t s)
     return hipGetLastError();
 }
 
-template <typename T, bool PRE, int LINEAR, bool ERR, bool CLZ>
-static hipError_t ys_launch(const FusedArgs& a, hipStream_t s)
+static int ys_tx(int rb, const Geo& g);
+
+template <typename T, bool PRE, int LINEAR, bool ERR, bool CLZ, int TXV>
+static hipError_t ys_launch_tx(const FusedArgs& a, hipStream_t s)
 {
-    using S = YsShape<T, PRE>;
+    using S = YsShape<T, PRE, TXV>;
     const Op<T, 2> op = make_op<T, 2>(a.h, a.cl);
     const unsigned nb = (unsigned)((a.g.nx / S::TX) * (a.g.ny / a.zc));
-    k_ys<T, PRE, LINEAR, ERR, CLZ><<<nb, S::NTL, 0, s>>>((const T*)a.src, (const T*)a.f, (T*)a.dst,
+    k_ys<T, PRE, LINEAR, ERR, CLZ, TXV><<<nb, S::NTL, 0, s>>>((const T*)a.src, (const T*)a.f, (T*)a.dst,
                                                          (const T*)(a.old ? a.old : a.dst), (T*)a.R, (const T*)a.V,
                                                          a.partials, a.g, a.gc, op, (T)a.clc, a.zc);
     return hipGetLastError();
+}
+
+template <typename T, bool PRE, int LINEAR, bool ERR, bool CLZ>
+static hipError_t ys_launch(const FusedArgs& a, hipStream_t s)
+{
+    constexpr int F = ys_tx_full<T>();
+    return ys_tx(sizeof(T), a.g) == F ? ys_launch_tx<T, PRE, LINEAR, ERR, CLZ, F>(a, s)
+                                      : ys_launch_tx<T, PRE, LINEAR, ERR, CLZ, F / 2>(a, s);
 }
 
 template <typename T, bool CLZ>
@@ -4305,7 +4318,8 @@ static void zs_tile(int rb, int& tx, int& ty, int pre = -1, bool clz = true)
 // 2D (k_ys): rows per z-chunk of a workgroup (MGP_YS_ROWS, default 32; even)
 static int ys_rows(const Geo& g)
 {
-    static const int rows = [] {
+    // read per call (plan time and launch), so that a process can build contexts under different settings
+    const int rows = [] {
         const char* v = std::getenv("MGP_YS_ROWS");
         const int r = v ? std::atoi(v) : 32;
         return r >= 8 && (r & 1) == 0 ? r : 32;
@@ -4315,11 +4329,27 @@ static int ys_rows(const Geo& g)
     return r;
 }
 
-static int ys_tx(int rb) { return rb == 4 ? YsShape<float, true>::TX : YsShape<double, true>::TX; }
+// segment width of a 2D level: the full width, or half of it when the full width gives fewer than
+// MGP_ZS_WGS (default 256) workgroups (MGP_YS_HALF: -1 that rule, 0 never, 1 always)
+static int ys_tx(int rb, const Geo& g)
+{
+    const int mode = [] {
+        const char* v = std::getenv("MGP_YS_HALF");
+        return v ? std::atoi(v) : -1;
+    }();
+    const int64_t target = [] {
+        const char* v = std::getenv("MGP_ZS_WGS");
+        return v ? std::atoll(v) : (int64_t)256;
+    }();
+    const int full = rb == 4 ? ys_tx_full<float>() : ys_tx_full<double>();
+    if (mode == 0 || g.nx % (full / 2) != 0) return full;
+    if (mode == 1 || g.nx % full != 0) return full / 2;
+    return (int64_t)(g.nx / full) * (g.ny / ys_rows(g)) < target ? full / 2 : full;
+}
 
 bool fused_supported(int rb, int dim, int ns, const Geo& g)
 {
-    if (dim == 2) return ns == 2 && g.nz == 1 && g.nx % ys_tx(rb) == 0 && g.ny >= 16 && g.ny % ys_rows(g) == 0;
+    if (dim == 2) return ns == 2 && g.nz == 1 && g.nx % ys_tx(rb, g) == 0 && g.ny >= 16 && g.ny % ys_rows(g) == 0;
     if (dim != 3 || ns != 2) return false;
     int TX, TY;
     zs_tile(rb, TX, TY);
@@ -4345,7 +4375,7 @@ int fused_zc(int rb, const Geo& g, bool pre, bool clz)
 
 int fused_blocks(int rb, const Geo& g, int zc)  // POST's workgroups (one err partial each)
 {
-    if (g.gnz == 1 && g.nz == 1) return (g.nx / ys_tx(rb)) * (g.ny / zc);
+    if (g.gnz == 1 && g.nz == 1) return (g.nx / ys_tx(rb, g)) * (g.ny / zc);
     int TX, TY;
     zs_tile(rb, TX, TY, 0);
     return (int)((int64_t)(g.nx / TX) * (g.ny / TY) * (g.nz / zc));

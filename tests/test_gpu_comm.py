@@ -50,16 +50,18 @@ def _run(box, world, cfg, cycles, env=None):
     return logs, timings
 
 
+# side: level 0 runs temporally blocked (k_zs), so its early POST exchange rides the side communicator (the
+# fp64 POST tile is 64 wide: a 32-wide box runs level 0 per piece, every exchange on the main one)
 CASES = [
-    ((64, 64, 256), 2, dict(cycle="V"), 4096),
-    ((64, 64, 512), 8, dict(cycle="V"), 4096),
-    ((64, 64, 256), 4, dict(cycle="F"), 4096),
-    ((32, 32, 256), 8, dict(cycle="F", real="double"), 512),
+    ((64, 64, 256), 2, dict(cycle="V"), 4096, True),
+    ((64, 64, 512), 8, dict(cycle="V"), 4096, True),
+    ((64, 64, 256), 4, dict(cycle="F"), 4096, True),
+    ((32, 32, 256), 8, dict(cycle="F", real="double"), 512, False),
 ]
 
 
-@pytest.mark.parametrize("box,world,extra,gather", CASES, ids=["w2-V", "w8-V", "w4-F", "w8-F-f64"])
-def test_executed_comm_log_equals_plan(box, world, extra, gather, monkeypatch):
+@pytest.mark.parametrize("box,world,extra,gather,side", CASES, ids=["w2-V", "w8-V", "w4-F", "w8-F-f64"])
+def test_executed_comm_log_equals_plan(box, world, extra, gather, side, monkeypatch):
     monkeypatch.setenv("MGP_FUSED", "1")
     monkeypatch.setenv("MGP_FUSED_MIN_CELLS", "65536")
     mg = _mg()
@@ -71,7 +73,7 @@ def test_executed_comm_log_equals_plan(box, world, extra, gather, monkeypatch):
     assert all(l == logs[0] for l in logs)  # call-order equality across ranks
     plan = mg.plan_comm(mg.make_opts(dim=3, n=box, rank=0, world=world, comm_id=b"\0" * 128, **cfg), cycles)
     assert logs[0] == plan
-    assert any(r[1] == 1 for r in plan)  # the early POST exchange rides the side communicator
+    assert any(r[1] == 1 for r in plan) == side  # the early POST exchange rides the side communicator
     # every exchange and collective was timed on its stream
     n_ex = sum(1 for r in plan if r[0] == "exchange")
     n_co = sum(1 for r in plan if r[0] != "exchange")
