@@ -1002,8 +1002,9 @@ int fused_post(mgp_ctx* c, int l, double h, bool want_err)
     L.ghost_ok = !L.p.dist;
     L.ghost_zero = false;
     if (want_err) {
-        HIP_TRY(c, mgp::launch_sum_partials(c->d_part, mgp::fused_blocks(c->rb, L.g, L.zc), c->err_dst, c->s,
-                                            c->err_ctr));
+        HIP_TRY(c, mgp::launch_sum_partials(c->d_part,
+                                            mgp::fused_blocks(c->rb, L.g, L.zc, coarse_coef(c->o.coarse_bc, l) == 0.0),
+                                            c->err_dst, c->s, c->err_ctr));
         c->err_done = true;
     }
     return MGP_OK;
@@ -1709,8 +1710,9 @@ static void select_engines(mgp_ctx* c)
             Level& L = c->lev[l];
             L.fused = on && level_cells(L) >= min_cells && mgp::fused_supported(c->rb, c->o.dim, 2, L.g);
             if (L.fused) {
-                L.zc = mgp::fused_zc(c->rb, L.g, false);
-                L.zc_pre = mgp::fused_zc(c->rb, L.g, true, coarse_coef(c->o.coarse_bc, (int)l) == 0.0);
+                const bool clz = coarse_coef(c->o.coarse_bc, (int)l) == 0.0;
+                L.zc = mgp::fused_zc(c->rb, L.g, false, clz);
+                L.zc_pre = mgp::fused_zc(c->rb, L.g, true, clz);
             }
             if (L.fused && L.p.dist) c->G = mgp::kGhostZs;
         }
@@ -1842,7 +1844,7 @@ static int create_impl(mgp_ctx** out, const mgp_opts* o, mgp_loopback* lb, ncclC
         c->use_gs = v && std::atoi(v) != 0;
     }
     int nb2 = 2 * mgp::half_blocks(c->rk, L0.g, c->use_gs);
-    if (L0.fused) nb2 = std::max(nb2, mgp::fused_blocks(c->rb, L0.g, L0.zc));
+    if (L0.fused) nb2 = std::max(nb2, mgp::fused_blocks(c->rb, L0.g, L0.zc, coarse_coef(c->o.coarse_bc, 0) == 0.0));
     c->part_cap = std::max<int64_t>(mgp::kSumBlocks, nb2 + mgp::sum_scratch(nb2));
     if (hipMalloc(&c->d_part, sizeof(double) * c->part_cap) != hipSuccess) {
         c->err = "hipMalloc failed for reduction partials";

@@ -139,7 +139,7 @@ bool fused_supported(int rb, int dim, int ns, const Geo& g);
 hipError_t prepare_kernels(int rb);
 // clz: the level's operator has no boundary modification (cl == 0): PRE's tile may differ otherwise
 int fused_zc(int rb, const Geo& g, bool pre, bool clz = true);
-int fused_blocks(int rb, const Geo& g, int zc);
+int fused_blocks(int rb, const Geo& g, int zc, bool clz = true);
 hipError_t launch_fused(int rb, const FusedArgs& a, hipStream_t s);
 
 // Tiled smoothing phases of a small replicated red/black level (k_blk: one launch per phase, the 3D

@@ -1745,6 +1745,16 @@ __device__ __forceinline__ void lds_barrier()
 #ifndef ZS_NPRE_CL_F32
 #define ZS_NPRE_CL_F32 ZS_NPRE_F32
 #endif
+// POST's wide tile (levels with cl = 0 whose box it divides; MGP_ZS_WIDE=0 turns it off): a 64-wide tile's row
+// of one colour is one 128-byte line, and its x halo (2 packed cells per side) touches the two neighbouring
+// lines, so every row costs 3 line requests per field for 1 line of data; 128 x 16 tiles cost 4 for 2.
+// 512^3 POST 480 -> 436 us (round 4).  Its 14 waves leave 128 VGPRs (a few spill).
+#ifndef ZS_TXPOST_W_F32
+#define ZS_TXPOST_W_F32 128
+#endif
+#ifndef ZS_TYPOST_W_F32
+#define ZS_TYPOST_W_F32 16
+#endif
 template <typename T>
 struct ZsTile;
 template <>
@@ -1752,6 +1762,7 @@ struct ZsTile<float> {
     static constexpr int TXPRE = ZS_TXPRE_F32, TXPOST = ZS_TXPOST_F32, TYPRE = ZS_TYPRE_F32, TYPOST = ZS_TYPOST_F32,
                          NPRE = ZS_NPRE_F32, NPOST = ZS_NPOST_F32;
     static constexpr int TXPRE_CL = ZS_TXPRE_CL_F32, TYPRE_CL = ZS_TYPRE_CL_F32, NPRE_CL = ZS_NPRE_CL_F32;
+    static constexpr int TXPOST_W = ZS_TXPOST_W_F32, TYPOST_W = ZS_TYPOST_W_F32;
 };
 #ifndef ZS_TXPRE_F64
 #define ZS_TXPRE_F64 32
@@ -1770,6 +1781,7 @@ struct ZsTile<double> {
     static constexpr int TXPRE = ZS_TXPRE_F64, TXPOST = ZS_TXPOST_F64, TYPRE = ZS_TYPRE_F64, TYPOST = ZS_TYPOST_F64,
                          NPRE = 2, NPOST = 2;
     static constexpr int TXPRE_CL = TXPRE, TYPRE_CL = TYPRE, NPRE_CL = NPRE;
+    static constexpr int TXPOST_W = TXPOST, TYPOST_W = TYPOST;  // (no wide fp64 variant is instantiated)
 };
 // Streaming (non-temporal) level-0 loads / stores of the phases: timing experiments (ZS_NT bit 0:
 // loads, bit 1: stores), so that the level-0 stream does not evict the coarse level it writes
@@ -1783,11 +1795,13 @@ constexpr bool kZsNTL = (ZS_NT & 1) != 0, kZsNTS = (ZS_NT & 2) != 0, kZsNTO = (Z
 #endif
 constexpr bool kZsPreRed = ZS_PRE_RED_STORE != 0;
 
-template <typename T, bool PRE, bool CLZ = true>
+template <typename T, bool PRE, bool CLZ = true, bool WIDE = false>
 struct ZsShape {
     static constexpr int N = PRE ? (CLZ ? ZsTile<T>::NPRE : ZsTile<T>::NPRE_CL) : ZsTile<T>::NPOST;
-    static constexpr int TX = PRE ? (CLZ ? ZsTile<T>::TXPRE : ZsTile<T>::TXPRE_CL) : ZsTile<T>::TXPOST;
-    static constexpr int TY = PRE ? (CLZ ? ZsTile<T>::TYPRE : ZsTile<T>::TYPRE_CL) : ZsTile<T>::TYPOST;
+    static constexpr int TX = PRE ? (CLZ ? ZsTile<T>::TXPRE : ZsTile<T>::TXPRE_CL)
+                                  : (WIDE ? ZsTile<T>::TXPOST_W : ZsTile<T>::TXPOST);
+    static constexpr int TY = PRE ? (CLZ ? ZsTile<T>::TYPRE : ZsTile<T>::TYPRE_CL)
+                                  : (WIDE ? ZsTile<T>::TYPOST_W : ZsTile<T>::TYPOST);
     static constexpr int H = PRE ? 5 : 4;              // y/z halo = stages that read neighbours
     // x halo cells per side: the trapezoid depth H in whole column groups (2 N cells of x each)
 #ifdef ZS_HX_FIXED  // timing experiment: the round-1 fixed 8-cell x halo
@@ -2130,14 +2144,14 @@ __device__ __forceinline__ void zs_unroll(F&& f)
 #ifndef ZS_WPE_POST
 #define ZS_WPE_POST 4
 #endif
-template <typename T, bool PRE, int LINEAR, bool ERR, bool CLZ>
-__global__ __launch_bounds__((ZsShape<T, PRE, CLZ>::NTL))
+template <typename T, bool PRE, int LINEAR, bool ERR, bool CLZ, bool WIDE = false>
+__global__ __launch_bounds__((ZsShape<T, PRE, CLZ, WIDE>::NTL))
 __attribute__((amdgpu_waves_per_eu(1, PRE ? ZS_WPE_PRE : ZS_WPE_POST))) void k_zs(const T* __restrict__ src, const T* __restrict__ f,
                                                                 T* __restrict__ dst, const T* old, T* __restrict__ R,
                                                                 const T* __restrict__ V, double* __restrict__ partials,
                                                                 Geo g, Geo gc, Op<T, 3> op, T clc, int zc, int gz)
 {
-    using S = ZsShape<T, PRE, CLZ>;
+    using S = ZsShape<T, PRE, CLZ, WIDE>;
     constexpr int N = S::N, H = S::H, HWE = S::HWE, G = S::G, YE = S::YE, SLOT = S::SLOT, TX = S::TX,
                   TY = S::TY, NS3 = S::NS3, NTL = S::NTL;
     // PRE: LINEAR selects the restriction: 0 = residual + 2^3 average here; 1 = none (both colours of the
@@ -2669,25 +2683,25 @@ __device__ __forceinline__ void ys_cells(const Vec<T, N>& ym, const Vec<T, N>& c
         t[e] = t[e] + ym.v[e];
         t[e] = t[e] + yp.v[e];
     }
-    if (CLZ || __all(nby == 0 && xin)) {
+    // cl != 0: nby is the row's (uniform across the workgroup), so the row's two diagonals (off / on an x
+    // face) are one uniform table walk and a cell selects between them: no divergent boundary path (a
+    // segment at an x face would otherwise hold its whole workgroup at every step's barrier)
+    T d0 = op.adiag, y0 = op.yadiag, d1 = op.adiag, y1 = op.yadiag;
+    if (!CLZ) op.row_diag(nby, d0, y0, d1, y1);
 #pragma unroll
-        for (int e = 0; e < N; ++e) {
-            if (RES) {
-                const T askew = t[e] * op.inv_hSq;
-                const T a_u = askew + op.adiag * uc.v[e];
-                out[e] = fv.v[e] - a_u;
-            } else {
-                out[e] = div_rn(fv.v[e] - t[e] * op.inv_hSq, op.adiag, op.yadiag);
-            }
-        }
-    } else {
-#pragma unroll
-        for (int e = 0; e < N; ++e) {
-            const int i = 2 * (gm + e) + o;
-            const int nbc = nby + (i == 0) + (i == nx - 1);
-            out[e] = RES ? op.residual_direct(t[e], fv.v[e], uc.v[e], nbc) : op.relax_direct(t[e], fv.v[e], nbc);
+    for (int e = 0; e < N; ++e) {
+        const int i = 2 * (gm + e) + o;
+        const bool xf = !CLZ && (i == 0 || i == nx - 1);
+        const T d = xf ? d1 : d0;
+        if (RES) {
+            const T askew = t[e] * op.inv_hSq;
+            const T a_u = askew + d * uc.v[e];
+            out[e] = fv.v[e] - a_u;
+        } else {
+            out[e] = div_rn(fv.v[e] - t[e] * op.inv_hSq, d, xf ? y1 : y0);
         }
     }
+    (void)xin;
 }
 
 // PRE: LINEAR selects the restriction (0: residual + 2x2 average here; 1: none, both colours stored)
@@ -4247,17 +4261,25 @@ hipError_t launch_prolong_correct(int rb, int dim, int linear, void* u, const vo
 
 // ---- fused smoothing phases ----
 
-template <typename T, bool PRE, int LINEAR, bool ERR, bool CLZ>
+template <typename T, bool PRE, int LINEAR, bool ERR, bool CLZ, bool WIDE = false>
 static hipError_t zs_launch(const FusedArgs& a, hipStream_t s)
 {
-    using S = ZsShape<T, PRE, CLZ>;
+    using S = ZsShape<T, PRE, CLZ, WIDE>;
     const Op<T, 3> op = make_op<T, 3>(a.h, a.cl);
     const unsigned nb = (unsigned)((a.g.nx / S::TX) * (a.g.ny / S::TY) * (a.g.nz / a.zc));
-    k_zs<T, PRE, LINEAR, ERR, CLZ><<<nb, S::NTL, S::lds_bytes, s>>>((const T*)a.src, (const T*)a.f, (T*)a.dst,
-                                                                     (const T*)(a.old ? a.old : a.dst), (T*)a.R,
-                                                                     (const T*)a.V, a.partials, a.g, a.gc,
-                                                                     op, (T)a.clc, a.zc, a.ghost);
+    k_zs<T, PRE, LINEAR, ERR, CLZ, WIDE><<<nb, S::NTL, S::lds_bytes, s>>>((const T*)a.src, (const T*)a.f, (T*)a.dst,
+                                                                           (const T*)(a.old ? a.old : a.dst), (T*)a.R,
+                                                                           (const T*)a.V, a.partials, a.g, a.gc,
+                                                                           op, (T)a.clc, a.zc, a.ghost);
     return hipGetLastError();
+}
+
+// POST's wide tile (ZsTile::TXPOST_W): fp32, cl = 0, a box it divides, MGP_ZS_WIDE not 0 (read per call)
+static bool zs_wide(int rb, const Geo& g, bool clz)
+{
+    const char* v = std::getenv("MGP_ZS_WIDE");
+    if (rb != 4 || !clz || (v && std::atoi(v) == 0)) return false;
+    return g.nx % ZsTile<float>::TXPOST_W == 0 && g.ny % ZsTile<float>::TYPOST_W == 0;
 }
 
 static int ys_tx(int rb, const Geo& g);
@@ -4296,12 +4318,20 @@ static hipError_t fused_dispatch(const FusedArgs& a, hipStream_t s)
 {
     const bool err = a.partials != nullptr;
     if (a.pre) return a.linear ? zs_launch<T, true, 1, false, CLZ>(a, s) : zs_launch<T, true, 0, false, CLZ>(a, s);
+    if constexpr (std::is_same<T, float>::value && CLZ) {
+        if (zs_wide(4, a.g, true)) {
+            if (a.linear)
+                return err ? zs_launch<T, false, 1, true, CLZ, true>(a, s) : zs_launch<T, false, 1, false, CLZ, true>(a, s);
+            return err ? zs_launch<T, false, 0, true, CLZ, true>(a, s) : zs_launch<T, false, 0, false, CLZ, true>(a, s);
+        }
+    }
     if (a.linear) return err ? zs_launch<T, false, 1, true, CLZ>(a, s) : zs_launch<T, false, 1, false, CLZ>(a, s);
     return err ? zs_launch<T, false, 0, true, CLZ>(a, s) : zs_launch<T, false, 0, false, CLZ>(a, s);
 }
 
-// tile of a phase (pre) or the largest of all (pre < 0); clz: the level operator has no boundary modification
-static void zs_tile(int rb, int& tx, int& ty, int pre = -1, bool clz = true)
+// tile of a phase (pre) or the largest of all (pre < 0); clz: the level operator has no boundary modification;
+// wide: POST's wide tile (zs_wide)
+static void zs_tile(int rb, int& tx, int& ty, int pre = -1, bool clz = true, bool wide = false)
 {
     const int xa = rb == 4 ? ZsTile<float>::TXPRE : ZsTile<double>::TXPRE;
     const int xc = rb == 4 ? ZsTile<float>::TXPRE_CL : ZsTile<double>::TXPRE_CL;
@@ -4313,6 +4343,10 @@ static void zs_tile(int rb, int& tx, int& ty, int pre = -1, bool clz = true)
     auto mx = [](int u, int v, int w) { return u > v ? (u > w ? u : w) : (v > w ? v : w); };
     tx = pre < 0 ? mx(xa, xb, xc) : (pre ? xp : xb);
     ty = pre < 0 ? mx(a, b, ac) : (pre ? yp : b);
+    if (pre == 0 && wide) {
+        tx = ZsTile<float>::TXPOST_W;
+        ty = ZsTile<float>::TYPOST_W;
+    }
 }
 
 // 2D (k_ys): rows per z-chunk of a workgroup (MGP_YS_ROWS, default 32; even)
@@ -4362,7 +4396,7 @@ int fused_zc(int rb, const Geo& g, bool pre, bool clz)
 {
     if (g.gnz == 1 && g.nz == 1) return ys_rows(g);  // 2D: rows per chunk
     int TX, TY;
-    zs_tile(rb, TX, TY, pre ? 1 : 0, clz);
+    zs_tile(rb, TX, TY, pre ? 1 : 0, clz, !pre && zs_wide(rb, g, clz));
     static const int64_t target = [] {
         const char* v = std::getenv("MGP_ZS_WGS");
         return v ? std::atoll(v) : (int64_t)256;
@@ -4373,11 +4407,11 @@ int fused_zc(int rb, const Geo& g, bool pre, bool clz)
     return (int)(g.nz / chunks);
 }
 
-int fused_blocks(int rb, const Geo& g, int zc)  // POST's workgroups (one err partial each)
+int fused_blocks(int rb, const Geo& g, int zc, bool clz)  // POST's workgroups (one err partial each)
 {
     if (g.gnz == 1 && g.nz == 1) return (g.nx / ys_tx(rb, g)) * (g.ny / zc);
     int TX, TY;
-    zs_tile(rb, TX, TY, 0);
+    zs_tile(rb, TX, TY, 0, clz, zs_wide(rb, g, clz));
     return (int)((int64_t)(g.nx / TX) * (g.ny / TY) * (g.nz / zc));
 }
 
@@ -4388,6 +4422,14 @@ static hipError_t fused_attr()
 {
     const int pre = (int)ZsShape<T, true, CLZ>::lds_bytes, post = (int)ZsShape<T, false, CLZ>::lds_bytes;
     const auto A = hipFuncAttributeMaxDynamicSharedMemorySize;
+    if constexpr (std::is_same<T, float>::value && CLZ) {
+        const int w = (int)ZsShape<T, false, CLZ, true>::lds_bytes;
+        hipError_t e = hipFuncSetAttribute((const void*)k_zs<T, false, 0, false, CLZ, true>, A, w);
+        if (e == hipSuccess) e = hipFuncSetAttribute((const void*)k_zs<T, false, 0, true, CLZ, true>, A, w);
+        if (e == hipSuccess) e = hipFuncSetAttribute((const void*)k_zs<T, false, 1, false, CLZ, true>, A, w);
+        if (e == hipSuccess) e = hipFuncSetAttribute((const void*)k_zs<T, false, 1, true, CLZ, true>, A, w);
+        if (e != hipSuccess) return e;
+    }
     hipError_t e = hipFuncSetAttribute((const void*)k_zs<T, true, 0, false, CLZ>, A, pre);
     if (e == hipSuccess) e = hipFuncSetAttribute((const void*)k_zs<T, true, 1, false, CLZ>, A, pre);
     if (e == hipSuccess) e = hipFuncSetAttribute((const void*)k_zs<T, false, 0, false, CLZ>, A, post);

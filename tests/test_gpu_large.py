@@ -255,17 +255,19 @@ def test_cpu_raw_fields(real):
     psi = r.psi
     ctx = r.ctx
     assert np.array_equal(r.psiOld, old)
-    d = psi - old
-    assert np.array_equal(r.errorBuf, d * d)
+    # cpu-raw.lua semantics (MultigridHIPRaw's default arith="double"): the difference and its square in double,
+    # stored once in the real type
+    d = psi.astype(np.float64) - old.astype(np.float64)
+    assert np.array_equal(r.errorBuf, (d * d).astype(psi.dtype))
     assert r.tmpU.shape == psi.shape  # Jacobi target buffer
     assert sorted(r.rs.keys(), reverse=True) == [32, 16, 8, 4, 2, 1]
     for size in (32, 16, 8):
         lvl = [lv["nx"] for lv in ctx.levels].index(size)
         u, f = r.Vs[size], r.Rs[size]
-        ref = residual_arr(2, u, f, (2.0 ** lvl) / 32, 0.0)
+        ref = residual_arr(2, u, f, (2.0 ** lvl) / 32, 0.0, arith="double")
         assert np.array_equal(r.rs[size], ref)
         V = r.Vs[size // 2]
-        assert np.array_equal(r.vs[size], prolong_correct_arr(2, np.zeros_like(u), V, "pc", 0.0))
+        assert np.array_equal(r.vs[size], prolong_correct_arr(2, np.zeros_like(u), V, "pc", 0.0, arith="double"))
     with pytest.raises(TypeError):
         r.rs[8] = np.zeros((8, 8))
 

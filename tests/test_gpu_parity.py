@@ -265,8 +265,11 @@ def test_tail_equals_launch_per_piece(cfg, monkeypatch):
         assert np.array_equal(a.get_f(level), b.get_f(level)), f"f level {level}"
 
 
+# fp32 boxes 128 wide run POST's wide 128 x 16 tile on level 0 (wide="0": the 64 x 32 tile)
 FUSED_CONFIGS = [
     dict(n=(128, 128, 128), real="float", prolong="linear", coarse_bc="consistent"),
+    dict(n=(128, 128, 128), real="float", prolong="linear", coarse_bc="consistent", wide="0"),
+    dict(n=(256, 64, 32), real="float", prolong="pc", coarse_bc="zero", err_mode=0),
     dict(n=(64, 64, 64), real="float", prolong="linear", coarse_bc="consistent", cycle="F"),
     dict(n=(128, 64, 32), real="double", prolong="pc", coarse_bc="zero"),
     dict(n=(64, 128, 64), real="double", prolong="linear", coarse_bc="consistent", coarse_init="warm"),
@@ -278,6 +281,8 @@ FUSED_CONFIGS = [
 def test_fused_phases_match_oracle(cfg, monkeypatch):
     """Temporally blocked RB-GS 2+2 phases (k_fused, forced down to 64^3 here) vs one launch per
     half-sweep vs the C oracle: psi bit-identical on every level; err to summation order."""
+    cfg = dict(cfg)
+    monkeypatch.setenv("MGP_ZS_WIDE", cfg.pop("wide", "1"))
     kw = dict(dim=3, smoother="rbgs", nu1=2, nu2=2, **cfg)
     monkeypatch.setenv("MGP_FUSED_MIN_CELLS", "65536")
     monkeypatch.setenv("MGP_FUSED", "1")
