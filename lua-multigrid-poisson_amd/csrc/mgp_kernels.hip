@@ -1755,6 +1755,9 @@ __device__ __forceinline__ void lds_barrier()
 #ifndef ZS_TYPOST_W_F32
 #define ZS_TYPOST_W_F32 16
 #endif
+#ifndef ZS_NPOST_W_F32  // (4: 128 x 16 POST at 18 x 24 threads measured 439 against 434 us)
+#define ZS_NPOST_W_F32 ZS_NPOST_F32
+#endif
 template <typename T>
 struct ZsTile;
 template <>
@@ -1762,7 +1765,7 @@ struct ZsTile<float> {
     static constexpr int TXPRE = ZS_TXPRE_F32, TXPOST = ZS_TXPOST_F32, TYPRE = ZS_TYPRE_F32, TYPOST = ZS_TYPOST_F32,
                          NPRE = ZS_NPRE_F32, NPOST = ZS_NPOST_F32;
     static constexpr int TXPRE_CL = ZS_TXPRE_CL_F32, TYPRE_CL = ZS_TYPRE_CL_F32, NPRE_CL = ZS_NPRE_CL_F32;
-    static constexpr int TXPOST_W = ZS_TXPOST_W_F32, TYPOST_W = ZS_TYPOST_W_F32;
+    static constexpr int TXPOST_W = ZS_TXPOST_W_F32, TYPOST_W = ZS_TYPOST_W_F32, NPOST_W = ZS_NPOST_W_F32;
 };
 #ifndef ZS_TXPRE_F64
 #define ZS_TXPRE_F64 32
@@ -1781,7 +1784,7 @@ struct ZsTile<double> {
     static constexpr int TXPRE = ZS_TXPRE_F64, TXPOST = ZS_TXPOST_F64, TYPRE = ZS_TYPRE_F64, TYPOST = ZS_TYPOST_F64,
                          NPRE = 2, NPOST = 2;
     static constexpr int TXPRE_CL = TXPRE, TYPRE_CL = TYPRE, NPRE_CL = NPRE;
-    static constexpr int TXPOST_W = TXPOST, TYPOST_W = TYPOST;  // (no wide fp64 variant is instantiated)
+    static constexpr int TXPOST_W = TXPOST, TYPOST_W = TYPOST, NPOST_W = NPOST;  // (no wide fp64 variant is instantiated)
 };
 // Streaming (non-temporal) level-0 loads / stores of the phases: timing experiments (ZS_NT bit 0:
 // loads, bit 1: stores), so that the level-0 stream does not evict the coarse level it writes
@@ -1797,7 +1800,8 @@ constexpr bool kZsPreRed = ZS_PRE_RED_STORE != 0;
 
 template <typename T, bool PRE, bool CLZ = true, bool WIDE = false>
 struct ZsShape {
-    static constexpr int N = PRE ? (CLZ ? ZsTile<T>::NPRE : ZsTile<T>::NPRE_CL) : ZsTile<T>::NPOST;
+    static constexpr int N = PRE ? (CLZ ? ZsTile<T>::NPRE : ZsTile<T>::NPRE_CL)
+                                 : (WIDE ? ZsTile<T>::NPOST_W : ZsTile<T>::NPOST);
     static constexpr int TX = PRE ? (CLZ ? ZsTile<T>::TXPRE : ZsTile<T>::TXPRE_CL)
                                   : (WIDE ? ZsTile<T>::TXPOST_W : ZsTile<T>::TXPOST);
     static constexpr int TY = PRE ? (CLZ ? ZsTile<T>::TYPRE : ZsTile<T>::TYPRE_CL)
