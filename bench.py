@@ -370,7 +370,13 @@ def run_workload(a, cfg, box, strong, rank, world, local, dist, steps, warmup, p
         if a.traffic and os.path.exists(a.traffic):
             with open(a.traffic) as fh:
                 tr = json.load(fh)
-            ent = tr.get("kernels", {}).get(kernels[dom])
+            # the launch's full template name carries the tile / segment variant the library picked (k_zs's WIDE,
+            # k_ys's segment width): match on the name this table knows plus any trailing template arguments
+            tk = tr.get("kernels", {})
+            full = [n for n in tk if n == kernels[dom] or n.startswith(kernels[dom][:-1] + ", ")]
+            ent = tk.get(full[0]) if len(full) == 1 else None
+            if len(full) == 1:
+                roof["kernel"] = full[0]
             src_ok = tr.get("source_hash") == source_hash()
             wl_ok = tr.get("cells_rank") in (None, cells_rank)
             roof["traffic_source"] = os.path.relpath(a.traffic, ROOT)
