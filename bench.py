@@ -420,6 +420,8 @@ def cycle_compulsory_bytes(levels, cfg, a, rb):
             reals = 2.0  # coarse solve: read f, write u
         elif lv["engine"] == "piece":
             reals = 3.0 * 2 * a.nu + 2 * (2 + coarse)
+        elif lv["engine"] == "zpost":  # PRE per piece (nu sweeps + residual / restriction), POST temporally blocked
+            reals = 3.0 * a.nu + (2 + coarse) + (2.5 + coarse)
         else:
             reals = (2 + coarse) + (2.5 + coarse)
         if l == 0:

@@ -118,7 +118,8 @@ const char* mgp_last_error(const mgp_ctx* c);
 
 /* Level hierarchy.  info[0..7] = {nx, ny, nz_global, nz_local, z0, distributed, engine, exchanges}; engine =
  * how a cycle runs the level's smoothing phases: 0 one launch per piece, 1 inside the single-launch coarse
- * tail (LDS-resident levels), 2 temporally blocked z-streamed phases, 3 3D-tiled one-launch phases; exchanges =
+ * tail (LDS-resident levels), 2 temporally blocked z-streamed phases, 3 3D-tiled one-launch phases, 4 PRE one
+ * launch per piece and POST temporally blocked; exchanges =
  * halo exchanges (grouped send/recv with the z-neighbours) of this level so far on this rank. */
 int         mgp_num_levels(const mgp_ctx* c);
 int         mgp_level_info(const mgp_ctx* c, int level, int64_t info[8]);

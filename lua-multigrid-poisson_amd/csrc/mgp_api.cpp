@@ -145,6 +145,7 @@ struct Level {
     bool fghost_ok = true;  // f's ghost planes likewise
     bool fused = false;     // smoothing phases run temporally blocked (k_zs); needs t
     bool blk = false;       // smoothing phases run as 3D-tiled one-launch phases (k_blk); needs t
+    bool zpost = false;     // PRE one launch per piece, POST temporally blocked (k_zs); needs t
     bool zero_pending = false;  // u is logically 0: the next red half-sweep reads c->zbuf instead
     bool ghost_zero = false;    // u is 0 everywhere, so ghost planes of any depth are current
     int64_t exchanges = 0;      // halo exchanges of this level so far (mgp_level_info info[7])
@@ -1235,6 +1236,7 @@ int cycle_rec(mgp_ctx* c, int l, double h, bool fcycle)
     }
     const bool fused = c->lev[l].fused && h == level_h(c, l);
     const bool blk = !fused && c->lev[l].blk && h == level_h(c, l);
+    const bool zpost = c->lev[l].zpost && h == level_h(c, l);
     std::optional<Range> pre_range(std::in_place, "L%d pre-smooth + restrict", l);
     if (fused) {
         TRY(fused_pre(c, l, h));
@@ -1251,7 +1253,7 @@ int cycle_rec(mgp_ctx* c, int l, double h, bool fcycle)
     TRY(cycle_rec(c, l + 1, 2 * h, false));
     const bool want_err = l == 0 && c->in_cycle && c->err_fuse;
     Range post_range("L%d prolong + post-smooth", l);
-    if (fused) {
+    if (fused || zpost) {
         TRY(fused_post(c, l, h, want_err));
     } else if (blk && !want_err) {
         TRY(block_post(c, l, h));
@@ -1691,7 +1693,7 @@ static void select_engines(mgp_ctx* c)
         c->err_fuse = false;
         c->fresh_sweep = false;
         c->post1 = false;
-        for (auto& L : c->lev) L.fused = L.blk = false;
+        for (auto& L : c->lev) L.fused = L.blk = L.zpost = false;
         c->tail_level = -1;
         return;
     }
@@ -1716,6 +1718,17 @@ static void select_engines(mgp_ctx* c)
             }
             if (L.fused && L.p.dist) c->G = mgp::kGhostZs;
         }
+        // POST alone temporally blocked on the 3D levels of >= MGP_ZPOST_MIN_CELLS cells (default 2^24) below that:
+        // at 256^3 (cl != 0) k_zs POST takes 66 us against 84 us for the prolongation + 4 half-sweeps, while
+        // its PRE (109 us + a 10 us fill of the fresh guess) loses to the per-piece 94 us
+        const char* vz = std::getenv("MGP_ZPOST_MIN_CELLS");
+        const int64_t zmin = vz ? std::atoll(vz) : (c->o.dim == 3 ? int64_t(1) << 24 : INT64_MAX);
+        for (size_t l = 1; l + 1 < c->lev.size(); ++l) {
+            Level& L = c->lev[l];
+            L.zpost = on && !L.fused && level_cells(L) >= zmin && mgp::fused_supported(c->rb, c->o.dim, 2, L.g);
+            if (L.zpost) L.zc = mgp::fused_zc(c->rb, L.g, false, coarse_coef(c->o.coarse_bc, (int)l) == 0.0);
+            if (L.zpost && L.p.dist) c->G = mgp::kGhostZs;
+        }
     }
     {
         // tiled one-launch phases (k_blk) on replicated RB-GS levels 1 .. of <= MGP_BLK_CELLS cells
@@ -1728,18 +1741,19 @@ static void select_engines(mgp_ctx* c)
         const bool on = !(v && std::atoi(v) == 0) && c->o.smoother == MGP_RBGS && c->o.nu1 >= 1 && c->o.nu2 >= 1;
         for (size_t l = 1; l + 1 < c->lev.size(); ++l) {
             Level& L = c->lev[l];
-            L.blk = on && !L.fused && !L.p.dist && level_cells(L) <= max_cells &&
+            L.blk = on && !L.fused && !L.zpost && !L.p.dist && level_cells(L) <= max_cells &&
                     mgp::block_supported(c->rb, c->o.dim, ns, L.g);
         }
     }
     plan_tail(c);
 }
 
-// mgp_level_info / mgp_plan engine code: 0 one launch per piece, 1 coarse tail, 2 k_zs, 3 k_blk
+// mgp_level_info / mgp_plan engine code: 0 one launch per piece, 1 coarse tail, 2 k_zs, 3 k_blk, 4 PRE per
+// piece + k_zs POST
 static int level_engine(const mgp_ctx* c, int l)
 {
     const Level& L = c->lev[l];
-    return c->tail_level >= 0 && l >= c->tail_level ? 1 : L.fused ? 2 : L.blk ? 3 : 0;
+    return c->tail_level >= 0 && l >= c->tail_level ? 1 : L.fused ? 2 : L.blk ? 3 : L.zpost ? 4 : 0;
 }
 
 static int create_impl(mgp_ctx** out, const mgp_opts* o, mgp_loopback* lb, ncclComm_t ext_comm, ncclComm_t ext_xcomm)
@@ -1792,7 +1806,7 @@ static int create_impl(mgp_ctx** out, const mgp_opts* o, mgp_loopback* lb, ncclC
     for (size_t l = 0; l < c->lev.size(); ++l) {
         Level& L = c->lev[l];
         const size_t bytes = (size_t)L.alloc * rb;
-        const bool need_t = c->o.smoother == MGP_JACOBI || (l == 0 && c->err_fuse) || L.fused || L.blk;
+        const bool need_t = c->o.smoother == MGP_JACOBI || (l == 0 && c->err_fuse) || L.fused || L.blk || L.zpost;
         if (hipMalloc(&L.u, bytes) != hipSuccess || hipMalloc(&L.f, bytes) != hipSuccess ||
             (need_t && hipMalloc(&L.t, bytes) != hipSuccess)) {
             c->err = "hipMalloc failed for level " + std::to_string(l) + " (" + std::to_string(bytes) + " bytes)";

@@ -179,13 +179,13 @@ def comm_unique_id() -> bytes:
 
 def plan(opts: MGPOpts, max_levels: int = 48):
     """Host-only level plan: list of dicts (nx, ny, nz_global, nz_local, z0, distributed, engine), engine =
-    how mgp_create would run the level's phases ("piece", "tail", "zs", "blk")."""
+    how mgp_create would run the level's phases ("piece", "tail", "zs", "blk", "zpost": PRE per piece, POST k_zs)."""
     rows = (ctypes.c_int64 * (8 * max_levels))()
     n = check(lib.mgp_plan(ctypes.byref(opts), rows, max_levels))
     keys = ("nx", "ny", "nz_global", "nz_local", "z0", "distributed")
     out = [dict(zip(keys, [rows[8 * l + i] for i in range(6)])) for l in range(n)]
     for l, d in enumerate(out):
-        d["engine"] = ("piece", "tail", "zs", "blk")[rows[8 * l + 6]]
+        d["engine"] = ("piece", "tail", "zs", "blk", "zpost")[rows[8 * l + 6]]
     return out
 
 

@@ -89,7 +89,7 @@ class Context:
             L.check(L.lib.mgp_level_info(self._h, l, info), self._h)
             self.levels.append(dict(nx=info[0], ny=info[1], nz_global=info[2], nz_local=info[3],
                                     z0=info[4], distributed=bool(info[5]), tail=info[6] == 1,
-                                    engine=("piece", "tail", "zs", "blk")[info[6]], exchanges=info[7]))
+                                    engine=("piece", "tail", "zs", "blk", "zpost")[info[6]], exchanges=info[7]))
 
     # -- lifecycle --
     def close(self):

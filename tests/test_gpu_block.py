@@ -109,12 +109,12 @@ def test_block_levels_of_the_2d_config():
 
 
 def test_block_levels_of_the_bench_config():
-    """512^3 fp32 RB-GS 2+2: level 0 temporally blocked, 256^3 and 128^3 per piece, 64^3 and 32^3 tiled, then
-    the tail."""
+    """512^3 fp32 RB-GS 2+2: level 0 temporally blocked, 256^3 PRE per piece and POST temporally blocked, 128^3 per
+    piece, 64^3 and 32^3 tiled, then the tail."""
     ctx = _ctx(dim=3, n=(512, 512, 512), real="float", smoother="rbgs", nu1=2, nu2=2, prolong="linear",
                coarse_bc="consistent")
     eng = [lv["engine"] for lv in ctx.levels]
-    assert eng[:5] == ["zs", "piece", "piece", "blk", "blk"] and eng[5] == "tail", eng
+    assert eng[:5] == ["zs", "zpost", "piece", "blk", "blk"] and eng[5] == "tail", eng
 
 
 FRESH_CONFIGS = [

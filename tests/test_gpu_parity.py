@@ -308,24 +308,25 @@ def test_fused_phases_match_oracle(cfg, monkeypatch):
 @pytest.mark.parametrize("real", ["float", "double"])
 def test_fused_level1_chunks_match_per_piece(real, monkeypatch):
     """k_zs on the 256^3 level of a 512^3 box (cl != 0, 32-plane z-chunks whose warm-up and drain steps run the
-    steady path): psi of every level bit-identical to one launch per piece after 2 cycles."""
+    steady path), both phases or POST alone (the default: PRE per piece): psi of every level bit-identical to
+    one launch per piece after 2 cycles."""
     kw = dict(dim=3, n=(512, 512, 512), real=real, smoother="rbgs", nu1=2, nu2=2, prolong="linear",
               coarse_bc="consistent")
-    monkeypatch.setenv("MGP_FUSED_MIN_CELLS", str(1 << 24))
-    a = _ctx(**kw)
-    assert [lv["engine"] for lv in a.levels[:2]] == ["zs", "zs"]
-    a.init_point_charge()
-    ea = a.cycles(2)
-    pa = [a.get_psi(l) for l in range(3)]
-    a.close()
-    monkeypatch.setenv("MGP_FUSED_MIN_CELLS", str(1 << 25))
-    b = _ctx(**kw)
-    assert [lv["engine"] for lv in b.levels[:2]] == ["zs", "piece"]
-    b.init_point_charge()
-    eb = b.cycles(2)
-    for l in range(3):
-        assert np.array_equal(pa[l], b.get_psi(l)), f"level {l}"
-    assert np.allclose(ea, eb, rtol=1e-12, atol=0)
+    runs = []
+    for fmin, zmin, eng in ((1 << 24, 1 << 24, "zs"), (1 << 25, 1 << 24, "zpost"), (1 << 25, 1 << 40, "piece")):
+        monkeypatch.setenv("MGP_FUSED_MIN_CELLS", str(fmin))
+        monkeypatch.setenv("MGP_ZPOST_MIN_CELLS", str(zmin))
+        a = _ctx(**kw)
+        assert [lv["engine"] for lv in a.levels[:3]] == ["zs", eng, "piece"]
+        a.init_point_charge()
+        e = a.cycles(2)
+        runs.append((e, [a.get_psi(l) for l in range(3)]))
+        a.close()
+    eb, pb = runs[-1]
+    for e, p in runs[:-1]:
+        for l in range(3):
+            assert np.array_equal(p[l], pb[l]), f"level {l}"
+        assert np.allclose(e, eb, rtol=1e-12, atol=0)
 
 
 YS_CONFIGS = [

@@ -1,6 +1,6 @@
 """CPU tests of the engine planning (host logic, no device): mgp_plan reports, per level, how mgp_create
 would run its smoothing phases — one launch per piece, the one-launch coarse tail, the temporally blocked
-phases (k_zs) or the tiled one-launch phases (k_blk).  The GPU tests prove every engine bit-exact against
+phases (k_zs; "zpost": POST only) or the tiled one-launch phases (k_blk).  The GPU tests prove every engine bit-exact against
 the oracle; these pin which engine each BASELINE workload gets."""
 import pytest
 
@@ -16,9 +16,10 @@ def engines(**kw):
 
 
 def test_bench_config_512_cube():
-    """configs[2]: k_zs on 512^3, 256^3 and 128^3 per piece, 64^3 and 32^3 tiled, 16^3 .. 1 in the tail."""
+    """configs[2]: k_zs on 512^3, 256^3 PRE per piece and POST k_zs, 128^3 per piece, 64^3 and 32^3 tiled, 16^3 .. 1
+    in the tail."""
     for real in ("float", "double"):
-        assert engines(dim=3, n=(512, 512, 512), real=real, **NS) == ["zs", "piece", "piece", "blk", "blk"] + ["tail"] * 5
+        assert engines(dim=3, n=(512, 512, 512), real=real, **NS) == ["zs", "zpost", "piece", "blk", "blk"] + ["tail"] * 5
 
 
 def test_2d_config_4096():
@@ -29,17 +30,17 @@ def test_2d_config_4096():
 
 
 def test_config5_rank_slab_f_cycle():
-    """configs[4] rank slab 4096 x 4096 x 512: three temporally blocked levels, tiled 128 x 128 x 16 and
-    64 x 64 x 8, the tail from 32 x 32 x 4."""
+    """configs[4] rank slab 4096 x 4096 x 512: three temporally blocked levels, 512 x 512 x 64 with POST temporally
+    blocked, tiled 128 x 128 x 16 and 64 x 64 x 8, the tail from 32 x 32 x 4."""
     e = engines(dim=3, n=(4096, 4096, 512), real="float", cycle="F", **NS)
-    assert e == ["zs"] * 3 + ["piece"] * 2 + ["blk"] * 2 + ["tail"] * 3
+    assert e == ["zs"] * 3 + ["zpost", "piece"] + ["blk"] * 2 + ["tail"] * 3
 
 
 def test_weak_scaling_rank_of_eight():
     """bench --gpus 8 (512 x 512 x 4096): distributed levels never tile (their halos come from the
     neighbours), the first replicated level after the all-gather does."""
     p = _lib.plan(mg.make_opts(dim=3, n=(512, 512, 4096), real="float", rank=3, world=8, comm_id=b"\0" * 128, **NS))
-    assert [d["engine"] for d in p] == ["zs"] + ["piece"] * 4 + ["blk"] + ["tail"] * 4
+    assert [d["engine"] for d in p] == ["zs", "zpost"] + ["piece"] * 3 + ["blk"] + ["tail"] * 4
     assert all(d["distributed"] for d in p[:5]) and not any(d["distributed"] for d in p[5:])
 
 
