@@ -1940,23 +1940,28 @@ struct ZsDiag {
 // (zl, cen, zr) and its in-plane operands: k_half's expressions.  Waves whose cells all have the
 // interior diagonal (every wave of a level with cl = 0) take the reciprocal form, which is what
 // Op::relax computes there.
+// ask: the cells' neighbour sums times 1/h^2 (the askew of k_resrestrict's expression, same operands and
+// order): a PRE black cell's residual one step later sees exactly these neighbours (zs_residual_a)
 template <typename T, int N, bool CLZ, bool ST = false>
-__device__ __forceinline__ Vec<T, N> zs_relax(const Vec<T, N>& zl, const Vec<T, N>& cen, const Vec<T, N>& zr,
-                                              const ZsNb<T, N>& nb, const Vec<T, N>& fv, const ZsCol& c, int o,
-                                              int nbyz, int nx, const Op<T, 3>& op, const ZsDiag<T>& dz)
+__device__ __forceinline__ Vec<T, N> zs_relax_a(const Vec<T, N>& zl, const Vec<T, N>& cen, const Vec<T, N>& zr,
+                                                const ZsNb<T, N>& nb, const Vec<T, N>& fv, const ZsCol& c, int o,
+                                                int nbyz, int nx, const Op<T, 3>& op, const ZsDiag<T>& dz,
+                                                T (&ask)[N])
 {
     Vec<T, N> out;
     T t[N];
     zs_nbsum<T, N>(zl, cen, zr, nb, o, t);
+#pragma unroll
+    for (int e = 0; e < N; ++e) ask[e] = t[e] * op.inv_hSq;
     if (!CLZ && ST) {
 #pragma unroll
         for (int e = 0; e < N; ++e) {
             const bool edge = (e == 0 && o == 0 && dz.left) || (e == N - 1 && o == 1 && dz.right);
-            out.v[e] = div_rn(fv.v[e] - t[e] * op.inv_hSq, edge ? dz.de : dz.db, edge ? dz.ye : dz.yb);
+            out.v[e] = div_rn(fv.v[e] - ask[e], edge ? dz.de : dz.db, edge ? dz.ye : dz.yb);
         }
     } else if (CLZ || __all(nbyz == 0 && c.xin)) {
 #pragma unroll
-        for (int e = 0; e < N; ++e) out.v[e] = div_rn(fv.v[e] - t[e] * op.inv_hSq, op.adiag, op.yadiag);
+        for (int e = 0; e < N; ++e) out.v[e] = div_rn(fv.v[e] - ask[e], op.adiag, op.yadiag);
     } else {
 #pragma unroll
         for (int e = 0; e < N; ++e) {
@@ -1965,6 +1970,15 @@ __device__ __forceinline__ Vec<T, N> zs_relax(const Vec<T, N>& zl, const Vec<T, 
         }
     }
     return out;
+}
+
+template <typename T, int N, bool CLZ, bool ST = false>
+__device__ __forceinline__ Vec<T, N> zs_relax(const Vec<T, N>& zl, const Vec<T, N>& cen, const Vec<T, N>& zr,
+                                              const ZsNb<T, N>& nb, const Vec<T, N>& fv, const ZsCol& c, int o,
+                                              int nbyz, int nx, const Op<T, 3>& op, const ZsDiag<T>& dz)
+{
+    T ask[N];
+    return zs_relax_a<T, N, CLZ, ST>(zl, cen, zr, nb, fv, c, o, nbyz, nx, op, dz, ask);
 }
 
 // Residual of my N cells of one colour (x parity o) at one plane: k_resrestrict's expressions.
@@ -1996,6 +2010,35 @@ __device__ __forceinline__ void zs_residual(const Vec<T, N>& zl, const Vec<T, N>
         for (int e = 0; e < N; ++e) {
             const int i = 2 * (c.gm + e) + o;
             rr[e] = op.residual_direct(t[e], fv.v[e], uc.v[e], nbyz + (i == 0) + (i == nx - 1));
+        }
+    }
+}
+
+// The same residual from the cells' askew (zs_relax_a of the half-sweep that last saw these neighbours)
+template <typename T, int N, bool CLZ, bool ST = false>
+__device__ __forceinline__ void zs_residual_a(const T (&ask)[N], const Vec<T, N>& uc, const Vec<T, N>& fv,
+                                              const ZsCol& c, int o, int nbyz, int nx, const Op<T, 3>& op,
+                                              const ZsDiag<T>& dz, T (&rr)[N])
+{
+    if (!CLZ && ST) {
+#pragma unroll
+        for (int e = 0; e < N; ++e) {
+            const bool edge = (e == 0 && o == 0 && dz.left) || (e == N - 1 && o == 1 && dz.right);
+            const T a_u = ask[e] + (edge ? dz.de : dz.db) * uc.v[e];
+            rr[e] = fv.v[e] - a_u;
+        }
+    } else if (CLZ || __all(nbyz == 0 && c.xin)) {
+#pragma unroll
+        for (int e = 0; e < N; ++e) {
+            const T a_u = ask[e] + op.adiag * uc.v[e];
+            rr[e] = fv.v[e] - a_u;
+        }
+    } else {
+#pragma unroll
+        for (int e = 0; e < N; ++e) {
+            const int i = 2 * (c.gm + e) + o;
+            const T a_u = ask[e] + op.diag_direct(nbyz + (i == 0) + (i == nx - 1)) * uc.v[e];
+            rr[e] = fv.v[e] - a_u;
         }
     }
 }
@@ -2145,6 +2188,12 @@ __device__ __forceinline__ void zs_unroll(F&& f)
 #ifndef ZS_BQ
 #define ZS_BQ 1  // POST: per-thread cache of the coarse planes' y-interpolation (zs_bq)
 #endif
+// PRE: the black cells' residual reuses the askew of the stage-4 half-sweep that relaxed them one step earlier
+// (the same red neighbours, sum order and scaling) instead of re-reading and re-summing those neighbours
+#ifndef ZS_RASK
+#define ZS_RASK 1
+#endif
+constexpr bool kZsRask = ZS_RASK != 0;
 #ifndef ZS_WPE_POST
 #define ZS_WPE_POST 4
 #endif
@@ -2321,6 +2370,9 @@ __attribute__((amdgpu_waves_per_eu(1, PRE ? ZS_WPE_PRE : ZS_WPE_POST))) void k_z
     // groups of four steps, so each step knows its slot offset R = (p - zlo) & 3 at compile time and
     // the rings never move (no register rotation).
     VT W0[4], W1[4], W2[4], W3[4], W4[4], FR[4], FB[4];
+    T AS[2][N];  // PRE (ZS_RASK): stage 4's askew of the last two steps (plane p - 4 at slot RS & 1)
+#pragma unroll
+    for (int e = 0; e < N; ++e) AS[0][e] = AS[1][e] = (T)0;
 #pragma unroll
     for (int i = 0; i < 4; ++i) W0[i] = W1[i] = W2[i] = W3[i] = W4[i] = FR[i] = FB[i] = vz;
     // W0: A0 black at p-2 .. p; W1: A1 red at p-3 .. p-1; W2: A2 black at p-4 .. p-2;
@@ -2439,8 +2491,8 @@ __attribute__((amdgpu_waves_per_eu(1, PRE ? ZS_WPE_PRE : ZS_WPE_POST))) void k_z
         if (!ST && !inz(p - 3)) o3 = vz;
         W3[sl(3)] = o3;
         zs_nb_load<T, N>(n4, slot(S::OFF3, NS3, p - 4), col);
-        VT o4 = zs_relax<T, N, CLZ, ST>(W3[sl(5)], W3[sl(4)], W3[sl(ZS_NC ? 2 : 3)], n4, FB[sl(4)], col, 1 ^ par(p - 4), nbyz(p - 4),
-                                    g.nx, op, dz);
+        VT o4 = zs_relax_a<T, N, CLZ, ST>(W3[sl(5)], W3[sl(4)], W3[sl(ZS_NC ? 2 : 3)], n4, FB[sl(4)], col, 1 ^ par(p - 4),
+                                      nbyz(p - 4), g.nx, op, dz, AS[RS & 1]);
         if (!ST && !inz(p - 4)) o4 = vz;
         W4[sl(4)] = o4;
 
@@ -2482,8 +2534,8 @@ __attribute__((amdgpu_waves_per_eu(1, PRE ? ZS_WPE_PRE : ZS_WPE_POST))) void k_z
         if (RR) {
             const int q = p - 5;
             const int pq = par(q);
-            zs_nb_load<T, N>(nr, slot(S::OFF3, NS3, q), col);  // red of A4 at q
-            zs_nb_load<T, N>(nk, slot(S::OFF4, 2, q), col);    // black of A4 at q
+            if (!kZsRask) zs_nb_load<T, N>(nr, slot(S::OFF3, NS3, q), col);  // red of A4 at q
+            zs_nb_load<T, N>(nk, slot(S::OFF4, 2, q), col);                  // black of A4 at q
             T xr[2 * N];
             {
                 const T* x = xs(q - 1);  // the odd row's residuals of plane q - 1 (even rows read them)
@@ -2494,8 +2546,13 @@ __attribute__((amdgpu_waves_per_eu(1, PRE ? ZS_WPE_PRE : ZS_WPE_POST))) void k_z
             T rred[N], rblk[N], rr[2][N];  // rr: [x parity][e]
             zs_residual<T, N, CLZ, ST>(W4[sl(6)], W4[sl(5)], W4[sl(ZS_NC ? 3 : 4)], nk, W3[sl(5)], FR[sl(5)], col, pq, nbyz(q), g.nx, op,
                                    dz, rred);
-            zs_residual<T, N, CLZ, ST>(W3[sl(6)], W3[sl(5)], W3[sl(4)], nr, W4[sl(5)], FB[sl(5)], col, 1 ^ pq, nbyz(q), g.nx,
-                                   op, dz, rblk);
+            // the black cells' neighbours are the red cells of the last step's stage 4 (its askew, ZS_RASK)
+            if (kZsRask)
+                zs_residual_a<T, N, CLZ, ST>(AS[(RS & 1) ^ 1], W4[sl(5)], FB[sl(5)], col, 1 ^ pq, nbyz(q), g.nx, op, dz,
+                                             rblk);
+            else
+                zs_residual<T, N, CLZ, ST>(W3[sl(6)], W3[sl(5)], W3[sl(4)], nr, W4[sl(5)], FB[sl(5)], col, 1 ^ pq, nbyz(q),
+                                           g.nx, op, dz, rblk);
 #pragma unroll
             for (int e = 0; e < N; ++e) {
                 rr[0][e] = pq == 0 ? rred[e] : rblk[e];
