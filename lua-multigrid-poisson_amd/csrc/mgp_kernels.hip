@@ -228,6 +228,24 @@ struct Op {
     }
 };
 
+// Op::row_diag with a wave-uniform shortcut: rows off every y / z face (nearly all of a level) take table
+// entries 0 and 1 without the walk (on a cl != 0 level the walk is 4 (2D) / 20 (3D) selects per row)
+#ifndef ROWDIAG_FAST  // timing switch (0: always the walk)
+#define ROWDIAG_FAST 1
+#endif
+template <typename T, int DIM>
+__device__ __forceinline__ void row_diag_fast(const Op<T, DIM>& op, int nbyz, T& d0, T& y0, T& d1, T& y1)
+{
+    if (ROWDIAG_FAST && __all(nbyz == 0)) {
+        d0 = op.dg[0];
+        y0 = op.ydg[0];
+        d1 = op.dg[1];
+        y1 = op.ydg[1];
+    } else {
+        op.row_diag(nbyz, d0, y0, d1, y1);
+    }
+}
+
 template <typename T, int DIM>
 Op<T, DIM> make_op(double h, double cl)
 {
@@ -498,7 +516,7 @@ __device__ __forceinline__ void half_store(const HalfIn<T, VN<T>::n>& in, T* __r
     constexpr int N = VN<T>::n;
     const int o = in.o;
     T d0, y0, d1, y1;
-    op.row_diag(in.nbyz, d0, y0, d1, y1);
+    row_diag_fast(op, in.nbyz, d0, y0, d1, y1);
     Vec<T, N> out;
 #pragma unroll
     for (int e = 0; e < N; ++e) {
@@ -659,7 +677,7 @@ __global__ __launch_bounds__(kBlock) void k_fresh(const T* __restrict__ f, T* __
     };
     auto row_diag = [&](int nbyz) {
         RowDiag r;
-        op.row_diag(nbyz, r.d0, r.y0, r.d1, r.y1);
+        row_diag_fast(op, nbyz, r.d0, r.y0, r.d1, r.y1);  // five rows per thread
         return r;
     };
     // red values of row (jj, kk) at m0 .. m0+N-1 (0 outside the box)
@@ -2726,40 +2744,44 @@ struct YsPrefetch {
 };
 
 // relax of my N cells of x parity o: rows ym / yp above and below (other colour), cen my row's other
-// colour, ep / en the x-edge cells beyond my group; nby = y faces of the row (0 with CLZ)
-template <typename T, int N, bool CLZ, bool RES>
+// colour, ep / en the x-edge cells beyond my group; nby = y faces of the row (0 with CLZ).  ask: the cells'
+// neighbour sums times 1/h^2, written (AIN = false) or, for a residual whose neighbours a half-sweep of the
+// previous step saw (PRE's black cells, as k_zs's ZS_RASK), read instead of re-summing them
+template <typename T, int N, bool CLZ, bool RES, bool AIN = false>
 __device__ __forceinline__ void ys_cells(const Vec<T, N>& ym, const Vec<T, N>& cen, const Vec<T, N>& yp, T ep, T en,
                                          const Vec<T, N>& fv, const Vec<T, N>& uc, int o, int nby, int gm, int nx,
-                                         bool xin, const Op<T, 2>& op, T (&out)[N])
+                                         bool xin, const Op<T, 2>& op, T (&out)[N], T (&ask)[N])
 {
-    ZsNb<T, N> nb;
-    nb.yl = ym;
-    nb.yr = yp;
-    nb.ep = ep;
-    nb.en = en;
-    T t[N];
-    zs_xsum<T, N>(cen, nb, o, t);
+    if (!AIN) {
+        ZsNb<T, N> nb;
+        nb.yl = ym;
+        nb.yr = yp;
+        nb.ep = ep;
+        nb.en = en;
+        T t[N];
+        zs_xsum<T, N>(cen, nb, o, t);
 #pragma unroll
-    for (int e = 0; e < N; ++e) {
-        t[e] = t[e] + ym.v[e];
-        t[e] = t[e] + yp.v[e];
+        for (int e = 0; e < N; ++e) {
+            t[e] = t[e] + ym.v[e];
+            t[e] = t[e] + yp.v[e];
+            ask[e] = t[e] * op.inv_hSq;
+        }
     }
     // cl != 0: nby is the row's (uniform across the workgroup), so the row's two diagonals (off / on an x
     // face) are one uniform table walk and a cell selects between them: no divergent boundary path (a
     // segment at an x face would otherwise hold its whole workgroup at every step's barrier)
     T d0 = op.adiag, y0 = op.yadiag, d1 = op.adiag, y1 = op.yadiag;
-    if (!CLZ) op.row_diag(nby, d0, y0, d1, y1);
+    if (!CLZ) row_diag_fast(op, nby, d0, y0, d1, y1);
 #pragma unroll
     for (int e = 0; e < N; ++e) {
         const int i = 2 * (gm + e) + o;
         const bool xf = !CLZ && (i == 0 || i == nx - 1);
         const T d = xf ? d1 : d0;
         if (RES) {
-            const T askew = t[e] * op.inv_hSq;
-            const T a_u = askew + d * uc.v[e];
+            const T a_u = ask[e] + d * uc.v[e];
             out[e] = fv.v[e] - a_u;
         } else {
-            out[e] = div_rn(fv.v[e] - t[e] * op.inv_hSq, d, xf ? y1 : y0);
+            out[e] = div_rn(fv.v[e] - ask[e], d, xf ? y1 : y0);
         }
     }
     (void)xin;
@@ -2861,6 +2883,9 @@ __global__ __launch_bounds__((YsShape<T, PRE, TXV>::NTL)) void k_ys(const T* __r
     VT W0[4], W1[4], W2[4], W3[4], W4[4], FR[4], FB[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) W0[i] = W1[i] = W2[i] = W3[i] = W4[i] = FR[i] = FB[i] = vz;
+    T AS[2][N], askd[N];  // PRE: stage 4's askew of the last two steps (row p - 4 at slot RS & 1); scratch
+#pragma unroll
+    for (int e = 0; e < N; ++e) AS[0][e] = AS[1][e] = askd[e] = (T)0;
     T acc[N];
 #pragma unroll
     for (int e = 0; e < N; ++e) acc[e] = (T)0;
@@ -2911,22 +2936,22 @@ __global__ __launch_bounds__((YsShape<T, PRE, TXV>::NTL)) void k_ys(const T* __r
         VT o1, o2, o3, o4;
         edges(eslot(0, 2, p - 1), ep, en);
         ys_cells<T, N, CLZ, false>(W0[sl(2)], W0[sl(1)], W0[sl(0)], ep, en, cur.f1, vz, par(1), nby(p - 1), gm, g.nx, xin,
-                                   op, o1.v);
+                                   op, o1.v, askd);
         if (!iny(p - 1) || !inx) o1 = vz;
         W1[sl(1)] = o1;
         edges(eslot(S::OFF1, 2, p - 2), ep, en);
         ys_cells<T, N, CLZ, false>(W1[sl(3)], W1[sl(2)], W1[sl(1)], ep, en, cur.f2, vz, 1 ^ par(2), nby(p - 2), gm, g.nx,
-                                   xin, op, o2.v);
+                                   xin, op, o2.v, askd);
         if (!iny(p - 2) || !inx) o2 = vz;
         W2[sl(2)] = o2;
         edges(eslot(S::OFF2, 2, p - 3), ep, en);
         ys_cells<T, N, CLZ, false>(W2[sl(4)], W2[sl(3)], W2[sl(2)], ep, en, FR[sl(3)], vz, par(3), nby(p - 3), gm, g.nx,
-                                   xin, op, o3.v);
+                                   xin, op, o3.v, askd);
         if (!iny(p - 3) || !inx) o3 = vz;
         W3[sl(3)] = o3;
         edges(eslot(S::OFF3, 4, p - 4), ep, en);
         ys_cells<T, N, CLZ, false>(W3[sl(5)], W3[sl(4)], W3[sl(3)], ep, en, FB[sl(4)], vz, 1 ^ par(4), nby(p - 4), gm,
-                                   g.nx, xin, op, o4.v);
+                                   g.nx, xin, op, o4.v, AS[RS & 1]);
         if (!iny(p - 4) || !inx) o4 = vz;
         W4[sl(4)] = o4;
         // ---- edge writes (slots no stage of this step reads) ----
@@ -2957,13 +2982,19 @@ __global__ __launch_bounds__((YsShape<T, PRE, TXV>::NTL)) void k_ys(const T* __r
         if (RR) {
             const int q = p - 5;
             T rred[N], rblk[N];
-            T bep, ben, rep, ren;
+            T bep, ben, rep = (T)0, ren = (T)0;
             edges(eslot(S::OFF4, 2, q), bep, ben);  // black (stage 4) cells of row q
-            edges(eslot(S::OFF3, 4, q), rep, ren);  // red (stage 3) cells of row q
             ys_cells<T, N, CLZ, true>(W4[sl(6)], W4[sl(5)], W4[sl(4)], bep, ben, FR[sl(5)], W3[sl(5)], par(5), nby(q), gm,
-                                      g.nx, xin, op, rred);
-            ys_cells<T, N, CLZ, true>(W3[sl(6)], W3[sl(5)], W3[sl(4)], rep, ren, FB[sl(5)], W4[sl(5)], 1 ^ par(5), nby(q),
-                                      gm, g.nx, xin, op, rblk);
+                                      g.nx, xin, op, rred, askd);
+            // the black cells' neighbours are the red cells the last step's stage 4 summed (its askew)
+            if (kZsRask) {
+                ys_cells<T, N, CLZ, true, true>(W3[sl(6)], W3[sl(5)], W3[sl(4)], rep, ren, FB[sl(5)], W4[sl(5)], 1 ^ par(5),
+                                                nby(q), gm, g.nx, xin, op, rblk, AS[(RS & 1) ^ 1]);
+            } else {
+                edges(eslot(S::OFF3, 4, q), rep, ren);  // red (stage 3) cells of row q
+                ys_cells<T, N, CLZ, true>(W3[sl(6)], W3[sl(5)], W3[sl(4)], rep, ren, FB[sl(5)], W4[sl(5)], 1 ^ par(5), nby(q),
+                                          gm, g.nx, xin, op, rblk, askd);
+            }
             if (q >= Y0 && q < Y0 + yc && tile_x) {
 #pragma unroll
                 for (int e = 0; e < N; ++e) {
