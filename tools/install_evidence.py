@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Copy the end-of-round evidence in gpurun_out/ (tools/r03_final_tests.sh + tools/r03_final.sh) into profiles/
+"""Copy the end-of-round evidence in gpurun_out/ (tools/r03_final_tests.sh + tools/r03_final.sh, or tools/r04_final.sh) into profiles/
 under a round prefix and print the bench lines.
 
 usage: tools/install_evidence.py [prefix]   (default r03)
@@ -35,9 +35,12 @@ shutil.copy(G + "pmc_traffic.txt", P + f"{pre}_pmc_traffic_summary.txt")
 shutil.copy(G + "prof/run_kernel_stats.csv", P + f"{pre}_kernel_stats.csv")
 if os.path.exists(G + "fetch_calib.json"):
     shutil.copy(G + "fetch_calib.json", P + f"{pre}_fetch_calib.json")
-tail = [l for l in open(G + "pytest_gpu.log").read().splitlines() if l.strip()][-1:]
-smoke = [l for l in open(G + "smoke.log").read().splitlines() if l.startswith("smoke")]
-open(P + f"{pre}_pytest_gpu.txt", "w").write("\n".join(tail + smoke) + "\n")
+if os.path.exists(G + "pytest_gpu.log") and os.path.exists(G + "smoke.log"):
+    tail = [l for l in open(G + "pytest_gpu.log").read().splitlines() if l.strip()][-1:]
+    smoke = [l for l in open(G + "smoke.log").read().splitlines() if l.startswith("smoke")]
+    open(P + f"{pre}_pytest_gpu.txt", "w").write("\n".join(tail + smoke) + "\n")
+if os.path.isdir(G + "sq"):  # SQ / TCC counter passes (tools/r04_final.sh)
+    tool(["tools/pmc_summary.py", G + "sq", "k_zs|k_tail_c|k_fresh"], f"{pre}_sq_counters_summary.txt")
 tool(["tools/trace_summary.py", G + "prof/run_kernel_trace.csv"], f"{pre}_trace_summary.txt")
 tool(["tools/cycle_breakdown.py", G + "prof/run_kernel_trace.csv", "8"], f"{pre}_cycle_breakdown.txt")
 if os.path.exists(G + "prof2d/run_kernel_stats.csv"):
