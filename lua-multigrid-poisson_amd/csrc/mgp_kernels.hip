@@ -680,15 +680,31 @@ __global__ __launch_bounds__(kBlock) void k_fresh(const T* __restrict__ f, T* __
         row_diag_fast(op, nbyz, r.d0, r.y0, r.d1, r.y1);  // five rows per thread
         return r;
     };
-    // red values of row (jj, kk) at m0 .. m0+N-1 (0 outside the box)
-    auto red_row = [&](int jj, int64_t kk, Vec<T, N>& r) {
-        const int64_t gkk = g.z0 + kk;
-        if (jj < 0 || jj >= g.ny || (DIM == 3 && (gkk < 0 || gkk >= g.gnz))) {
+    // Every load is issued before any arithmetic (round 4: with a load per red-row evaluation behind its box
+    // test, each thread waited for five memory latencies one after another; 256^3 31.8 us)
+    const int64_t own = k * g.P + (int64_t)j * g.hw + m0;
+    const bool vyl = j > 0, vyr = j < g.ny - 1;
+    const bool vzl = DIM == 3 && gk > 0, vzr = DIM == 3 && gk < g.gnz - 1;
+    const Vec<T, N> fc = vload<T, N>(f + own);  // red half of the row (colour 0)
+    const Vec<T, N> fyl = vload<T, N>(f + own - (vyl ? g.hw : 0));
+    const Vec<T, N> fyr = vload<T, N>(f + own + (vyr ? g.hw : 0));
+    Vec<T, N> fzl = fc, fzr = fc;
+    if (DIM == 3) {
+        fzl = vload<T, N>(f + own - (vzl ? g.P : 0));
+        fzr = vload<T, N>(f + own + (vzr ? g.P : 0));
+    }
+    // the red x-neighbour outside the segment: m0 - 1 (black cells at even x) or m0 + N (odd x)
+    const int me = ob == 0 ? m0 - 1 : m0 + N;
+    const bool ve = me >= 0 && me < g.hw;
+    const T fe = f[own + (ve ? me - m0 : 0)];
+    const Vec<T, N> fb = vload<T, N>(f + own + g.H);
+    // red values of row (jj, gkk) at m0 .. m0+N-1 from its f (0 outside the box)
+    auto red_row = [&](const Vec<T, N>& fv, bool valid, int jj, int64_t gkk, Vec<T, N>& r) {
+        if (!valid) {
             r = vzero<T, N>();
             return;
         }
         const int orr = (int)((jj + gkk) & 1);  // x parity of red cells in that row
-        const Vec<T, N> fv = vload<T, N>(f + kk * g.P + (int64_t)jj * g.hw + m0);
         const int nbyz = (jj == 0) + (jj == g.ny - 1) + (DIM == 3 ? (gkk == 0) + (gkk == g.gnz - 1) : 0);
         const RowDiag rd = row_diag(nbyz);
 #pragma unroll
@@ -699,23 +715,19 @@ __global__ __launch_bounds__(kBlock) void k_fresh(const T* __restrict__ f, T* __
         }
     };
     Vec<T, N> rc, ryl, ryr, rzl, rzr;
-    red_row(j, k, rc);
-    red_row(j - 1, k, ryl);
-    red_row(j + 1, k, ryr);
+    red_row(fc, true, j, gk, rc);
+    red_row(fyl, vyl, j - 1, gk, ryl);
+    red_row(fyr, vyr, j + 1, gk, ryr);
     if (DIM == 3) {
-        red_row(j, k - 1, rzl);
-        red_row(j, k + 1, rzr);
+        red_row(fzl, vzl, j, gk - 1, rzl);
+        red_row(fzr, vzr, j, gk + 1, rzr);
     }
-    // the red x-neighbour outside the segment: m0 - 1 (black cells at even x) or m0 + N (odd x)
-    const int me = ob == 0 ? m0 - 1 : m0 + N;
     const int nbyz = (j == 0) + (j == g.ny - 1) + (DIM == 3 ? (gk == 0) + (gk == g.gnz - 1) : 0);
     T edge = (T)0;
-    if (me >= 0 && me < g.hw) {
+    if (ve) {
         const int i = 2 * me + (ob ^ 1);
-        edge = op.relax((T)0, f[k * g.P + (int64_t)j * g.hw + me], nbyz + (i == 0) + (i == g.nx - 1));
+        edge = op.relax((T)0, fe, nbyz + (i == 0) + (i == g.nx - 1));
     }
-    const int64_t own = k * g.P + (int64_t)j * g.hw + m0;
-    const Vec<T, N> fb = vload<T, N>(f + own + g.H);
     const RowDiag bd = row_diag(nbyz);
     Vec<T, N> out;
 #pragma unroll
