@@ -4378,11 +4378,15 @@ static hipError_t zs_launch(const FusedArgs& a, hipStream_t s)
     return hipGetLastError();
 }
 
-// POST's wide tile (ZsTile::TXPOST_W): fp32, cl = 0, a box it divides, MGP_ZS_WIDE not 0 (read per call)
+// POST's wide tile (ZsTile::TXPOST_W): fp32, cl = 0 (or any level with ZS_WIDE_CL: on the 256^3 level of the
+// 512^3 box measured +10-16 us per cycle, off), a box it divides, MGP_ZS_WIDE not 0 (read per call)
+#ifndef ZS_WIDE_CL
+#define ZS_WIDE_CL 0
+#endif
 static bool zs_wide(int rb, const Geo& g, bool clz)
 {
     const char* v = std::getenv("MGP_ZS_WIDE");
-    if (rb != 4 || !clz || (v && std::atoi(v) == 0)) return false;
+    if (rb != 4 || (!clz && !ZS_WIDE_CL) || (v && std::atoi(v) == 0)) return false;
     return g.nx % ZsTile<float>::TXPOST_W == 0 && g.ny % ZsTile<float>::TYPOST_W == 0;
 }
 
@@ -4428,6 +4432,10 @@ static hipError_t fused_dispatch(const FusedArgs& a, hipStream_t s)
                 return err ? zs_launch<T, false, 1, true, CLZ, true>(a, s) : zs_launch<T, false, 1, false, CLZ, true>(a, s);
             return err ? zs_launch<T, false, 0, true, CLZ, true>(a, s) : zs_launch<T, false, 0, false, CLZ, true>(a, s);
         }
+    }
+    if constexpr (std::is_same<T, float>::value && !CLZ && ZS_WIDE_CL) {
+        if (!err && zs_wide(4, a.g, false))
+            return a.linear ? zs_launch<T, false, 1, false, CLZ, true>(a, s) : zs_launch<T, false, 0, false, CLZ, true>(a, s);
     }
     if (a.linear) return err ? zs_launch<T, false, 1, true, CLZ>(a, s) : zs_launch<T, false, 1, false, CLZ>(a, s);
     return err ? zs_launch<T, false, 0, true, CLZ>(a, s) : zs_launch<T, false, 0, false, CLZ>(a, s);
@@ -4532,6 +4540,12 @@ static hipError_t fused_attr()
         if (e == hipSuccess) e = hipFuncSetAttribute((const void*)k_zs<T, false, 0, true, CLZ, true>, A, w);
         if (e == hipSuccess) e = hipFuncSetAttribute((const void*)k_zs<T, false, 1, false, CLZ, true>, A, w);
         if (e == hipSuccess) e = hipFuncSetAttribute((const void*)k_zs<T, false, 1, true, CLZ, true>, A, w);
+        if (e != hipSuccess) return e;
+    }
+    if constexpr (std::is_same<T, float>::value && !CLZ && ZS_WIDE_CL) {
+        const int w = (int)ZsShape<T, false, CLZ, true>::lds_bytes;
+        hipError_t e = hipFuncSetAttribute((const void*)k_zs<T, false, 0, false, CLZ, true>, A, w);
+        if (e == hipSuccess) e = hipFuncSetAttribute((const void*)k_zs<T, false, 1, false, CLZ, true>, A, w);
         if (e != hipSuccess) return e;
     }
     hipError_t e = hipFuncSetAttribute((const void*)k_zs<T, true, 0, false, CLZ>, A, pre);
