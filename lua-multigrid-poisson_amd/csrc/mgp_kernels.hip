@@ -3424,6 +3424,43 @@ __device__ __forceinline__ void tc_copy(T* U, T* F, T* gu, T* gf, bool in, bool 
     }
 }
 
+// Copy-in in two halves, so that every level's global loads are in flight together (round 4: tc_copy level by
+// level waited for one level's loads before issuing the next level's: seven load latencies in a row in 2D)
+template <typename T, int DIM, int N>
+struct TcRegs {
+    static constexpr int IT = (TcLev<DIM, N>::P + kTcThreads - 1) / kTcThreads;
+    T u[IT], f[IT];
+};
+template <typename T, int DIM, int N>
+__device__ __forceinline__ void tc_load(TcRegs<T, DIM, N>& rg, const T* gu, const T* gf, bool zero_u, int tid)
+{
+    using L = TcLev<DIM, N>;
+    constexpr int HW = N >= 2 ? N / 2 : 1;
+    constexpr int64_t H = (int64_t)HW * N, P = 2 * H;
+#pragma unroll
+    for (int r = 0; r < TcRegs<T, DIM, N>::IT; ++r) {
+        const int q = tid + r * kTcThreads;
+        const int i = q % L::W - 1, j = (q / L::W) % L::W - 1, k = DIM == 3 ? q / (L::W * L::W) - 1 : 0;
+        const bool inside = q < L::P && i >= 0 && i < N && j >= 0 && j < N && k >= 0 && k < N;
+        const int64_t gi = (int64_t)k * P + ((i + j + k) & 1) * H + (int64_t)j * HW + (i >> 1);
+        rg.u[r] = inside && !zero_u ? gu[gi] : (T)0;
+        rg.f[r] = inside ? gf[gi] : (T)0;
+    }
+}
+template <typename T, int DIM, int N>
+__device__ __forceinline__ void tc_store(T* U, T* F, const TcRegs<T, DIM, N>& rg, int tid)
+{
+    using L = TcLev<DIM, N>;
+#pragma unroll
+    for (int r = 0; r < TcRegs<T, DIM, N>::IT; ++r) {
+        const int q = tid + r * kTcThreads;
+        if (q < L::P) {
+            U[q] = rg.u[r];
+            F[q] = rg.f[r];
+        }
+    }
+}
+
 template <typename T, int DIM, int LINEAR>
 __global__ __launch_bounds__(kTcThreads) void k_tail_c(const TailArgs<T, DIM> a)
 {
@@ -3438,8 +3475,22 @@ __global__ __launch_bounds__(kTcThreads) void k_tail_c(const TailArgs<T, DIM> a)
 #define TC_COPY(l, IN)                                                                                    \
     if constexpr ((l) < NL) tc_copy<T, DIM, (TN >> (l))>(TC_U(l), TC_F(l), a.u[l], a.f[l], IN, IN && (l) == 0 && a.zero0, \
                                                          threadIdx.x);
-    TC_COPY(0, true) TC_COPY(1, true) TC_COPY(2, true) TC_COPY(3, true) TC_COPY(4, true) TC_COPY(5, true)
-    TC_COPY(6, true)
+#define TC_N(l) ((TN >> (l)) > 0 ? (TN >> (l)) : 1)
+#define TC_LOAD(l)                         \
+    TcRegs<T, DIM, TC_N(l)> rg##l;         \
+    if constexpr ((l) < NL) tc_load<T, DIM, TC_N(l)>(rg##l, a.u[l], a.f[l], (l) == 0 && a.zero0, threadIdx.x);
+#define TC_STORE(l) \
+    if constexpr ((l) < NL) tc_store<T, DIM, TC_N(l)>(TC_U(l), TC_F(l), rg##l, threadIdx.x);
+    if constexpr (DIM == 2) {  // (3D: the held values push the kernel past 64 VGPRs into spills; level by level)
+        TC_LOAD(0) TC_LOAD(1) TC_LOAD(2) TC_LOAD(3) TC_LOAD(4) TC_LOAD(5) TC_LOAD(6)
+        TC_STORE(0) TC_STORE(1) TC_STORE(2) TC_STORE(3) TC_STORE(4) TC_STORE(5) TC_STORE(6)
+    } else {
+        TC_COPY(0, true) TC_COPY(1, true) TC_COPY(2, true) TC_COPY(3, true) TC_COPY(4, true) TC_COPY(5, true)
+        TC_COPY(6, true)
+    }
+#undef TC_STORE
+#undef TC_LOAD
+#undef TC_N
     __syncthreads();
     for (int pc = 0; pc < a.nops; ++pc) {
         const uint32_t w = a.ops[pc];
