@@ -3492,6 +3492,10 @@ __global__ __launch_bounds__(kTcThreads) void k_tail_c(const TailArgs<T, DIM> a)
 #undef TC_LOAD
 #undef TC_N
     __syncthreads();
+#ifdef TC_PROF  // timing experiment: wall-clock ticks (100 MHz) per op into f of the first level (tools/tail_prof.py)
+    __shared__ long long tcp[130];
+    if (threadIdx.x == 0) tcp[0] = wall_clock64();
+#endif
     for (int pc = 0; pc < a.nops; ++pc) {
         const uint32_t w = a.ops[pc];
         const int op = (int)(w & 15), l = (int)((w >> 4) & 15), arg = (int)(w >> 8);
@@ -3523,6 +3527,16 @@ __global__ __launch_bounds__(kTcThreads) void k_tail_c(const TailArgs<T, DIM> a)
                         tc_rr_fw<T, DIM, N>(TC_U(L), TC_F(L), TC_F((L) + 1), sop[L], (T)3 - sop[(L) + 1].cl, tid); \
                     else                                                                               \
                         tc_rr<T, DIM, N>(TC_U(L), TC_F(L), TC_F((L) + 1), sop[L], tid);                \
+                    /* a fresh guess of the next level (its ZERO op follows) in the same phase: RR writes */ \
+                    /* that level's f, ZERO its u                                                        */ \
+                    const uint32_t wn = pc + 1 < a.nops ? a.ops[pc + 1] : 0u;                          \
+                    if ((int)(wn & 15) == TAIL_ZERO && (int)((wn >> 4) & 15) == (L) + 1) {              \
+                        constexpr int M = N / 2;                                                       \
+                        T* uc = TC_U((L) + 1);                                                         \
+                        for (int q = tid; q < TcLev<DIM, M>::CELLS; q += kTcThreads)                   \
+                            uc[TcLev<DIM, M>::idx(q % M, (q / M) % M, DIM == 3 ? q / (M * M) : 0)] = (T)0; \
+                        ++pc;                                                                          \
+                    }                                                                                  \
                     __syncthreads();                                                                   \
                 } else if (op == TAIL_PROLONG) {                                                       \
                     tc_prolong<T, DIM, N, LINEAR>(TC_U(L), TC_U((L) + 1), sop[(L) + 1].cl, tid);       \
@@ -3542,7 +3556,28 @@ __global__ __launch_bounds__(kTcThreads) void k_tail_c(const TailArgs<T, DIM> a)
             default: break;
         }
 #undef TC_CASE
+#ifdef TC_PROF
+        __syncthreads();
+        if (threadIdx.x == 0 && pc < 128) tcp[pc + 1] = wall_clock64();
+#endif
     }
+#ifdef TC_PROF
+    if (threadIdx.x == 0) {
+        // op q's ticks at cell (q % TN, q / TN, 0) of the first level's f, then 0; op code (op | level << 4) + 1
+        // at the cell after the ticks' row block (rows 2 and 3)
+        T* F0 = TC_F(0);
+        const int n = a.nops < 2 * TN ? a.nops : 2 * TN;
+        for (int q = 0; q < n; ++q) {
+            F0[TcLev<DIM, TN>::idx(q % TN, q / TN, 0)] = (T)(tcp[q + 1] - tcp[q]);
+            F0[TcLev<DIM, TN>::idx(q % TN, 2 + q / TN, 0)] = (T)((a.ops[q] & 255) + 1);
+        }
+        if (n < 2 * TN) {
+            F0[TcLev<DIM, TN>::idx(n % TN, n / TN, 0)] = (T)0;
+            F0[TcLev<DIM, TN>::idx(n % TN, 2 + n / TN, 0)] = (T)0;
+        }
+    }
+    __syncthreads();
+#endif
     TC_COPY(0, false) TC_COPY(1, false) TC_COPY(2, false) TC_COPY(3, false) TC_COPY(4, false) TC_COPY(5, false)
     TC_COPY(6, false)
 #undef TC_COPY
