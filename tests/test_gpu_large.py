@@ -330,3 +330,57 @@ def test_device_cg_matches_reference_operator_on_cpu_lua_path():
     x, iters, err = ctx.cg_solve(epsilon=1e-28, maxiter=2000)
     mg = ctx.get_psi()
     assert np.abs(x - mg).max() <= 1e-8 * np.abs(mg).max()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_loopback_zpost_distributed_level(world, monkeypatch):
+    """Engine 4 (zpost: PRE per piece, POST temporally blocked) on a distributed level: loopback slabs of a 256^3
+    box with level 0 fused and level 1 (128 x 128 x 128 / world) zpost equal the single domain bit for bit, and
+    the single domain equals one launch per piece on that level."""
+    import threading
+
+    monkeypatch.setenv("MGP_FUSED_MIN_CELLS", str(1 << 23 if world == 2 else 1 << 22))
+    monkeypatch.setenv("MGP_ZPOST_MIN_CELLS", str(1 << 19))
+    mg = _mg()
+    box = (256, 256, 256)
+    cfg = dict(real="float", smoother="rbgs", nu1=2, nu2=2, prolong="linear", coarse_bc="consistent")
+    lb = mg.Loopback(world)
+    res, errors = [None] * world, []
+
+    def rank_main(r):
+        try:
+            ctx = mg.Context(mg.make_opts(dim=3, n=box, rank=r, world=world, device=0, comm_id=b"\0" * 128, **cfg),
+                             loopback=lb)
+            eng = [lv["engine"] for lv in ctx.levels]
+            assert eng[:2] == ["zs", "zpost"] and ctx.levels[1]["distributed"], eng
+            ctx.init_point_charge()
+            errs = ctx.cycles(3)
+            res[r] = (ctx.field_stats(), errs)
+            ctx.close()
+        except Exception as e:  # noqa: BLE001
+            errors.append((r, repr(e)))
+
+    th = [threading.Thread(target=rank_main, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=600)
+    lb.close()
+    assert not errors, errors
+    ref = _ctx(dim=3, n=box, **cfg)
+    assert [lv["engine"] for lv in ref.levels][1] == "zpost"
+    ref.init_point_charge()
+    e_ref = ref.cycles(3)
+    h_ref = ref.field_stats()[0]
+    assert sum(res[r][0][0] for r in range(world)) & M64 == h_ref
+    for r in range(world):
+        np.testing.assert_allclose(res[r][1], e_ref, rtol=1e-12, atol=0)
+    psi_ref = ref.get_psi()
+    ref.close()
+    monkeypatch.setenv("MGP_ZPOST_MIN_CELLS", str(1 << 40))
+    pp = _ctx(dim=3, n=box, **cfg)
+    assert [lv["engine"] for lv in pp.levels][1] == "piece"
+    pp.init_point_charge()
+    e_pp = pp.cycles(3)
+    assert np.array_equal(pp.get_psi(), psi_ref)
+    np.testing.assert_allclose(e_pp, e_ref, rtol=1e-12, atol=0)
