@@ -501,7 +501,7 @@ int exchange_buf_impl(mgp_ctx* c, Level& L, char* buf, int depth, int colour, hi
     // one message per direction (whole planes) or one per plane (a colour half of each)
     const int msgs = colour < 0 ? 1 : depth;
     const size_t cnt = colour < 0 ? (size_t)(depth * L.g.P) : (size_t)L.g.H;
-    ncclComm_t comm = st == c->xs && c->xcomm ? c->xcomm : c->comm;
+    ncclComm_t comm = c->xs && st == c->xs && c->xcomm ? c->xcomm : c->comm;
     NcclScope scope(c);
     if (c->stopped()) return c->fail(MGP_ERR_STATE, "group aborted: another rank failed");
     ncclResult_t r = ncclGroupStart();
@@ -532,7 +532,8 @@ int exchange_buf(mgp_ctx* c, Level& L, char* buf, int depth = 1, int colour = -1
     // bytes this rank sends per neighbour: depth planes, or the colour half of each
     const int64_t per_nb = (int64_t)depth * (colour < 0 ? L.g.P : L.g.H) * c->rb;
     const int nbs = (c->o.rank > 0) + (c->o.rank < c->o.world - 1);
-    comm_log(c, 0, st == c->xs, (int)(&L - c->lev.data()), colour < 0 ? 1 : depth, per_nb);
+    // (side: the xs stream exists and is the one used; a host-only plan without it has s == xs == null)
+    comm_log(c, 0, c->xs != nullptr && st == c->xs, (int)(&L - c->lev.data()), colour < 0 ? 1 : depth, per_nb);
     if (c->dry) return MGP_OK;
     hipEvent_t e;
     TRY(timed_begin_on(c, st, &e));

@@ -86,3 +86,18 @@ def test_plan_comm_is_identical_on_every_rank():
                 for r in range(w)]
         assert all(l == logs[0] for l in logs), (box, cyc, w)
         assert logs[0][-1] == ("allreduce", 0, 0, 1, 8)
+
+
+def test_plan_comm_without_side_stream(monkeypatch):
+    """MGP_EARLY_X=0: POST's halo goes out on the compute stream before POST, so the plan lists no side-stream
+    exchange (the host-only plan has neither stream: only an existing side stream marks an exchange as its)."""
+    sys.path.insert(0, os.path.join(ROOT, "lua-multigrid-poisson_amd"))
+    import mgpoisson as mg
+
+    kw = dict(dim=3, n=(512, 512, 1024), real="float", smoother="rbgs", nu1=2, nu2=2, prolong="linear",
+              coarse_bc="consistent", rank=0, world=2, comm_id=b"\0" * 128)
+    on = mg.plan_comm(mg.make_opts(**kw), 1)
+    monkeypatch.setenv("MGP_EARLY_X", "0")
+    off = mg.plan_comm(mg.make_opts(**kw), 1)
+    assert any(r[1] == 1 for r in on) and not any(r[1] == 1 for r in off)
+    assert len(off) == len(on)

@@ -6,6 +6,7 @@ the same sequence per communicator; the early POST halo exchange goes to the sid
 code path with device copies for the transfers) is compared with mgp_plan_comm (the same cycle logic run on
 the host with every device call skipped — what bench.py --plan-only reports for the driver's N-GPU lines).
 """
+import os
 import threading
 
 import numpy as np
@@ -73,7 +74,9 @@ def test_executed_comm_log_equals_plan(box, world, extra, gather, side, monkeypa
     assert all(l == logs[0] for l in logs)  # call-order equality across ranks
     plan = mg.plan_comm(mg.make_opts(dim=3, n=box, rank=0, world=world, comm_id=b"\0" * 128, **cfg), cycles)
     assert logs[0] == plan
-    assert any(r[1] == 1 for r in plan) == side  # the early POST exchange rides the side communicator
+    # the early POST exchange rides the side communicator (MGP_EARLY_X=0: no side stream, POST's halo goes out on
+    # the compute stream before POST)
+    assert any(r[1] == 1 for r in plan) == (side and os.environ.get("MGP_EARLY_X", "1") != "0")
     # every exchange and collective was timed on its stream
     n_ex = sum(1 for r in plan if r[0] == "exchange")
     n_co = sum(1 for r in plan if r[0] != "exchange")
