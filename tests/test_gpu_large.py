@@ -384,3 +384,31 @@ def test_loopback_zpost_distributed_level(world, monkeypatch):
     e_pp = pp.cycles(3)
     assert np.array_equal(pp.get_psi(), psi_ref)
     np.testing.assert_allclose(e_pp, e_ref, rtol=1e-12, atol=0)
+
+
+@pytest.mark.parametrize("dim,box,real,cycle", [
+    (3, (512, 512, 512), "float", "V"),
+    (3, (512, 512, 512), "double", "V"),
+    (2, (4096, 4096, 1), "float", "V"),
+    (3, (256, 256, 256), "float", "F"),
+], ids=["configs2-f32", "configs2-f64", "configs1-2d", "256cube-F"])
+def test_run_to_run_determinism_full_size(dim, box, real, cycle, monkeypatch):
+    """The bench workloads at full size, 40 cycles, three fresh contexts (graph replay twice, eager
+    launches once): psi's device fingerprint and every err identical.  Every kernel of the path writes
+    each cell once per phase and sums in fixed orders, so any difference is a race (a wave reading an
+    LDS slot or a plane before its producer wrote it) — the class of bug round 3 found late."""
+    kw = dict(dim=dim, n=box, real=real, smoother="rbgs", nu1=2, nu2=2, cycle=cycle, prolong="linear",
+              coarse_bc="consistent")
+    runs = []
+    for graph in ("1", "1", "0"):
+        monkeypatch.setenv("MGP_GRAPH", graph)
+        ctx = _ctx(**kw)
+        try:
+            ctx.init_point_charge()
+            errs = np.concatenate([ctx.cycles(20), ctx.cycles(20)])
+            runs.append((ctx.field_stats()[0], errs))
+        finally:
+            ctx.close()
+    assert runs[0][0] == runs[1][0] == runs[2][0], "psi fingerprints differ between runs"
+    assert np.array_equal(runs[0][1], runs[1][1]) and np.array_equal(runs[0][1], runs[2][1])
+    assert np.all(np.isfinite(runs[0][1])) and runs[0][1][-1] < runs[0][1][0]
