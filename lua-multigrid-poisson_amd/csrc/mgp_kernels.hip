@@ -1966,6 +1966,20 @@ struct ZsDiag {
     bool left, right;
 };
 
+// dz's diagonals as register values.  Without the opaque copy the compiler turns `edge ? dz.de : dz.db`
+// into a select of the two members' addresses and keeps dz in private memory: six scratch loads per
+// step on every cl != 0 PRE step (5x the launch's vector memory reads, 670 against 407 us for the
+// same launch with the cl = 0 code at 1024^2 x 128).
+template <typename T>
+__device__ __forceinline__ void zs_dvals(const ZsDiag<T>& dz, T& db, T& yb, T& de, T& ye)
+{
+    db = dz.db;
+    yb = dz.yb;
+    de = dz.de;
+    ye = dz.ye;
+    asm("" : "+v"(db), "+v"(yb), "+v"(de), "+v"(ye));
+}
+
 // One half-sweep of my N cells of one colour (x parity o) from the other colour's window
 // (zl, cen, zr) and its in-plane operands: k_half's expressions.  Waves whose cells all have the
 // interior diagonal (every wave of a level with cl = 0) take the reciprocal form, which is what
@@ -1984,10 +1998,12 @@ __device__ __forceinline__ Vec<T, N> zs_relax_a(const Vec<T, N>& zl, const Vec<T
 #pragma unroll
     for (int e = 0; e < N; ++e) ask[e] = t[e] * op.inv_hSq;
     if (!CLZ && ST) {
+        T db, yb, de, ye;
+        zs_dvals(dz, db, yb, de, ye);
 #pragma unroll
         for (int e = 0; e < N; ++e) {
             const bool edge = (e == 0 && o == 0 && dz.left) || (e == N - 1 && o == 1 && dz.right);
-            out.v[e] = div_rn(fv.v[e] - ask[e], edge ? dz.de : dz.db, edge ? dz.ye : dz.yb);
+            out.v[e] = div_rn(fv.v[e] - ask[e], edge ? de : db, edge ? ye : yb);
         }
     } else if (CLZ || __all(nbyz == 0 && c.xin)) {
 #pragma unroll
@@ -2021,11 +2037,13 @@ __device__ __forceinline__ void zs_residual(const Vec<T, N>& zl, const Vec<T, N>
     T t[N];
     zs_nbsum<T, N>(zl, cen, zr, nb, o, t);
     if (!CLZ && ST) {
+        T db, yb, de, ye;
+        zs_dvals(dz, db, yb, de, ye);
 #pragma unroll
         for (int e = 0; e < N; ++e) {
             const bool edge = (e == 0 && o == 0 && dz.left) || (e == N - 1 && o == 1 && dz.right);
             const T askew = t[e] * op.inv_hSq;
-            const T a_u = askew + (edge ? dz.de : dz.db) * uc.v[e];
+            const T a_u = askew + (edge ? de : db) * uc.v[e];
             rr[e] = fv.v[e] - a_u;
         }
     } else if (CLZ || __all(nbyz == 0 && c.xin)) {
@@ -2051,10 +2069,12 @@ __device__ __forceinline__ void zs_residual_a(const T (&ask)[N], const Vec<T, N>
                                               const ZsDiag<T>& dz, T (&rr)[N])
 {
     if (!CLZ && ST) {
+        T db, yb, de, ye;
+        zs_dvals(dz, db, yb, de, ye);
 #pragma unroll
         for (int e = 0; e < N; ++e) {
             const bool edge = (e == 0 && o == 0 && dz.left) || (e == N - 1 && o == 1 && dz.right);
-            const T a_u = ask[e] + (edge ? dz.de : dz.db) * uc.v[e];
+            const T a_u = ask[e] + (edge ? de : db) * uc.v[e];
             rr[e] = fv.v[e] - a_u;
         }
     } else if (CLZ || __all(nbyz == 0 && c.xin)) {
@@ -4513,6 +4533,9 @@ template <typename T, bool CLZ>
 static hipError_t fused_dispatch(const FusedArgs& a, hipStream_t s)
 {
     const bool err = a.partials != nullptr;
+#ifdef ZS_CL_AS_CLZ  // timing experiment only (wrong at the box faces): cl != 0 PRE runs the cl = 0 code
+    if (a.pre) return a.linear ? zs_launch<T, true, 1, false, true>(a, s) : zs_launch<T, true, 0, false, true>(a, s);
+#endif
     if (a.pre) return a.linear ? zs_launch<T, true, 1, false, CLZ>(a, s) : zs_launch<T, true, 0, false, CLZ>(a, s);
     if constexpr (std::is_same<T, float>::value && CLZ) {
         if (zs_wide(4, a.g, true)) {
