@@ -191,6 +191,7 @@ struct mgp_ctx {
     bool deep_halo = true;  // smooth_deep on distributed levels below the finest
     bool fresh_sweep = true;        // k_fresh for the first sweep of a lazily zeroed level (MGP_FRESH=0: off)
     bool lazy_zero = true;          // fresh coarse guesses without a memset where a reader can take it (MGP_LAZY_ZERO=0: off)
+    bool lazy_zero_fused = true;    // ... on k_zs levels too (their PRE reads none of it; MGP_LAZY_ZERO_FUSED=0: off)
     bool post_black = true;         // the cycle's prolongation corrects the black cells only (MGP_POST_BLACK=0: both)
     bool post1 = false;             // k_post1: prolongation fused into the first post red half-sweep (MGP_POST1=1;
                                     // measured slower: 5 rows of P V per thread cost more VALU and L2 loads
@@ -862,7 +863,8 @@ bool lazy_zero_ok(const mgp_ctx* c, const Level& L)
     if (l == c->handoff_level || !c->lazy_zero) return false;
     if (l == c->tail_level) return true;  // run_tail loads it as zeros (any smoother)
     const bool sweeps_first = c->o.nu1 >= 1 || l == (int)c->lev.size() - 1;
-    return c->zbuf && sweeps_first && c->o.smoother == MGP_RBGS && !L.fused && L.alloc <= c->zbuf_reals;
+    if (L.fused) return c->lazy_zero_fused && c->o.dim == 3 && c->o.nu1 >= 1;  // k_zs PRE loads none of it
+    return c->zbuf && sweeps_first && c->o.smoother == MGP_RBGS && L.alloc <= c->zbuf_reals;
 }
 
 int zero_level(mgp_ctx* c, Level& L)
@@ -918,7 +920,8 @@ int fused_pre(mgp_ctx* c, int l, double h)
     Level& L = c->lev[l];
     Level& C = c->lev[l + 1];
     if (L.p.dist) {  // the trapezoid reads kZsHaloPre planes of u and f beyond the slab
-        TRY(exchange_buf(c, L, L.u, mgp::kZsHaloPre, 1));  // k_zs reads only black cells of its input
+        // k_zs reads only black cells of its input, and none of a pending fresh zero
+        if (!L.zero_pending) TRY(exchange_buf(c, L, L.u, mgp::kZsHaloPre, 1));
         if (!L.fghost_ok) TRY(exchange_buf(c, L, L.f, mgp::kZsHaloPre));
         L.fghost_ok = true;
     }
@@ -928,7 +931,7 @@ int fused_pre(mgp_ctx* c, int l, double h)
     mgp::FusedArgs a{};
     a.pre = true;
     a.linear = fw;  // PRE: 1 = smoothing only (both colours stored), the full weighting follows
-    a.src = c->ui(L, L.u);
+    a.src = L.zero_pending ? nullptr : c->ui(L, L.u);  // null: a fresh zero guess (lazy_zero_ok)
     a.f = c->ui(L, L.f);
     a.dst = c->ui(L, L.t);
     a.R = c->ui(C, C.f) + (size_t)(zc * C.g.P) * c->rb;
@@ -946,6 +949,7 @@ int fused_pre(mgp_ctx* c, int l, double h)
     const double coarse = std::ldexp(1.0, -c->o.dim);
     TRY(timed_end(c, e, MGP_TIMING_FUSED_PRE, (fw ? 2.5 : 2.0 + coarse) * c->rb * (double)level_cells(L)));
     std::swap(L.u, L.t);  // u = smoothed; t = the previous iterate (psiOld on level 0)
+    L.zero_pending = false;
     L.ghost_ok = !L.p.dist;
     L.ghost_zero = false;
     if (l == 0 && c->in_cycle) c->first_done = true;
@@ -1883,6 +1887,8 @@ static int create_impl(mgp_ctx** out, const mgp_opts* o, mgp_loopback* lb, ncclC
         }
         const char* v = std::getenv("MGP_LAZY_ZERO");  // 0: memset every fresh coarse guess instead
         if (v && std::atoi(v) == 0) c->lazy_zero = false;
+        const char* vf = std::getenv("MGP_LAZY_ZERO_FUSED");
+        if (vf && std::atoi(vf) == 0) c->lazy_zero_fused = false;
     }
     he = mgp::prepare_kernels(c->rb);
     if (he != hipSuccess) {

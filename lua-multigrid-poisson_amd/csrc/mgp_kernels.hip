@@ -2260,6 +2260,9 @@ __attribute__((amdgpu_waves_per_eu(1, PRE ? ZS_WPE_PRE : ZS_WPE_POST))) void k_z
     // PRE: LINEAR selects the restriction: 0 = residual + 2^3 average here; 1 = none (both colours of the
     // smoothed level stored; the host runs the full-weighting restriction after the phase)
     constexpr bool RR = PRE && LINEAR == 0;
+    // PRE with ERR (which only POST uses): the input is a fresh zero guess, never loaded (src may be null); this
+    // replaces the memset of a fused coarse level's u before its PRE
+    constexpr bool ZSRC = PRE && ERR;
     using VT = Vec<T, N>;
     using PF = ZsPrefetch<T, N>;
     constexpr int PFD = PRE ? (CLZ ? ZS_PFD_PRE : ZS_PFD_PRE_CL) : ZS_PFD_POST, NPF = PFD + 1, UNR = NPF == 3 ? 12 : 4;
@@ -2335,7 +2338,7 @@ __attribute__((amdgpu_waves_per_eu(1, PRE ? ZS_WPE_PRE : ZS_WPE_POST))) void k_z
         return CLZ ? 0 : (gy == 0) + (gy == g.ny - 1) + (z0 + q == 0) + (z0 + q == gnz - 1);
     };
     const int rowpar = (gy + z0) & 1;
-    const T* const src_black = src + Hh;
+    const T* const src_black = ZSRC ? nullptr : src + Hh;
 
     for (int i = tid; i < (int)(S::lds_bytes / sizeof(T)); i += NTL) lds[i] = (T)0;
     __syncthreads();
@@ -2395,7 +2398,10 @@ __attribute__((amdgpu_waves_per_eu(1, PRE ? ZS_WPE_PRE : ZS_WPE_POST))) void k_z
 #else
             const int64_t pP = (int64_t)p * P, Pz = P;
 #endif
-            r.u = gload<T, N, kZsNTL>(src_black + pP + goff);
+            if constexpr (ZSRC)
+                r.u = vzero<T, N>();
+            else
+                r.u = gload<T, N, kZsNTL>(src_black + pP + goff);
             r.f1 = gload<T, N, kZsNTL>(f + (pP - Pz) + goff);
             r.f2 = gload<T, N, kZsNTL>(f + (pP - 2 * Pz) + Hh + goff);
             if (!PRE && ERR && tile_xy) {  // psiOld of plane p - 4, for the tile's own columns only
@@ -2404,7 +2410,10 @@ __attribute__((amdgpu_waves_per_eu(1, PRE ? ZS_WPE_PRE : ZS_WPE_POST))) void k_z
                 r.o1 = gload<T, N, kZsNTO>(dp + Hh + goff);
             }
         } else {
-            r.u = gload<T, N, kZsNTL>(src_black + (int64_t)ZS_PLANE(pcl(p)) * P + goff);
+            if constexpr (ZSRC)
+                r.u = vzero<T, N>();
+            else
+                r.u = gload<T, N, kZsNTL>(src_black + (int64_t)ZS_PLANE(pcl(p)) * P + goff);
             r.f1 = gload<T, N, kZsNTL>(f + (int64_t)ZS_PLANE(pcl(p - 1)) * P + goff);
             r.f2 = gload<T, N, kZsNTL>(f + (int64_t)ZS_PLANE(pcl(p - 2)) * P + Hh + goff);
             if (!PRE && ERR && tile_xy) {
@@ -2713,7 +2722,7 @@ __attribute__((amdgpu_waves_per_eu(1, PRE ? ZS_WPE_PRE : ZS_WPE_POST))) void k_z
         steady(RPL);
     }
     for (; p <= p_end; p += UNR) group(GEN, RPL, p, p_end);
-    if (ERR) block_partial_t<NTL>(err + err1, partials);
+    if constexpr (ERR && !PRE) block_partial_t<NTL>(err + err1, partials);  // (PRE: ERR is ZSRC, no partials)
 }
 
 // ---- y-streamed temporally blocked smoothing (2D, red/black 2+2) -------------------------------
@@ -4536,6 +4545,8 @@ static hipError_t fused_dispatch(const FusedArgs& a, hipStream_t s)
 #ifdef ZS_CL_AS_CLZ  // timing experiment only (wrong at the box faces): cl != 0 PRE runs the cl = 0 code
     if (a.pre) return a.linear ? zs_launch<T, true, 1, false, true>(a, s) : zs_launch<T, true, 0, false, true>(a, s);
 #endif
+    if (a.pre && !a.src)  // a fresh zero guess (ERR marks it in PRE)
+        return a.linear ? zs_launch<T, true, 1, true, CLZ>(a, s) : zs_launch<T, true, 0, true, CLZ>(a, s);
     if (a.pre) return a.linear ? zs_launch<T, true, 1, false, CLZ>(a, s) : zs_launch<T, true, 0, false, CLZ>(a, s);
     if constexpr (std::is_same<T, float>::value && CLZ) {
         if (zs_wide(4, a.g, true)) {
@@ -4661,6 +4672,8 @@ static hipError_t fused_attr()
     }
     hipError_t e = hipFuncSetAttribute((const void*)k_zs<T, true, 0, false, CLZ>, A, pre);
     if (e == hipSuccess) e = hipFuncSetAttribute((const void*)k_zs<T, true, 1, false, CLZ>, A, pre);
+    if (e == hipSuccess) e = hipFuncSetAttribute((const void*)k_zs<T, true, 0, true, CLZ>, A, pre);
+    if (e == hipSuccess) e = hipFuncSetAttribute((const void*)k_zs<T, true, 1, true, CLZ>, A, pre);
     if (e == hipSuccess) e = hipFuncSetAttribute((const void*)k_zs<T, false, 0, false, CLZ>, A, post);
     if (e == hipSuccess) e = hipFuncSetAttribute((const void*)k_zs<T, false, 0, true, CLZ>, A, post);
     if (e == hipSuccess) e = hipFuncSetAttribute((const void*)k_zs<T, false, 1, false, CLZ>, A, post);

@@ -5,6 +5,8 @@ multiply-add and IEEE division, so psi must be BIT-IDENTICAL to the oracle in fp
 after every piece and every cycle.  The only reduction, err = RMS update, is summed in a
 different order on the GPU: tolerance |err_gpu - err_oracle| <= 1e-12 * err_oracle (fp64 sum).
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -402,11 +404,20 @@ def test_fused_timing_kinds(monkeypatch):
     dict(dim=3, n=(64, 64, 64), real="float", prolong="linear", coarse_bc="consistent"),
     dict(dim=3, n=(128, 64, 32), real="double", prolong="pc", cycle="F"),
     dict(dim=2, n=(256, 256, 1), real="float", prolong="linear", coarse_bc="consistent"),
-], ids=["3d-f32", "3d-F-f64", "2d-f32"])
+    dict(dim=3, n=(128, 128, 128), real="float", prolong="linear", coarse_bc="consistent", fused=True),
+    dict(dim=3, n=(128, 128, 64), real="double", prolong="pc", cycle="F", fused=True),
+    dict(dim=3, n=(128, 128, 128), real="float", prolong="linear", coarse_bc="consistent", cycle="F",
+         restriction="full_weighting", fused=True),
+], ids=["3d-f32", "3d-F-f64", "2d-f32", "3d-fused-f32", "3d-fused-F-f64", "3d-fused-F-fw"])
 def test_lazy_zero_equals_memset(kw, monkeypatch):
     """A fresh coarse guess read from the shared zero buffer by the first red half-sweep (no memset)
-    == zeroing u with a memset, bit for bit, with the coarse tail on and off."""
+    == zeroing u with a memset, bit for bit, with the coarse tail on and off.  fused: levels 0 and 1 run
+    k_zs, whose PRE on level 1 reads the pending zero as such (no loads) instead of a memset."""
     kw = dict(smoother="rbgs", nu1=2, nu2=2, **kw)
+    if kw.pop("fused", False):
+        monkeypatch.setenv("MGP_FUSED", "1")
+        monkeypatch.setenv("MGP_FUSED_MIN_CELLS", "65536")
+        monkeypatch.setenv("MGP_ZPOST_MIN_CELLS", str(1 << 40))
     for tail in ("1", "0"):
         monkeypatch.setenv("MGP_TAIL", tail)
         monkeypatch.setenv("MGP_LAZY_ZERO", "0")
@@ -418,6 +429,8 @@ def test_lazy_zero_equals_memset(kw, monkeypatch):
         ea, eb = a.cycles(3), b.cycles(3)
         assert np.array_equal(a.get_psi(), b.get_psi())
         assert list(ea) == list(eb)
+        if os.environ.get("MGP_FUSED") == "1":
+            assert [lv["engine"] for lv in b.levels][:2] == ["zs", "zs"], b.levels
 
 
 @pytest.mark.parametrize("kw", [
