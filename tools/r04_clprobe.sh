@@ -1,7 +1,8 @@
 #!/bin/bash
 # Round 4 probe: the cl != 0 fused PRE's step cost.  Kernel traces of the configs[3] rank slab under the
 # default library and two timing variants (var/pfd1: cl = 0 PRE with one plane of prefetch; var/asclz: cl != 0
-# PRE running the cl = 0 code, wrong at the faces).  Stops at the first failure.
+# PRE running the cl = 0 code, wrong at the faces; build them with tools/build_variants.sh and drop ./var from
+# .gpurunignore first).  Stops at the first failure.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out/clprobe
