@@ -24,6 +24,7 @@
 // parity tests check every piece bit for bit against the C oracle's plain divisions.
 #include "mgp_internal.h"
 
+#include <cstdio>
 #include <cstdlib>
 #include <type_traits>
 #include <utility>
@@ -2252,7 +2253,8 @@ __global__ __launch_bounds__((ZsShape<T, PRE, CLZ, WIDE>::NTL))
 __attribute__((amdgpu_waves_per_eu(1, PRE ? ZS_WPE_PRE : ZS_WPE_POST))) void k_zs(const T* __restrict__ src, const T* __restrict__ f,
                                                                 T* __restrict__ dst, const T* old, T* __restrict__ R,
                                                                 const T* __restrict__ V, double* __restrict__ partials,
-                                                                Geo g, Geo gc, Op<T, 3> op, T clc, int zc, int gz)
+                                                                Geo g, Geo gc, Op<T, 3> op, T clc, int zc, int gz,
+                                                                int patch)
 {
     using S = ZsShape<T, PRE, CLZ, WIDE>;
     constexpr int N = S::N, H = S::H, HWE = S::HWE, G = S::G, YE = S::YE, SLOT = S::SLOT, TX = S::TX,
@@ -2275,7 +2277,14 @@ __attribute__((amdgpu_waves_per_eu(1, PRE ? ZS_WPE_PRE : ZS_WPE_POST))) void k_z
     const int b = xcd_remap(blockIdx.x, gridDim.x);
     const int tile = b % (tiles_x * tiles_y);
     const int Z0 = (b / (tiles_x * tiles_y)) * zc;
-    const int X0 = (tile % tiles_x) * TX, Y0 = (tile / tiles_x) * TY;
+    int tx_ = tile % tiles_x, ty_ = tile / tiles_x;
+    if (patch) {  // the tiles an XCD runs at once form px x py patches (host: px | tiles_x, py | tiles_y)
+        const int px = patch & 255, py = patch >> 8, per = px * py, prow = tiles_x / px;
+        const int pi = tile / per, q = tile % per;
+        tx_ = (pi % prow) * px + q % px;
+        ty_ = (pi / prow) * py + q / px;
+    }
+    const int X0 = tx_ * TX, Y0 = ty_ * TY;
     const int hw = g.hw, Hh = (int)g.H;
     const int z0 = (int)g.z0, gnz = (int)g.gnz, cz0 = (int)gc.z0;
     const int64_t P = g.P;
@@ -4482,6 +4491,18 @@ hipError_t launch_prolong_correct(int rb, int dim, int linear, void* u, const vo
 
 // ---- fused smoothing phases ----
 
+// Tile order of a launch with more tiles than run at once (MGP_ZS_PATCH = "px,py", "0" off, read per call):
+// consecutive tiles of an XCD's band as px x py patches instead of whole tile rows, so that the y neighbours
+// whose halo rows a tile reads stream through z at the same time.  Returns px | py << 8, or 0.
+static int zs_patch(int tiles_x, int tiles_y, unsigned nb)
+{
+    const char* v = std::getenv("MGP_ZS_PATCH");
+    int px = 0, py = 0;
+    if (!v || std::sscanf(v, "%d,%d", &px, &py) != 2) return 0;
+    if (px < 1 || py < 1 || px > 255 || py > 255 || tiles_x % px || tiles_y % py || nb <= 512) return 0;
+    return px | (py << 8);
+}
+
 template <typename T, bool PRE, int LINEAR, bool ERR, bool CLZ, bool WIDE = false>
 static hipError_t zs_launch(const FusedArgs& a, hipStream_t s)
 {
@@ -4491,7 +4512,8 @@ static hipError_t zs_launch(const FusedArgs& a, hipStream_t s)
     k_zs<T, PRE, LINEAR, ERR, CLZ, WIDE><<<nb, S::NTL, S::lds_bytes, s>>>((const T*)a.src, (const T*)a.f, (T*)a.dst,
                                                                            (const T*)(a.old ? a.old : a.dst), (T*)a.R,
                                                                            (const T*)a.V, a.partials, a.g, a.gc,
-                                                                           op, (T)a.clc, a.zc, a.ghost);
+                                                                           op, (T)a.clc, a.zc, a.ghost,
+                                                                           zs_patch(a.g.nx / S::TX, a.g.ny / S::TY, nb));
     return hipGetLastError();
 }
 
