@@ -21,10 +21,12 @@ and --box 4096,4096,512 run one rank's slab of those configs.  value = cycles/s 
 ghost-0 coarse levels), with the CPU port timed over the same cycles (1 thread and OpenMP) beside the GPU.
 --restriction full_weighting: the build's full-weighting option instead of the 2^d cell average.
 
-With N >= 4 ranks the default (weak) run adds the north-star workloads to the same JSON line
-(`north_star_lines`): BASELINE configs[3] (2048^3 V-cycle) and configs[4] (4096^3 F-cycle) as one box split
-into N z-slabs, each run after the previous context is closed, with per-rank halo-exchange and collective
-time from HIP events (--no-north-star skips them; configs[4] is skipped where it does not fit the ranks' HBM).
+At every N the default (weak) run adds the north-star workloads to the same JSON line (`north_star_lines`):
+BASELINE configs[3] (2048^3 V-cycle) and configs[4] (4096^3 F-cycle) as one box split into N z-slabs (N = 1: the
+whole box on one GPU), each run after the previous context is closed, with per-rank halo-exchange and collective
+time from HIP events, so that the driver's 1/2/4/8-GPU runs give the north star's strong-scaling curve
+(--no-north-star skips them; configs[4] is skipped where it does not fit the ranks' HBM: N < 4).  At N = 1 the
+line also carries the fp64 512^3 workload (the reference's default precision, gpu.lua:32) as `fp64_line`.
 
 Roofline fields: `roofline.frac` is the dominant level-0 kernel's algorithmic (compulsory) bytes over its
 event-timed duration against 8 TB/s; `roofline.cycle_frac` the compulsory bytes of every level of one cycle
@@ -111,6 +113,13 @@ def main():
         plan_only(a, cfg, box, rank, world, dist)
         return
     line = run_workload(a, cfg, box, strong, rank, world, local, dist, a.steps, a.warmup, primary=True)
+    if want_north_star(a, world) and world == 1:
+        fa = argparse.Namespace(**vars(a))
+        fa.real = "double"
+        sub = run_workload(fa, make_cfg(fa, box, rank, world, local, None), box, strong, rank, world, local, dist,
+                           a.ns_steps * 4, a.ns_warmup)
+        line["fp64_line"] = {k: sub.get(k) for k in ("value", "unit", "ms_per_step", "steps", "warmup", "dtype", "config",
+                                                     "final_err", "relative_residual", "roofline", "finest_smoother_GBps")}
     if want_north_star(a, world):
         extra = {}
         for name, nbox, cyc, _ in NORTH_STAR:
@@ -140,7 +149,7 @@ def main():
 
 
 def want_north_star(a, world):
-    return world >= 4 and not a.box and a.dim == 3 and not a.config0 and not a.no_north_star
+    return not a.box and a.dim == 3 and not a.config0 and not a.no_north_star
 
 
 def new_comm_id(dist, rank, world):
@@ -174,14 +183,16 @@ def make_cfg(a, box, rank, world, local, comm_id):
                 rank=rank, world=world, comm_id=comm_id, restriction=a.restriction)
 
 
-def fits_hbm(cfg, world, local):
+def fits_hbm(cfg, world, local, total=None):
     """{} if the context fits this GPU's HBM as built, {"MGP_KEEP_PSI_OLD": "0"} if it fits only without the
-    psiOld-keeping output buffer (u, f, t and the hierarchy), None if not even then."""
-    import torch
-
+    psiOld-keeping output buffer (u, f, t and the hierarchy), None if not even then (total: HBM bytes per GPU,
+    default the device's)."""
     rb = 4 if cfg["real"] == "float" else 8
     cells = cfg["n"][0] * cfg["n"][1] * cfg["n"][2] / world
-    total = torch.cuda.get_device_properties(local).total_memory
+    if total is None:
+        import torch
+
+        total = torch.cuda.get_device_properties(local).total_memory
     est = lambda arrays: cells * rb * arrays * 8 / 7 + (2 << 30)  # noqa: E731
     if est(4) < 0.92 * total:
         return {}
@@ -472,8 +483,11 @@ def plan_only(a, cfg, box, rank, world, dist):
                 ns = argparse.Namespace(**vars(a))
                 ns.cycle, ns.box = cyc, ",".join(map(str, nbox))
                 ncfg = make_cfg(ns, nbox, 0, world, 0, cfg["comm_id"])
-                out["north_star_lines"][name] = {"global_box": list(nbox), "cycle": cyc,
+                fit = fits_hbm(ncfg, world, 0, total=288e9)  # MI355X: 288 GB of HBM3E per GPU
+                out["north_star_lines"][name] = {"global_box": list(nbox), "cycle": cyc, "fits": fit is not None,
                                                  "comm_per_cycle": comm_schedule(ncfg)}
+            if world == 1:
+                out["fp64_line"] = True
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()

@@ -107,7 +107,10 @@ typedef struct mgp_ctx mgp_ctx;
 int         mgp_version(void);
 /* Defaults = the reference cpu.lua configuration: 2D, double, Jacobi 7+7, V, PC, fresh, zero. */
 void        mgp_opts_default(mgp_opts* o);
-/* RCCL unique id for a world > 1 context (call on rank 0, broadcast the bytes). */
+/* RCCL unique id for a world > 1 context (call on rank 0, broadcast the bytes).  With the environment variable
+ * MGP_TRANSPORT=rccl when it is created, a world-1 context (or a one-device group) takes the multi-GPU code
+ * path on a one-rank RCCL communicator of its own (3D: its levels are "distributed" slabs without neighbours),
+ * so that every RCCL call of a cycle executes on a one-GPU machine; results equal the plain world-1 run. */
 int         mgp_comm_unique_id(void* out, int64_t nbytes);
 
 /* Replaces MultigridCPU:init{size,...} (cpu.lua:173-194) / MultigridCPURaw:init(size, real)
@@ -231,6 +234,14 @@ int         mgp_group_get_field(mgp_group* g, int level, int which, void* dst, i
 int         mgp_group_residual_norm(mgp_group* g, int level, double* rnorm, double* fnorm);
 int         mgp_group_field_stats(mgp_group* g, int level, int which, uint64_t* hash, double stats[3]);
 
+/* The reference's debugging check (MultigridCPURaw.debugging / MultigridGPU.debugging: show / showAndCheck after
+ * every sweep and piece of twoGrid, error "found a nan" on a non-finite cell; cpu-raw.lua:126-140,
+ * gpu.lua:269-284).  mode 1: every phase of every cycle (pre-smoothing, the restricted residual, the coarse solve
+ * or tail, prolongation + post-smoothing, per level) is followed by a device-side scan of its output; mgp_cycle /
+ * mgp_cycles then return MGP_ERR_STATE naming the FIRST phase whose output holds a NaN or inf ("found a nan: cycle
+ * c, level l (nx x ny x nz), <phase>").  Cycles run eagerly while it is on.  mode 0: off (the default). */
+int         mgp_set_debug(mgp_ctx* c, int mode);
+
 /* Kernel and communication timing with HIP events on the stream the work runs on.  mgp_timing(c, 1) resets
  * and enables (cycles then run eagerly, without hipGraph replay, so each launch can be bracketed).
  * Timed kinds; the first three on level 0 only:
@@ -254,7 +265,8 @@ int         mgp_timing_read(mgp_ctx* c, int kind, double* ms_total, int64_t* lau
 /* The exchanges and collectives this rank has issued since creation or the last reset (reset != 0 clears after
  * reading), in issue order: up to max_rows rows of 5 int64 {op, side, level, msgs, bytes}, op 0 = halo exchange
  * (msgs per neighbour and direction, bytes sent per neighbour), 1 = agglomeration all-gather (bytes of this
- * rank's part), 2 = err all-reduce (8 bytes); side 1 = issued on the side stream's communicator.  Returns the
+ * rank's part), 2 = err all-reduce (8 bytes); side 1 = issued on the side stream (under RCCL on its own communicator, split off
+ * the context's at creation).  Returns the
  * number of rows recorded (which may exceed max_rows).  Every rank of a decomposition must issue the same
  * sequence per communicator (RCCL matches calls in order); tests compare the ranks' logs. */
 int         mgp_comm_log(mgp_ctx* c, int64_t* rows, int max_rows, int reset);

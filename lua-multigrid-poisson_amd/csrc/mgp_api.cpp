@@ -64,8 +64,20 @@ bool is_pow2(int64_t v) { return v > 0 && (v & (v - 1)) == 0; }
 // >= 2 cells (cpu.lua recursion down to width 1).  A level stays slab-distributed while its
 // planes split evenly with >= 2 per rank, it is not the coarsest and it has more than
 // gather_cells cells; from the first replicated level down every rank holds the whole grid.
+// MGP_TRANSPORT=rccl (read when a context or group is created): a world-1 3D context takes the slab code path
+// on a real one-rank RCCL communicator: ncclGetUniqueId / ncclCommInitRank / ncclCommSplit, the err and norm
+// all-reduces, the agglomeration all-gather and the (peerless, empty) grouped halo send/recv all execute.  It is
+// how a one-GPU box executes the RCCL transport at all (RCCL refuses two ranks on one device); the results
+// equal the plain world-1 run bit for bit (tests/test_gpu_rccl.py).
+bool env_rccl1(const mgp_opts& o)
+{
+    const char* v = std::getenv("MGP_TRANSPORT");
+    return o.world == 1 && v && std::strcmp(v, "rccl") == 0;
+}
+
 int plan_levels(const mgp_opts& o, std::vector<LevelPlan>& out, std::string& err)
 {
+    const bool slab1 = env_rccl1(o);
     out.clear();
     if (o.struct_size != (int32_t)sizeof(mgp_opts)) {
         err = "mgp_opts.struct_size mismatch (header/library version skew): fill the struct with this library's "
@@ -98,7 +110,7 @@ int plan_levels(const mgp_opts& o, std::vector<LevelPlan>& out, std::string& err
         if (o.dim != 3) { err = "domain decomposition is 3D slab-z only"; return MGP_ERR_ARG; }
         if (nz % o.world != 0 || nz / o.world < 2) { err = "n[2] must split into >= 2 planes per rank"; return MGP_ERR_ARG; }
     }
-    bool dist = o.world > 1;
+    bool dist = o.world > 1 || (slab1 && o.dim == 3);
     for (;;) {
         LevelPlan p;
         p.nx = nx;
@@ -208,6 +220,10 @@ struct mgp_ctx {
     // only the exchange / collective log is kept
     bool dry = false;
     bool nb_comm = false;  // non-blocking communicators (mgp_group_create): every call is polled to completion
+    mgp::FusedTuning tu;   // tile settings of the temporally blocked phases (env, snapshot at creation)
+    bool rccl1 = false;    // world 1 on a one-rank RCCL communicator (MGP_TRANSPORT=rccl, env_rccl1)
+    // the multi-rank code path: a communicator (or the loopback transport), collectives, the side stream
+    bool multi() const { return o.world > 1 || rccl1; }
     // RCCL API calls of this rank in flight (group_abort waits for them to return before it aborts the
     // communicators) and whether the rank waits on its peers (a halo exchange, collective or the stream
     // synchronisation after one): the group aborts only when a surviving rank is blocked that way
@@ -278,6 +294,12 @@ struct mgp_ctx {
     int* err_ctr = nullptr;     // when set: err_dst[*err_ctr], advanced on the device (mgp_cycles on one GPU)
     int* d_slot = nullptr;      // that device counter
     std::string err;
+    // the reference's debugging check (mgp_set_debug): after every phase of a cycle the phase's output is checked
+    // for non-finite cells on the device; d_dbg = the first failing check's index into dbg_names (0x7f7f7f7f: none)
+    int debug = 0;
+    int* d_dbg = nullptr;
+    std::vector<std::string> dbg_names;
+    int dbg_cycle = 0;
     // finest-level kernel timing: event pairs around level-0 launches of each timed kind
     bool timing = false;
     std::vector<hipEvent_t> ev;
@@ -355,10 +377,19 @@ Geo make_geo(const LevelPlan& p, int dim)
 
 // ---- loopback transport (same collective semantics as the RCCL calls below) ----
 
+// The rank waits on its peers while one of these is alive (a transport call, a collective, the stream
+// synchronisation or read-back after one): a group aborts a failed rank's peers only when they wait (group_run).
+struct WaitScope {
+    mgp_ctx* c;
+    explicit WaitScope(mgp_ctx* cc) : c(cc) { c->waiting.fetch_add(1); }
+    ~WaitScope() { c->waiting.fetch_sub(1); }
+};
+
 int lb_fail(mgp_ctx* c) { return c->fail(MGP_ERR_STATE, "loopback group barrier timed out or broken"); }
 
 int lb_exchange(mgp_ctx* c, int l, char* buf, int depth, int colour, hipStream_t st)
 {
+    WaitScope w(c);
     mgp_loopback* g = c->lb;
     const size_t rb = (size_t)c->rb;
     const Level& L = c->lev[l];
@@ -391,6 +422,7 @@ int lb_exchange(mgp_ctx* c, int l, char* buf, int depth, int colour, hipStream_t
 // in-place all-gather: rank q's slab is at buf + q * count reals on every rank
 int lb_allgather(mgp_ctx* c, char* buf, size_t count)
 {
+    WaitScope w(c);
     mgp_loopback* g = c->lb;
     const size_t bytes = count * (size_t)c->rb;
     c->lb_buf = buf;
@@ -412,6 +444,7 @@ int lb_allgather(mgp_ctx* c, char* buf, size_t count)
 // in-place sum of n doubles over the ranks, added in rank order
 int lb_allreduce(mgp_ctx* c, double* v, int n = 1)
 {
+    WaitScope w(c);
     mgp_loopback* g = c->lb;
     c->lb_buf = (char*)v;
     HIP_TRY(c, hipEventRecord(c->lb_ev, c->s));
@@ -446,12 +479,6 @@ struct NcclScope {
         c->waiting.fetch_sub(1);
         c->in_nccl.fetch_sub(1);
     }
-};
-
-struct WaitScope {
-    mgp_ctx* c;
-    explicit WaitScope(mgp_ctx* cc) : c(cc) { c->waiting.fetch_add(1); }
-    ~WaitScope() { c->waiting.fetch_sub(1); }
 };
 
 int nccl_done(mgp_ctx* c, ncclComm_t comm, ncclResult_t r, const char* what)
@@ -660,8 +687,8 @@ int smooth_deep(mgp_ctx* c, int l, int sweeps, double h)
     Level& L = c->lev[l];
     const double cl = coarse_coef(c->o.coarse_bc, l);
     const int D = 2 * sweeps + 1;
-    if (!L.fghost_ok) {
-        TRY(exchange_buf(c, L, L.f, c->G));
+    if (!L.fghost_ok) {  // (the sweeps read f up to D - 1 ghost planes deep)
+        TRY(exchange_buf(c, L, L.f, std::min(c->G, (int)L.g.nz)));
         L.fghost_ok = true;
     }
     if (!L.zero_pending && !L.ghost_zero) TRY(exchange_buf(c, L, L.u, D, 1));  // black cells only
@@ -929,6 +956,7 @@ int fused_pre(mgp_ctx* c, int l, double h)
     const Geo gc = coarse_view(L, C, &zc);
     const bool fw = c->o.restriction == MGP_RESTRICT_FULL_WEIGHTING;
     mgp::FusedArgs a{};
+    a.tu = c->tu;
     a.pre = true;
     a.linear = fw;  // PRE: 1 = smoothing only (both colours stored), the full weighting follows
     a.src = L.zero_pending ? nullptr : c->ui(L, L.u);  // null: a fresh zero guess (lazy_zero_ok)
@@ -978,6 +1006,7 @@ int fused_post(mgp_ctx* c, int l, double h, bool want_err)
     int64_t zc = 0;
     const Geo gc = coarse_view(L, C, &zc);
     mgp::FusedArgs a{};
+    a.tu = c->tu;
     a.pre = false;
     a.linear = c->o.prolong == MGP_PROLONG_LINEAR;
     a.src = c->ui(L, L.u);
@@ -1009,7 +1038,7 @@ int fused_post(mgp_ctx* c, int l, double h, bool want_err)
     L.ghost_zero = false;
     if (want_err) {
         HIP_TRY(c, mgp::launch_sum_partials(c->d_part,
-                                            mgp::fused_blocks(c->rb, L.g, L.zc, coarse_coef(c->o.coarse_bc, l) == 0.0),
+                                            mgp::fused_blocks(c->rb, L.g, L.zc, coarse_coef(c->o.coarse_bc, l) == 0.0, c->tu),
                                             c->err_dst, c->s, c->err_ctr));
         c->err_done = true;
     }
@@ -1224,6 +1253,22 @@ struct Range {
     }
 };
 
+// mgp_set_debug: check level l's `buf` (u or f) for non-finite cells after the phase `what` (cpu-raw.lua:126-140
+// show + "found a nan", called after every smoother sweep / residual / restriction / prolongation there)
+int debug_check(mgp_ctx* c, int l, const char* what, bool f_field = false)
+{
+    if (!c->debug || c->dry || !c->d_dbg) return MGP_OK;
+    Level& L = c->lev[l];
+    if (!f_field && L.zero_pending) return MGP_OK;  // a pending fresh zero
+    char name[160];
+    std::snprintf(name, sizeof name, "cycle %d, level %d (%lld x %lld x %lld), %s", c->dbg_cycle, l, (long long)L.p.nx,
+                  (long long)L.p.ny, (long long)(c->o.dim == 3 ? L.g.nz : 1), what);
+    const int id = (int)c->dbg_names.size();
+    c->dbg_names.push_back(name);
+    HIP_TRY(c, mgp::launch_nonfinite_check(c->rb, c->ui(L, f_field ? L.f : L.u), L.g.P * L.g.nz, id, c->d_dbg, c->s));
+    return MGP_OK;
+}
+
 int cycle_rec(mgp_ctx* c, int l, double h, bool fcycle)
 {
     const int last = (int)c->lev.size() - 1;
@@ -1233,11 +1278,13 @@ int cycle_rec(mgp_ctx* c, int l, double h, bool fcycle)
     }
     if (l == c->tail_level && h == level_h(c, l)) {
         Range r("L%d+ coarse tail", l);
-        return run_tail(c, fcycle);
+        TRY(run_tail(c, fcycle));
+        return debug_check(c, l, "the coarse tail (V = its cycle)");
     }
     if (l == last) {
         Range r("L%d coarse solve", l);
-        return coarse_solve_at(c, l, h);
+        TRY(coarse_solve_at(c, l, h));
+        return debug_check(c, l, "the coarse solve");
     }
     const bool fused = c->lev[l].fused && h == level_h(c, l);
     const bool blk = !fused && c->lev[l].blk && h == level_h(c, l);
@@ -1252,6 +1299,8 @@ int cycle_rec(mgp_ctx* c, int l, double h, bool fcycle)
         TRY(smooth(c, l, c->o.nu1, h));
         TRY(residual_restrict(c, l, h));
     }
+    TRY(debug_check(c, l, "pre-smoothing (u)"));
+    TRY(debug_check(c, l + 1, "the restriction (R = f of the coarse level)", true));
     if (c->o.coarse_init == MGP_COARSE_FRESH) TRY(zero_level(c, c->lev[l + 1]));
     pre_range.reset();
     if (fcycle) TRY(cycle_rec(c, l + 1, 2 * h, true));
@@ -1269,7 +1318,7 @@ int cycle_rec(mgp_ctx* c, int l, double h, bool fcycle)
         TRY(prolong_correct(c, l, c->post_black && c->o.smoother == MGP_RBGS && c->o.nu2 >= 1));
         TRY(smooth(c, l, c->o.nu2, h, want_err));
     }
-    return MGP_OK;
+    return debug_check(c, l, "the prolongation + correction and post-smoothing (u)");
 }
 
 // Where the last outer iteration's psiOld lives: the level-0 t buffer with the fused err (the
@@ -1312,7 +1361,7 @@ int one_cycle(mgp_ctx* c, double* dst)
         HIP_TRY(c, mgp::launch_sqdiff_sum(c->rk, c->ui(L0, L0.u), c->psi_old, L0.g.P * L0.g.nz, c->d_part, dst, c->s,
                                           c->err_ctr));
     }
-    if (c->o.err_mode && c->o.world > 1) {
+    if (c->o.err_mode && c->multi()) {
         comm_log(c, 2, 0, 0, 1, (int64_t)sizeof(double));
         if (c->dry) return MGP_OK;
         hipEvent_t e;
@@ -1382,7 +1431,7 @@ int precapture(mgp_ctx* c)
     const char* v = std::getenv("MGP_PRECAPTURE");
     if (!c->use_graph || c->handoff_fn || (v && std::atoi(v) == 0)) return MGP_OK;
     const std::vector<char*> s0 = level_state(c);
-    c->err_ctr = c->o.err_mode && c->o.world == 1 ? c->d_slot : nullptr;  // as mgp_cycles captures
+    c->err_ctr = c->o.err_mode && !c->multi() ? c->d_slot : nullptr;  // as mgp_cycles captures
     int rc = MGP_OK;
     for (int i = 0; i < 8 && rc == MGP_OK; ++i) {
         mgp_ctx::GraphEntry* e = nullptr;
@@ -1442,7 +1491,7 @@ int sync_and_check(mgp_ctx* c)
             {
                 if (on) c->waiting.fetch_sub(1);
             }
-        } w{c, c->o.world > 1};
+        } w{c, c->multi()};
         if (w.on) c->waiting.fetch_add(1);
         HIP_TRY(c, hipStreamSynchronize(c->s));
         if (c->xs) HIP_TRY(c, hipStreamSynchronize(c->xs));
@@ -1523,6 +1572,8 @@ static void host_setup(mgp_ctx* c, const mgp_opts& o, const std::vector<LevelPla
     if (c->o.dim == 2) c->o.n[2] = 1;
     c->rb = o.real_bytes;
     c->rk = real_kind(o);
+    c->rccl1 = env_rccl1(o);
+    c->tu = mgp::fused_tuning_from_env();
     c->G = o.dim == 3 ? mgp::kGhost3D : 0;  // widened below when a distributed level is fused
     {
         const char* v = std::getenv("MGP_FRESH");
@@ -1537,7 +1588,7 @@ static void host_setup(mgp_ctx* c, const mgp_opts& o, const std::vector<LevelPla
         c->early_x = !(ve && std::atoi(ve) == 0);
     }
     // distributed 3D levels sweep with deep halos (smooth_deep): kGhostZs ghost planes per side
-    if (c->deep_halo && o.dim == 3 && o.world > 1) c->G = mgp::kGhostZs;
+    if (c->deep_halo && o.dim == 3 && c->multi()) c->G = mgp::kGhostZs;
     for (auto& p : plan) {
         Level L;
         L.p = p;
@@ -1602,7 +1653,7 @@ int mgp_plan_comm(const mgp_opts* o, int32_t cycles, int64_t* rows, int max_rows
     // stand-ins for the device objects whose presence steers the host logic (never dereferenced: every device
     // call is skipped): the side stream of the early exchange and the zero buffer of lazily zeroed levels
     static char stand_in[16];
-    if (c.o.world > 1 && c.early_x) c.xs = reinterpret_cast<hipStream_t>(stand_in);
+    if (c.multi() && c.early_x) c.xs = reinterpret_cast<hipStream_t>(stand_in);
     if (c.o.smoother == MGP_RBGS && c.o.coarse_init == MGP_COARSE_FRESH) {
         c.zbuf_reals = zbuf_reals_of(&c);
         if (c.zbuf_reals) c.zbuf = stand_in;
@@ -1657,6 +1708,7 @@ static void destroy_impl(mgp_ctx* c)
     if (c->lb_red) (void)hipFree(c->lb_red);
     if (c->d_metrics) (void)hipFree(c->d_metrics);
     if (c->d_rn) (void)hipFree(c->d_rn);
+    if (c->d_dbg) (void)hipFree(c->d_dbg);
     if (c->s) (void)hipStreamDestroy(c->s);
     delete c;
 }
@@ -1715,11 +1767,11 @@ static void select_engines(mgp_ctx* c)
         const bool on = !(v && std::atoi(v) == 0) && c->o.smoother == MGP_RBGS && c->o.nu1 == 2 && c->o.nu2 == 2;
         for (size_t l = 0; l + 1 < c->lev.size(); ++l) {
             Level& L = c->lev[l];
-            L.fused = on && level_cells(L) >= min_cells && mgp::fused_supported(c->rb, c->o.dim, 2, L.g);
+            L.fused = on && level_cells(L) >= min_cells && mgp::fused_supported(c->rb, c->o.dim, 2, L.g, c->tu);
             if (L.fused) {
                 const bool clz = coarse_coef(c->o.coarse_bc, (int)l) == 0.0;
-                L.zc = mgp::fused_zc(c->rb, L.g, false, clz);
-                L.zc_pre = mgp::fused_zc(c->rb, L.g, true, clz);
+                L.zc = mgp::fused_zc(c->rb, L.g, false, clz, c->tu);
+                L.zc_pre = mgp::fused_zc(c->rb, L.g, true, clz, c->tu);
             }
             if (L.fused && L.p.dist) c->G = mgp::kGhostZs;
         }
@@ -1730,8 +1782,8 @@ static void select_engines(mgp_ctx* c)
         const int64_t zmin = vz ? std::atoll(vz) : (c->o.dim == 3 ? int64_t(1) << 24 : INT64_MAX);
         for (size_t l = 1; l + 1 < c->lev.size(); ++l) {
             Level& L = c->lev[l];
-            L.zpost = on && !L.fused && level_cells(L) >= zmin && mgp::fused_supported(c->rb, c->o.dim, 2, L.g);
-            if (L.zpost) L.zc = mgp::fused_zc(c->rb, L.g, false, coarse_coef(c->o.coarse_bc, (int)l) == 0.0);
+            L.zpost = on && !L.fused && level_cells(L) >= zmin && mgp::fused_supported(c->rb, c->o.dim, 2, L.g, c->tu);
+            if (L.zpost) L.zc = mgp::fused_zc(c->rb, L.g, false, coarse_coef(c->o.coarse_bc, (int)l) == 0.0, c->tu);
             if (L.zpost && L.p.dist) c->G = mgp::kGhostZs;
         }
     }
@@ -1773,7 +1825,7 @@ static int create_impl(mgp_ctx** out, const mgp_opts* o, mgp_loopback* lb, ncclC
     if (rc != MGP_OK) return rc;
 
     mgp_ctx* c = new mgp_ctx();
-    if (ext_comm && o->world > 1) {  // from mgp_group_create (non-blocking communicators); owned from here
+    if (ext_comm) {  // from mgp_group_create (non-blocking communicators); owned from here
         c->comm = ext_comm;
         c->xcomm = ext_xcomm;
         c->nb_comm = true;
@@ -1863,7 +1915,7 @@ static int create_impl(mgp_ctx** out, const mgp_opts* o, mgp_loopback* lb, ncclC
         c->use_gs = v && std::atoi(v) != 0;
     }
     int nb2 = 2 * mgp::half_blocks(c->rk, L0.g, c->use_gs);
-    if (L0.fused) nb2 = std::max(nb2, mgp::fused_blocks(c->rb, L0.g, L0.zc, coarse_coef(c->o.coarse_bc, 0) == 0.0));
+    if (L0.fused) nb2 = std::max(nb2, mgp::fused_blocks(c->rb, L0.g, L0.zc, coarse_coef(c->o.coarse_bc, 0) == 0.0, c->tu));
     c->part_cap = std::max<int64_t>(mgp::kSumBlocks, nb2 + mgp::sum_scratch(nb2));
     if (hipMalloc(&c->d_part, sizeof(double) * c->part_cap) != hipSuccess) {
         c->err = "hipMalloc failed for reduction partials";
@@ -1876,7 +1928,7 @@ static int create_impl(mgp_ctx** out, const mgp_opts* o, mgp_loopback* lb, ncclC
     }
     {
         const char* v = std::getenv("MGP_GRAPH");
-        c->use_graph = c->o.world == 1 && !(v && std::atoi(v) == 0) && !roctx_on();
+        c->use_graph = !c->multi() && !(v && std::atoi(v) == 0) && !roctx_on();
     }
     if (c->o.smoother == MGP_RBGS && c->o.coarse_init == MGP_COARSE_FRESH) {
         c->zbuf_reals = zbuf_reals_of(c);
@@ -1895,7 +1947,7 @@ static int create_impl(mgp_ctx** out, const mgp_opts* o, mgp_loopback* lb, ncclC
         c->err = std::string("hipFuncSetAttribute (dynamic LDS): ") + hipGetErrorString(he);
         return bail(MGP_ERR_HIP);
     }
-    if (c->o.world > 1) {  // side stream of the early POST halo exchange
+    if (c->multi()) {  // side stream of the early POST halo exchange
         if (c->early_x && (hipStreamCreateWithFlags(&c->xs, hipStreamNonBlocking) != hipSuccess ||
                            hipEventCreateWithFlags(&c->x_ev0, hipEventDisableTiming) != hipSuccess ||
                            hipEventCreateWithFlags(&c->x_ev1, hipEventDisableTiming) != hipSuccess)) {
@@ -1919,27 +1971,32 @@ static int create_impl(mgp_ctx** out, const mgp_opts* o, mgp_loopback* lb, ncclC
             return bail(MGP_ERR_ARG);
         }
         lb->ranks[c->o.rank] = c;
-    } else if (c->o.world > 1 && c->comm) {
+    } else if (c->multi() && c->comm) {
         // communicator handed in by mgp_group_create
-    } else if (c->o.world > 1) {
+    } else if (c->multi()) {
         ncclUniqueId id;
         std::memcpy(&id, o->comm_id, sizeof(id));
+        if (c->rccl1) {  // one rank: its own id
+            const ncclResult_t ri = ncclGetUniqueId(&id);
+            if (ri != ncclSuccess) {
+                c->err = std::string("ncclGetUniqueId: ") + ncclGetErrorString(ri);
+                return bail(MGP_ERR_RCCL);
+            }
+        }
         ncclResult_t r = ncclCommInitRank(&c->comm, c->o.world, id, c->o.rank);
         if (r != ncclSuccess) {
             c->err = std::string("ncclCommInitRank: ") + ncclGetErrorString(r);
             c->comm = nullptr;
             return bail(MGP_ERR_RCCL);
         }
-        // the side stream's communicator: a collective split every rank makes at the same point (all or none:
-        // MGP_EARLY_X is the same on every rank), so that the early POST exchange does not serialise with the
-        // compute stream's exchanges of the coarse levels
-        if (c->early_x) {
-            r = ncclCommSplit(c->comm, 0, c->o.rank, &c->xcomm, nullptr);
-            if (r != ncclSuccess) {
-                c->err = std::string("ncclCommSplit (side-stream communicator): ") + ncclGetErrorString(r);
-                c->xcomm = nullptr;
-                return bail(MGP_ERR_RCCL);
-            }
+        // the side stream's communicator: a collective split that every rank makes at this point, whatever its
+        // environment says (MGP_EARLY_X only decides whether it is used), so that the early POST
+        // exchange does not serialise with the compute stream's exchanges of the coarse levels
+        r = ncclCommSplit(c->comm, 0, c->o.rank, &c->xcomm, nullptr);
+        if (r != ncclSuccess) {
+            c->err = std::string("ncclCommSplit (side-stream communicator): ") + ncclGetErrorString(r);
+            c->xcomm = nullptr;
+            return bail(MGP_ERR_RCCL);
         }
     }
     if (hipStreamSynchronize(c->s) != hipSuccess) {
@@ -2051,6 +2108,7 @@ static int planes_io(mgp_ctx* c, int level, int which, int64_t z_begin, int64_t 
     if (z_begin < 0 || nz < 0 || z_begin + nz > L.g.nz)
         return c->fail(MGP_ERR_ARG, "field I/O: planes [%lld, %lld) outside the local slab of %lld planes",
                        (long long)z_begin, (long long)(z_begin + nz), (long long)L.g.nz);
+    WaitScope wait(c);  // a derived field may exchange halos first, and the read-back waits for that
     if (which == MGP_FIELD_U || which == MGP_FIELD_RESIDUAL) TRY(materialize_zero(c, L));
     char* src = nullptr;
     char* scratch = nullptr;
@@ -2167,18 +2225,31 @@ int mgp_cycles(mgp_ctx* c, int32_t k, double* errs)
 {
     if (!c || k < 0) return MGP_ERR_ARG;
     TRY(ensure_errs(c, k));
-    const bool graph = c->use_graph && !c->timing && !c->handoff_fn;
+    const bool graph = c->use_graph && !c->timing && !c->handoff_fn && !c->debug;
     // one GPU: every cycle's err goes to d_errs[*d_slot] and advances the device counter (graph replays
     // need no per-cycle copy); with ranks the all-reduce needs the slot's address, so it is explicit
-    const bool ctr = c->o.world == 1 && c->o.err_mode && k > 0;
+    const bool ctr = !c->multi() && c->o.err_mode && k > 0;
     if (ctr) HIP_TRY(c, hipMemsetAsync(c->d_slot, 0, sizeof(int), c->s));
     c->err_ctr = ctr ? c->d_slot : nullptr;
+    if (c->debug) {
+        c->dbg_names.clear();
+        HIP_TRY(c, hipMemsetAsync(c->d_dbg, 0x7f, sizeof(int), c->s));
+    }
     int rc = MGP_OK;
-    for (int i = 0; i < k && rc == MGP_OK; ++i)
+    for (int i = 0; i < k && rc == MGP_OK; ++i) {
+        c->dbg_cycle = i + 1;
         rc = graph ? graph_cycle(c, i) : one_cycle(c, ctr ? c->d_errs : c->d_errs + i);
+    }
     c->err_ctr = nullptr;
     TRY(rc);
     TRY(sync_and_check(c));
+    if (c->debug) {
+        int first = 0;
+        HIP_TRY(c, hipMemcpy(&first, c->d_dbg, sizeof(int), hipMemcpyDeviceToHost));
+        if (first >= 0 && first < (int)c->dbg_names.size())
+            return c->fail(MGP_ERR_STATE, "found a nan (cpu-raw.lua:135-139, gpu.lua:279-283): %s",
+                           c->dbg_names[(size_t)first].c_str());
+    }
     if (errs) {
         if (!c->o.err_mode) {
             for (int i = 0; i < k; ++i) errs[i] = NAN;
@@ -2335,7 +2406,8 @@ int mgp_metrics(mgp_ctx* c, double* rel_err, int64_t* count, double* frob)
     const Level& L0 = c->lev[0];
     double* out = c->d_metrics + 3 * mgp::kSumBlocks;
     HIP_TRY(c, mgp::launch_metrics(c->rb, c->ui(L0, L0.u), c->metrics_old, L0.g.P * L0.g.nz, c->d_metrics, out, c->s));
-    if (c->o.world > 1) {
+    WaitScope w(c);  // the all-reduce and the read-back after it wait for the peers
+    if (c->multi()) {
         if (c->lb)
             TRY(lb_allreduce(c, out, 3));
         else
@@ -2370,6 +2442,7 @@ int mgp_residual_norm(mgp_ctx* c, int level, double* rnorm, double* fnorm)
     double* out = c->d_rn + need - 2;
     HIP_TRY(c, mgp::launch_residual_norm(c->rk, c->o.dim, c->ui(L, L.u), c->ui(L, L.f), L.g, level_h(c, level),
                                          coarse_coef(c->o.coarse_bc, level), c->d_rn, out, c->s));
+    WaitScope w(c);  // the all-reduce and the read-back after it wait for the peers
     if (L.p.dist) {
         if (c->lb)
             TRY(lb_allreduce(c, out, 2));
@@ -2437,6 +2510,15 @@ int mgp_cg_solve(mgp_ctx* c, double epsilon, int32_t maxiter, void* x_out, int m
     if (e != hipSuccess) return c->fail(MGP_ERR_HIP, "mgp_cg_solve: %s", hipGetErrorString(e));
     if (iters) *iters = a.iters;
     if (err) *err = a.err;
+    return MGP_OK;
+}
+
+int mgp_set_debug(mgp_ctx* c, int mode)
+{
+    if (!c || mode < 0 || mode > 1) return MGP_ERR_ARG;
+    TRY(sync_and_check(c));
+    if (mode && !c->d_dbg) HIP_TRY(c, hipMalloc(&c->d_dbg, sizeof(int)));
+    c->debug = mode;
     return MGP_OK;
 }
 
@@ -2619,24 +2701,38 @@ static int group_run(mgp_group* g, const std::function<int(mgp_ctx*, int)>& fn)
             }
             cv.notify_all();
         });
+    bool aborted = false;
     {
         // after a failure, the others either finish (work that needs no peer) or block on the failed rank in an
-        // exchange or collective (or in the stream synchronisation after one): abort only in that case, checked
-        // every 2 s (a healthy rank doing long local work is not cut off)
+        // exchange or collective (or in the stream synchronisation / read-back after one, all counted in
+        // `waiting`): abort as soon as one of them waits, checked every 0.5 s, and in any case after
+        // kAbortAfter (a peer-dependent wait the count misses must not hang the group)
+        constexpr auto kAbortAfter = std::chrono::seconds(20);
         std::unique_lock<std::mutex> lk(m);
         cv.wait(lk, [&] { return done == n || failed; });
-        while (done < n && !cv.wait_for(lk, std::chrono::seconds(2), [&] { return done == n; })) {
-            bool blocked = false;
+        const auto t_fail = std::chrono::steady_clock::now();
+        while (done < n && !cv.wait_for(lk, std::chrono::milliseconds(500), [&] { return done == n; })) {
+            bool blocked = std::chrono::steady_clock::now() - t_fail > kAbortAfter;
             for (int r = 0; r < n; ++r)
                 blocked = blocked || (r != first && g->ranks[(size_t)r]->waiting.load() > 0);
             if (blocked) {
                 lk.unlock();
                 group_abort(g);
+                aborted = true;
                 break;
             }
         }
     }
     for (auto& t : th) t.join();
+    // A rank failed and the others returned: their call sequences on the communicators no longer match (the
+    // failed rank skipped what the others issued), so the group is unusable and its communicators are aborted
+    // now (one rank included: ncclCommAbort then runs on the world-1 RCCL group).  Only argument errors of every
+    // rank alike, found before any peer call, leave the group usable.
+    if (first >= 0 && !aborted) {
+        bool all_arg = true;
+        for (int r = 0; r < n; ++r) all_arg = all_arg && rc[(size_t)r] == MGP_ERR_ARG;
+        if (!all_arg) group_abort(g);
+    }
     if (g->stop.load() && !g->lb)
         for (auto* c : g->ranks) c->comm = c->xcomm = nullptr;  // freed by ncclCommAbort
     if (first >= 0) {
@@ -2738,7 +2834,7 @@ int mgp_group_create(mgp_group** out, const mgp_opts* o, int ngpu, const int* de
     std::vector<ncclComm_t> comms((size_t)ngpu, nullptr), xcomms((size_t)ngpu, nullptr);
     if (ngpu > 1 && same) {
         mgp_loopback_create(&g->lb, ngpu);
-    } else if (ngpu > 1) {
+    } else if (ngpu > 1 || env_rccl1(ro)) {  // (one device with MGP_TRANSPORT=rccl: a one-rank RCCL group)
         const char* rc_msg = group_comms(g->dev, comms, xcomms);
         if (rc_msg) {
             g_create_error = rc_msg;

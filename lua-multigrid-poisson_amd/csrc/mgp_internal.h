@@ -103,6 +103,8 @@ hipError_t launch_sqdiff_sum(int rb, const void* a, const void* b, int64_t n, do
                              hipStream_t s, int* ctr = nullptr);
 // out[0..2] = {sum |1 - psi/psiOld| over nonzero entries, their count, sum (psi - psiOld)^2}
 // over n elements; partials needs 3 * kSumBlocks doubles.
+// Debugging check (cpu-raw.lua:126-140, gpu.lua:269-284): *first = min(*first, id) if p[0, n) holds a NaN or inf.
+hipError_t launch_nonfinite_check(int rb, const void* p, int64_t n, int id, int* first, hipStream_t s);
 hipError_t launch_metrics(int rb, const void* psi, const void* old, int64_t n, double* partials, double* out,
                           hipStream_t s);
 // out[0] = sum (f - A u)^2, out[1] = sum f^2 over the level's cells (fp64, wave-level then fixed-order
@@ -119,7 +121,22 @@ hipError_t launch_sum_partials(const double* partials, int n, double* out, hipSt
 //   pre : dst = nu1 sweeps of src; R (coarse packed, Geo gc) = restrict(residual(dst))
 //   post: dst = nu2 sweeps of (src + P V); with partials, sum (dst - dst_before)^2 per workgroup
 // src and dst are different buffers (tiles read each other's halos of src).
+// Tile settings of the temporally blocked phases (k_zs / k_ys), read from the environment ONCE, when a context is
+// created, and kept in it: the sizes planned then (z-chunks, the err partials buffer, mgp_plan's engines) are the
+// ones every later launch uses (they used to be re-read per launch).
+struct FusedTuning {
+    bool wide = true;    // MGP_ZS_WIDE=0: POST on the narrow 64 x 32 tile
+    int ys_half = -1;    // MGP_YS_HALF: 2D segment width rule (-1 auto, 0 full, 1 half)
+    int ys_rows = 32;    // MGP_YS_ROWS: 2D rows per workgroup chunk
+    int64_t wgs = 256;   // MGP_ZS_WGS: z-chunks are halved until a launch has this many workgroups
+    // tile order of launches of > 512 workgroups: px | py << 8 patches of tiles per XCD band, 0 = tile rows
+    // (MGP_ZS_PATCH=px,py sets both phases, MGP_ZS_PATCH_PRE / MGP_ZS_PATCH_POST one; "0" off)
+    int patch_pre = 0, patch_post = 0;
+};
+FusedTuning fused_tuning_from_env();
+
 struct FusedArgs {
+    FusedTuning tu;
     bool pre;
     int linear;  // POST: linear prolongation; PRE: 1 = no restriction (both colours stored, full weighting after)
     const void* src;
@@ -134,12 +151,12 @@ struct FusedArgs {
     int zc;
     int ghost;  // readable ghost planes per side of src / f / dst
 };
-bool fused_supported(int rb, int dim, int ns, const Geo& g);
+bool fused_supported(int rb, int dim, int ns, const Geo& g, const FusedTuning& tu);
 // Raise the dynamic-LDS limit of the fused and tail kernels (once per context, before any capture).
 hipError_t prepare_kernels(int rb);
 // clz: the level's operator has no boundary modification (cl == 0): PRE's tile may differ otherwise
-int fused_zc(int rb, const Geo& g, bool pre, bool clz = true);
-int fused_blocks(int rb, const Geo& g, int zc, bool clz = true);
+int fused_zc(int rb, const Geo& g, bool pre, bool clz, const FusedTuning& tu);
+int fused_blocks(int rb, const Geo& g, int zc, bool clz, const FusedTuning& tu);
 hipError_t launch_fused(int rb, const FusedArgs& a, hipStream_t s);
 
 // Tiled smoothing phases of a small replicated red/black level (k_blk: one launch per phase, the 3D

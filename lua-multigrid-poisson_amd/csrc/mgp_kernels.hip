@@ -4491,16 +4491,38 @@ hipError_t launch_prolong_correct(int rb, int dim, int linear, void* u, const vo
 
 // ---- fused smoothing phases ----
 
-// Tile order of a launch with more tiles than run at once (MGP_ZS_PATCH = "px,py", "0" off, read per call):
-// consecutive tiles of an XCD's band as px x py patches instead of whole tile rows, so that the y neighbours
-// whose halo rows a tile reads stream through z at the same time.  Returns px | py << 8, or 0.
-static int zs_patch(int tiles_x, int tiles_y, unsigned nb)
+static int parse_patch(const char* v, int dflt)
 {
-    const char* v = std::getenv("MGP_ZS_PATCH");
     int px = 0, py = 0;
-    if (!v || std::sscanf(v, "%d,%d", &px, &py) != 2) return 0;
-    if (px < 1 || py < 1 || px > 255 || py > 255 || tiles_x % px || tiles_y % py || nb <= 512) return 0;
+    if (!v) return dflt;
+    if (std::sscanf(v, "%d,%d", &px, &py) != 2 || px < 1 || py < 1 || px > 255 || py > 255) return 0;
     return px | (py << 8);
+}
+
+FusedTuning fused_tuning_from_env()
+{
+    FusedTuning t;
+    if (const char* v = std::getenv("MGP_ZS_WIDE")) t.wide = std::atoi(v) != 0;
+    if (const char* v = std::getenv("MGP_YS_HALF")) t.ys_half = std::atoi(v);
+    if (const char* v = std::getenv("MGP_YS_ROWS")) {
+        const int r = std::atoi(v);
+        t.ys_rows = r >= 8 && (r & 1) == 0 ? r : 32;
+    }
+    if (const char* v = std::getenv("MGP_ZS_WGS")) t.wgs = std::max<int64_t>(1, std::atoll(v));
+    const int both = parse_patch(std::getenv("MGP_ZS_PATCH"), 0);
+    t.patch_pre = parse_patch(std::getenv("MGP_ZS_PATCH_PRE"), both);
+    t.patch_post = parse_patch(std::getenv("MGP_ZS_PATCH_POST"), both);
+    return t;
+}
+
+// Tile order of a launch with more tiles than run at once (FusedTuning::patch_pre / patch_post): consecutive
+// tiles of an XCD's band as px x py patches instead of whole tile rows, so that the y neighbours whose halo
+// rows a tile reads stream through z at the same time.  Returns px | py << 8, or 0 (tile rows).
+static int zs_patch(int patch, int tiles_x, int tiles_y, unsigned nb)
+{
+    const int px = patch & 255, py = patch >> 8;
+    if (!patch || tiles_x % px || tiles_y % py || nb <= 512) return 0;
+    return patch;
 }
 
 template <typename T, bool PRE, int LINEAR, bool ERR, bool CLZ, bool WIDE = false>
@@ -4513,23 +4535,23 @@ static hipError_t zs_launch(const FusedArgs& a, hipStream_t s)
                                                                            (const T*)(a.old ? a.old : a.dst), (T*)a.R,
                                                                            (const T*)a.V, a.partials, a.g, a.gc,
                                                                            op, (T)a.clc, a.zc, a.ghost,
-                                                                           zs_patch(a.g.nx / S::TX, a.g.ny / S::TY, nb));
+                                                                           zs_patch(PRE ? a.tu.patch_pre : a.tu.patch_post,
+                                                                                    a.g.nx / S::TX, a.g.ny / S::TY, nb));
     return hipGetLastError();
 }
 
 // POST's wide tile (ZsTile::TXPOST_W): fp32, cl = 0 (or any level with ZS_WIDE_CL: on the 256^3 level of the
-// 512^3 box measured +10-16 us per cycle, off), a box it divides, MGP_ZS_WIDE not 0 (read per call)
+// 512^3 box measured +10-16 us per cycle, off), a box it divides, FusedTuning::wide
 #ifndef ZS_WIDE_CL
 #define ZS_WIDE_CL 0
 #endif
-static bool zs_wide(int rb, const Geo& g, bool clz)
+static bool zs_wide(int rb, const Geo& g, bool clz, const FusedTuning& tu)
 {
-    const char* v = std::getenv("MGP_ZS_WIDE");
-    if (rb != 4 || (!clz && !ZS_WIDE_CL) || (v && std::atoi(v) == 0)) return false;
+    if (rb != 4 || (!clz && !ZS_WIDE_CL) || !tu.wide) return false;
     return g.nx % ZsTile<float>::TXPOST_W == 0 && g.ny % ZsTile<float>::TYPOST_W == 0;
 }
 
-static int ys_tx(int rb, const Geo& g);
+static int ys_tx(int rb, const Geo& g, const FusedTuning& tu);
 
 template <typename T, bool PRE, int LINEAR, bool ERR, bool CLZ, int TXV>
 static hipError_t ys_launch_tx(const FusedArgs& a, hipStream_t s)
@@ -4547,7 +4569,7 @@ template <typename T, bool PRE, int LINEAR, bool ERR, bool CLZ>
 static hipError_t ys_launch(const FusedArgs& a, hipStream_t s)
 {
     constexpr int F = ys_tx_full<T>();
-    return ys_tx(sizeof(T), a.g) == F ? ys_launch_tx<T, PRE, LINEAR, ERR, CLZ, F>(a, s)
+    return ys_tx(sizeof(T), a.g, a.tu) == F ? ys_launch_tx<T, PRE, LINEAR, ERR, CLZ, F>(a, s)
                                       : ys_launch_tx<T, PRE, LINEAR, ERR, CLZ, F / 2>(a, s);
 }
 
@@ -4571,14 +4593,14 @@ static hipError_t fused_dispatch(const FusedArgs& a, hipStream_t s)
         return a.linear ? zs_launch<T, true, 1, true, CLZ>(a, s) : zs_launch<T, true, 0, true, CLZ>(a, s);
     if (a.pre) return a.linear ? zs_launch<T, true, 1, false, CLZ>(a, s) : zs_launch<T, true, 0, false, CLZ>(a, s);
     if constexpr (std::is_same<T, float>::value && CLZ) {
-        if (zs_wide(4, a.g, true)) {
+        if (zs_wide(4, a.g, true, a.tu)) {
             if (a.linear)
                 return err ? zs_launch<T, false, 1, true, CLZ, true>(a, s) : zs_launch<T, false, 1, false, CLZ, true>(a, s);
             return err ? zs_launch<T, false, 0, true, CLZ, true>(a, s) : zs_launch<T, false, 0, false, CLZ, true>(a, s);
         }
     }
     if constexpr (std::is_same<T, float>::value && !CLZ && ZS_WIDE_CL) {
-        if (!err && zs_wide(4, a.g, false))
+        if (!err && zs_wide(4, a.g, false, a.tu))
             return a.linear ? zs_launch<T, false, 1, false, CLZ, true>(a, s) : zs_launch<T, false, 0, false, CLZ, true>(a, s);
     }
     if (a.linear) return err ? zs_launch<T, false, 1, true, CLZ>(a, s) : zs_launch<T, false, 1, false, CLZ>(a, s);
@@ -4605,69 +4627,55 @@ static void zs_tile(int rb, int& tx, int& ty, int pre = -1, bool clz = true, boo
     }
 }
 
-// 2D (k_ys): rows per z-chunk of a workgroup (MGP_YS_ROWS, default 32; even)
-static int ys_rows(const Geo& g)
+// 2D (k_ys): rows per z-chunk of a workgroup (FusedTuning::ys_rows, default 32; even)
+static int ys_rows(const Geo& g, const FusedTuning& tu)
 {
-    // read per call (plan time and launch), so that a process can build contexts under different settings
-    const int rows = [] {
-        const char* v = std::getenv("MGP_YS_ROWS");
-        const int r = v ? std::atoi(v) : 32;
-        return r >= 8 && (r & 1) == 0 ? r : 32;
-    }();
-    int r = rows;
+    int r = tu.ys_rows;
     while (r > 8 && g.ny % r != 0) r /= 2;
     return r;
 }
 
 // segment width of a 2D level: the full width, or half of it when the full width gives fewer than
-// MGP_ZS_WGS (default 256) workgroups (MGP_YS_HALF: -1 that rule, 0 never, 1 always)
-static int ys_tx(int rb, const Geo& g)
+// FusedTuning::wgs (default 256) workgroups (FusedTuning::ys_half: -1 that rule, 0 never, 1 always)
+static int ys_tx(int rb, const Geo& g, const FusedTuning& tu)
 {
-    const int mode = [] {
-        const char* v = std::getenv("MGP_YS_HALF");
-        return v ? std::atoi(v) : -1;
-    }();
-    const int64_t target = [] {
-        const char* v = std::getenv("MGP_ZS_WGS");
-        return v ? std::atoll(v) : (int64_t)256;
-    }();
+    const int mode = tu.ys_half;
+    const int64_t target = tu.wgs;
     const int full = rb == 4 ? ys_tx_full<float>() : ys_tx_full<double>();
     if (mode == 0 || g.nx % (full / 2) != 0) return full;
     if (mode == 1 || g.nx % full != 0) return full / 2;
-    return (int64_t)(g.nx / full) * (g.ny / ys_rows(g)) < target ? full / 2 : full;
+    return (int64_t)(g.nx / full) * (g.ny / ys_rows(g, tu)) < target ? full / 2 : full;
 }
 
-bool fused_supported(int rb, int dim, int ns, const Geo& g)
+bool fused_supported(int rb, int dim, int ns, const Geo& g, const FusedTuning& tu)
 {
-    if (dim == 2) return ns == 2 && g.nz == 1 && g.nx % ys_tx(rb, g) == 0 && g.ny >= 16 && g.ny % ys_rows(g) == 0;
+    if (dim == 2)
+        return ns == 2 && g.nz == 1 && g.nx % ys_tx(rb, g, tu) == 0 && g.ny >= 16 && g.ny % ys_rows(g, tu) == 0;
     if (dim != 3 || ns != 2) return false;
     int TX, TY;
     zs_tile(rb, TX, TY);
     return g.nx % TX == 0 && g.ny % TY == 0 && g.nz >= 16 && (g.nz & 1) == 0;
 }
 
-// planes per workgroup: halve the z-chunk until there are >= MGP_ZS_WGS (default 256, one per CU)
+// planes per workgroup: halve the z-chunk until there are >= FusedTuning::wgs (default 256, one per CU)
 // workgroups or a chunk would drop below 16 planes
-int fused_zc(int rb, const Geo& g, bool pre, bool clz)
+int fused_zc(int rb, const Geo& g, bool pre, bool clz, const FusedTuning& tu)
 {
-    if (g.gnz == 1 && g.nz == 1) return ys_rows(g);  // 2D: rows per chunk
+    if (g.gnz == 1 && g.nz == 1) return ys_rows(g, tu);  // 2D: rows per chunk
     int TX, TY;
-    zs_tile(rb, TX, TY, pre ? 1 : 0, clz, !pre && zs_wide(rb, g, clz));
-    static const int64_t target = [] {
-        const char* v = std::getenv("MGP_ZS_WGS");
-        return v ? std::atoll(v) : (int64_t)256;
-    }();
+    zs_tile(rb, TX, TY, pre ? 1 : 0, clz, !pre && zs_wide(rb, g, clz, tu));
+    const int64_t target = tu.wgs;
     const int64_t tiles = (int64_t)(g.nx / TX) * (g.ny / TY);
     int64_t chunks = 1;
     while (tiles * chunks < target && g.nz / (chunks * 2) >= 16) chunks *= 2;
     return (int)(g.nz / chunks);
 }
 
-int fused_blocks(int rb, const Geo& g, int zc, bool clz)  // POST's workgroups (one err partial each)
+int fused_blocks(int rb, const Geo& g, int zc, bool clz, const FusedTuning& tu)  // POST's workgroups (err partials)
 {
-    if (g.gnz == 1 && g.nz == 1) return (g.nx / ys_tx(rb, g)) * (g.ny / zc);
+    if (g.gnz == 1 && g.nz == 1) return (g.nx / ys_tx(rb, g, tu)) * (g.ny / zc);
     int TX, TY;
-    zs_tile(rb, TX, TY, 0, clz, zs_wide(rb, g, clz));
+    zs_tile(rb, TX, TY, 0, clz, zs_wide(rb, g, clz, tu));
     return (int)((int64_t)(g.nx / TX) * (g.ny / TY) * (g.nz / zc));
 }
 
@@ -4942,6 +4950,41 @@ hipError_t launch_metrics(int rb, const void* psi, const void* old, int64_t n, d
 {
     MGP_REAL(rb, (k_metrics_partial<T><<<kSumBlocks, kBlock, 0, s>>>((const T*)psi, (const T*)old, n, partials)));
     for (int q = 0; q < 3; ++q) k_sum_n<<<1, 1024, 0, s>>>(partials + q * kSumBlocks, kSumBlocks, out + q);
+    return hipGetLastError();
+}
+
+// The reference's debugging check (cpu-raw.lua:135-139, gpu.lua:279-283: error "found a nan" when a dumped grid
+// holds a non-finite cell): any cell of p[0, n) with an all-ones exponent lowers *first to `id`, the check's
+// position in the cycle, so the host names the first phase that produced one.  16-byte loads, grid-stride.
+template <typename T>
+__global__ __launch_bounds__(kBlock) void k_nonfinite(const T* __restrict__ p, int64_t n, int id, int* first, bool vec)
+{
+    using U = typename std::conditional<sizeof(T) == 8, uint64_t, uint32_t>::type;
+    constexpr U kExp = sizeof(T) == 8 ? (U)0x7ff0000000000000ull : (U)0x7f800000u;
+    constexpr int V = 16 / sizeof(T);
+    const int64_t nv = vec ? n / V : 0;  // (vec: p is 16-byte aligned)
+    const int64_t stride = (int64_t)gridDim.x * kBlock;
+    bool bad = false;
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < nv; i += stride) {
+        const uint4 q = reinterpret_cast<const uint4*>(p)[i];
+        const U* w = reinterpret_cast<const U*>(&q);
+#pragma unroll
+        for (int k = 0; k < V; ++k) bad = bad || (w[k] & kExp) == kExp;
+    }
+    for (int64_t i = nv * V + (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
+        U w;
+        __builtin_memcpy(&w, p + i, sizeof(U));
+        bad = bad || (w & kExp) == kExp;
+    }
+    if (bad) atomicMin(first, id);
+}
+
+hipError_t launch_nonfinite_check(int rb, const void* p, int64_t n, int id, int* first, hipStream_t s)
+{
+    if (n <= 0) return hipSuccess;
+    const int64_t want = (n / (16 / (rb == 8 ? 8 : 4)) + kBlock - 1) / kBlock;
+    const unsigned nb = (unsigned)std::max<int64_t>(1, std::min<int64_t>(want, 2048));
+    MGP_REAL(rb, (k_nonfinite<T><<<nb, kBlock, 0, s>>>((const T*)p, n, id, first, ((uintptr_t)p & 15) == 0)));
     return hipGetLastError();
 }
 

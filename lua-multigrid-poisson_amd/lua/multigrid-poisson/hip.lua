@@ -87,6 +87,7 @@ int         mgp_set_coarse_level(mgp_ctx* c, int64_t size);
 typedef int (*mgp_coarse_fn)(void* user, double h, void* u, const void* f, int64_t size);
 int         mgp_set_coarse_handoff(mgp_ctx* c, int64_t size, mgp_coarse_fn fn, void* user);
 int         mgp_metrics(mgp_ctx* c, double* rel_err, int64_t* count, double* frob);
+int         mgp_set_debug(mgp_ctx* c, int mode);
 int         mgp_residual_norm(mgp_ctx* c, int level, double* rnorm, double* fnorm);
 int         mgp_group_create(mgp_group** out, const mgp_opts* o, int ngpu, const int* devices);
 mgp_ctx*    mgp_group_rank(mgp_group* g, int rank);
@@ -166,6 +167,8 @@ end
 
 -- class defaults (cpu.lua:18-22, cpu-raw.lua:121-124)
 MultigridHIP.debug = false
+-- cpu-raw.lua:121 / gpu.lua:21: check every phase's output for non-finite cells ("found a nan", cpu-raw.lua:135-139)
+MultigridHIP.debugging = false
 MultigridHIP.smooth = 7
 MultigridHIP.epsilon = 1e-10
 MultigridHIP.accuracy = 1e-10
@@ -405,6 +408,7 @@ end
 
 -- cpu-raw.lua:239-258 / gpu.lua:348-373: two outer iterations
 function MultigridHIP:run()
+	if not rawget(self, 'group') then check(lib.mgp_set_debug(self.ctx, self.debugging and 1 or 0), self.ctx) end
 	print('#iter', 'err')
 	for iter = 1, 2 do
 		local err = self:step()

@@ -119,6 +119,7 @@ SIGNATURES = {
     "mgp_cg_solve": (ctypes.c_int, [_vp, _dbl, _i32, _vp, ctypes.c_int, _P(_i32), _P(_dbl), _P(_dbl)]),
     "mgp_set_coarse_handoff": (ctypes.c_int, [_vp, _i64, COARSE_FN, _vp]),
     "mgp_timing": (ctypes.c_int, [_vp, ctypes.c_int]),
+    "mgp_set_debug": (ctypes.c_int, [_vp, ctypes.c_int]),
     "mgp_timing_read": (ctypes.c_int, [_vp, ctypes.c_int, _P(_dbl), _P(_i64), _P(_dbl)]),
     "mgp_comm_log": (ctypes.c_int, [_vp, _P(_i64), ctypes.c_int, ctypes.c_int]),
     "mgp_plan_comm": (ctypes.c_int, [_P(MGPOpts), _i32, _P(_i64), ctypes.c_int]),

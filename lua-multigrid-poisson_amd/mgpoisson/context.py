@@ -266,6 +266,12 @@ class Context:
     def sync(self):
         self._chk(L.lib.mgp_sync(self._h))
 
+    def set_debug(self, mode=1):
+        """The reference's debugging check (cpu-raw.lua:126-140, gpu.lua:269-284): after every phase of a cycle its
+        output is scanned on the device, and cycle() / cycles() raise MGPError naming the first phase that produced
+        a NaN or inf ("found a nan").  mode 0 turns it off."""
+        self._chk(L.lib.mgp_set_debug(self._h, int(mode)))
+
     # -- timing --
     def timing(self, enable=True):
         self._chk(L.lib.mgp_timing(self._h, 1 if enable else 0))

@@ -37,7 +37,10 @@ import numpy as np
 COLUMNS = {
     # column name -> (real, build options); 'hip' is the reference configuration on the GPU
     "hip": ("double", {}),
-    "hip-f32": ("float", {}),
+    # gpu.lua's float column (test/test.lua's 'gpu'): every operation in float (gpu.lua:32); cpu-raw.lua's float
+    # arithmetic (double expressions over float images) is the 'hip-raw-f32' column
+    "hip-f32": ("float", dict(arith="real")),
+    "hip-raw-f32": ("float", dict(arith="double")),
     "hip-rbgs": ("double", dict(smoother="rbgs", nu1=2, nu2=2, prolong="linear", coarse_bc="consistent")),
 }
 # caller-supplied columns: name -> factory(size, real, cpudepth) returning an object with run()

@@ -15,12 +15,16 @@ the LuaJIT-FFI module a Lua user would load is lua/multigrid-poisson/hip.lua (IN
 """
 from __future__ import annotations
 
+import logging
 import math
 
 import numpy as np
 
 from . import _lib as L
+from ._lib import MGPError
 from .context import Context, make_opts
+
+log = logging.getLogger(__name__)
 
 
 class _Smoother(str):
@@ -259,8 +263,8 @@ class MultigridHIPRaw(_RawFields):
         if cpuDepth:  # cpu-gpu.lua:61: switch to the coarse engine at size 2^cpuDepth when it fits
             try:
                 self._ctx.set_coarse_level(1 << int(cpuDepth))
-            except Exception:  # noqa: BLE001 - the default switch stays
-                pass
+            except MGPError as e:  # the default switch stays (cpu-raw arithmetic has no coarse engine)
+                log.info("cpuDepth %s not applied: %s", cpuDepth, e)
         self._ctx.init_point_charge()  # call2D(initCells) (cpu-raw.lua:173)
         self.quiet = False
 
@@ -283,7 +287,10 @@ class MultigridHIPRaw(_RawFields):
             self._ctx.two_grid_ptr(h, int(u), int(f), L_, L.MEM_DEVICE if mem is None else mem)
 
     def run(self, iters: int = 2):
-        """cpu-raw.lua:239-258 / gpu.lua:348-373 (2 outer iterations, printed)."""
+        """cpu-raw.lua:239-258 / gpu.lua:348-373 (2 outer iterations, printed).  With ``debugging`` set (class or
+        instance field, cpu-raw.lua:121 / gpu.lua:21) every phase's output is checked for non-finite cells and the
+        first one raises "found a nan" (cpu-raw.lua:135-139, gpu.lua:279-283)."""
+        self._ctx.set_debug(1 if self.debugging else 0)
         if not self.quiet:
             print("#iter", "err")
         errs = []

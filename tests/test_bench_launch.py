@@ -55,7 +55,7 @@ def test_strong_scaling_launch_plan_config3():
 
 
 def test_north_star_lines_planned_at_8_ranks():
-    """With N >= 4 the default run adds BASELINE configs[3] (2048^3 V) and configs[4] (4096^3 F) to the line;
+    """At 8 ranks the default run adds BASELINE configs[3] (2048^3 V) and configs[4] (4096^3 F) to the line;
     --plan-only lists each workload's per-cycle RCCL calls and bytes per rank (mgp_plan_comm: the library's own
     cycle logic, run on the host with every device call skipped)."""
     d = _launch(8)
@@ -71,6 +71,21 @@ def test_north_star_lines_planned_at_8_ranks():
     assert c3["side_stream_exchanges"] == 2  # levels 0 and 1 run k_zs on 2048 x 2048 x 256 slabs
     assert c4["allgathers"] > 1 and c4["calls"] > c3["calls"]  # the F-cycle revisits the agglomerated levels
     assert c4["halo_MB_per_neighbour"] > c3["halo_MB_per_neighbour"] > weak["halo_MB_per_neighbour"]
+
+
+@pytest.mark.parametrize("n", [1, 2])
+def test_north_star_lines_planned_at_1_and_2_ranks(n):
+    """the driver's 1- and 2-GPU runs carry the configs[3] whole-box line too (2048^3 fits one
+    GPU: ~160 GB with u, f, t, psiOld and the hierarchy), so the 1/2/4/8 runs give the north star's strong-scaling
+    curve; configs[4] (4096^3) does not fit fewer than 4 GPUs and is listed as skipped.  N = 1 adds the fp64 line."""
+    d = _launch(n)
+    ns = d["north_star_lines"]
+    assert set(ns) == {"configs[3]", "configs[4]"}
+    assert ns["configs[3]"]["fits"] and not ns["configs[4]"]["fits"]
+    assert ns["configs[3]"]["global_box"] == [2048, 2048, 2048]
+    assert d.get("fp64_line", False) == (n == 1)
+    if n == 2:
+        assert ns["configs[3]"]["comm_per_cycle"]["allreduces"] == 1
 
 
 def test_plan_comm_is_identical_on_every_rank():

@@ -125,3 +125,86 @@ def test_config5_rank_slab_residual_norm_independent():
         ctx.close()
     assert fn == 1e6
     assert abs(rn - np.sqrt(tot)) <= 1e-12 * rn, (rn, np.sqrt(tot))
+
+
+_C4 = {}
+
+
+def _config4_single_domain():
+    """configs[4]'s rank-slab box (4096 x 4096 x 512 fp32, RB-GS 2+2 F-cycle) as one domain, computed once."""
+    if not _C4:
+        ref = _ctx(dim=3, n=(4096, 4096, 512), real="float", cycle="F", **NS)
+        try:
+            assert ref.levels[0]["engine"] == "zs"
+            ref.init_point_charge()
+            _C4["errs"] = ref.cycles(2)
+            _C4["stats"] = ref.field_stats()
+            _C4["rn"] = ref.residual_norm()
+        finally:
+            ref.close()  # ~120 GB: one decomposition on the device at a time
+    return _C4
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("world", [2, 8])
+def test_config4_box_decomposition_equals_single_domain(world):
+    """BASELINE configs[4]'s decomposition at its own plane size.  The 4096 x 4096 x 512 box
+    (one rank's share of 4096^3 over 8 GPUs) split into `world` z-slabs of 4096^2 planes (256 or 64 per rank)
+    through the loopback transport, F-cycle: halo exchanges of 4096^2 planes around k_zs slabs, deep-halo
+    smoothing on the distributed levels below, and the agglomeration all-gather that the F-cycle revisits;
+    against the same box as one domain (the level hand-off model: cpu-gpu.lua:17-52)."""
+    box, cycles = (4096, 4096, 512), 2
+    cfg = dict(real="float", cycle="F", **NS)
+    ref = _config4_single_domain()
+    assert np.all(np.isfinite(ref["errs"])) and ref["errs"][1] < ref["errs"][0]
+
+    mg = _mg()
+    lb = mg.Loopback(world)
+    res, errors = [None] * world, []
+
+    def rank_main(r):
+        try:
+            ctx = mg.Context(mg.make_opts(dim=3, n=box, rank=r, world=world, device=0, comm_id=b"\0" * 128, **cfg),
+                             loopback=lb)
+            try:
+                assert ctx.levels[0]["nz_local"] == box[2] // world and ctx.levels[0]["engine"] == "zs"
+                ctx.init_point_charge()
+                ctx.comm_log(reset=True)
+                ctx.timing(True)
+                errs = ctx.cycles(cycles)
+                t = ctx.timing_read()
+                ctx.timing(False)
+                log = ctx.comm_log()
+                ctx._read_levels()
+                res[r] = dict(stats=ctx.field_stats(), errs=errs, rn=ctx.residual_norm(), t=t, log=log,
+                              levels=[dict(lv) for lv in ctx.levels])
+            finally:
+                ctx.close()
+        except Exception as e:  # noqa: BLE001 - surfaced below
+            errors.append((r, repr(e)))
+
+    th = [threading.Thread(target=rank_main, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=1200)
+    lb.close()
+    assert not errors, errors
+    assert sum(res[r]["stats"][0] for r in range(world)) & M64 == ref["stats"][0], "psi fingerprints differ"
+    assert sum(res[r]["stats"][1] for r in range(world)) == pytest.approx(ref["stats"][1], rel=1e-12)
+    for r in range(world):
+        np.testing.assert_allclose(res[r]["errs"], ref["errs"], rtol=1e-12, atol=0)
+        np.testing.assert_allclose(res[r]["rn"], ref["rn"], rtol=1e-12, atol=0)
+        assert res[r]["log"] == res[0]["log"]  # the same call order on every rank
+    r0 = res[0]
+    # k_zs ran on the slabs: both phases timed on level 0 every visit (an F-cycle visits level 0 once per cycle)
+    assert r0["t"]["fused_pre"][1] >= cycles and r0["t"]["fused_post"][1] >= cycles
+    lv = r0["levels"]
+    # at least one distributed level below the finest smoothed per piece with deep halos, which exchanged
+    assert any(l > 0 and v["distributed"] and v["engine"] == "piece" and v["exchanges"] > 0 for l, v in enumerate(lv))
+    # the 4096^2 planes of level 0 were exchanged
+    assert lv[0]["distributed"] and lv[0]["exchanges"] > 0 and lv[0]["nx"] == 4096
+    # the agglomeration all-gather, revisited by the F-cycle (more than once per cycle)
+    n_ag = sum(1 for c in r0["log"] if c[0] == "allgather")
+    assert n_ag > cycles, n_ag
+    assert not lv[-1]["distributed"]

@@ -1,0 +1,80 @@
+"""GPU: the reference's debugging check (VERDICT r4 missing 6).
+
+MultigridCPURaw.debugging / MultigridGPU.debugging dump every grid after every sweep and piece of twoGrid and
+raise "found a nan" on a non-finite cell (cpu-raw.lua:126-140, gpu.lua:269-284).  mgp_set_debug(ctx, 1) scans the
+output of every phase of every level on the device (k_nonfinite) and mgp_cycle fails naming the first phase that
+produced a NaN / inf.  Bar: a clean run is unchanged bit for bit and raises nothing, on every engine; a NaN planted
+in f is reported at the first phase that reads it (level 0's pre-smoothing); without the check the cycle returns a
+non-finite err, the reference's silent outer-loop break (cpu.lua:214)."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+NS = dict(smoother="rbgs", nu1=2, nu2=2, prolong="linear", coarse_bc="consistent")
+CASES = [
+    (dict(dim=3, n=(64, 64, 64), real="float", **NS), None),
+    (dict(dim=3, n=(128, 128, 128), real="float", cycle="F", **NS), "65536"),  # k_zs levels
+    (dict(dim=2, n=(256, 256, 1), real="double", **NS), None),
+    (dict(dim=2, n=(64, 64, 1), real="double"), None),  # the cpu.lua reference configuration (Jacobi 7+7)
+]
+
+
+def _mg():
+    import mgpoisson
+
+    return mgpoisson
+
+
+@pytest.mark.parametrize("kw,fused", CASES, ids=["3d", "3d-zs-F", "2d-rbgs", "2d-jacobi"])
+def test_debug_check_clean_run_is_unchanged(kw, fused, monkeypatch):
+    mg = _mg()
+    if fused:
+        monkeypatch.setenv("MGP_FUSED_MIN_CELLS", fused)
+    ref = mg.Context(mg.make_opts(**kw))
+    ref.init_point_charge()
+    e_ref = ref.cycles(2)
+    ctx = mg.Context(mg.make_opts(**kw))
+    if fused:
+        assert ctx.levels[0]["engine"] == "zs"
+    ctx.init_point_charge()
+    ctx.set_debug(1)
+    e = ctx.cycles(2)
+    assert np.array_equal(ctx.get_psi(), ref.get_psi())
+    np.testing.assert_array_equal(e, e_ref)
+    ctx.set_debug(0)
+    ctx.cycle()
+
+
+@pytest.mark.parametrize("kw,fused", CASES, ids=["3d", "3d-zs-F", "2d-rbgs", "2d-jacobi"])
+def test_debug_check_names_the_first_phase_with_a_nan(kw, fused, monkeypatch):
+    mg = _mg()
+    if fused:
+        monkeypatch.setenv("MGP_FUSED_MIN_CELLS", fused)
+    ctx = mg.Context(mg.make_opts(**kw))
+    ctx.init_point_charge()
+    f = ctx.get_f()
+    f.flat[f.size // 3] = np.nan
+    ctx.set_f(f)
+    assert not np.isfinite(ctx.cycle())  # unchecked: a non-finite err, the outer loop's break (cpu.lua:214)
+    ctx.init_point_charge()
+    ctx.set_f(f)
+    ctx.set_debug(1)
+    with pytest.raises(mg.MGPError, match=r"found a nan .*cycle 1, level 0 .*pre-smoothing"):
+        ctx.cycles(2)
+
+
+def test_positional_protocol_debugging_field():
+    """MultigridHIPRaw(n, real).debugging = true (cpu-raw.lua:121) makes run() raise on the first NaN."""
+    mg = _mg()
+    s = mg.MultigridHIPRaw(16, "double")
+    s.quiet = True
+    f = s.ctx.get_f()
+    f[3, 5] = np.inf
+    s.ctx.set_f(f)
+    s.debugging = True
+    with pytest.raises(mg.MGPError, match="found a nan"):
+        s.run()
+    s.debugging = False
+    s.ctx.init_point_charge()
+    assert len(s.run()) == 2
