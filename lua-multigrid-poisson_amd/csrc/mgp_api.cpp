@@ -2757,7 +2757,7 @@ void mgp_group_destroy(mgp_group* g)
 
 // The group's communicators: one rank per device, created by this one thread as NON-BLOCKING communicators
 // (ncclConfig_t.blocking = 0; group_abort may then abort them from another thread), plus each rank's side-stream
-// communicator (a grouped ncclCommSplit).  Returns nullptr or an error message.
+// communicator.  Returns nullptr or an error message.
 static const char* group_comms(const std::vector<int>& dev, std::vector<ncclComm_t>& comms, std::vector<ncclComm_t>& xcomms)
 {
     static thread_local std::string msg;
@@ -2794,18 +2794,27 @@ static const char* group_comms(const std::vector<int>& dev, std::vector<ncclComm
         return msg.c_str();
     }
     if (const char* m = wait_all(comms, "communicator init")) return m;
+    // the side-stream communicators: a second grouped non-blocking init with an id of their own (a grouped
+    // ncclCommSplit of non-blocking communicators fails in RCCL 7.2 with "internal error": measured on the
+    // one-device group, tests/test_gpu_rccl.py; the multi-process contexts split, one blocking call per rank)
+    ncclUniqueId xid;
+    r = ncclGetUniqueId(&xid);
+    if (r != ncclSuccess) {
+        msg = std::string("ncclGetUniqueId: ") + ncclGetErrorString(r);
+        return msg.c_str();
+    }
     r = ncclGroupStart();
     for (int q = 0; q < n && (r == ncclSuccess || r == ncclInProgress); ++q) {
         (void)hipSetDevice(dev[(size_t)q]);
-        r = ncclCommSplit(comms[(size_t)q], 0, q, &xcomms[(size_t)q], &cfg);
+        r = ncclCommInitRankConfig(&xcomms[(size_t)q], n, xid, q, &cfg);
     }
     const ncclResult_t e2 = ncclGroupEnd();
     if (r == ncclSuccess) r = e2;
     if (r != ncclSuccess && r != ncclInProgress) {
-        msg = std::string("ncclCommSplit (side-stream communicators): ") + ncclGetErrorString(r);
+        msg = std::string("ncclCommInitRankConfig (side-stream communicators): ") + ncclGetErrorString(r);
         return msg.c_str();
     }
-    return wait_all(xcomms, "side-stream communicator split");
+    return wait_all(xcomms, "side-stream communicator init");
 }
 
 int mgp_group_create(mgp_group** out, const mgp_opts* o, int ngpu, const int* devices)

@@ -3243,94 +3243,125 @@ __global__ __launch_bounds__(tail_threads<T>()) void k_tail(const TailArgs<T, DI
     }
 }
 
-// ---- cubic coarse tail with compile-time level shapes (k_tail_c) ------------------------------
+// ---- coarse tail with compile-time level shapes (k_tail_c) -------------------------------------
 //
-// The same op program as k_tail for the common case of a cubic (square) red/black tail whose first
-// level is TN^DIM (3D: TN = 16, levels 16 .. 1; 2D: TN = 64, levels 64 .. 1).  Each level lives in
-// LDS as an unpacked (n+2)^DIM array with a zero halo (the Dirichlet ghost), so a cell's neighbours
-// are fixed offsets, every loop bound and index is a compile-time constant and no box test is
-// needed.  The per-cell arithmetic is half_item's / residual_at + resrestrict_item's /
-// prolong_value's, so results are bit-identical to k_tail and to the launch-per-piece path.
-template <int DIM, int N>
+// The same op program as k_tail for a red/black tail whose first level has one of the compile-time shapes of
+// TcTops below (the cubic / square tails of cubic / square boxes, and the tails of the slab-shaped boxes: one
+// rank's slab of configs[3] / configs[4] ends in 32 x 32 x 4 -> 16 x 16 x 2 -> 8 x 8 x 1, the weak-scaling box
+// 512 x 512 x 512 N in 8 x 8 x 8 N ... 1 x 1 x N).  Level l is (TX >> l, TY >> l, TZ >> l), down to the first
+// level with an axis of one cell.  Each level lives in LDS as an unpacked (nx+2)(ny+2)(nz+2) array with a zero
+// halo (the Dirichlet ghost), so a cell's neighbours are fixed offsets, every loop bound and index is a
+// compile-time constant and no box test is needed.  The per-cell arithmetic is half_item's / residual_at +
+// resrestrict_item's / prolong_value's, so results are bit-identical to k_tail and to the launch-per-piece path.
+template <int DIM, int NX, int NY, int NZ>
 struct TcLev {
-    static constexpr int W = N + 2, P = DIM == 3 ? W * W * W : W * W;
-    static constexpr int CELLS = DIM == 3 ? N * N * N : N * N;
+    static constexpr int W = NX + 2, WY = NY + 2, WZ = NZ + 2, P = DIM == 3 ? W * WY * WZ : W * WY;
+    static constexpr int CELLS = DIM == 3 ? NX * NY * NZ : NX * NY;
+    static constexpr int SZ = W * WY;  // z stride
     static __device__ __forceinline__ int idx(int i, int j, int k)
     {
-        return DIM == 3 ? ((k + 1) * W + (j + 1)) * W + (i + 1) : (j + 1) * W + (i + 1);
+        return DIM == 3 ? ((k + 1) * WY + (j + 1)) * W + (i + 1) : (j + 1) * W + (i + 1);
+    }
+    static __device__ __forceinline__ int nb(int i, int j, int k)  // faces on the box boundary
+    {
+        return (i == 0) + (i == NX - 1) + (j == 0) + (j == NY - 1) + (DIM == 3 ? (k == 0) + (k == NZ - 1) : 0);
     }
 };
-template <int DIM, int TN>
+template <int T0, int L>
+constexpr int tc_dim_at() { return (T0 >> L) > 0 ? (T0 >> L) : 1; }
+// level count of a top shape: the levels down to the first one with an axis of one cell
+template <int DIM, int TX, int TY, int TZ>
+constexpr int tc_levels()
+{
+    int m = TX < TY ? TX : TY;
+    if (DIM == 3 && TZ < m) m = TZ;
+    int n = 1;
+    for (int t = m; t > 1; t >>= 1) ++n;
+    return n;
+}
+template <int DIM, int TX, int TY, int TZ>
 constexpr int tc_off(int l)  // element offset of level l's (u, f) pair
 {
     int o = 0;
     for (int q = 0; q < l; ++q) {
-        const int w = (TN >> q) + 2;
-        o += 2 * (DIM == 3 ? w * w * w : w * w);
+        const int wx = (TX >> q > 0 ? TX >> q : 1) + 2, wy = (TY >> q > 0 ? TY >> q : 1) + 2,
+                  wz = (TZ >> q > 0 ? TZ >> q : 1) + 2;
+        o += 2 * (DIM == 3 ? wx * wy * wz : wx * wy);
     }
     return o;
 }
-template <int DIM, int TN>
-constexpr int tc_levels()
-{
-    int n = 0;
-    for (int t = TN; t >= 1; t >>= 1) ++n;
-    return n;
-}
-template <int DIM>
-constexpr int tc_top() { return DIM == 3 ? 16 : 64; }
-constexpr int kTcThreads = 1024;
+// 16 waves in fp32; fp64 takes 8, so that the kernel keeps 256 VGPRs (at 16 waves it spilled 100-240 VGPRs)
+template <typename T>
+constexpr int tc_threads() { return sizeof(T) == 4 ? 1024 : 512; }
 #ifndef TC_MAXL  // timing experiment: skip the ops of levels >= TC_MAXL (wrong results)
 #define TC_MAXL 16
 #endif
 
-template <typename T, int DIM, int N>
+template <typename T, int DIM, int NX, int NY, int NZ>
 __device__ __forceinline__ void tc_half(T* U, const T* F, const Op<T, DIM>& op, int c, int tid)
 {
-    using L = TcLev<DIM, N>;
-    constexpr int HN = N >= 2 ? N / 2 : 1;
-    constexpr int CNT = N >= 2 ? L::CELLS / 2 : 1;
-    if (N == 1 && c == 1) return;  // the single cell is red
+    using L = TcLev<DIM, NX, NY, NZ>;
+    if constexpr (NX >= 2) {
+        constexpr int HN = NX / 2, CNT = L::CELLS / 2;
 #pragma unroll
-    for (int q0 = 0; q0 < CNT; q0 += kTcThreads) {
-        const int q = q0 + tid;
-        if (q < CNT) {
-            const int i2 = q % HN, j = (q / HN) % N, k = DIM == 3 ? q / (HN * N) : 0;
-            const int i = N >= 2 ? 2 * i2 + ((j + k + c) & 1) : 0;
-            const int x = L::idx(i, j, k);
+        for (int q0 = 0; q0 < CNT; q0 += tc_threads<T>()) {
+            const int q = q0 + tid;
+            if (q < CNT) {
+                const int i2 = q % HN, j = (q / HN) % NY, k = DIM == 3 ? q / (HN * NY) : 0;
+                const int i = 2 * i2 + ((j + k + c) & 1);
+                const int x = L::idx(i, j, k);
+                T sm = U[x - 1] + U[x + 1];
+                sm = sm + U[x - L::W];
+                sm = sm + U[x + L::W];
+                if (DIM == 3) {
+                    sm = sm + U[x - L::SZ];
+                    sm = sm + U[x + L::SZ];
+                }
+                U[x] = op.relax_idx(sm, F[x], L::nb(i, j, k));
+            }
+        }
+    } else {  // one cell per row: cell (0, j, k) has colour (j + k) & 1 (half_item's empty slot is skipped)
+        constexpr int CNT = L::CELLS;
+        for (int q = tid; q < CNT; q += tc_threads<T>()) {
+            const int j = q % NY, k = DIM == 3 ? q / NY : 0;
+            if (((j + k) & 1) != c) continue;
+            const int x = L::idx(0, j, k);
             T sm = U[x - 1] + U[x + 1];
             sm = sm + U[x - L::W];
             sm = sm + U[x + L::W];
             if (DIM == 3) {
-                sm = sm + U[x - L::W * L::W];
-                sm = sm + U[x + L::W * L::W];
+                sm = sm + U[x - L::SZ];
+                sm = sm + U[x + L::SZ];
             }
-            const int nb = (i == 0) + (i == N - 1) + (j == 0) + (j == N - 1) + (DIM == 3 ? (k == 0) + (k == N - 1) : 0);
-            U[x] = op.relax_idx(sm, F[x], nb);
+            U[x] = op.relax_idx(sm, F[x], L::nb(0, j, k));
         }
     }
 }
 
-template <typename T, int DIM, int N>
+template <typename T, int DIM, int NX, int NY, int NZ>
+__device__ __forceinline__ T tc_res(const T* U, const T* F, const Op<T, DIM>& op, int i, int j, int k)
+{
+    using L = TcLev<DIM, NX, NY, NZ>;
+    const int x = L::idx(i, j, k);
+    T sm = U[x - 1] + U[x + 1];
+    sm = sm + U[x - L::W];
+    sm = sm + U[x + L::W];
+    if (DIM == 3) {
+        sm = sm + U[x - L::SZ];
+        sm = sm + U[x + L::SZ];
+    }
+    return op.residual_idx(sm, F[x], U[x], L::nb(i, j, k));
+}
+
+template <typename T, int DIM, int NX, int NY, int NZ>
 __device__ __forceinline__ void tc_rr(const T* U, const T* F, T* Fc, const Op<T, DIM>& op, int tid)
 {
-    using L = TcLev<DIM, N>;
-    using C = TcLev<DIM, N / 2>;
-    constexpr int M = N / 2, CNT = C::CELLS;
-    auto res = [&](int i, int j, int k) {
-        const int x = L::idx(i, j, k);
-        T sm = U[x - 1] + U[x + 1];
-        sm = sm + U[x - L::W];
-        sm = sm + U[x + L::W];
-        if (DIM == 3) {
-            sm = sm + U[x - L::W * L::W];
-            sm = sm + U[x + L::W * L::W];
-        }
-        const int nb = (i == 0) + (i == N - 1) + (j == 0) + (j == N - 1) + (DIM == 3 ? (k == 0) + (k == N - 1) : 0);
-        return op.residual_idx(sm, F[x], U[x], nb);
-    };
-    for (int q = tid; q < CNT; q += kTcThreads) {
-        const int I = q % M, J = (q / M) % M, K = DIM == 3 ? q / (M * M) : 0;
+    constexpr int MX = NX / 2, MY = NY / 2, MZ = DIM == 3 ? NZ / 2 : 1;
+    using C = TcLev<DIM, MX, MY, MZ>;
+    constexpr int CNT = C::CELLS;
+    auto res = [&](int i, int j, int k) { return tc_res<T, DIM, NX, NY, NZ>(U, F, op, i, j, k); };
+    for (int q = tid; q < CNT; q += tc_threads<T>()) {
+        const int I = q % MX, J = (q / MX) % MY, K = DIM == 3 ? q / (MX * MY) : 0;
         const int i = 2 * I, j = 2 * J, k = 2 * K;
         T sm = res(i, j, k) + res(i + 1, j, k);
         sm = sm + res(i, j + 1, k);
@@ -3346,47 +3377,38 @@ __device__ __forceinline__ void tc_rr(const T* U, const T* F, T* Fc, const Op<T,
 }
 
 // tc_rr with the full-weighting restriction (fw_eval over the residuals of the 4^DIM fine cells)
-template <typename T, int DIM, int N>
+template <typename T, int DIM, int NX, int NY, int NZ>
 __device__ __forceinline__ void tc_rr_fw(const T* U, const T* F, T* Fc, const Op<T, DIM>& op, T wf, int tid)
 {
-    using L = TcLev<DIM, N>;
-    using C = TcLev<DIM, N / 2>;
-    constexpr int M = N / 2, CNT = C::CELLS;
+    constexpr int MX = NX / 2, MY = NY / 2, MZ = DIM == 3 ? NZ / 2 : 1;
+    using C = TcLev<DIM, MX, MY, MZ>;
+    constexpr int CNT = C::CELLS;
     Geo g{}, gc{};
-    g.nx = g.ny = N;
-    g.gnz = DIM == 3 ? N : 1;
-    gc.nx = gc.ny = M;
-    gc.gnz = DIM == 3 ? M : 1;
-    auto res = [&](int i, int j, int64_t k64) {
-        const int k = (int)k64;
-        const int x = L::idx(i, j, k);
-        T sm = U[x - 1] + U[x + 1];
-        sm = sm + U[x - L::W];
-        sm = sm + U[x + L::W];
-        if (DIM == 3) {
-            sm = sm + U[x - L::W * L::W];
-            sm = sm + U[x + L::W * L::W];
-        }
-        const int nb = (i == 0) + (i == N - 1) + (j == 0) + (j == N - 1) + (DIM == 3 ? (k == 0) + (k == N - 1) : 0);
-        return op.residual_idx(sm, F[x], U[x], nb);
-    };
-    for (int q = tid; q < CNT; q += kTcThreads) {
-        const int I = q % M, J = (q / M) % M, K = DIM == 3 ? q / (M * M) : 0;
+    g.nx = NX;
+    g.ny = NY;
+    g.gnz = DIM == 3 ? NZ : 1;
+    gc.nx = MX;
+    gc.ny = MY;
+    gc.gnz = MZ;
+    auto res = [&](int i, int j, int64_t k64) { return tc_res<T, DIM, NX, NY, NZ>(U, F, op, i, j, (int)k64); };
+    for (int q = tid; q < CNT; q += tc_threads<T>()) {
+        const int I = q % MX, J = (q / MX) % MY, K = DIM == 3 ? q / (MX * MY) : 0;
         Fc[C::idx(I, J, K)] = fw_eval<T, DIM>(res, g, gc, wf, I, J, (int64_t)K);
     }
 }
 
-template <typename T, int DIM, int N, int LINEAR>
+template <typename T, int DIM, int NX, int NY, int NZ, int LINEAR>
 __device__ __forceinline__ void tc_prolong(T* U, const T* V, T cl, int tid)
 {
-    using L = TcLev<DIM, N>;
-    using C = TcLev<DIM, N / 2>;
-    constexpr int M = N / 2, CNT = L::CELLS;
+    using L = TcLev<DIM, NX, NY, NZ>;
+    constexpr int MX = NX / 2, MY = NY / 2, MZ = DIM == 3 ? NZ / 2 : 1;
+    using C = TcLev<DIM, MX, MY, MZ>;
+    constexpr int CNT = L::CELLS;
 #pragma unroll 1
-    for (int q0 = 0; q0 < CNT; q0 += kTcThreads) {
+    for (int q0 = 0; q0 < CNT; q0 += tc_threads<T>()) {
         const int q = q0 + tid;
         if (q < CNT) {
-            const int i = q % N, j = (q / N) % N, k = DIM == 3 ? q / (N * N) : 0;
+            const int i = q % NX, j = (q / NX) % NY, k = DIM == 3 ? q / (NX * NY) : 0;
             const int I = i >> 1, J = j >> 1, K = k >> 1;
             T v;
             if (!LINEAR) {
@@ -3394,7 +3416,7 @@ __device__ __forceinline__ void tc_prolong(T* U, const T* V, T cl, int tid)
             } else {
                 const T w0 = (T)0.75, w1 = (T)0.25;
                 int In = (i & 1) ? I + 1 : I - 1, Jn = (j & 1) ? J + 1 : J - 1, Kn = (k & 1) ? K + 1 : K - 1;
-                const bool ox = In < 0 || In >= M, oy = Jn < 0 || Jn >= M, oz = DIM == 3 && (Kn < 0 || Kn >= M);
+                const bool ox = In < 0 || In >= MX, oy = Jn < 0 || Jn >= MY, oz = DIM == 3 && (Kn < 0 || Kn >= MZ);
                 if (ox) In = I;
                 if (oy) Jn = J;
                 if (oz || DIM == 2) Kn = K;
@@ -3426,26 +3448,34 @@ __device__ __forceinline__ void tc_prolong(T* U, const T* V, T cl, int tid)
     }
 }
 
+// the packed global offset of LDS element q of a level (its (i, j, k), -1 in the halo)
+template <int DIM, int NX, int NY, int NZ>
+__device__ __forceinline__ int64_t tc_global(int q)
+{
+    using L = TcLev<DIM, NX, NY, NZ>;
+    constexpr int HW = NX >= 2 ? NX / 2 : 1;
+    constexpr int64_t H = (int64_t)HW * NY, P = 2 * H;
+    const int i = q % L::W - 1, j = (q / L::W) % L::WY - 1, k = DIM == 3 ? q / (L::W * L::WY) - 1 : 0;
+    const bool inside = q < L::P && i >= 0 && i < NX && j >= 0 && j < NY && k >= 0 && k < (DIM == 3 ? NZ : 1);
+    return inside ? (int64_t)k * P + ((i + j + k) & 1) * H + (int64_t)j * HW + (i >> 1) : -1;
+}
+
 // level l of the tail: copy in (zero halo; zero_u: a fresh guess) or out, packed global layout; a
 // thread's loads are all issued before its LDS stores (compile-time trip count)
-template <typename T, int DIM, int N>
+template <typename T, int DIM, int NX, int NY, int NZ>
 __device__ __forceinline__ void tc_copy(T* U, T* F, T* gu, T* gf, bool in, bool zero_u, int tid)
 {
-    using L = TcLev<DIM, N>;
-    constexpr int HW = N >= 2 ? N / 2 : 1;
-    constexpr int64_t H = (int64_t)HW * N, P = 2 * H;
-    constexpr int IT = (L::P + kTcThreads - 1) / kTcThreads;
+    using L = TcLev<DIM, NX, NY, NZ>;
+    constexpr int IT = (L::P + tc_threads<T>() - 1) / tc_threads<T>();
     T uv[IT], fv[IT];
 #pragma unroll
     for (int r = 0; r < IT; ++r) {
-        const int q = tid + r * kTcThreads;
-        const int i = q % L::W - 1, j = (q / L::W) % L::W - 1, k = DIM == 3 ? q / (L::W * L::W) - 1 : 0;
-        const bool inside = q < L::P && i >= 0 && i < N && j >= 0 && j < N && k >= 0 && k < N;
-        const int64_t gi = (int64_t)k * P + ((i + j + k) & 1) * H + (int64_t)j * HW + (i >> 1);
+        const int q = tid + r * tc_threads<T>();
+        const int64_t gi = tc_global<DIM, NX, NY, NZ>(q);
         if (in) {
-            uv[r] = inside && !zero_u ? gu[gi] : (T)0;
-            fv[r] = inside ? gf[gi] : (T)0;
-        } else if (inside) {
+            uv[r] = gi >= 0 && !zero_u ? gu[gi] : (T)0;
+            fv[r] = gi >= 0 ? gf[gi] : (T)0;
+        } else if (gi >= 0) {
             gu[gi] = U[q];
             gf[gi] = F[q];
         }
@@ -3453,7 +3483,7 @@ __device__ __forceinline__ void tc_copy(T* U, T* F, T* gu, T* gf, bool in, bool 
     if (in) {
 #pragma unroll
         for (int r = 0; r < IT; ++r) {
-            const int q = tid + r * kTcThreads;
+            const int q = tid + r * tc_threads<T>();
             if (q < L::P) {
                 U[q] = uv[r];
                 F[q] = fv[r];
@@ -3464,34 +3494,28 @@ __device__ __forceinline__ void tc_copy(T* U, T* F, T* gu, T* gf, bool in, bool 
 
 // Copy-in in two halves, so that every level's global loads are in flight together (round 4: tc_copy level by
 // level waited for one level's loads before issuing the next level's: seven load latencies in a row in 2D)
-template <typename T, int DIM, int N>
+template <typename T, int DIM, int NX, int NY, int NZ>
 struct TcRegs {
-    static constexpr int IT = (TcLev<DIM, N>::P + kTcThreads - 1) / kTcThreads;
+    static constexpr int IT = (TcLev<DIM, NX, NY, NZ>::P + tc_threads<T>() - 1) / tc_threads<T>();
     T u[IT], f[IT];
 };
-template <typename T, int DIM, int N>
-__device__ __forceinline__ void tc_load(TcRegs<T, DIM, N>& rg, const T* gu, const T* gf, bool zero_u, int tid)
+template <typename T, int DIM, int NX, int NY, int NZ>
+__device__ __forceinline__ void tc_load(TcRegs<T, DIM, NX, NY, NZ>& rg, const T* gu, const T* gf, bool zero_u, int tid)
 {
-    using L = TcLev<DIM, N>;
-    constexpr int HW = N >= 2 ? N / 2 : 1;
-    constexpr int64_t H = (int64_t)HW * N, P = 2 * H;
 #pragma unroll
-    for (int r = 0; r < TcRegs<T, DIM, N>::IT; ++r) {
-        const int q = tid + r * kTcThreads;
-        const int i = q % L::W - 1, j = (q / L::W) % L::W - 1, k = DIM == 3 ? q / (L::W * L::W) - 1 : 0;
-        const bool inside = q < L::P && i >= 0 && i < N && j >= 0 && j < N && k >= 0 && k < N;
-        const int64_t gi = (int64_t)k * P + ((i + j + k) & 1) * H + (int64_t)j * HW + (i >> 1);
-        rg.u[r] = inside && !zero_u ? gu[gi] : (T)0;
-        rg.f[r] = inside ? gf[gi] : (T)0;
+    for (int r = 0; r < TcRegs<T, DIM, NX, NY, NZ>::IT; ++r) {
+        const int64_t gi = tc_global<DIM, NX, NY, NZ>(tid + r * tc_threads<T>());
+        rg.u[r] = gi >= 0 && !zero_u ? gu[gi] : (T)0;
+        rg.f[r] = gi >= 0 ? gf[gi] : (T)0;
     }
 }
-template <typename T, int DIM, int N>
-__device__ __forceinline__ void tc_store(T* U, T* F, const TcRegs<T, DIM, N>& rg, int tid)
+template <typename T, int DIM, int NX, int NY, int NZ>
+__device__ __forceinline__ void tc_store(T* U, T* F, const TcRegs<T, DIM, NX, NY, NZ>& rg, int tid)
 {
-    using L = TcLev<DIM, N>;
+    using L = TcLev<DIM, NX, NY, NZ>;
 #pragma unroll
-    for (int r = 0; r < TcRegs<T, DIM, N>::IT; ++r) {
-        const int q = tid + r * kTcThreads;
+    for (int r = 0; r < TcRegs<T, DIM, NX, NY, NZ>::IT; ++r) {
+        const int q = tid + r * tc_threads<T>();
         if (q < L::P) {
             U[q] = rg.u[r];
             F[q] = rg.f[r];
@@ -3499,26 +3523,29 @@ __device__ __forceinline__ void tc_store(T* U, T* F, const TcRegs<T, DIM, N>& rg
     }
 }
 
-template <typename T, int DIM, int LINEAR>
-__global__ __launch_bounds__(kTcThreads) void k_tail_c(const TailArgs<T, DIM> a)
+template <typename T, int DIM, int LINEAR, int TX, int TY, int TZ>
+__global__ __launch_bounds__(tc_threads<T>()) void k_tail_c(const TailArgs<T, DIM> a)
 {
-    constexpr int TN = tc_top<DIM>(), NL = tc_levels<DIM, TN>();
+    constexpr int NL = tc_levels<DIM, TX, TY, TZ>();
     extern __shared__ __align__(16) unsigned char tc_smem[];
     T* const lds = reinterpret_cast<T*>(tc_smem);
     // the level operators in LDS, read per op (held in registers for all levels they spill)
     __shared__ Op<T, DIM> sop[NL];
     if ((int)threadIdx.x < NL) sop[threadIdx.x] = a.op[threadIdx.x];
-#define TC_U(l) (lds + tc_off<DIM, TN>(l))
-#define TC_F(l) (lds + tc_off<DIM, TN>(l) + TcLev<DIM, (TN >> (l))>::P)
-#define TC_COPY(l, IN)                                                                                    \
-    if constexpr ((l) < NL) tc_copy<T, DIM, (TN >> (l))>(TC_U(l), TC_F(l), a.u[l], a.f[l], IN, IN && (l) == 0 && a.zero0, \
-                                                         threadIdx.x);
-#define TC_N(l) ((TN >> (l)) > 0 ? (TN >> (l)) : 1)
+#define TC_NX(l) tc_dim_at<TX, (l)>()
+#define TC_NY(l) tc_dim_at<TY, (l)>()
+#define TC_NZ(l) (DIM == 3 ? tc_dim_at<TZ, (l)>() : 1)
+#define TC_SH(l) TC_NX(l), TC_NY(l), TC_NZ(l)
+#define TC_U(l) (lds + tc_off<DIM, TX, TY, TZ>(l))
+#define TC_F(l) (lds + tc_off<DIM, TX, TY, TZ>(l) + TcLev<DIM, TC_SH(l)>::P)
+#define TC_COPY(l, IN)                                                                                        \
+    if constexpr ((l) < NL) tc_copy<T, DIM, TC_SH(l)>(TC_U(l), TC_F(l), a.u[l], a.f[l], IN, IN && (l) == 0 && a.zero0, \
+                                                      threadIdx.x);
 #define TC_LOAD(l)                         \
-    TcRegs<T, DIM, TC_N(l)> rg##l;         \
-    if constexpr ((l) < NL) tc_load<T, DIM, TC_N(l)>(rg##l, a.u[l], a.f[l], (l) == 0 && a.zero0, threadIdx.x);
+    TcRegs<T, DIM, TC_SH(l)> rg##l;        \
+    if constexpr ((l) < NL) tc_load<T, DIM, TC_SH(l)>(rg##l, a.u[l], a.f[l], (l) == 0 && a.zero0, threadIdx.x);
 #define TC_STORE(l) \
-    if constexpr ((l) < NL) tc_store<T, DIM, TC_N(l)>(TC_U(l), TC_F(l), rg##l, threadIdx.x);
+    if constexpr ((l) < NL) tc_store<T, DIM, TC_SH(l)>(TC_U(l), TC_F(l), rg##l, threadIdx.x);
     if constexpr (DIM == 2) {  // (3D: the held values push the kernel past 64 VGPRs into spills; level by level)
         TC_LOAD(0) TC_LOAD(1) TC_LOAD(2) TC_LOAD(3) TC_LOAD(4) TC_LOAD(5) TC_LOAD(6)
         TC_STORE(0) TC_STORE(1) TC_STORE(2) TC_STORE(3) TC_STORE(4) TC_STORE(5) TC_STORE(6)
@@ -3528,7 +3555,6 @@ __global__ __launch_bounds__(kTcThreads) void k_tail_c(const TailArgs<T, DIM> a)
     }
 #undef TC_STORE
 #undef TC_LOAD
-#undef TC_N
     __syncthreads();
 #ifdef TC_PROF  // timing experiment: wall-clock ticks (100 MHz) per op into f of the first level (tools/tail_prof.py)
     __shared__ long long tcp[130];
@@ -3544,40 +3570,42 @@ __global__ __launch_bounds__(kTcThreads) void k_tail_c(const TailArgs<T, DIM> a)
 #define TC_CASE(L)                                                                                     \
     case L:                                                                                            \
         if constexpr ((L) < NL && (L) < TC_MAXL) {                                                     \
-            constexpr int N = TN >> (L);                                                               \
+            using LV = TcLev<DIM, TC_SH(L)>;                                                           \
             if (op == TAIL_SMOOTH) {                                                                   \
                 for (int sw = 0; sw < arg; ++sw) {                                                     \
-                    tc_half<T, DIM, N>(TC_U(L), TC_F(L), sop[L], 0, tid);                              \
+                    tc_half<T, DIM, TC_SH(L)>(TC_U(L), TC_F(L), sop[L], 0, tid);                       \
                     __syncthreads();                                                                   \
-                    if (N >= 2) {                                                                      \
-                        tc_half<T, DIM, N>(TC_U(L), TC_F(L), sop[L], 1, tid);                          \
+                    if (LV::CELLS >= 2) {                                                              \
+                        tc_half<T, DIM, TC_SH(L)>(TC_U(L), TC_F(L), sop[L], 1, tid);                   \
                         __syncthreads();                                                               \
                     }                                                                                  \
                 }                                                                                      \
             } else if (op == TAIL_ZERO) {                                                              \
                 T* u = TC_U(L);                                                                        \
-                for (int q = tid; q < TcLev<DIM, N>::CELLS; q += kTcThreads)                           \
-                    u[TcLev<DIM, N>::idx(q % N, (q / N) % N, DIM == 3 ? q / (N * N) : 0)] = (T)0;      \
+                constexpr int NXL = TC_NX(L), NYL = TC_NY(L);                                          \
+                for (int q = tid; q < LV::CELLS; q += tc_threads<T>())                                      \
+                    u[LV::idx(q % NXL, (q / NXL) % NYL, DIM == 3 ? q / (NXL * NYL) : 0)] = (T)0;       \
                 __syncthreads();                                                                       \
-            } else if constexpr (N >= 2 && (L) + 1 < NL) {                                             \
+            } else if constexpr ((L) + 1 < NL) {                                                       \
                 if (op == TAIL_RR) {                                                                   \
                     if (a.fw)                                                                          \
-                        tc_rr_fw<T, DIM, N>(TC_U(L), TC_F(L), TC_F((L) + 1), sop[L], (T)3 - sop[(L) + 1].cl, tid); \
+                        tc_rr_fw<T, DIM, TC_SH(L)>(TC_U(L), TC_F(L), TC_F((L) + 1), sop[L], (T)3 - sop[(L) + 1].cl, tid); \
                     else                                                                               \
-                        tc_rr<T, DIM, N>(TC_U(L), TC_F(L), TC_F((L) + 1), sop[L], tid);                \
+                        tc_rr<T, DIM, TC_SH(L)>(TC_U(L), TC_F(L), TC_F((L) + 1), sop[L], tid);         \
                     /* a fresh guess of the next level (its ZERO op follows) in the same phase: RR writes */ \
                     /* that level's f, ZERO its u                                                        */ \
                     const uint32_t wn = pc + 1 < a.nops ? a.ops[pc + 1] : 0u;                          \
                     if ((int)(wn & 15) == TAIL_ZERO && (int)((wn >> 4) & 15) == (L) + 1) {              \
-                        constexpr int M = N / 2;                                                       \
+                        using CV = TcLev<DIM, TC_SH((L) + 1)>;                                         \
+                        constexpr int MX = TC_NX((L) + 1), MY = TC_NY((L) + 1);                        \
                         T* uc = TC_U((L) + 1);                                                         \
-                        for (int q = tid; q < TcLev<DIM, M>::CELLS; q += kTcThreads)                   \
-                            uc[TcLev<DIM, M>::idx(q % M, (q / M) % M, DIM == 3 ? q / (M * M) : 0)] = (T)0; \
+                        for (int q = tid; q < CV::CELLS; q += tc_threads<T>())                              \
+                            uc[CV::idx(q % MX, (q / MX) % MY, DIM == 3 ? q / (MX * MY) : 0)] = (T)0;   \
                         ++pc;                                                                          \
                     }                                                                                  \
                     __syncthreads();                                                                   \
                 } else if (op == TAIL_PROLONG) {                                                       \
-                    tc_prolong<T, DIM, N, LINEAR>(TC_U(L), TC_U((L) + 1), sop[(L) + 1].cl, tid);       \
+                    tc_prolong<T, DIM, TC_SH(L), LINEAR>(TC_U(L), TC_U((L) + 1), sop[(L) + 1].cl, tid); \
                     __syncthreads();                                                                   \
                 }                                                                                      \
             }                                                                                          \
@@ -3601,17 +3629,18 @@ __global__ __launch_bounds__(kTcThreads) void k_tail_c(const TailArgs<T, DIM> a)
     }
 #ifdef TC_PROF
     if (threadIdx.x == 0) {
-        // op q's ticks at cell (q % TN, q / TN, 0) of the first level's f, then 0; op code (op | level << 4) + 1
+        // op q's ticks at cell (q % TX, q / TX, 0) of the first level's f, then 0; op code (op | level << 4) + 1
         // at the cell after the ticks' row block (rows 2 and 3)
+        using L0 = TcLev<DIM, TC_SH(0)>;
         T* F0 = TC_F(0);
-        const int n = a.nops < 2 * TN ? a.nops : 2 * TN;
+        const int n = a.nops < 2 * TX ? a.nops : 2 * TX;
         for (int q = 0; q < n; ++q) {
-            F0[TcLev<DIM, TN>::idx(q % TN, q / TN, 0)] = (T)(tcp[q + 1] - tcp[q]);
-            F0[TcLev<DIM, TN>::idx(q % TN, 2 + q / TN, 0)] = (T)((a.ops[q] & 255) + 1);
+            F0[L0::idx(q % TX, q / TX, 0)] = (T)(tcp[q + 1] - tcp[q]);
+            F0[L0::idx(q % TX, 2 + q / TX, 0)] = (T)((a.ops[q] & 255) + 1);
         }
-        if (n < 2 * TN) {
-            F0[TcLev<DIM, TN>::idx(n % TN, n / TN, 0)] = (T)0;
-            F0[TcLev<DIM, TN>::idx(n % TN, 2 + n / TN, 0)] = (T)0;
+        if (n < 2 * TX) {
+            F0[L0::idx(n % TX, n / TX, 0)] = (T)0;
+            F0[L0::idx(n % TX, 2 + n / TX, 0)] = (T)0;
         }
     }
     __syncthreads();
@@ -3621,13 +3650,27 @@ __global__ __launch_bounds__(kTcThreads) void k_tail_c(const TailArgs<T, DIM> a)
 #undef TC_COPY
 #undef TC_F
 #undef TC_U
+#undef TC_SH
+#undef TC_NZ
+#undef TC_NY
+#undef TC_NX
 }
 
-template <int DIM>
+template <int DIM, int TX, int TY, int TZ>
 constexpr size_t tc_lds(int rb)
 {
-    return (size_t)tc_off<DIM, tc_top<DIM>()>(tc_levels<DIM, tc_top<DIM>()>()) * rb;
+    return (size_t)tc_off<DIM, TX, TY, TZ>(tc_levels<DIM, TX, TY, TZ>()) * rb;
 }
+
+// The compile-time tail shapes (first level nx x ny x nz; nz = 1 in 2D) and their kernels.  k_tail_c runs a
+// tail whose first level is one of these (tail_shape); any other red/black tail runs the generic k_tail.
+#define MGP_TC_SHAPES(X)   \
+    X(3, 16, 16, 16)       \
+    X(3, 32, 32, 4)        \
+    X(3, 8, 8, 16)         \
+    X(3, 8, 8, 32)         \
+    X(3, 8, 8, 64)         \
+    X(2, 64, 64, 1)
 
 // ---- 3D-tiled smoothing phases of small levels (k_blk) ----------------------------------------
 //
@@ -4776,19 +4819,27 @@ size_t tail_lds_bytes(int rb, int dim, int jacobi, const Geo* g, int nlev)
     return n * (size_t)rb;
 }
 
-// k_tail_c applies: red/black, levels TN^DIM, (TN/2)^DIM, ... 1 (TN = tc_top<DIM>()), one rank's box
-static bool tail_cubic(const TailSpec& t, int dim)
+// k_tail_c applies: red/black, the first level one of MGP_TC_SHAPES and the levels below it the tail's levels
+// (one rank's replicated box); returns the shape's index, or -1 (MGP_TAIL_CUBIC=0: always the generic k_tail)
+static int tail_shape(const TailSpec& t, int dim)
 {
-    const char* v = std::getenv("MGP_TAIL_CUBIC");  // 0: the generic k_tail
-    const int top = dim == 3 ? tc_top<3>() : tc_top<2>();
-    const int nl = dim == 3 ? tc_levels<3, tc_top<3>()>() : tc_levels<2, tc_top<2>()>();
-    if ((v && std::atoi(v) == 0) || t.jacobi || t.nlev != nl) return false;
-    for (int l = 0; l < t.nlev; ++l) {
-        const Geo& g = t.g[l];
-        const int n = top >> l;
-        if (g.nx != n || g.ny != n || (dim == 3 && (g.nz != n || g.gnz != n)) || g.z0 != 0) return false;
-    }
-    return true;
+    const char* v = std::getenv("MGP_TAIL_CUBIC");
+    if ((v && std::atoi(v) == 0) || t.jacobi) return -1;
+    int idx = -1, found = -1;
+    auto match = [&](int D, int TX, int TY, int TZ, int NL) {
+        ++idx;
+        if (found >= 0 || D != dim || t.nlev != NL) return;
+        for (int l = 0; l < t.nlev; ++l) {
+            const Geo& g = t.g[l];
+            const int nx = TX >> l > 0 ? TX >> l : 1, ny = TY >> l > 0 ? TY >> l : 1, nz = TZ >> l > 0 ? TZ >> l : 1;
+            if (g.nx != nx || g.ny != ny || g.z0 != 0 || (dim == 3 && (g.nz != nz || g.gnz != nz))) return;
+        }
+        found = idx;
+    };
+#define X(D, TX, TY, TZ) match(D, TX, TY, TZ, tc_levels<D, TX, TY, TZ>());
+    MGP_TC_SHAPES(X)
+#undef X
+    return found;
 }
 
 template <typename T, int D>
@@ -4812,10 +4863,23 @@ static hipError_t tail_t(const TailSpec& t, hipStream_t s)
         off += a.region[l] * (t.jacobi ? 3 : 2);
     }
     for (int i = 0; i < t.nops; ++i) a.ops[i] = t.ops[i];
-    if (tail_cubic(t, D)) {
-        auto kc = t.linear ? k_tail_c<T, D, 1> : k_tail_c<T, D, 0>;
-        kc<<<1, kTcThreads, tc_lds<D>(sizeof(T)), s>>>(a);
-        return hipGetLastError();
+    const int sh = tail_shape(t, D);
+    if (sh >= 0) {
+        int idx = -1;
+        bool done = false;
+#define X(DD, TX, TY, TZ)                                                                                    \
+        if constexpr (DD == D) {                                                                             \
+            if (++idx == sh && !done) {                                                                      \
+                auto kc = t.linear ? k_tail_c<T, D, 1, TX, TY, TZ> : k_tail_c<T, D, 0, TX, TY, TZ>;          \
+                kc<<<1, tc_threads<T>(), tc_lds<D, TX, TY, TZ>(sizeof(T)), s>>>(a);                               \
+                done = true;                                                                                 \
+            }                                                                                                \
+        } else {                                                                                             \
+            ++idx;                                                                                           \
+        }
+        MGP_TC_SHAPES(X)
+#undef X
+        return done ? hipGetLastError() : hipErrorInvalidValue;
     }
     const size_t bytes = (size_t)off * sizeof(T);
     auto kern = t.linear ? k_tail<T, D, 1> : k_tail<T, D, 0>;
@@ -4827,11 +4891,14 @@ template <typename T>
 static hipError_t tail_c_attr()
 {
     const auto A = hipFuncAttributeMaxDynamicSharedMemorySize;
-    const int b3 = (int)tc_lds<3>(sizeof(T)), b2 = (int)tc_lds<2>(sizeof(T));
-    hipError_t e = hipFuncSetAttribute((const void*)k_tail_c<T, 3, 0>, A, b3);
-    if (e == hipSuccess) e = hipFuncSetAttribute((const void*)k_tail_c<T, 3, 1>, A, b3);
-    if (e == hipSuccess) e = hipFuncSetAttribute((const void*)k_tail_c<T, 2, 0>, A, b2);
-    if (e == hipSuccess) e = hipFuncSetAttribute((const void*)k_tail_c<T, 2, 1>, A, b2);
+    hipError_t e = hipSuccess;
+#define X(D, TX, TY, TZ)                                                                                 \
+    if (e == hipSuccess)                                                                                 \
+        e = hipFuncSetAttribute((const void*)k_tail_c<T, D, 0, TX, TY, TZ>, A, (int)tc_lds<D, TX, TY, TZ>(sizeof(T))); \
+    if (e == hipSuccess)                                                                                 \
+        e = hipFuncSetAttribute((const void*)k_tail_c<T, D, 1, TX, TY, TZ>, A, (int)tc_lds<D, TX, TY, TZ>(sizeof(T)));
+    MGP_TC_SHAPES(X)
+#undef X
     return e;
 }
 

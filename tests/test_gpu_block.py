@@ -159,21 +159,34 @@ CUBIC_TAIL_CONFIGS = [
     # 2D: levels 64^2 .. 1
     dict(dim=2, n=(256, 256, 1), real="float", nu1=2, nu2=2, prolong="linear", coarse_bc="consistent"),
     dict(dim=2, n=(128, 128, 1), real="double", nu1=2, nu2=2, prolong="pc", coarse_bc="zero", cycle="F", coarse_init="warm"),
+    # the slab tails: a configs[3] / configs[4] rank slab's ratio 8:8:1 ends in 32 x 32 x 4 ..
+    # 8 x 8 x 1 (64 cells, coarse_sweeps sweeps); the weak-scaling box 512 x 512 x 512 N in 8 x 8 x 8 N .. 1 x 1 x N
+    dict(n=(256, 256, 32), real="float", nu1=2, nu2=2, prolong="linear", coarse_bc="consistent", tail=(32, 32, 4)),
+    dict(n=(128, 128, 16), real="double", nu1=2, nu2=2, prolong="linear", coarse_bc="consistent", cycle="F",
+         tail=(32, 32, 4)),
+    dict(n=(64, 64, 512), real="float", nu1=2, nu2=2, prolong="linear", coarse_bc="consistent", tail=(8, 8, 64)),
+    dict(n=(32, 32, 64), real="double", nu1=2, nu2=2, prolong="pc", coarse_bc="zero", cycle="F", coarse_init="warm",
+         tail=(8, 8, 16)),
+    dict(n=(64, 64, 256), real="float", nu1=2, nu2=2, prolong="linear", coarse_bc="consistent", cycle="F",
+         restriction="full_weighting", tail=(8, 8, 32)),
 ]
 
 
 @pytest.mark.parametrize("cfg", CUBIC_TAIL_CONFIGS, ids=_id)
 def test_cubic_tail_equals_generic_tail_and_oracle(cfg, monkeypatch):
-    """k_tail_c (compile-time cubic tail: 16^3 .. 1 in 3D, 64^2 .. 1 in 2D, zero-halo LDS levels) == the
-    generic k_tail == the oracle: psi and f bit-identical on every level."""
+    """k_tail_c (compile-time tail shapes: 16^3 .. 1 in 3D, 64^2 .. 1 in 2D, the slab tails 32 x 32 x 4 .. 8 x 8 x 1
+    and 8 x 8 x 8N .. 1 x 1 x N; zero-halo LDS levels) == the generic k_tail == the oracle: psi and f bit-identical
+    on every level."""
     kw = dict(smoother="rbgs", **cfg)
     kw.setdefault("dim", 3)
+    top = kw.pop("tail", (16, 16, 16) if kw["dim"] == 3 else (64, 64, 1))
     monkeypatch.setenv("MGP_TAIL_CUBIC", "1")
     a = _ctx(**kw)
     monkeypatch.setenv("MGP_TAIL_CUBIC", "0")
     b = _ctx(**kw)
-    top = 16 if kw["dim"] == 3 else 64
-    assert [lv["nx"] for lv in a.levels if lv["tail"]] == [top >> l for l in range(top.bit_length())]
+    tl = [(lv["nx"], lv["ny"], lv["nz_global"]) for lv in a.levels if lv["tail"]]
+    nl = min(top[:kw["dim"]]).bit_length()
+    assert tl == [tuple(max(1, t >> l) if (d < kw["dim"]) else 1 for d, t in enumerate(top)) for l in range(nl)]
     o = Oracle(threads=8, **kw)
     for x in (a, b, o):
         x.init_point_charge()
