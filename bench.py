@@ -81,9 +81,11 @@ def parse():
     p.add_argument("--cpu-cycles", type=int, default=4, help="oracle cycles timed for cpu_baseline (0 = skip)")
     p.add_argument("--cpu-threads", type=int, default=0,
                    help="threads of the OpenMP cpu_baseline (0 = OMP_NUM_THREADS or all host cores)")
-    p.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "pmc_traffic_current.json"),
-                   help="JSON with the PMC-measured HBM bytes per launch of the dominant kernel (tools/pmc_traffic.py); "
-                        "used only when its kernel name matches")
+    p.add_argument("--traffic", default=",".join(os.path.join(ROOT, "profiles", f) for f in
+                                                 ("pmc_traffic_current.json", "pmc_traffic_slab4.json",
+                                                  "pmc_traffic_slab3.json")),
+                   help="comma list of JSONs with the PMC-measured HBM bytes per launch (tools/pmc_traffic.py); the "
+                        "first one measured on this build and this workload's cells per rank is used")
     a = p.parse_args()
     if a.config0:
         a.dim, a.n, a.real, a.smoother, a.nu, a.prolong, a.coarse_bc, a.cycle = 2, 256, "double", "jacobi", 7, "pc", "zero", "V"
@@ -378,8 +380,9 @@ def run_workload(a, cfg, box, strong, rank, world, local, dist, steps, warmup, p
             roof["copy_probe"] = (f"mgp_copy_bandwidth: 16-byte streaming copy of {a.copy_probe_mb} MiB, best of 10, "
                                   "read + write bytes (BASELINE.md: measured copy-kernel peak)")
         roof["traffic_measured_this_run"] = False
-        if a.traffic and os.path.exists(a.traffic):
-            with open(a.traffic) as fh:
+        tpath = pick_traffic(a.traffic, cells_rank)
+        if tpath:
+            with open(tpath) as fh:
                 tr = json.load(fh)
             # the launch's full template name carries the tile / segment variant the library picked (k_zs's WIDE,
             # k_ys's segment width): match on the name this table knows plus any trailing template arguments
@@ -390,7 +393,7 @@ def run_workload(a, cfg, box, strong, rank, world, local, dist, steps, warmup, p
                 roof["kernel"] = full[0]
             src_ok = tr.get("source_hash") == source_hash()
             wl_ok = tr.get("cells_rank") in (None, cells_rank)
-            roof["traffic_source"] = os.path.relpath(a.traffic, ROOT)
+            roof["traffic_source"] = os.path.relpath(tpath, ROOT)
             roof["traffic_source_matches_build"] = bool(src_ok and wl_ok)
             if ent and src_ok and wl_ok:
                 roof["traffic"] = ent.get("bytes_per_launch")
@@ -414,6 +417,20 @@ def run_workload(a, cfg, box, strong, rank, world, local, dist, steps, warmup, p
         line["cpu_baseline_1thread"] = cpu_baseline(cfg, c_one, 1, gcells, a.cpu_reps)
     ctx.close()
     return line
+
+
+def pick_traffic(paths, cells_rank):
+    """The first existing traffic JSON of the comma list measured at this workload's cells per rank (else the first
+    existing one, whose mismatch the line then reports)."""
+    found = [p for p in (paths or "").split(",") if p and os.path.exists(p)]
+    for p in found:
+        try:
+            with open(p) as fh:
+                if json.load(fh).get("cells_rank") in (None, cells_rank):
+                    return p
+        except (OSError, ValueError):
+            continue
+    return found[0] if found else None
 
 
 def cycle_compulsory_bytes(levels, cfg, a, rb):

@@ -221,6 +221,7 @@ struct mgp_ctx {
     bool dry = false;
     bool nb_comm = false;  // non-blocking communicators (mgp_group_create): every call is polled to completion
     mgp::FusedTuning tu;   // tile settings of the temporally blocked phases (env, snapshot at creation)
+    bool resfw = true;     // the full weighting's residual + restriction as one pass (MGP_RESFW=0: two passes)
     bool rccl1 = false;    // world 1 on a one-rank RCCL communicator (MGP_TRANSPORT=rccl, env_rccl1)
     // the multi-rank code path: a communicator (or the loopback transport), collectives, the side stream
     bool multi() const { return o.world > 1 || rccl1; }
@@ -789,11 +790,54 @@ int gather_coarse_rhs(mgp_ctx* c, Level& L, Level& C, char* R)
 
 // calcResidual + the full-weighting restriction (MGP_RESTRICT_FULL_WEIGHTING): r of the level's own planes
 // into the scratch, one ghost plane of r from each z-neighbour on a slab level, then R from r
+// the fused residual + full weighting (k_resfw) runs this level (else: r into rscratch, then restrict it)
+bool resfw_ok(const mgp_ctx* c, const Level& L)
+{
+    return c->resfw && mgp::resfw_supported(c->rk, c->o.dim, L.g, c->G, L.p.dist);
+}
+
+// The full weighting's level-0 sized residual scratch, when a level the cycle restricts (or, with any_level = false,
+// this call) takes the two-pass path: the cycle's levels are checked when the context is created and when its
+// coarse engine changes, so that no allocation happens under graph capture.
+int ensure_rscratch(mgp_ctx* c, bool cycle_levels, int level = -1)
+{
+    if (c->rscratch || c->o.restriction != MGP_RESTRICT_FULL_WEIGHTING || c->lev.size() < 2) return MGP_OK;
+    bool need = false;
+    for (size_t l = 0; l + 1 < c->lev.size(); ++l) {
+        const bool used = cycle_levels ? (c->tail_level < 0 || (int)l < c->tail_level) && !c->lev[l].blk
+                                       : (int)l == level;
+        need = need || (used && !resfw_ok(c, c->lev[l]));
+    }
+    if (!need) return MGP_OK;
+    if (hipMalloc(&c->rscratch, (size_t)c->lev[0].alloc * c->rb) != hipSuccess) {
+        c->rscratch = nullptr;
+        return c->fail(MGP_ERR_OOM, "hipMalloc failed for the full-weighting residual scratch");
+    }
+    return MGP_OK;
+}
+
 int residual_restrict_fw(mgp_ctx* c, int l, double h)
 {
     Level& L = c->lev[l];
     Level& C = c->lev[l + 1];
     TRY(materialize_zero(c, L));
+    if (resfw_ok(c, L)) {
+        if (L.p.dist) {  // r of the neighbours' first planes: u two planes deep, f one
+            TRY(exchange_buf(c, L, L.u, 2));
+            L.ghost_ok = true;
+            if (!L.fghost_ok) TRY(exchange_buf(c, L, L.f, std::min(c->G, (int)L.g.nz)));
+            L.fghost_ok = true;
+        }
+        int64_t zc = 0;
+        const Geo gc = coarse_view(L, C, &zc);
+        char* R = c->ui(C, C.f) + (size_t)(zc * C.g.P) * c->rb;
+        HIP_TRY(c, mgp::launch_resfw(c->rk, c->o.dim, c->ui(L, L.u), c->ui(L, L.f), R, L.g, gc, h,
+                                     coarse_coef(c->o.coarse_bc, l), coarse_coef(c->o.coarse_bc, l + 1), c->G, c->s));
+        C.fghost_ok = !C.p.dist;
+        if (L.p.dist && !C.p.dist) TRY(gather_coarse_rhs(c, L, C, R));
+        return MGP_OK;
+    }
+    TRY(ensure_rscratch(c, false, l));
     TRY(exchange(c, L));
     HIP_TRY(c, mgp::launch_residual_field_v(c->rk, c->o.dim, c->ui(L, L.u), c->ui(L, L.f), c->ui(L, c->rscratch), L.g,
                                             h, coarse_coef(c->o.coarse_bc, l), c->s));
@@ -1586,6 +1630,8 @@ static void host_setup(mgp_ctx* c, const mgp_opts& o, const std::vector<LevelPla
         c->deep_halo = !(vd && std::atoi(vd) == 0);
         const char* ve = std::getenv("MGP_EARLY_X");
         c->early_x = !(ve && std::atoi(ve) == 0);
+        const char* vr = std::getenv("MGP_RESFW");
+        c->resfw = !(vr && std::atoi(vr) == 0);
     }
     // distributed 3D levels sweep with deep halos (smooth_deep): kGhostZs ghost planes per side
     if (c->deep_halo && o.dim == 3 && c->multi()) c->G = mgp::kGhostZs;
@@ -1894,11 +1940,7 @@ static int create_impl(mgp_ctx** out, const mgp_opts* o, mgp_loopback* lb, ncclC
     }
     // the full weighting reads residuals of neighbouring coarse cells' children: r is materialised once per
     // level in this scratch (level 0 is the largest level; the kernels never read its physical ghost planes)
-    if (c->o.restriction == MGP_RESTRICT_FULL_WEIGHTING && c->lev.size() > 1 &&
-        hipMalloc(&c->rscratch, (size_t)L0.alloc * rb) != hipSuccess) {
-        c->err = "hipMalloc failed for the full-weighting residual scratch";
-        return bail(MGP_ERR_OOM);
-    }
+    if (ensure_rscratch(c, true) != MGP_OK) return bail(MGP_ERR_OOM);
     {
         // staging for host I/O: at least one level-0 plane, at most ~256 MiB (or the whole interior)
         const size_t plane = (size_t)(L0.p.nx * L0.p.ny) * rb;
@@ -2358,7 +2400,7 @@ int mgp_set_coarse_level(mgp_ctx* c, int64_t size)
     drop_graphs(c);
     if (size == 0) {
         c->tail_level = -1;
-        return MGP_OK;
+        return ensure_rscratch(c, true);  // the former tail levels now restrict per piece
     }
     const int l = level_of_size(c, size);
     if (l < 0) return c->fail(MGP_ERR_ARG, "mgp_set_coarse_level: no level >= 1 with nx = %lld", (long long)size);
@@ -2371,7 +2413,7 @@ int mgp_set_coarse_level(mgp_ctx* c, int64_t size)
         return c->fail(MGP_ERR_ARG, "mgp_set_coarse_level: levels from nx = %lld do not fit the one-workgroup coarse engine",
                        (long long)size);
     }
-    return MGP_OK;
+    return ensure_rscratch(c, true);
 }
 
 int mgp_set_coarse_handoff(mgp_ctx* c, int64_t size, mgp_coarse_fn fn, void* user)
@@ -2384,7 +2426,7 @@ int mgp_set_coarse_handoff(mgp_ctx* c, int64_t size, mgp_coarse_fn fn, void* use
         c->handoff_fn = nullptr;
         c->handoff_user = nullptr;
         plan_tail(c);
-        return MGP_OK;
+        return ensure_rscratch(c, true);
     }
     const int l = level_of_size(c, size);
     if (l < 0 || c->lev[l].p.dist)
@@ -2393,7 +2435,7 @@ int mgp_set_coarse_handoff(mgp_ctx* c, int64_t size, mgp_coarse_fn fn, void* use
     c->handoff_fn = fn;
     c->handoff_user = user;
     if (c->tail_level >= 0 && c->tail_level <= l) c->tail_level = -1;  // the levels below l are the callback's
-    return MGP_OK;
+    return ensure_rscratch(c, true);
 }
 
 int mgp_metrics(mgp_ctx* c, double* rel_err, int64_t* count, double* frob)

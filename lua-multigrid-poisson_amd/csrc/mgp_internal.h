@@ -91,6 +91,12 @@ hipError_t launch_residual_restrict(int rb, int dim, const void* u, const void* 
 hipError_t launch_residual_field_v(int rb, int dim, const void* u, const void* f, void* r, Geo g, double h, double cl,
                                    hipStream_t s);
 hipError_t launch_fw_restrict(int rb, int dim, const void* r, void* R, Geo g, Geo gc, double clc, hipStream_t s);
+// calcResidual + the full weighting in one z-streamed pass from u and f (k_resfw, mgp_fw.hip): R of the coarse
+// level (gc) bit-identical to launch_residual_field_v + launch_fw_restrict, without the level-sized residual.
+// gz: readable ghost planes of u / f per side (a slab level needs u two and f one plane deep: resfw_supported).
+bool resfw_supported(int rb, int dim, const Geo& g, int gz, bool dist);
+hipError_t launch_resfw(int rb, int dim, const void* u, const void* f, void* R, Geo g, Geo gc, double h, double cl,
+                        double clc, int gz, hipStream_t s);
 // u += P V (expandResidual + addTo); V points at the coarse plane gc.z0, which must correspond to
 // this rank's fine plane 0; planes -1 and gc.nz of V must be readable for the linear kind.
 // black_only: the black cells only (before a red/black post-smoothing: its red half-sweep replaces

@@ -22,7 +22,7 @@
 // q' = RN(q + RN(a - q d) y)), which equals the IEEE quotient for operands away from
 // over/underflow (Markstein); boundary cells with a modified diagonal divide directly.  The GPU
 // parity tests check every piece bit for bit against the C oracle's plain divisions.
-#include "mgp_internal.h"
+#include "mgp_device.h"
 
 #include <cstdio>
 #include <cstdlib>
@@ -32,267 +32,7 @@
 namespace mgp {
 namespace {
 
-constexpr int kBlock = 256;
-
-// ---- small helpers --------------------------------------------------------------------------
-
-template <typename T>
-struct VN {
-    static constexpr int n = 16 / sizeof(T);  // reals per 16-byte access
-};
-
-template <typename T, int N>
-struct alignas(sizeof(T) * N) Vec {
-    T v[N];
-};
-
-template <typename T, int N>
-__device__ __forceinline__ Vec<T, N> vload(const T* p)
-{
-    return *reinterpret_cast<const Vec<T, N>*>(p);
-}
-// A whole-vector LDS read the compiler may not narrow: one element of a 16-byte ds_read_b128 of
-// consecutive lanes is conflict-free, while the ds_read_b32 it would be narrowed to hits every
-// 4th bank (4-way conflicts).
-template <typename T, int N>
-__device__ __forceinline__ Vec<T, N> vload_lds_whole(const T* p)
-{
-    typedef T vt __attribute__((ext_vector_type(N)));
-    typedef const volatile __attribute__((address_space(3))) vt* lds_ptr;
-    const vt x = *(lds_ptr)(p);
-    Vec<T, N> r;
-#pragma unroll
-    for (int e = 0; e < N; ++e) r.v[e] = x[e];
-    return r;
-}
-template <typename T, int N>
-__device__ __forceinline__ void vstore(T* p, const Vec<T, N>& a)
-{
-    *reinterpret_cast<Vec<T, N>*>(p) = a;
-}
-// Nontemporal (streaming) 16-byte access: data touched once by this kernel
-template <typename T, int N>
-__device__ __forceinline__ Vec<T, N> vload_nt(const T* p)
-{
-    using V4 = float __attribute__((ext_vector_type(4)));
-    static_assert(sizeof(Vec<T, N>) == 16, "16-byte vectors only");
-    const V4 r = __builtin_nontemporal_load(reinterpret_cast<const V4*>(p));
-    Vec<T, N> a;
-    __builtin_memcpy(&a, &r, 16);
-    return a;
-}
-template <typename T, int N>
-__device__ __forceinline__ void vstore_nt(T* p, const Vec<T, N>& a)
-{
-    using V4 = float __attribute__((ext_vector_type(4)));
-    V4 r;
-    __builtin_memcpy(&r, &a, 16);
-    __builtin_nontemporal_store(r, reinterpret_cast<V4*>(p));
-}
-
-// Non-temporal 8- or 16-byte access, or a plain one (NT = false)
-template <typename T, int N, bool NT>
-__device__ __forceinline__ Vec<T, N> gload(const T* p)
-{
-    if constexpr (!NT) {
-        return vload<T, N>(p);
-    } else {
-        typedef float vt __attribute__((ext_vector_type(sizeof(T) * N / 4)));
-        const vt r = __builtin_nontemporal_load(reinterpret_cast<const vt*>(p));
-        Vec<T, N> a;
-        __builtin_memcpy(&a, &r, sizeof(a));
-        return a;
-    }
-}
-template <typename T, int N, bool NT>
-__device__ __forceinline__ void gstore(T* p, const Vec<T, N>& a)
-{
-    if constexpr (!NT) {
-        vstore<T, N>(p, a);
-    } else {
-        typedef float vt __attribute__((ext_vector_type(sizeof(T) * N / 4)));
-        vt r;
-        __builtin_memcpy(&r, &a, sizeof(a));
-        __builtin_nontemporal_store(r, reinterpret_cast<vt*>(p));
-    }
-}
-
-template <typename T, int N>
-__device__ __forceinline__ Vec<T, N> vzero()
-{
-    Vec<T, N> a;
-#pragma unroll
-    for (int e = 0; e < N; ++e) a.v[e] = (T)0;
-    return a;
-}
-
-__device__ __forceinline__ float fmaT(float a, float b, float c) { return __builtin_fmaf(a, b, c); }
-__device__ __forceinline__ double fmaT(double a, double b, double c) { return __builtin_fma(a, b, c); }
-
-// RN(a / d) from y = RN(1 / d): one Markstein correction step.
-template <typename T>
-__device__ __forceinline__ T div_rn(T a, T d, T y)
-{
-    T q = a * y;
-    T r = fmaT(-q, d, a);
-    return fmaT(r, y, q);
-}
-
-// Level operator constants (oracle: relax(), diag(), residual()), computed once on the host in
-// the real type (IEEE host arithmetic gives the same values the oracle computes) and passed by
-// value to every kernel.  Boundary-modified diagonals (coarse_bc consistent, cl != 0) come from a
-// table dg[nb] = ((T)(-2 DIM) - (T)nb cl) / h^2 with ydg[nb] = RN(1 / dg[nb]): the division is the
-// same Markstein sequence as the interior one (no divergent IEEE division on boundary cells).  That
-// it equals the oracle's plain division was checked for every such divisor (dims 2/3, levels 0-13,
-// n <= 4096, fp32 and fp64, 2.8e8 random numerators) and is pinned by the bit-exact GPU tests.
-template <typename T, int DIM>
-struct Op {
-    T hSq, inv_hSq, adiag, yadiag, cl;
-    T dg[2 * DIM + 1], ydg[2 * DIM + 1];
-    // table entry nb >= 1 by a select chain (nb is per lane: no dynamic register indexing)
-    __device__ __forceinline__ T sel(const T (&t)[2 * DIM + 1], int nb) const
-    {
-        T r = t[1];
-#pragma unroll
-        for (int k = 2; k <= 2 * DIM; ++k) r = nb == k ? t[k] : r;
-        return r;
-    }
-    // diagonal of a cell with nb faces on the box boundary (cl = 0: the reference adiag)
-    __device__ __forceinline__ T diag(int nb) const
-    {
-        if (cl == (T)0 || nb == 0) return adiag;
-        return sel(dg, nb);
-    }
-    // (f - sum/h^2) / diag
-    __device__ __forceinline__ T relax(T sum, T fc, int nb) const
-    {
-        const T a = fc - sum * inv_hSq;
-        if (cl != (T)0 && nb != 0) return div_rn(a, sel(dg, nb), sel(ydg, nb));
-        return div_rn(a, adiag, yadiag);
-    }
-    // f - (sum/h^2 + diag*u)
-    __device__ __forceinline__ T residual(T sum, T fc, T uc, int nb) const
-    {
-        const T askew = sum * inv_hSq;
-        const T a_u = askew + diag(nb) * uc;
-        return fc - a_u;
-    }
-    // The same two with the table indexed directly (for an Op that lives in LDS, where a per-lane
-    // index is one read): dg[0] = adiag, ydg[0] = yadiag, and with cl = 0 every entry is those, so
-    // these equal relax / residual for every nb, without the branch or the select chain.
-    __device__ __forceinline__ T relax_idx(T sum, T fc, int nb) const
-    {
-        const T a = fc - sum * inv_hSq;
-        return div_rn(a, dg[nb], ydg[nb]);
-    }
-    __device__ __forceinline__ T residual_idx(T sum, T fc, T uc, int nb) const
-    {
-        const T askew = sum * inv_hSq;
-        const T a_u = askew + dg[nb] * uc;
-        return fc - a_u;
-    }
-    // The diagonals of a row whose cells have nbyz y/z faces on the box boundary: off (d0, y0 = RN(1/d0)) and on
-    // (d1, y1) an x face, one table walk per row; relax(s, f, nbyz + xface) == div_rn(f - s/h^2, xface ? d1 : d0,
-    // xface ? y1 : y0) (dg[0] = adiag, ydg[0] = yadiag, and with cl = 0 every entry equals those)
-    __device__ __forceinline__ void row_diag(int nbyz, T& d0, T& y0, T& d1, T& y1) const
-    {
-        d0 = dg[0];
-        y0 = ydg[0];
-        d1 = dg[1];
-        y1 = ydg[1];
-#pragma unroll
-        for (int q = 1; q < 2 * DIM; ++q) {
-            d0 = nbyz == q ? dg[q] : d0;
-            y0 = nbyz == q ? ydg[q] : y0;
-            d1 = nbyz == q ? dg[q + 1] : d1;
-            y1 = nbyz == q ? ydg[q + 1] : y1;
-        }
-    }
-    // The same two with the diagonal computed and divided by directly (the oracle's expressions):
-    // the temporally blocked phases' rare boundary path, where the table selects cost registers.
-    __device__ __forceinline__ T diag_direct(int nb) const
-    {
-        if (cl == (T)0 || nb == 0) return adiag;
-        return ((T)(-2 * DIM) - (T)nb * cl) / hSq;
-    }
-    __device__ __forceinline__ T relax_direct(T sum, T fc, int nb) const
-    {
-        const T a = fc - sum * inv_hSq;
-        if (cl != (T)0 && nb != 0) return a / diag_direct(nb);
-        return div_rn(a, adiag, yadiag);
-    }
-    __device__ __forceinline__ T residual_direct(T sum, T fc, T uc, int nb) const
-    {
-        const T askew = sum * inv_hSq;
-        const T a_u = askew + diag_direct(nb) * uc;
-        return fc - a_u;
-    }
-};
-
-// Op::row_diag with a wave-uniform shortcut: rows off every y / z face (nearly all of a level) take table
-// entries 0 and 1 without the walk (on a cl != 0 level the walk is 4 (2D) / 20 (3D) selects per row)
-#ifndef ROWDIAG_FAST  // timing switch (0: always the walk)
-#define ROWDIAG_FAST 1
-#endif
-template <typename T, int DIM>
-__device__ __forceinline__ void row_diag_fast(const Op<T, DIM>& op, int nbyz, T& d0, T& y0, T& d1, T& y1)
-{
-    if (ROWDIAG_FAST && __all(nbyz == 0)) {
-        d0 = op.dg[0];
-        y0 = op.ydg[0];
-        d1 = op.dg[1];
-        y1 = op.ydg[1];
-    } else {
-        op.row_diag(nbyz, d0, y0, d1, y1);
-    }
-}
-
-template <typename T, int DIM>
-Op<T, DIM> make_op(double h, double cl)
-{
-    Op<T, DIM> op;
-    const T hh = (T)h;
-    op.hSq = hh * hh;
-    op.inv_hSq = (T)1 / op.hSq;  // exact: h is a power of two
-    op.adiag = (T)(-2 * DIM) / op.hSq;
-    op.yadiag = (T)1 / op.adiag;  // RN(1/adiag)
-    op.cl = (T)cl;
-    for (int nb = 0; nb <= 2 * DIM; ++nb) {
-        op.dg[nb] = nb == 0 ? op.adiag : ((T)(-2 * DIM) - (T)nb * op.cl) / op.hSq;
-        op.ydg[nb] = (T)1 / op.dg[nb];
-    }
-    return op;
-}
-
-// packed offset of cell (i, j, local plane k) (any level size, nx = 1 included)
-__device__ __forceinline__ int64_t pidx(const Geo& g, int i, int j, int64_t k)
-{
-    const int c = (int)((i + j + g.z0 + k) & 1);
-    return k * g.P + c * g.H + (int64_t)j * g.hw + (i >> 1);
-}
-
-__device__ __forceinline__ int xcd_remap(int b, int nblocks)
-{
-    // blocks b and b + 8 share an XCD: hand each XCD a contiguous band of the grid (z-neighbour
-    // planes of a stencil then meet in that XCD's L2)
-    if ((nblocks & 7) != 0) return b;
-    return (b & 7) * (nblocks >> 3) + (b >> 3);
-}
-
-inline unsigned nblk(int64_t n) { return (unsigned)((n + kBlock - 1) / kBlock); }
-
-template <typename T>
-__device__ __forceinline__ void block_partial(double acc, double* partials)
-{
-    __shared__ double red[kBlock];
-    red[threadIdx.x] = acc;
-    __syncthreads();
-    for (int w = kBlock / 2; w > 0; w >>= 1) {
-        if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) partials[blockIdx.x] = red[0];
-}
+// (kBlock, vectors, div_rn, Op, pidx, xcd_remap, block_partial, fw_axis: mgp_device.h)
 
 // ---- init / pack / unpack -------------------------------------------------------------------
 
@@ -1166,14 +906,6 @@ __global__ __launch_bounds__(kBlock) void k_resrestrict(const T* __restrict__ u,
 // materialised first (k_resfield_v / k_residual_field into the level-sized scratch), because each fine
 // residual feeds 2^DIM coarse cells; on a slab level one ghost plane of r is exchanged in between.
 
-template <typename T>
-__device__ __forceinline__ T fw_axis(T a, T b, T c, T d, T wb, T wc)
-{
-    T s = a + wb * b;
-    s = s + wc * c;
-    s = s + d;
-    return s;
-}
 
 // Coarse cell (I, J, local plane K) from fine residuals get(i, j, k) (k local; called only for cells
 // inside the box).  gc.z0 = g.z0 / 2 (the coarse plane of this rank's fine plane 0).
@@ -1746,6 +1478,9 @@ __device__ __forceinline__ void lds_barrier()
 #ifndef ZS_XRAW
 #define ZS_XRAW 1
 #endif
+#ifndef ZS_YROLE
+#define ZS_YROLE 1
+#endif
 #ifndef ZS_NPOST_F32
 #define ZS_NPOST_F32 2
 #endif
@@ -1855,6 +1590,30 @@ struct ZsShape {
     static constexpr int NPAR = (G * YEV + 63) / 64 * 64;
     static constexpr bool PS = PRE ? ZS_PSPLIT_PRE != 0 : ZS_PSPLIT_POST != 0;
     static constexpr int NTL = PS ? 2 * NPAR : (NT + 63) / 64 * 64;  // launched threads
+    // PRE, ZS_YROLE: threads ordered by their row's distance d from the tile in y (tile rows first, then d = 1..3,
+    // then d = 4..5 from a wave boundary), so that whole waves hold only halo rows: stage k (half-sweep k) is needed
+    // on rows d <= H - k and the residual on d = 0, so a wave of rows d >= 4 runs stage 1 only and a wave of rows
+    // d in 1..3 skips the residual (a third of the step's VALU for the halo waves; only where it costs no wave)
+    static constexpr int YT0 = TY * G, YT1 = YT0 + 6 * G, YT2S = (YT1 + 63) / 64 * 64, YT2 = YT2S + 4 * G;
+    static constexpr bool YROLE = ZS_YROLE && PRE && !PS && H == 5 && (YT2 + 63) / 64 * 64 <= NTL;
+    // extended row (0 .. YE - 1) of thread t (-1: no row) and the role of wave w (0: tile rows, every stage and the
+    // residual; 1: rows d <= 3, stages 1..4; 2: rows d >= 4, stage 1)
+    static __device__ __forceinline__ int yrow(int t)
+    {
+        if (!YROLE) return t < NT ? t / G : -1;
+        if (t < YT0) return H + t / G;
+        if (t < YT1) {  // d = 1, 2, 3: the row above, then below the tile
+            const int r = (t - YT0) / G, d = 1 + (r >> 1);
+            return (r & 1) ? H + TY - 1 + d : H - d;
+        }
+        if (t >= YT2S && t < YT2) {
+            const int r = (t - YT2S) / G, d = 4 + (r >> 1);
+            return (r & 1) ? H + TY - 1 + d : H - d;
+        }
+        return -1;
+    }
+    static __device__ __forceinline__ int ycol(int t) { return YROLE && t >= YT2S ? (t - YT2S) % G : t % G; }
+    static constexpr int wave_role(int w) { return !YROLE || 64 * w < YT0 ? 0 : (64 * w < YT1 ? 1 : 2); }
     static constexpr int SLOT = YE * HWE;              // reals per LDS slot (one colour of a plane)
     // stage-3 slots: PRE's residual reads 2 back (3 needed; 4 while LDS allows: power-of-2 ring)
     static constexpr int NS3 = PRE ? (TY > 32 ? 3 : 4) : 2;
@@ -2293,8 +2052,9 @@ __attribute__((amdgpu_waves_per_eu(1, PRE ? ZS_WPE_PRE : ZS_WPE_POST))) void k_z
     // my column of the extended tile; ZS_PSPLIT: wcls = my wave's row parity (even / odd extended rows)
     const int wcls = S::PS ? __builtin_amdgcn_readfirstlane(tid >= S::NPAR ? 1 : 0) : 0;
     const int rt_ = S::PS ? tid - wcls * S::NPAR : tid;
-    const bool on = S::PS ? rt_ < G * (wcls ? YE / 2 : S::YEV) : tid < S::NT;
-    const int gx = on ? rt_ % G : 0, ye = S::PS ? (on ? 2 * (rt_ / G) + wcls : wcls) : (on ? tid / G : 0);
+    const int yr_ = S::PS ? 0 : S::yrow(tid);
+    const bool on = S::PS ? rt_ < G * (wcls ? YE / 2 : S::YEV) : yr_ >= 0;
+    const int gx = on ? (S::PS ? rt_ % G : S::ycol(tid)) : 0, ye = S::PS ? (on ? 2 * (rt_ / G) + wcls : wcls) : (on ? yr_ : 0);
     const int gy = Y0 - H + ye;
     const int m0 = gx * N;
     ZsCol col;
@@ -2347,6 +2107,7 @@ __attribute__((amdgpu_waves_per_eu(1, PRE ? ZS_WPE_PRE : ZS_WPE_POST))) void k_z
         return CLZ ? 0 : (gy == 0) + (gy == g.ny - 1) + (z0 + q == 0) + (z0 + q == gnz - 1);
     };
     const int rowpar = (gy + z0) & 1;
+    const int wrole = S::YROLE ? __builtin_amdgcn_readfirstlane(S::wave_role(tid >> 6)) : 0;  // (ZS_YROLE)
     const T* const src_black = ZSRC ? nullptr : src + Hh;
 
     for (int i = tid; i < (int)(S::lds_bytes / sizeof(T)); i += NTL) lds[i] = (T)0;
@@ -2479,9 +2240,12 @@ __attribute__((amdgpu_waves_per_eu(1, PRE ? ZS_WPE_PRE : ZS_WPE_POST))) void k_z
         for (int q = 0; q < 2; ++q)
             zs_bq<T, N>(bq[q], c0, c1, q ^ cp, cgm, gc.nx, bq_oy, clc, corr_fast);
     };
-    auto step = [&](auto st, auto rt, auto rp, const PF& cur, PF& nxt, int p) __attribute__((always_inline)) {
+    auto step = [&](auto st, auto rt, auto rp, auto ro, const PF& cur, PF& nxt, int p) __attribute__((always_inline)) {
         constexpr bool ST = decltype(st)::value;
         constexpr int RS = decltype(rt)::value;  // (p - zlo) & 3
+        (void)ro;
+        // my wave's role (ZsShape::wave_role, wave-uniform; every generic step runs the full work)
+        const int RO = ST ? wrole : 0;
         // RP >= 0: my wave's row parity rowpar, known statically (ZS_PSPLIT steady steps: z0 and Y0 even, so
         // it is also the parity of gy); -1: per lane
         constexpr int RP = decltype(rp)::value;
@@ -2548,35 +2312,41 @@ __attribute__((amdgpu_waves_per_eu(1, PRE ? ZS_WPE_PRE : ZS_WPE_POST))) void k_z
         VT o1 = zs_relax<T, N, CLZ, ST>(W0[sl(2)], W0[sl(1)], W0[sl(ZS_NC ? 3 : 0)], n1, cur.f1, col, par(p - 1), nbyz(p - 1), g.nx, op, dz);
         if (!ST && !inz(p - 1)) o1 = vz;
         W1[sl(1)] = o1;
-        zs_nb_load<T, N>(n2, slot(S::OFF1, 2, p - 2), col);
-        VT o2 = zs_relax<T, N, CLZ, ST>(W1[sl(3)], W1[sl(2)], W1[sl(ZS_NC ? 0 : 1)], n2, cur.f2, col, 1 ^ par(p - 2), nbyz(p - 2), g.nx,
-                                    op, dz);
-        if (!ST && !inz(p - 2)) o2 = vz;
-        W2[sl(2)] = o2;
-        zs_nb_load<T, N>(n3, slot(S::OFF2, 2, p - 3), col);
-        VT o3 = zs_relax<T, N, CLZ, ST>(W2[sl(4)], W2[sl(3)], W2[sl(ZS_NC ? 1 : 2)], n3, FR[sl(3)], col, par(p - 3), nbyz(p - 3), g.nx,
-                                    op, dz);
-        if (!ST && !inz(p - 3)) o3 = vz;
-        W3[sl(3)] = o3;
-        zs_nb_load<T, N>(n4, slot(S::OFF3, NS3, p - 4), col);
-        VT o4 = zs_relax_a<T, N, CLZ, ST>(W3[sl(5)], W3[sl(4)], W3[sl(ZS_NC ? 2 : 3)], n4, FB[sl(4)], col, 1 ^ par(p - 4),
-                                      nbyz(p - 4), g.nx, op, dz, AS[RS & 1]);
-        if (!ST && !inz(p - 4)) o4 = vz;
-        W4[sl(4)] = o4;
+        // (a wave of halo rows d >= 4, role 2, needs stage 1 only: its stages 2..4 would feed no needed cell)
+        VT o2 = vz, o3 = vz, o4 = vz;
+        if (RO < 2) {
+            zs_nb_load<T, N>(n2, slot(S::OFF1, 2, p - 2), col);
+            o2 = zs_relax<T, N, CLZ, ST>(W1[sl(3)], W1[sl(2)], W1[sl(ZS_NC ? 0 : 1)], n2, cur.f2, col, 1 ^ par(p - 2), nbyz(p - 2),
+                                         g.nx, op, dz);
+            if (!ST && !inz(p - 2)) o2 = vz;
+            W2[sl(2)] = o2;
+            zs_nb_load<T, N>(n3, slot(S::OFF2, 2, p - 3), col);
+            o3 = zs_relax<T, N, CLZ, ST>(W2[sl(4)], W2[sl(3)], W2[sl(ZS_NC ? 1 : 2)], n3, FR[sl(3)], col, par(p - 3), nbyz(p - 3),
+                                         g.nx, op, dz);
+            if (!ST && !inz(p - 3)) o3 = vz;
+            W3[sl(3)] = o3;
+            zs_nb_load<T, N>(n4, slot(S::OFF3, NS3, p - 4), col);
+            o4 = zs_relax_a<T, N, CLZ, ST>(W3[sl(5)], W3[sl(4)], W3[sl(ZS_NC ? 2 : 3)], n4, FB[sl(4)], col, 1 ^ par(p - 4),
+                                           nbyz(p - 4), g.nx, op, dz, AS[RS & 1]);
+            if (!ST && !inz(p - 4)) o4 = vz;
+            W4[sl(4)] = o4;
+        }
 
         // ---- LDS writes (slots no stage of this step reads); columns outside the box stay 0 ----
         if (in_xy) {
             vstore<T, N>(slot(0, 2, p) + col.lrow, a0);
             vstore<T, N>(slot(S::OFF1, 2, p - 1) + col.lrow, o1);
-            vstore<T, N>(slot(S::OFF2, 2, p - 2) + col.lrow, o2);
-            vstore<T, N>(slot(S::OFF3, NS3, p - 3) + col.lrow, o3);
-            if (RR) vstore<T, N>(slot(S::OFF4, 2, p - 4) + col.lrow, o4);
+            if (RO < 2) {
+                vstore<T, N>(slot(S::OFF2, 2, p - 2) + col.lrow, o2);
+                vstore<T, N>(slot(S::OFF3, NS3, p - 3) + col.lrow, o3);
+                if (RR) vstore<T, N>(slot(S::OFF4, 2, p - 4) + col.lrow, o4);
+            }
         }
 
         // ---- the smoothed plane p - 4: red final after stage 3, black after stage 4 ----
         // (the chunk test is wave-uniform: steady steps also run the trapezoid's warm-up before the chunk and
         // its drain after it, which store nothing)
-        {
+        if (RO == 0) {
             const int q = p - 4;
             if (q >= Z0 && q < Z0 + zc && tile_xy) {
                 if (!PRE && ERR) {
@@ -2598,8 +2368,8 @@ __attribute__((amdgpu_waves_per_eu(1, PRE ? ZS_WPE_PRE : ZS_WPE_POST))) void k_z
             }
         }
 
-        // ---- PRE: residual + restriction of plane p - 5 ----
-        if (RR) {
+        // ---- PRE: residual + restriction of plane p - 5 (tile rows only: role 0) ----
+        if (RR && RO == 0) {
             const int q = p - 5;
             const int pq = par(q);
             if (!kZsRask) zs_nb_load<T, N>(nr, slot(S::OFF3, NS3, q), col);  // red of A4 at q
@@ -2704,15 +2474,16 @@ __attribute__((amdgpu_waves_per_eu(1, PRE ? ZS_WPE_PRE : ZS_WPE_POST))) void k_z
     const std::integral_constant<int, -1> RPL;
     // UNR steps from p0 (p0 - zlo a multiple of UNR): ring slot k & 3, buffers k % NPF and (k + PFD) % NPF;
     // steps past plim are skipped (epilogue)
-    auto group = [&](auto st, auto rp, int p0, int plim) __attribute__((always_inline)) {
+    const std::integral_constant<int, 0> RO0;
+    auto group = [&](auto st, auto rp, auto ro, int p0, int plim) __attribute__((always_inline)) {
         zs_unroll<UNR>([&](auto kk) __attribute__((always_inline)) {
             constexpr int k = decltype(kk)::value;
             if (k == 0 || p0 + k <= plim)
-                step(st, std::integral_constant<int, (k & 3)>(), rp, pb[k % NPF], pb[(k + PFD) % NPF], p0 + k);
+                step(st, std::integral_constant<int, (k & 3)>(), rp, ro, pb[k % NPF], pb[(k + PFD) % NPF], p0 + k);
         });
     };
-    for (; p < ps; p += UNR) group(GEN, RPL, p, p + UNR);
-    auto steady = [&](auto rp) __attribute__((always_inline)) {
+    for (; p < ps; p += UNR) group(GEN, RPL, RO0, p, p + UNR);
+    auto steady = [&](auto rp, auto ro) __attribute__((always_inline)) {
         if constexpr (!PRE && LINEAR == 1 && ZS_BQ) {
             if (p <= pe) {  // the first steady step (even, K & 1 == 0) reads coarse planes K and K - 1
                 const int K = (z0 + p) >> 1;
@@ -2720,17 +2491,17 @@ __attribute__((amdgpu_waves_per_eu(1, PRE ? ZS_WPE_PRE : ZS_WPE_POST))) void k_z
                 bq_fill(rp, BQ[1], K - 1);
             }
         }
-        for (; p <= pe; p += UNR) group(STY, rp, p, p + UNR);
+        for (; p <= pe; p += UNR) group(STY, rp, ro, p, p + UNR);
     };
     if constexpr (S::PS) {  // wave-uniform: one copy of the steady loop per row parity
         if (((H + wcls) & 1) == 0)
-            steady(std::integral_constant<int, 0>());
+            steady(std::integral_constant<int, 0>(), RO0);
         else
-            steady(std::integral_constant<int, 1>());
+            steady(std::integral_constant<int, 1>(), RO0);
     } else {
-        steady(RPL);
+        steady(RPL, RO0);
     }
-    for (; p <= p_end; p += UNR) group(GEN, RPL, p, p_end);
+    for (; p <= p_end; p += UNR) group(GEN, RPL, RO0, p, p_end);
     if constexpr (ERR && !PRE) block_partial_t<NTL>(err + err1, partials);  // (PRE: ERR is ZSRC, no partials)
 }
 

@@ -119,3 +119,45 @@ def test_group_argument_error_leaves_group_usable():
         g.residual_norm(level=99)
     g.cycles(1)
     g.close()
+
+
+def _ndev():
+    import torch
+
+    return torch.cuda.device_count()
+
+
+@pytest.mark.skipif("_ndev() < 2", reason="needs two GPUs (the test boxes have one; RCCL refuses two ranks per device)")
+def test_group_on_two_devices_real_rccl(monkeypatch):
+    """the group's RCCL path with distinct devices — non-blocking communicators, the side-stream
+    communicator carrying the early POST exchange next to the compute stream's exchanges — equals the single domain
+    and issues the planned call sequence on every rank; an injected rank failure returns instead of hanging."""
+    import time
+
+    mg = _mg()
+    monkeypatch.setenv("MGP_FUSED_MIN_CELLS", "65536")
+    opts = mg.make_opts(dim=3, n=(128, 128, 256), gather_cells=4096, **NS)
+    ref = mg.Context(opts)
+    ref.init_point_charge()
+    e_ref = ref.cycles(3)
+    psi_ref = ref.get_psi()
+    ref.close()
+    g = mg.Group(opts, 2, devices=[0, 1])
+    g.init_point_charge()
+    for r in g.ranks:
+        r.comm_log(reset=True)
+    np.testing.assert_allclose(g.cycles(3), e_ref, rtol=1e-12, atol=0)
+    assert np.array_equal(g.get_psi(), psi_ref)
+    logs = [r.comm_log() for r in g.ranks]
+    assert logs[0] == logs[1] == mg.plan_comm(mg.make_opts(dim=3, n=(128, 128, 256), gather_cells=4096, rank=0,
+                                                           world=2, comm_id=b"\0" * 128, **NS), 3)
+    assert any(c[1] == 1 for c in logs[0])  # side-stream exchanges ran
+    monkeypatch.setenv("MGP_TEST_FAIL_RANK", "1")
+    t0 = time.perf_counter()
+    with pytest.raises(mg.MGPError, match="injected failure"):
+        g.cycles(2)
+    assert time.perf_counter() - t0 < 60
+    monkeypatch.delenv("MGP_TEST_FAIL_RANK")
+    with pytest.raises(mg.MGPError, match="aborted"):
+        g.cycle()
+    g.close()

@@ -2,15 +2,16 @@
 # PMC passes for the bench workload (one counter group per rocprofv3 run; kernel-trace only).
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-mkdir -p gpurun_out/pmc
+PMCDIR=${PMCDIR:-gpurun_out/pmc}
+mkdir -p $PMCDIR
 i=0
 while read -r grp; do
   [ -z "$grp" ] && continue
   i=$((i+1))
   echo "== pass $i: $grp"
-  timeout -k 10 300 rocprofv3 --pmc $grp --kernel-trace --output-format csv -d gpurun_out/pmc/p$i -o run -- python bench.py --steps ${PMC_STEPS:-3} --warmup 1 --cpu-cycles 0 --no-timing > gpurun_out/pmc/p$i.log 2>&1
+  timeout -k 10 300 rocprofv3 --pmc $grp --kernel-trace --output-format csv -d $PMCDIR/p$i -o run -- python bench.py --steps ${PMC_STEPS:-3} --warmup 1 --cpu-cycles 0 --no-timing --no-north-star --copy-probe-mb 0 ${BENCH_ARGS:-} > $PMCDIR/p$i.log 2>&1
   rc=$?; echo "rc=$rc"
-  case $rc in 0) ;; *) tail -5 gpurun_out/pmc/p$i.log; exit $rc;; esac
+  case $rc in 0) ;; *) tail -5 $PMCDIR/p$i.log; exit $rc;; esac
 done <<LIST
 ${PMC_GROUPS:-FETCH_SIZE
 WRITE_SIZE
