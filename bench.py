@@ -340,8 +340,11 @@ def run_workload(a, cfg, box, strong, rank, world, local, dist, steps, warmup, p
     lin = 1 if a.prolong == "linear" else 0
     fw = a.restriction == "full_weighting"
     kz = "k_zs" if cfg["dim"] == 3 else "k_ys"  # the temporally blocked phases: planes / rows streamed
+    # PRE's LINEAR: 0 the average restriction inside, 1 smoothing only (the full weighting after it), 2 the full weighting
+    # inside (fp32 3D one-rank levels: mgp_kernels.hip fused_fwf_supported)
+    pre_lin = (2 if (tname == "float" and cfg["dim"] == 3 and world == 1) else 1) if fw else 0
     kernels = {"half_sweep": f"k_half<{tname}, {cfg['dim']}, 1, false>",
-               "fused_pre": f"{kz}<{tname}, true, {1 if fw else 0}, false, true>",
+               "fused_pre": f"{kz}<{tname}, true, {pre_lin}, false, true>",
                "fused_post": f"{kz}<{tname}, false, {lin}, true, true>"}
     coarse = 0.5 ** cfg["dim"]
     # SURVEY.md §8(d) per-sweep accounting (what one launch per half-sweep would move) of the fused phases

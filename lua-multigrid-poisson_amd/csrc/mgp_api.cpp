@@ -999,10 +999,14 @@ int fused_pre(mgp_ctx* c, int l, double h)
     int64_t zc = 0;
     const Geo gc = coarse_view(L, C, &zc);
     const bool fw = c->o.restriction == MGP_RESTRICT_FULL_WEIGHTING;
+    // the full weighting fused into the phase (fp32 level 0 of one rank's whole box), else smoothing only (both
+    // colours stored) and the full weighting after it
+    const bool fwf = fw && mgp::fused_fwf_supported(c->rb, coarse_coef(c->o.coarse_bc, l) == 0.0, L.p.dist);
     mgp::FusedArgs a{};
     a.tu = c->tu;
     a.pre = true;
-    a.linear = fw;  // PRE: 1 = smoothing only (both colours stored), the full weighting follows
+    a.linear = fwf ? 2 : fw;  // PRE: 1 = smoothing only (both colours stored), the full weighting follows
+    a.clc = coarse_coef(c->o.coarse_bc, l + 1);  // (the fused full weighting's face weight 3 - c)
     a.src = L.zero_pending ? nullptr : c->ui(L, L.u);  // null: a fresh zero guess (lazy_zero_ok)
     a.f = c->ui(L, L.f);
     a.dst = c->ui(L, L.t);
@@ -1019,13 +1023,13 @@ int fused_pre(mgp_ctx* c, int l, double h)
     // algorithmic bytes (include/mgpoisson.h): read black u and f, write black u and R / 2^dim
     // (full weighting: both colours of u, the restriction runs after the phase)
     const double coarse = std::ldexp(1.0, -c->o.dim);
-    TRY(timed_end(c, e, MGP_TIMING_FUSED_PRE, (fw ? 2.5 : 2.0 + coarse) * c->rb * (double)level_cells(L)));
+    TRY(timed_end(c, e, MGP_TIMING_FUSED_PRE, (fw && !fwf ? 2.5 : 2.0 + coarse) * c->rb * (double)level_cells(L)));
     std::swap(L.u, L.t);  // u = smoothed; t = the previous iterate (psiOld on level 0)
     L.zero_pending = false;
     L.ghost_ok = !L.p.dist;
     L.ghost_zero = false;
     if (l == 0 && c->in_cycle) c->first_done = true;
-    if (fw) return residual_restrict_fw(c, l, h);
+    if (fw && !fwf) return residual_restrict_fw(c, l, h);
     C.fghost_ok = !C.p.dist;
     if (L.p.dist && !C.p.dist) TRY(gather_coarse_rhs(c, L, C, (char*)a.R));  // as residual_restrict
     return MGP_OK;

@@ -13,14 +13,22 @@
 // so R is bit-identical to the two-pass path and to the oracle (restrict_fw in oracle/mgp_oracle_impl.h).
 #include "mgp_device.h"
 
+#include <type_traits>
+
 namespace mgp {
 namespace {
 
 // fine tile of a workgroup (even, so that a tile's coarse cells are whole) and its threads: one coarse cell each
 template <int DIM>
 struct FwShape {
-    static constexpr int TX = 64, TY = DIM == 3 ? 16 : 32;
-    static constexpr int NT = (TX / 2) * (TY / 2);         // 256 (3D) / 512 (2D) threads
+#ifndef FW_TX
+#define FW_TX 64
+#endif
+#ifndef FW_TY3
+#define FW_TY3 16
+#endif
+    static constexpr int TX = FW_TX, TY = DIM == 3 ? FW_TY3 : 32;
+    static constexpr int NT = (TX / 2) * (TY / 2);         // 256 (3D) / 512 (2D) threads at 64 x 16 / 64 x 32
     static constexpr int UW = TX + 4, UH = TY + 4;         // u staged with 2 cells of halo per side
     static constexpr int RW = TX + 2, RH = TY + 2;         // r with one
     static constexpr int USLOT = UW * UH, RSLOT = RW * RH;
@@ -28,28 +36,15 @@ struct FwShape {
     static constexpr int MW = TX / 2 + 2;                  // packed cells of one colour per staged row
 };
 
-// Stage u of local plane k (both colours, cells X0-2 .. X0+TX+1, Y0-2 .. Y0+TY+1, zero outside the box or the
-// readable planes) into `dst`, unpacked: a thread reads runs of one colour's packed row (coalesced).
-template <typename T, int DIM>
-__device__ __forceinline__ void fw_stage(T* dst, const T* __restrict__ u, const Geo& g, int64_t k, int X0, int Y0,
-                                         int gz, int tid)
-{
+// A thread's share of the staging of one u plane (both colours, cells X0-2 .. X0+TX+1, Y0-2 .. Y0+TY+1, zero outside
+// the box; runs of one colour's packed row per wave, coalesced) and of the residual ring: fixed items, so the
+// in-plane addressing is computed once and each plane's loads are issued a step ahead of their use.
+template <int DIM>
+struct FwItems {
     using S = FwShape<DIM>;
-    const int64_t gk = g.z0 + k;
-    const bool readable = DIM == 2 || (k >= -gz && k < g.nz + gz);
-    const int m0 = X0 / 2 - 1;
-    for (int q = tid; q < 2 * S::UH * S::MW; q += S::NT) {
-        const int mm = q % S::MW, c = (q / S::MW) & 1, jl = q / (2 * S::MW);
-        const int j = Y0 - 2 + jl, m = m0 + mm;
-        const int par = (int)((c + j + gk) & 1);  // x parity of colour c's cells in row j
-        const int i = 2 * m + par;
-        T v = (T)0;
-        if (readable && j >= 0 && j < g.ny && m >= 0 && m < g.hw && i < g.nx)
-            v = u[k * g.P + c * g.H + (int64_t)j * g.hw + m];
-        const int il = i - (X0 - 2);
-        if (il >= 0 && il < S::UW) dst[jl * S::UW + il] = v;
-    }
-}
+    static constexpr int NUI = 2 * S::UH * S::MW, IU = (NUI + S::NT - 1) / S::NT;  // u items per thread
+    static constexpr int IR = (S::RSLOT + S::NT - 1) / S::NT;                      // r cells per thread
+};
 
 template <typename T, int DIM>
 __global__ __launch_bounds__(FwShape<DIM>::NT) void k_resfw(const T* __restrict__ u, const T* __restrict__ f,
@@ -57,6 +52,7 @@ __global__ __launch_bounds__(FwShape<DIM>::NT) void k_resfw(const T* __restrict_
                                                             int kc, int gz)
 {
     using S = FwShape<DIM>;
+    using I = FwItems<DIM>;
     __shared__ T us[S::NU][S::USLOT];
     __shared__ T rs[S::RSLOT];
     const int tid = threadIdx.x;
@@ -68,33 +64,84 @@ __global__ __launch_bounds__(FwShape<DIM>::NT) void k_resfw(const T* __restrict_
     const int cx = g.nx >> 1, cy = g.ny >> 1;
     // my coarse cell and its weights (fw_eval's wb / wc per axis)
     const int Il = tid % (S::TX / 2), Jl = tid / (S::TX / 2);
-    const int I = X0 / 2 + Il, J = Y0 / 2 + Jl;
+    const int Ic = X0 / 2 + Il, Jc = Y0 / 2 + Jl;
     const T w3 = (T)3;
-    const T wbx = I == 0 ? wf : w3, wcx = I == cx - 1 ? wf : w3;
-    const T wby = J == 0 ? wf : w3, wcy = J == cy - 1 ? wf : w3;
+    const T wbx = Ic == 0 ? wf : w3, wcx = Ic == cx - 1 ? wf : w3;
+    const T wby = Jc == 0 ? wf : w3, wcy = Jc == cy - 1 ? wf : w3;
 
-    // r of local plane k on the tile and its one-cell ring into rs (0 outside the box), then my cell's `ay`
-    auto plane_ay = [&](int64_t k, const T* um, const T* uc, const T* up) -> T {
+    // u items: in-plane packed offset (colour c's row j at m) and the LDS cell of each of the two plane parities
+    // (the x parity of colour c's cells in row j flips with the plane); -1 = outside the box (stays 0)
+    int uoff[I::IU], ul0[I::IU], ul1[I::IU];
+#pragma unroll
+    for (int e = 0; e < I::IU; ++e) {
+        const int q = tid + e * S::NT;
+        const int mm = q % S::MW, c = (q / S::MW) & 1, jl = q / (2 * S::MW);
+        const int j = Y0 - 2 + jl, m = X0 / 2 - 1 + mm;
+        const int par0 = (int)((c + j + g.z0) & 1);  // x parity of colour c's cells in row j at even local planes
+        const bool ok = q < I::NUI && j >= 0 && j < g.ny && m >= 0 && m < g.hw;
+        uoff[e] = ok ? (int)(c * g.H + (int64_t)j * g.hw + m) : -1;
+        const int i0 = 2 * m + par0, i1 = 2 * m + (par0 ^ 1);
+        ul0[e] = q < I::NUI && i0 - (X0 - 2) >= 0 && i0 - (X0 - 2) < S::UW ? jl * S::UW + i0 - (X0 - 2) : -1;
+        ul1[e] = q < I::NUI && i1 - (X0 - 2) >= 0 && i1 - (X0 - 2) < S::UW ? jl * S::UW + i1 - (X0 - 2) : -1;
+    }
+    // r cells: in-plane packed offset of f (colour parity of even local planes), box face count, inside the box
+    int foff[I::IR], fpar[I::IR], fnb[I::IR];
+#pragma unroll
+    for (int e = 0; e < I::IR; ++e) {
+        const int q = tid + e * S::NT;
+        const int il = q % S::RW, jl = q / S::RW;
+        const int i = X0 - 1 + il, j = Y0 - 1 + jl;
+        const bool in = q < S::RSLOT && i >= 0 && i < g.nx && j >= 0 && j < g.ny;
+        foff[e] = in ? (int)((int64_t)j * g.hw + (i >> 1)) : -1;
+        fpar[e] = (int)((i + j + g.z0) & 1);
+        fnb[e] = (i == 0) + (i == g.nx - 1) + (j == 0) + (j == g.ny - 1);
+    }
+    auto uload = [&](T (&v)[I::IU], int64_t k) {
+        const bool readable = DIM == 2 || (k >= -gz && k < g.nz + gz);
+        const T* up = u + k * g.P;
+#pragma unroll
+        for (int e = 0; e < I::IU; ++e) v[e] = readable && uoff[e] >= 0 ? up[uoff[e]] : (T)0;
+    };
+    auto ustore = [&](T* dst, const T (&v)[I::IU], int64_t k) {
+        const bool odd = ((k & 1) != 0);
+#pragma unroll
+        for (int e = 0; e < I::IU; ++e) {
+            const int x = odd ? ul1[e] : ul0[e];
+            if (x >= 0) dst[x] = v[e];
+        }
+    };
+    auto fload = [&](T (&v)[I::IR], int64_t k) {
         const int64_t gk = g.z0 + k;
         const bool kin = DIM == 2 || (gk >= 0 && gk < g.gnz);
-        for (int q = tid; q < S::RSLOT; q += S::NT) {
-            const int il = q % S::RW, jl = q / S::RW;
-            const int i = X0 - 1 + il, j = Y0 - 1 + jl;
-            T r = (T)0;
-            if (kin && i >= 0 && i < g.nx && j >= 0 && j < g.ny) {
-                const int x = (jl + 1) * S::UW + (il + 1);  // in the staged planes
-                T s = uc[x - 1] + uc[x + 1];
-                s = s + uc[x - S::UW];
-                s = s + uc[x + S::UW];
-                if (DIM == 3) {
-                    s = s + um[x];
-                    s = s + up[x];
+        const T* fp = f + k * g.P;
+        const int kp = (int)(k & 1);
+#pragma unroll
+        for (int e = 0; e < I::IR; ++e) v[e] = kin && foff[e] >= 0 ? fp[((fpar[e] ^ kp) * g.H) + foff[e]] : (T)0;
+    };
+    // r of local plane k on the tile and its one-cell ring into rs (0 outside the box), then my cell's `ay`
+    auto plane_ay = [&](int64_t k, const T* um, const T* uc, const T* up, const T (&fv)[I::IR]) -> T {
+        const int64_t gk = g.z0 + k;
+        const bool kin = DIM == 2 || (gk >= 0 && gk < g.gnz);
+        const int nbz = DIM == 3 ? (gk == 0) + (gk == g.gnz - 1) : 0;
+#pragma unroll
+        for (int e = 0; e < I::IR; ++e) {
+            const int q = tid + e * S::NT;
+            if (q < S::RSLOT) {
+                T r = (T)0;
+                if (kin && foff[e] >= 0) {
+                    const int il = q % S::RW, jl = q / S::RW;
+                    const int x = (jl + 1) * S::UW + (il + 1);  // in the staged planes
+                    T sm = uc[x - 1] + uc[x + 1];
+                    sm = sm + uc[x - S::UW];
+                    sm = sm + uc[x + S::UW];
+                    if (DIM == 3) {
+                        sm = sm + um[x];
+                        sm = sm + up[x];
+                    }
+                    r = op.residual(sm, fv[e], uc[x], fnb[e] + nbz);
                 }
-                const int nb = (i == 0) + (i == g.nx - 1) + (j == 0) + (j == g.ny - 1) +
-                               (DIM == 3 ? (gk == 0) + (gk == g.gnz - 1) : 0);
-                r = op.residual(s, f[pidx(g, i, j, k)], uc[x], nb);
+                rs[q] = r;
             }
-            rs[q] = r;
         }
         __syncthreads();
         T ay = (T)0;
@@ -111,43 +158,61 @@ __global__ __launch_bounds__(FwShape<DIM>::NT) void k_resfw(const T* __restrict_
     };
     const T scale = DIM == 3 ? (T)(1.0 / 512.0) : (T)(1.0 / 64.0);
     if constexpr (DIM == 2) {
-        fw_stage<T, 2>(us[0], u, g, 0, X0, Y0, gz, tid);
+        T uv[I::IU], fv[I::IR];
+        uload(uv, 0);
+        fload(fv, 0);
+        ustore(us[0], uv, 0);
         __syncthreads();
-        const T ay = plane_ay(0, us[0], us[0], us[0]);
-        const int pc = J & 1;
-        R[((I + pc) & 1) * gc.H + (int64_t)J * gc.hw + (I >> 1)] = scale * ay;
+        const T ay = plane_ay(0, us[0], us[0], us[0], fv);
+        R[((Ic + Jc) & 1) * gc.H + (int64_t)Jc * gc.hw + (Ic >> 1)] = scale * ay;
         return;
     } else {
-        // ring slot of local plane k: (k + 3) mod 3 (k >= -2)
+        // ring slot of local plane k: (k + 6) mod 3 (k >= -3)
         auto slot = [&](int64_t k) { return us[(int)((k + 6) % 3)]; };
         const int64_t k0 = 2 * (int64_t)K0 - 1;  // the chunk's first fine plane
-        fw_stage<T, 3>(slot(k0 - 1), u, g, k0 - 1, X0, Y0, gz, tid);
-        fw_stage<T, 3>(slot(k0), u, g, k0, X0, Y0, gz, tid);
-        T a0 = (T)0, a1 = (T)0, a2 = (T)0, a3 = (T)0;
         const int kend = K0 + kc < (int)(g.nz >> 1) ? K0 + kc : (int)(g.nz >> 1);
-        for (int K = K0; K < kend; ++K) {
-            // fine planes 2K-1 .. 2K+2 (the first coarse plane of the chunk computes all four, the others two)
-            for (int64_t k = K == K0 ? 2 * (int64_t)K - 1 : 2 * (int64_t)K + 1; k <= 2 * (int64_t)K + 2; ++k) {
-                fw_stage<T, 3>(slot(k + 1), u, g, k + 1, X0, Y0, gz, tid);
-                __syncthreads();
-                const T ay = plane_ay(k, slot(k - 1), slot(k), slot(k + 1));
-                a0 = a1;
-                a1 = a2;
-                a2 = a3;
-                a3 = ay;
-                __syncthreads();  // rs and the ring slot about to be restaged are free again
+        const int64_t klast = 2 * (int64_t)kend;  // the last fine plane (2 K + 2 of the last coarse plane)
+        // plane k + 1's u (loaded during step k - 1) goes into its slot at the top of step k, f of plane k was loaded
+        // during step k - 1 as well (a prefetch distance of 2 with double buffers measured slower: 134 VGPRs, 3
+        // workgroups per CU, 609 against 470 us at 512^3)
+        T uv[I::IU], fv[I::IR], fn[I::IR];
+        uload(uv, k0 - 1);
+        ustore(slot(k0 - 1), uv, k0 - 1);
+        uload(uv, k0);
+        ustore(slot(k0), uv, k0);
+        uload(uv, k0 + 1);  // in flight into the first step
+        fload(fv, k0);
+        T a0 = (T)0, a1 = (T)0, a2 = (T)0, a3 = (T)0;
+        int K = K0;
+        for (int64_t k = k0; k <= klast; ++k) {
+            ustore(slot(k + 1), uv, k + 1);
+            if (k + 2 <= klast + 1) uload(uv, k + 2);
+            if (k + 1 <= klast) fload(fn, k + 1);
+            __syncthreads();
+            const T ay = plane_ay(k, slot(k - 1), slot(k), slot(k + 1), fv);
+            a0 = a1;
+            a1 = a2;
+            a2 = a3;
+            a3 = ay;
+#pragma unroll
+            for (int e = 0; e < I::IR; ++e) fv[e] = fn[e];
+            if (k == 2 * (int64_t)K + 2) {  // coarse plane K complete (fine planes 2K-1 .. 2K+2)
+                const int64_t gK = gc.z0 + K;
+                T az = a0;
+                az = az + (gK == 0 ? wf : w3) * a1;
+                az = az + (gK == gc.gnz - 1 ? wf : w3) * a2;
+                az = az + a3;
+                R[(int64_t)K * gc.P + ((Ic + Jc + gK) & 1) * gc.H + (int64_t)Jc * gc.hw + (Ic >> 1)] = scale * az;
+                ++K;
             }
-            const int64_t gK = gc.z0 + K;
-            T az = a0;
-            az = az + (gK == 0 ? wf : w3) * a1;
-            az = az + (gK == gc.gnz - 1 ? wf : w3) * a2;
-            az = az + a3;
-            const int pc = (int)((J + gK) & 1);
-            R[(int64_t)K * gc.P + ((I + pc) & 1) * gc.H + (int64_t)J * gc.hw + (I >> 1)] = scale * az;
+            __syncthreads();  // rs and the slot restaged next are free again
         }
     }
 }
 
+#ifndef FW_WGS  // (build knob: workgroups the z-chunking aims for; 512^3 FW cycle 1.600 ms at 1024, 1.620 at 2048, 1.639 at 4096)
+#define FW_WGS 1024
+#endif
 template <typename T, int DIM>
 hipError_t resfw_t(const void* u, const void* f, void* R, Geo g, Geo gc, double h, double cl, double clc, int gz,
                    hipStream_t s)
@@ -162,7 +227,7 @@ hipError_t resfw_t(const void* u, const void* f, void* R, Geo g, Geo gc, double 
         // coarse planes per chunk: halve while there are fewer than 2048 workgroups (8 per CU) and a chunk keeps
         // >= 8 coarse planes (a chunk re-reads 2 of every 2 kc + 2 fine planes of its neighbours)
         kc = cz;
-        while (tiles * (cz / kc) < 2048 && kc >= 16) kc /= 2;
+        while (tiles * (cz / kc) < FW_WGS && kc >= 16) kc /= 2;
         chunks = (cz + kc - 1) / kc;
     }
     const int64_t nb = tiles * chunks;
@@ -175,7 +240,7 @@ hipError_t resfw_t(const void* u, const void* f, void* R, Geo g, Geo gc, double 
 bool resfw_supported(int rb, int dim, const Geo& g, int gz, bool dist)
 {
     if (rb != 4 && rb != 8) return false;  // (the cpu-raw float arithmetic keeps the two scalar passes)
-    const int tx = 64, ty = dim == 3 ? FwShape<3>::TY : FwShape<2>::TY;
+    const int tx = FwShape<3>::TX, ty = dim == 3 ? FwShape<3>::TY : FwShape<2>::TY;
     if (g.nx % tx || g.ny % ty) return false;
     if (dim == 3 && ((g.nz & 1) || g.nz < 2)) return false;
     // a slab level reads r at the neighbours' first planes: u two and f one ghost plane deep

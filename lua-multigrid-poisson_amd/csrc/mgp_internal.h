@@ -136,15 +136,17 @@ struct FusedTuning {
     int ys_rows = 32;    // MGP_YS_ROWS: 2D rows per workgroup chunk
     int64_t wgs = 256;   // MGP_ZS_WGS: z-chunks are halved until a launch has this many workgroups
     // tile order of launches of > 512 workgroups: px | py << 8 patches of tiles per XCD band, 0 = tile rows
-    // (MGP_ZS_PATCH=px,py sets both phases, MGP_ZS_PATCH_PRE / MGP_ZS_PATCH_POST one; "0" off)
-    int patch_pre = 0, patch_post = 0;
+    // (MGP_ZS_PATCH=px,py sets both phases, MGP_ZS_PATCH_PRE / MGP_ZS_PATCH_POST one; "0" off; -1: POST's default,
+    // 4 x 8 on planes of >= 4096 tiles)
+    int patch_pre = 0, patch_post = -1;
 };
 FusedTuning fused_tuning_from_env();
 
 struct FusedArgs {
     FusedTuning tu;
     bool pre;
-    int linear;  // POST: linear prolongation; PRE: 1 = no restriction (both colours stored, full weighting after)
+    int linear;  // POST: linear prolongation; PRE: 1 = no restriction (both colours stored, full weighting after),
+                 // 2 = the full-weighting restriction fused (fused_fwf_supported)
     const void* src;
     const void* f;
     void* dst;
@@ -164,6 +166,8 @@ hipError_t prepare_kernels(int rb);
 int fused_zc(int rb, const Geo& g, bool pre, bool clz, const FusedTuning& tu);
 int fused_blocks(int rb, const Geo& g, int zc, bool clz, const FusedTuning& tu);
 hipError_t launch_fused(int rb, const FusedArgs& a, hipStream_t s);
+// PRE with the full weighting fused (FusedArgs::linear = 2): fp32, cl = 0, a replicated level (MGP_ZS_FWF=0: off)
+bool fused_fwf_supported(int rb, bool clz, bool dist);
 
 // Tiled smoothing phases of a small replicated red/black level (k_blk: one launch per phase, the 3D
 // or 2D tile and its halo in LDS):

@@ -1481,6 +1481,9 @@ __device__ __forceinline__ void lds_barrier()
 #ifndef ZS_YROLE
 #define ZS_YROLE 1
 #endif
+#ifndef ZS_FHALO
+#define ZS_FHALO 1
+#endif
 #ifndef ZS_NPOST_F32
 #define ZS_NPOST_F32 2
 #endif
@@ -1564,7 +1567,9 @@ constexpr bool kZsNTL = (ZS_NT & 1) != 0, kZsNTS = (ZS_NT & 2) != 0, kZsNTO = (Z
 #endif
 constexpr bool kZsPreRed = ZS_PRE_RED_STORE != 0;
 
-template <typename T, bool PRE, bool CLZ = true, bool WIDE = false>
+// FWF (PRE only): the full-weighting restriction fused into the phase (k_zs LINEAR = 2): the residual is needed one
+// cell beyond the tile (the full weighting's 4-cell stencil), so the trapezoid is one stage deeper (H = 6)
+template <typename T, bool PRE, bool CLZ = true, bool WIDE = false, bool FWF = false>
 struct ZsShape {
     static constexpr int N = PRE ? (CLZ ? ZsTile<T>::NPRE : ZsTile<T>::NPRE_CL)
                                  : (WIDE ? ZsTile<T>::NPOST_W : ZsTile<T>::NPOST);
@@ -1572,7 +1577,7 @@ struct ZsShape {
                                   : (WIDE ? ZsTile<T>::TXPOST_W : ZsTile<T>::TXPOST);
     static constexpr int TY = PRE ? (CLZ ? ZsTile<T>::TYPRE : ZsTile<T>::TYPRE_CL)
                                   : (WIDE ? ZsTile<T>::TYPOST_W : ZsTile<T>::TYPOST);
-    static constexpr int H = PRE ? 5 : 4;              // y/z halo = stages that read neighbours
+    static constexpr int H = PRE ? (FWF ? 6 : 5) : 4;  // y/z halo = stages that read neighbours
     // x halo cells per side: the trapezoid depth H in whole column groups (2 N cells of x each)
 #ifdef ZS_HX_FIXED  // timing experiment: the round-1 fixed 8-cell x halo
     static constexpr int HX = ZS_HX_FIXED;
@@ -1626,7 +1631,12 @@ struct ZsShape {
     static constexpr int CJ = PRE ? 0 : TY / 2 + 6, CI = PRE ? N : TX / 2 + 16;
     static constexpr int CSLOT = CJ * CI, CPAIRS = CSLOT / 2;
     static constexpr int OFFC = OFFX + 2 * XSLOT;
-    static constexpr size_t lds_bytes = (size_t)(OFFC + 4 * CSLOT) * sizeof(T);
+    // FWF: the residual rows in x order (RXSLOT per step parity), their x-combinations (AXSLOT per step parity) and a
+    // ring of the y-combinations of 4 fine planes per coarse cell of the tile (AYSLOT per plane)
+    static constexpr int RXSLOT = FWF ? YE * G * 2 * N : 0, AXSLOT = FWF ? YE * G * N : 0,
+                         AYSLOT = FWF ? (TY / 2) * (TX / 2) : 0;
+    static constexpr int OFFRX = OFFC + 4 * CSLOT, OFFAX = OFFRX + 2 * RXSLOT, OFFAY = OFFAX + 2 * AXSLOT;
+    static constexpr size_t lds_bytes = (size_t)(OFFAY + 4 * AYSLOT) * sizeof(T);
     static_assert(CPAIRS <= 2 * NTL, "coarse staging: two pairs per thread");
     static_assert(CI % N == 0 && OFFC % N == 0, "coarse rows must hold aligned groups");
     static_assert(NTL <= 1024, "too many threads");
@@ -2008,18 +2018,20 @@ constexpr bool kZsRask = ZS_RASK != 0;
 #define ZS_WPE_POST 4
 #endif
 template <typename T, bool PRE, int LINEAR, bool ERR, bool CLZ, bool WIDE = false>
-__global__ __launch_bounds__((ZsShape<T, PRE, CLZ, WIDE>::NTL))
+__global__ __launch_bounds__((ZsShape<T, PRE, CLZ, WIDE, PRE && LINEAR == 2>::NTL))
 __attribute__((amdgpu_waves_per_eu(1, PRE ? ZS_WPE_PRE : ZS_WPE_POST))) void k_zs(const T* __restrict__ src, const T* __restrict__ f,
                                                                 T* __restrict__ dst, const T* old, T* __restrict__ R,
                                                                 const T* __restrict__ V, double* __restrict__ partials,
                                                                 Geo g, Geo gc, Op<T, 3> op, T clc, int zc, int gz,
                                                                 int patch)
 {
-    using S = ZsShape<T, PRE, CLZ, WIDE>;
+    // PRE: LINEAR selects the restriction: 0 = residual + 2^3 average here; 1 = none (both colours of the
+    // smoothed level stored; the host runs the full-weighting restriction after the phase); 2 = residual + the full
+    // weighting here (FWF)
+    constexpr bool FWF = PRE && LINEAR == 2;
+    using S = ZsShape<T, PRE, CLZ, WIDE, FWF>;
     constexpr int N = S::N, H = S::H, HWE = S::HWE, G = S::G, YE = S::YE, SLOT = S::SLOT, TX = S::TX,
                   TY = S::TY, NS3 = S::NS3, NTL = S::NTL;
-    // PRE: LINEAR selects the restriction: 0 = residual + 2^3 average here; 1 = none (both colours of the
-    // smoothed level stored; the host runs the full-weighting restriction after the phase)
     constexpr bool RR = PRE && LINEAR == 0;
     // PRE with ERR (which only POST uses): the input is a fresh zero guess, never loaded (src may be null); this
     // replaces the memset of a fused coarse level's u before its PRE
@@ -2084,6 +2096,12 @@ __attribute__((amdgpu_waves_per_eu(1, PRE ? ZS_WPE_PRE : ZS_WPE_POST))) void k_z
     const int goff = cgy * hw + cgm;  // in-plane offset (nx * ny < 2^31)
 #endif
     const bool tile_xy = on && ye >= H && ye < H + TY && gx >= S::HXG && gx < G - S::HXG;
+    // ZS_FHALO: the y-halo rows load only the f their stages can use: stage k is needed on rows d <= H - k from the
+    // tile, so f1 (red f: stages 1 and 3) only on d <= H - 1 and f2 (black f: stages 2, 4, the residual) only on
+    // d <= H - 2; the others keep zeros (their outputs lie outside every later stage's region)
+    const int ydist = ye < H ? H - ye : (ye >= H + TY ? ye - (H + TY) + 1 : 0);
+    // (POST only: in PRE it measured slower, 335.5 -> 341 us, against POST 435 -> 432 us at 512^3)
+    const bool need_f1 = !ZS_FHALO || PRE || ydist <= H - 1, need_f2 = !ZS_FHALO || PRE || ydist <= H - 2;
     const int zlo = Z0 - H;
     ZsDiag<T> dz;
     {
@@ -2095,7 +2113,8 @@ __attribute__((amdgpu_waves_per_eu(1, PRE ? ZS_WPE_PRE : ZS_WPE_POST))) void k_z
         dz.left = col.gm == 0;
         dz.right = col.gm + N == hw;
     }
-    const int p_end = Z0 + zc + (PRE ? 5 : 3);
+    // (FWF: the x- and y-combinations of the full weighting follow the residual of plane p - 5 one and two steps later)
+    const int p_end = Z0 + zc + (PRE ? (FWF ? 7 : 5) : 3);
     auto inz = [&](int q) { return z0 + q >= 0 && z0 + q < gnz; };  // inside the global box
     auto pcl = [&](int q) { return q < qlo ? qlo : (q > qhi ? qhi : q); };
     // ring slot of plane q (q may be negative; ns = 3 as q mod 3)
@@ -2172,8 +2191,8 @@ __attribute__((amdgpu_waves_per_eu(1, PRE ? ZS_WPE_PRE : ZS_WPE_POST))) void k_z
                 r.u = vzero<T, N>();
             else
                 r.u = gload<T, N, kZsNTL>(src_black + pP + goff);
-            r.f1 = gload<T, N, kZsNTL>(f + (pP - Pz) + goff);
-            r.f2 = gload<T, N, kZsNTL>(f + (pP - 2 * Pz) + Hh + goff);
+            if (need_f1) r.f1 = gload<T, N, kZsNTL>(f + (pP - Pz) + goff);
+            if (need_f2) r.f2 = gload<T, N, kZsNTL>(f + (pP - 2 * Pz) + Hh + goff);
             if (!PRE && ERR && tile_xy) {  // psiOld of plane p - 4, for the tile's own columns only
                 const T* dp = old + (pP - 4 * Pz);
                 r.o0 = gload<T, N, kZsNTO>(dp + goff);
@@ -2184,8 +2203,8 @@ __attribute__((amdgpu_waves_per_eu(1, PRE ? ZS_WPE_PRE : ZS_WPE_POST))) void k_z
                 r.u = vzero<T, N>();
             else
                 r.u = gload<T, N, kZsNTL>(src_black + (int64_t)ZS_PLANE(pcl(p)) * P + goff);
-            r.f1 = gload<T, N, kZsNTL>(f + (int64_t)ZS_PLANE(pcl(p - 1)) * P + goff);
-            r.f2 = gload<T, N, kZsNTL>(f + (int64_t)ZS_PLANE(pcl(p - 2)) * P + Hh + goff);
+            if (need_f1) r.f1 = gload<T, N, kZsNTL>(f + (int64_t)ZS_PLANE(pcl(p - 1)) * P + goff);
+            if (need_f2) r.f2 = gload<T, N, kZsNTL>(f + (int64_t)ZS_PLANE(pcl(p - 2)) * P + Hh + goff);
             if (!PRE && ERR && tile_xy) {
                 const T* dp = old + (int64_t)pcl(p - 4) * P;
                 r.o0 = gload<T, N, kZsNTO>(dp + goff);
@@ -2339,7 +2358,7 @@ __attribute__((amdgpu_waves_per_eu(1, PRE ? ZS_WPE_PRE : ZS_WPE_POST))) void k_z
             if (RO < 2) {
                 vstore<T, N>(slot(S::OFF2, 2, p - 2) + col.lrow, o2);
                 vstore<T, N>(slot(S::OFF3, NS3, p - 3) + col.lrow, o3);
-                if (RR) vstore<T, N>(slot(S::OFF4, 2, p - 4) + col.lrow, o4);
+                if (RR || FWF) vstore<T, N>(slot(S::OFF4, 2, p - 4) + col.lrow, o4);
             }
         }
 
@@ -2363,7 +2382,7 @@ __attribute__((amdgpu_waves_per_eu(1, PRE ? ZS_WPE_PRE : ZS_WPE_POST))) void k_z
                 T* dp = dst + (int64_t)q * P;
                 // PRE: the red cells are not stored.  Its output is read only by POST, whose stage 0
                 // loads the black cells (the first post half-sweep replaces the red ones unread).
-                if (!RR || kZsPreRed) gstore<T, N, kZsNTS>(dp + goff, W3[sl(4)]);
+                if (!(RR || FWF) || kZsPreRed) gstore<T, N, kZsNTS>(dp + goff, W3[sl(4)]);
                 gstore<T, N, kZsNTS>(dp + Hh + goff, o4);
             }
         }
@@ -2438,6 +2457,78 @@ __attribute__((amdgpu_waves_per_eu(1, PRE ? ZS_WPE_PRE : ZS_WPE_POST))) void k_z
                 }
             }
         }
+        // ---- PRE, FWF: residual of plane p - 5 into RX, the x-combination of plane p - 6, the y-combination and the
+        // coarse planes of plane p - 7 (fw_eval's order; cells outside the box weigh 0) ----
+        if constexpr (FWF) {
+            const int q = p - 5;
+            const int pq = par(q);
+            if (!kZsRask) zs_nb_load<T, N>(nr, slot(S::OFF3, NS3, q), col);
+            zs_nb_load<T, N>(nk, slot(S::OFF4, 2, q), col);
+            T rred[N], rblk[N];
+            zs_residual<T, N, CLZ, ST>(W4[sl(6)], W4[sl(5)], W4[sl(ZS_NC ? 3 : 4)], nk, W3[sl(5)], FR[sl(5)], col, pq, nbyz(q), g.nx, op,
+                                   dz, rred);
+            if (kZsRask)
+                zs_residual_a<T, N, CLZ, ST>(AS[(RS & 1) ^ 1], W4[sl(5)], FB[sl(5)], col, 1 ^ pq, nbyz(q), g.nx, op, dz,
+                                             rblk);
+            else
+                zs_residual<T, N, CLZ, ST>(W3[sl(6)], W3[sl(5)], W3[sl(4)], nr, W4[sl(5)], FB[sl(5)], col, 1 ^ pq, nbyz(q),
+                                           g.nx, op, dz, rblk);
+            const bool rin = in_xy && (ST || inz(q));  // (the residuals of cells outside the box weigh 0)
+            T* const rxw = lds + S::OFFRX + (p & 1) * S::RXSLOT + (ye * G + gx) * 2 * N;
+#pragma unroll
+            for (int e = 0; e < N; ++e) {  // x order: cell 2 (gm + e) + parity
+                rxw[2 * e + pq] = rin ? rred[e] : (T)0;
+                rxw[2 * e + (pq ^ 1)] = rin ? rblk[e] : (T)0;
+            }
+            // the x-combination of plane p - 6 (written to RX one step ago) for the tile's coarse columns, rows within
+            // one of the tile: fine cells 2I - 1 .. 2I + 2 of coarse I = gm + e
+            const bool tile_x = gx >= S::HXG && gx < G - S::HXG;
+            if (tile_x && ydist <= 1) {
+                const T* rxr = lds + S::OFFRX + ((p - 1) & 1) * S::RXSLOT + (ye * G + gx) * 2 * N;
+                T* const axw = lds + S::OFFAX + (p & 1) * S::AXSLOT + (ye * G + gx) * N;
+                const T wfv = (T)3 - clc, w3 = (T)3;
+                const int cxn = g.nx >> 1;
+#pragma unroll
+                for (int e = 0; e < N; ++e) {
+                    const int I = col.gm + e;
+                    axw[e] = fw_axis(rxr[2 * e - 1], rxr[2 * e], rxr[2 * e + 1], rxr[2 * e + 2], I == 0 ? wfv : w3,
+                                     I == cxn - 1 ? wfv : w3);
+                }
+            }
+            // the y-combination of plane p - 7 (its x-combinations were written one step ago) in the owner rows (even
+            // tile rows: coarse row J = gy / 2, fine rows 2J - 1 .. 2J + 2), then coarse plane K when p - 7 = 2K + 2
+            const int rl = ye - H;
+            if (tile_x && rl >= 0 && rl < TY && (rl & 1) == 0) {
+                const T* axr = lds + S::OFFAX + ((p - 1) & 1) * S::AXSLOT + gx * N;
+                const T wfv = (T)3 - clc, w3 = (T)3;
+                const int J = gy >> 1, cyn = g.ny >> 1;
+                const int q2 = p - 7;
+                T* const ayw = lds + S::OFFAY + (rl >> 1) * (TX / 2) + (gx - S::HXG) * N;
+#pragma unroll
+                for (int e = 0; e < N; ++e) {
+                    T ay = axr[(ye - 1) * G * N + e];
+                    ay = ay + (J == 0 ? wfv : w3) * axr[ye * G * N + e];
+                    ay = ay + (J == cyn - 1 ? wfv : w3) * axr[(ye + 1) * G * N + e];
+                    ay = ay + axr[(ye + 2) * G * N + e];
+                    ayw[(q2 & 3) * S::AYSLOT + e] = ay;
+                }
+                const int dq2 = q2 - 2 - (ST ? (Z0 & ~1) : Z0);  // 2K - z0 - Z0 for the coarse plane K ending at q2
+                if (dq2 >= 0 && dq2 < zc && (dq2 & 1) == 0) {
+                    const int K = (z0 + q2 - 2) >> 1;  // global coarse plane
+                    const T wk0 = K == 0 ? wfv : w3, wk1 = K == gc.gnz - 1 ? wfv : w3;
+                    T* rowc = R + (int64_t)(K - cz0) * gc.P + (int64_t)J * gc.hw;
+#pragma unroll
+                    for (int e = 0; e < N; ++e) {
+                        T az = ayw[((q2 - 3) & 3) * S::AYSLOT + e];
+                        az = az + wk0 * ayw[((q2 - 2) & 3) * S::AYSLOT + e];
+                        az = az + wk1 * ayw[((q2 - 1) & 3) * S::AYSLOT + e];
+                        az = az + ayw[(q2 & 3) * S::AYSLOT + e];
+                        const int I = col.gm + e;
+                        rowc[((I + J + K) & 1) * gc.H + (I >> 1)] = (T)(1.0 / 512.0) * az;
+                    }
+                }
+            }
+        }
         FR[sl(1)] = cur.f1;  // red f of plane p - 1 (replaces p - 5, read above)
         FB[sl(2)] = cur.f2;  // black f of plane p - 2
         lds_barrier();
@@ -2446,6 +2537,8 @@ __attribute__((amdgpu_waves_per_eu(1, PRE ? ZS_WPE_PRE : ZS_WPE_POST))) void k_z
     const std::false_type GEN;
     const std::true_type STY;
     PF pb[NPF];
+#pragma unroll
+    for (int k = 0; k < NPF; ++k) pb[k].f1 = pb[k].f2 = vz;  // (the halo rows that skip f loads keep zeros)
     if (!PRE) {  // the coarse planes the first fine plane needs
         const int K = (z0 + zlo) >> 1;
         for (int k = K - 1; k <= K + 1; ++k) {
@@ -3061,9 +3154,23 @@ constexpr int tc_off(int l)  // element offset of level l's (u, f) pair
     }
     return o;
 }
+// the full weighting's residual scratch (one array of the first level's layout after the levels): where the levels
+// and it fit the LDS with 4 KB to spare for the static part (all fp32 shapes, fp64 16^3)
+template <typename T, int DIM, int TX, int TY, int TZ>
+constexpr bool tc_fw_scratch()
+{
+    const int p0 = DIM == 3 ? (TX + 2) * (TY + 2) * (TZ + 2) : (TX + 2) * (TY + 2);
+    int n = 1, m = TX < TY ? TX : TY;
+    if (DIM == 3 && TZ < m) m = TZ;
+    for (int t = m; t > 1; t >>= 1) ++n;
+    return (size_t)(tc_off<DIM, TX, TY, TZ>(n) + p0) * sizeof(T) + 4096 <= 160 * 1024;
+}
 // 16 waves in fp32; fp64 takes 8, so that the kernel keeps 256 VGPRs (at 16 waves it spilled 100-240 VGPRs)
-template <typename T>
-constexpr int tc_threads() { return sizeof(T) == 4 ? 1024 : 512; }
+#ifndef TC_THREADS_2D_F32  // (build knob: threads of the 2D fp32 tail)
+#define TC_THREADS_2D_F32 1024
+#endif
+template <typename T, int DIM>
+constexpr int tc_threads() { return sizeof(T) == 4 ? (DIM == 2 ? TC_THREADS_2D_F32 : 1024) : 512; }
 #ifndef TC_MAXL  // timing experiment: skip the ops of levels >= TC_MAXL (wrong results)
 #define TC_MAXL 16
 #endif
@@ -3075,7 +3182,7 @@ __device__ __forceinline__ void tc_half(T* U, const T* F, const Op<T, DIM>& op, 
     if constexpr (NX >= 2) {
         constexpr int HN = NX / 2, CNT = L::CELLS / 2;
 #pragma unroll
-        for (int q0 = 0; q0 < CNT; q0 += tc_threads<T>()) {
+        for (int q0 = 0; q0 < CNT; q0 += tc_threads<T, DIM>()) {
             const int q = q0 + tid;
             if (q < CNT) {
                 const int i2 = q % HN, j = (q / HN) % NY, k = DIM == 3 ? q / (HN * NY) : 0;
@@ -3093,7 +3200,7 @@ __device__ __forceinline__ void tc_half(T* U, const T* F, const Op<T, DIM>& op, 
         }
     } else {  // one cell per row: cell (0, j, k) has colour (j + k) & 1 (half_item's empty slot is skipped)
         constexpr int CNT = L::CELLS;
-        for (int q = tid; q < CNT; q += tc_threads<T>()) {
+        for (int q = tid; q < CNT; q += tc_threads<T, DIM>()) {
             const int j = q % NY, k = DIM == 3 ? q / NY : 0;
             if (((j + k) & 1) != c) continue;
             const int x = L::idx(0, j, k);
@@ -3131,7 +3238,7 @@ __device__ __forceinline__ void tc_rr(const T* U, const T* F, T* Fc, const Op<T,
     using C = TcLev<DIM, MX, MY, MZ>;
     constexpr int CNT = C::CELLS;
     auto res = [&](int i, int j, int k) { return tc_res<T, DIM, NX, NY, NZ>(U, F, op, i, j, k); };
-    for (int q = tid; q < CNT; q += tc_threads<T>()) {
+    for (int q = tid; q < CNT; q += tc_threads<T, DIM>()) {
         const int I = q % MX, J = (q / MX) % MY, K = DIM == 3 ? q / (MX * MY) : 0;
         const int i = 2 * I, j = 2 * J, k = 2 * K;
         T sm = res(i, j, k) + res(i + 1, j, k);
@@ -3162,9 +3269,37 @@ __device__ __forceinline__ void tc_rr_fw(const T* U, const T* F, T* Fc, const Op
     gc.ny = MY;
     gc.gnz = MZ;
     auto res = [&](int i, int j, int64_t k64) { return tc_res<T, DIM, NX, NY, NZ>(U, F, op, i, j, (int)k64); };
-    for (int q = tid; q < CNT; q += tc_threads<T>()) {
+    for (int q = tid; q < CNT; q += tc_threads<T, DIM>()) {
         const int I = q % MX, J = (q / MX) % MY, K = DIM == 3 ? q / (MX * MY) : 0;
         Fc[C::idx(I, J, K)] = fw_eval<T, DIM>(res, g, gc, wf, I, J, (int64_t)K);
+    }
+}
+
+// tc_rr_fw through a residual scratch: r of every cell of the level into RS (the level's unpacked layout) once, then
+// the full weighting of each coarse cell from RS (tc_rr_fw evaluates each fine residual for all 8 coarse cells that
+// weight it: 64 residuals per coarse cell, the FW tail's extra 27 us per 512^3 cycle)
+template <typename T, int DIM, int NX, int NY, int NZ>
+__device__ __forceinline__ void tc_rr_fw_s(const T* U, const T* F, T* Fc, const Op<T, DIM>& op, T wf, int tid, T* RS)
+{
+    using L = TcLev<DIM, NX, NY, NZ>;
+    constexpr int MX = NX / 2, MY = NY / 2, MZ = DIM == 3 ? NZ / 2 : 1;
+    using C = TcLev<DIM, MX, MY, MZ>;
+    for (int q = tid; q < L::CELLS; q += tc_threads<T, DIM>()) {
+        const int i = q % NX, j = (q / NX) % NY, k = DIM == 3 ? q / (NX * NY) : 0;
+        RS[L::idx(i, j, k)] = tc_res<T, DIM, NX, NY, NZ>(U, F, op, i, j, k);
+    }
+    __syncthreads();
+    Geo g{}, gc{};
+    g.nx = NX;
+    g.ny = NY;
+    g.gnz = DIM == 3 ? NZ : 1;
+    gc.nx = MX;
+    gc.ny = MY;
+    gc.gnz = MZ;
+    auto get = [&](int i, int j, int64_t k) { return RS[L::idx(i, j, (int)k)]; };
+    for (int q = tid; q < C::CELLS; q += tc_threads<T, DIM>()) {
+        const int I = q % MX, J = (q / MX) % MY, K = DIM == 3 ? q / (MX * MY) : 0;
+        Fc[C::idx(I, J, K)] = fw_eval<T, DIM>(get, g, gc, wf, I, J, (int64_t)K);
     }
 }
 
@@ -3176,7 +3311,7 @@ __device__ __forceinline__ void tc_prolong(T* U, const T* V, T cl, int tid)
     using C = TcLev<DIM, MX, MY, MZ>;
     constexpr int CNT = L::CELLS;
 #pragma unroll 1
-    for (int q0 = 0; q0 < CNT; q0 += tc_threads<T>()) {
+    for (int q0 = 0; q0 < CNT; q0 += tc_threads<T, DIM>()) {
         const int q = q0 + tid;
         if (q < CNT) {
             const int i = q % NX, j = (q / NX) % NY, k = DIM == 3 ? q / (NX * NY) : 0;
@@ -3237,11 +3372,11 @@ template <typename T, int DIM, int NX, int NY, int NZ>
 __device__ __forceinline__ void tc_copy(T* U, T* F, T* gu, T* gf, bool in, bool zero_u, int tid)
 {
     using L = TcLev<DIM, NX, NY, NZ>;
-    constexpr int IT = (L::P + tc_threads<T>() - 1) / tc_threads<T>();
+    constexpr int IT = (L::P + tc_threads<T, DIM>() - 1) / tc_threads<T, DIM>();
     T uv[IT], fv[IT];
 #pragma unroll
     for (int r = 0; r < IT; ++r) {
-        const int q = tid + r * tc_threads<T>();
+        const int q = tid + r * tc_threads<T, DIM>();
         const int64_t gi = tc_global<DIM, NX, NY, NZ>(q);
         if (in) {
             uv[r] = gi >= 0 && !zero_u ? gu[gi] : (T)0;
@@ -3254,7 +3389,7 @@ __device__ __forceinline__ void tc_copy(T* U, T* F, T* gu, T* gf, bool in, bool 
     if (in) {
 #pragma unroll
         for (int r = 0; r < IT; ++r) {
-            const int q = tid + r * tc_threads<T>();
+            const int q = tid + r * tc_threads<T, DIM>();
             if (q < L::P) {
                 U[q] = uv[r];
                 F[q] = fv[r];
@@ -3267,7 +3402,7 @@ __device__ __forceinline__ void tc_copy(T* U, T* F, T* gu, T* gf, bool in, bool 
 // level waited for one level's loads before issuing the next level's: seven load latencies in a row in 2D)
 template <typename T, int DIM, int NX, int NY, int NZ>
 struct TcRegs {
-    static constexpr int IT = (TcLev<DIM, NX, NY, NZ>::P + tc_threads<T>() - 1) / tc_threads<T>();
+    static constexpr int IT = (TcLev<DIM, NX, NY, NZ>::P + tc_threads<T, DIM>() - 1) / tc_threads<T, DIM>();
     T u[IT], f[IT];
 };
 template <typename T, int DIM, int NX, int NY, int NZ>
@@ -3275,7 +3410,7 @@ __device__ __forceinline__ void tc_load(TcRegs<T, DIM, NX, NY, NZ>& rg, const T*
 {
 #pragma unroll
     for (int r = 0; r < TcRegs<T, DIM, NX, NY, NZ>::IT; ++r) {
-        const int64_t gi = tc_global<DIM, NX, NY, NZ>(tid + r * tc_threads<T>());
+        const int64_t gi = tc_global<DIM, NX, NY, NZ>(tid + r * tc_threads<T, DIM>());
         rg.u[r] = gi >= 0 && !zero_u ? gu[gi] : (T)0;
         rg.f[r] = gi >= 0 ? gf[gi] : (T)0;
     }
@@ -3286,7 +3421,7 @@ __device__ __forceinline__ void tc_store(T* U, T* F, const TcRegs<T, DIM, NX, NY
     using L = TcLev<DIM, NX, NY, NZ>;
 #pragma unroll
     for (int r = 0; r < TcRegs<T, DIM, NX, NY, NZ>::IT; ++r) {
-        const int q = tid + r * tc_threads<T>();
+        const int q = tid + r * tc_threads<T, DIM>();
         if (q < L::P) {
             U[q] = rg.u[r];
             F[q] = rg.f[r];
@@ -3295,9 +3430,12 @@ __device__ __forceinline__ void tc_store(T* U, T* F, const TcRegs<T, DIM, NX, NY
 }
 
 template <typename T, int DIM, int LINEAR, int TX, int TY, int TZ>
-__global__ __launch_bounds__(tc_threads<T>()) void k_tail_c(const TailArgs<T, DIM> a)
+__global__ __launch_bounds__((tc_threads<T, DIM>())) void k_tail_c(const TailArgs<T, DIM> a)
 {
     constexpr int NL = tc_levels<DIM, TX, TY, TZ>();
+    // the full weighting's residual scratch after the levels, where it fits (tc_lds_total)
+    constexpr bool FWR = tc_fw_scratch<T, DIM, TX, TY, TZ>();
+    constexpr int FWR_OFF = tc_off<DIM, TX, TY, TZ>(NL);
     extern __shared__ __align__(16) unsigned char tc_smem[];
     T* const lds = reinterpret_cast<T*>(tc_smem);
     // the level operators in LDS, read per op (held in registers for all levels they spill)
@@ -3354,14 +3492,19 @@ __global__ __launch_bounds__(tc_threads<T>()) void k_tail_c(const TailArgs<T, DI
             } else if (op == TAIL_ZERO) {                                                              \
                 T* u = TC_U(L);                                                                        \
                 constexpr int NXL = TC_NX(L), NYL = TC_NY(L);                                          \
-                for (int q = tid; q < LV::CELLS; q += tc_threads<T>())                                      \
+                for (int q = tid; q < LV::CELLS; q += tc_threads<T, DIM>())                                      \
                     u[LV::idx(q % NXL, (q / NXL) % NYL, DIM == 3 ? q / (NXL * NYL) : 0)] = (T)0;       \
                 __syncthreads();                                                                       \
             } else if constexpr ((L) + 1 < NL) {                                                       \
                 if (op == TAIL_RR) {                                                                   \
-                    if (a.fw)                                                                          \
-                        tc_rr_fw<T, DIM, TC_SH(L)>(TC_U(L), TC_F(L), TC_F((L) + 1), sop[L], (T)3 - sop[(L) + 1].cl, tid); \
-                    else                                                                               \
+                    if (a.fw) {                                                                        \
+                        if constexpr (FWR)                                                             \
+                            tc_rr_fw_s<T, DIM, TC_SH(L)>(TC_U(L), TC_F(L), TC_F((L) + 1), sop[L],          \
+                                                         (T)3 - sop[(L) + 1].cl, tid, lds + FWR_OFF);      \
+                        else                                                                           \
+                            tc_rr_fw<T, DIM, TC_SH(L)>(TC_U(L), TC_F(L), TC_F((L) + 1), sop[L],            \
+                                                       (T)3 - sop[(L) + 1].cl, tid);                      \
+                    } else                                                                             \
                         tc_rr<T, DIM, TC_SH(L)>(TC_U(L), TC_F(L), TC_F((L) + 1), sop[L], tid);         \
                     /* a fresh guess of the next level (its ZERO op follows) in the same phase: RR writes */ \
                     /* that level's f, ZERO its u                                                        */ \
@@ -3370,7 +3513,7 @@ __global__ __launch_bounds__(tc_threads<T>()) void k_tail_c(const TailArgs<T, DI
                         using CV = TcLev<DIM, TC_SH((L) + 1)>;                                         \
                         constexpr int MX = TC_NX((L) + 1), MY = TC_NY((L) + 1);                        \
                         T* uc = TC_U((L) + 1);                                                         \
-                        for (int q = tid; q < CV::CELLS; q += tc_threads<T>())                              \
+                        for (int q = tid; q < CV::CELLS; q += tc_threads<T, DIM>())                              \
                             uc[CV::idx(q % MX, (q / MX) % MY, DIM == 3 ? q / (MX * MY) : 0)] = (T)0;   \
                         ++pc;                                                                          \
                     }                                                                                  \
@@ -3431,6 +3574,13 @@ template <int DIM, int TX, int TY, int TZ>
 constexpr size_t tc_lds(int rb)
 {
     return (size_t)tc_off<DIM, TX, TY, TZ>(tc_levels<DIM, TX, TY, TZ>()) * rb;
+}
+// the dynamic LDS of a launch: the levels, and the full weighting's scratch where it fits
+template <typename T, int DIM, int TX, int TY, int TZ>
+constexpr size_t tc_lds_total()
+{
+    return tc_lds<DIM, TX, TY, TZ>(sizeof(T)) +
+           (tc_fw_scratch<T, DIM, TX, TY, TZ>() ? (size_t)TcLev<DIM, TX, TY, DIM == 3 ? TZ : 1>::P * sizeof(T) : 0);
 }
 
 // The compile-time tail shapes (first level nx x ny x nz; nz = 1 in 2D) and their kernels.  k_tail_c runs a
@@ -4323,9 +4473,12 @@ FusedTuning fused_tuning_from_env()
         t.ys_rows = r >= 8 && (r & 1) == 0 ? r : 32;
     }
     if (const char* v = std::getenv("MGP_ZS_WGS")) t.wgs = std::max<int64_t>(1, std::atoll(v));
-    const int both = parse_patch(std::getenv("MGP_ZS_PATCH"), 0);
+    const char* vb = std::getenv("MGP_ZS_PATCH");
+    const int both = parse_patch(vb, 0);
     t.patch_pre = parse_patch(std::getenv("MGP_ZS_PATCH_PRE"), both);
-    t.patch_post = parse_patch(std::getenv("MGP_ZS_PATCH_POST"), both);
+    // POST's default: 4 x 8 patches on planes of >= 4096 tiles (auto, -1; round 5: the configs[4] slab's POST
+    // 32.7 -> 30.8 ms per F-cycle, while on the configs[3] slab's 2048 tiles per plane it lost 3.50 -> 3.80 ms)
+    t.patch_post = parse_patch(std::getenv("MGP_ZS_PATCH_POST"), vb ? both : -1);
     return t;
 }
 
@@ -4334,6 +4487,7 @@ FusedTuning fused_tuning_from_env()
 // rows a tile reads stream through z at the same time.  Returns px | py << 8, or 0 (tile rows).
 static int zs_patch(int patch, int tiles_x, int tiles_y, unsigned nb)
 {
+    if (patch == -1) patch = tiles_x * tiles_y >= 4096 ? 4 | (8 << 8) : 0;  // POST's default (FusedTuning)
     const int px = patch & 255, py = patch >> 8;
     if (!patch || tiles_x % px || tiles_y % py || nb <= 512) return 0;
     return patch;
@@ -4342,7 +4496,7 @@ static int zs_patch(int patch, int tiles_x, int tiles_y, unsigned nb)
 template <typename T, bool PRE, int LINEAR, bool ERR, bool CLZ, bool WIDE = false>
 static hipError_t zs_launch(const FusedArgs& a, hipStream_t s)
 {
-    using S = ZsShape<T, PRE, CLZ, WIDE>;
+    using S = ZsShape<T, PRE, CLZ, WIDE, PRE && LINEAR == 2>;
     const Op<T, 3> op = make_op<T, 3>(a.h, a.cl);
     const unsigned nb = (unsigned)((a.g.nx / S::TX) * (a.g.ny / S::TY) * (a.g.nz / a.zc));
     k_zs<T, PRE, LINEAR, ERR, CLZ, WIDE><<<nb, S::NTL, S::lds_bytes, s>>>((const T*)a.src, (const T*)a.f, (T*)a.dst,
@@ -4403,6 +4557,11 @@ static hipError_t fused_dispatch(const FusedArgs& a, hipStream_t s)
 #ifdef ZS_CL_AS_CLZ  // timing experiment only (wrong at the box faces): cl != 0 PRE runs the cl = 0 code
     if (a.pre) return a.linear ? zs_launch<T, true, 1, false, true>(a, s) : zs_launch<T, true, 0, false, true>(a, s);
 #endif
+    if constexpr (std::is_same<T, float>::value && CLZ) {  // the full weighting fused into PRE (fused_fwf_supported)
+        if (a.pre && a.linear == 2)
+            return a.src ? zs_launch<T, true, 2, false, CLZ>(a, s) : zs_launch<T, true, 2, true, CLZ>(a, s);
+    }
+    if (a.pre && a.linear == 2) return hipErrorInvalidValue;
     if (a.pre && !a.src)  // a fresh zero guess (ERR marks it in PRE)
         return a.linear ? zs_launch<T, true, 1, true, CLZ>(a, s) : zs_launch<T, true, 0, true, CLZ>(a, s);
     if (a.pre) return a.linear ? zs_launch<T, true, 1, false, CLZ>(a, s) : zs_launch<T, true, 0, false, CLZ>(a, s);
@@ -4495,11 +4654,25 @@ int fused_blocks(int rb, const Geo& g, int zc, bool clz, const FusedTuning& tu) 
 
 int fused_halo(bool pre) { return pre ? 5 : 4; }
 
+bool fused_fwf_supported(int rb, bool clz, bool dist)
+{
+    // fp32 levels without a boundary-modified operator (level 0), one rank's whole level: the fused PRE's trapezoid
+    // is 6 deep with the full weighting, deeper than a slab's kZsHaloPre ghost planes; fp64 tiles would exceed the LDS
+    const char* v = std::getenv("MGP_ZS_FWF");
+    return rb == 4 && clz && !dist && !(v && std::atoi(v) == 0);
+}
+
 template <typename T, bool CLZ>
 static hipError_t fused_attr()
 {
     const int pre = (int)ZsShape<T, true, CLZ>::lds_bytes, post = (int)ZsShape<T, false, CLZ>::lds_bytes;
     const auto A = hipFuncAttributeMaxDynamicSharedMemorySize;
+    if constexpr (std::is_same<T, float>::value && CLZ) {
+        const int w = (int)ZsShape<T, true, CLZ, false, true>::lds_bytes;
+        hipError_t e = hipFuncSetAttribute((const void*)k_zs<T, true, 2, false, CLZ>, A, w);
+        if (e == hipSuccess) e = hipFuncSetAttribute((const void*)k_zs<T, true, 2, true, CLZ>, A, w);
+        if (e != hipSuccess) return e;
+    }
     if constexpr (std::is_same<T, float>::value && CLZ) {
         const int w = (int)ZsShape<T, false, CLZ, true>::lds_bytes;
         hipError_t e = hipFuncSetAttribute((const void*)k_zs<T, false, 0, false, CLZ, true>, A, w);
@@ -4642,7 +4815,7 @@ static hipError_t tail_t(const TailSpec& t, hipStream_t s)
         if constexpr (DD == D) {                                                                             \
             if (++idx == sh && !done) {                                                                      \
                 auto kc = t.linear ? k_tail_c<T, D, 1, TX, TY, TZ> : k_tail_c<T, D, 0, TX, TY, TZ>;          \
-                kc<<<1, tc_threads<T>(), tc_lds<D, TX, TY, TZ>(sizeof(T)), s>>>(a);                               \
+                kc<<<1, tc_threads<T, D>(), tc_lds_total<T, D, TX, TY, TZ>(), s>>>(a);                               \
                 done = true;                                                                                 \
             }                                                                                                \
         } else {                                                                                             \
@@ -4665,9 +4838,9 @@ static hipError_t tail_c_attr()
     hipError_t e = hipSuccess;
 #define X(D, TX, TY, TZ)                                                                                 \
     if (e == hipSuccess)                                                                                 \
-        e = hipFuncSetAttribute((const void*)k_tail_c<T, D, 0, TX, TY, TZ>, A, (int)tc_lds<D, TX, TY, TZ>(sizeof(T))); \
+        e = hipFuncSetAttribute((const void*)k_tail_c<T, D, 0, TX, TY, TZ>, A, (int)tc_lds_total<T, D, TX, TY, TZ>()); \
     if (e == hipSuccess)                                                                                 \
-        e = hipFuncSetAttribute((const void*)k_tail_c<T, D, 1, TX, TY, TZ>, A, (int)tc_lds<D, TX, TY, TZ>(sizeof(T)));
+        e = hipFuncSetAttribute((const void*)k_tail_c<T, D, 1, TX, TY, TZ>, A, (int)tc_lds_total<T, D, TX, TY, TZ>());
     MGP_TC_SHAPES(X)
 #undef X
     return e;

@@ -58,10 +58,12 @@ CASES = [
     ((64, 64, 512), 8, dict(cycle="V"), 4096, True),
     ((64, 64, 256), 4, dict(cycle="F"), 4096, True),
     ((32, 32, 256), 8, dict(cycle="F", real="double"), 512, False),
+    # full weighting: k_resfw on the 64-wide slab levels (u exchanged two planes deep), the two-pass form below
+    ((64, 64, 256), 2, dict(cycle="V", restriction="full_weighting"), 4096, True),
 ]
 
 
-@pytest.mark.parametrize("box,world,extra,gather,side", CASES, ids=["w2-V", "w8-V", "w4-F", "w8-F-f64"])
+@pytest.mark.parametrize("box,world,extra,gather,side", CASES, ids=["w2-V", "w8-V", "w4-F", "w8-F-f64", "w2-V-fw"])
 def test_executed_comm_log_equals_plan(box, world, extra, gather, side, monkeypatch):
     monkeypatch.setenv("MGP_FUSED", "1")
     monkeypatch.setenv("MGP_FUSED_MIN_CELLS", "65536")

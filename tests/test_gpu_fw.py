@@ -67,6 +67,8 @@ FW_CONFIGS = [
     dict(dim=2, n=(256, 128, 1), real="double", smoother="rbgs", nu1=2, nu2=2, cycle="F", prolong="linear",
          coarse_bc="zero"),
     dict(dim=2, n=(1024, 1024, 1), real="float", smoother="rbgs", nu1=2, nu2=2, prolong="linear", coarse_bc="consistent"),
+    # zs engine: level 1 (64^3, cl = 0, a fresh guess) also runs the fused full weighting (k_zs PRE, LINEAR 2, ZSRC)
+    dict(dim=3, n=(128, 128, 128), real="float", smoother="rbgs", nu1=2, nu2=2, prolong="pc", coarse_bc="zero"),
 ]
 
 
