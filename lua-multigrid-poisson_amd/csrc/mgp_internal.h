@@ -167,7 +167,7 @@ int fused_zc(int rb, const Geo& g, bool pre, bool clz, const FusedTuning& tu);
 int fused_blocks(int rb, const Geo& g, int zc, bool clz, const FusedTuning& tu);
 hipError_t launch_fused(int rb, const FusedArgs& a, hipStream_t s);
 // PRE with the full weighting fused (FusedArgs::linear = 2): fp32, cl = 0, a replicated level (MGP_ZS_FWF=0: off)
-bool fused_fwf_supported(int rb, bool clz, bool dist);
+bool fused_fwf_supported(int rb, int dim, bool clz, bool dist);
 
 // Tiled smoothing phases of a small replicated red/black level (k_blk: one launch per phase, the 3D
 // or 2D tile and its halo in LDS):

@@ -4654,12 +4654,12 @@ int fused_blocks(int rb, const Geo& g, int zc, bool clz, const FusedTuning& tu) 
 
 int fused_halo(bool pre) { return pre ? 5 : 4; }
 
-bool fused_fwf_supported(int rb, bool clz, bool dist)
+bool fused_fwf_supported(int rb, int dim, bool clz, bool dist)
 {
     // fp32 levels without a boundary-modified operator (level 0), one rank's whole level: the fused PRE's trapezoid
     // is 6 deep with the full weighting, deeper than a slab's kZsHaloPre ghost planes; fp64 tiles would exceed the LDS
     const char* v = std::getenv("MGP_ZS_FWF");
-    return rb == 4 && clz && !dist && !(v && std::atoi(v) == 0);
+    return rb == 4 && dim == 3 && clz && !dist && !(v && std::atoi(v) == 0);  // (3D: k_zs; k_ys has no variant)
 }
 
 template <typename T, bool CLZ>
