@@ -1634,8 +1634,13 @@ struct ZsShape {
     // FWF: the residual rows in x order (RXSLOT per step parity), their x-combinations (AXSLOT per step parity) and a
     // ring of the y-combinations of 4 fine planes per coarse cell of the tile (AYSLOT per plane)
     static constexpr int RXSLOT = FWF ? YE * G * 2 * N : 0, AXSLOT = FWF ? YE * G * N : 0,
-                         AYSLOT = FWF ? (TY / 2) * (TX / 2) : 0;
+                         AYSLOT = FWF ? (TY / 2) * (TX / 2) : 0;  // (item i's N cells at i N)
     static constexpr int OFFRX = OFFC + 4 * CSLOT, OFFAX = OFFRX + 2 * RXSLOT, OFFAY = OFFAX + 2 * AXSLOT;
+    // FWF: the wave running the y-combinations (the 4th when the workgroup has 7 waves: alone on its SIMD) and its
+    // items per lane
+    static constexpr int FWY = NTL >= 4 * 64 ? 3 : 0;
+    static constexpr int FWYI = FWF ? (TY / 2) * (TX / (2 * N)) / 64 : 0;
+    static_assert(!FWF || ((TY / 2) * (TX / (2 * N)) % 64 == 0 && FWY * 64 + 64 <= NTL), "FWF: whole waves of y items");
     static constexpr size_t lds_bytes = (size_t)(OFFAY + 4 * AYSLOT) * sizeof(T);
     static_assert(CPAIRS <= 2 * NTL, "coarse staging: two pairs per thread");
     static_assert(CI % N == 0 && OFFC % N == 0, "coarse rows must hold aligned groups");
@@ -2474,57 +2479,91 @@ __attribute__((amdgpu_waves_per_eu(1, PRE ? ZS_WPE_PRE : ZS_WPE_POST))) void k_z
                 zs_residual<T, N, CLZ, ST>(W3[sl(6)], W3[sl(5)], W3[sl(4)], nr, W4[sl(5)], FB[sl(5)], col, 1 ^ pq, nbyz(q),
                                            g.nx, op, dz, rblk);
             const bool rin = in_xy && (ST || inz(q));  // (the residuals of cells outside the box weigh 0)
-            T* const rxw = lds + S::OFFRX + (p & 1) * S::RXSLOT + (ye * G + gx) * 2 * N;
+            // RX: the group's 2N cells in x order, the low N at t N and the high N at RXH + t N (t = ye G + gx), so
+            // that every access is one conflict-free 16-byte vector per lane
+            constexpr int RXH = S::RXSLOT / 2;
+            const int t = ye * G + gx;
+            if (ydist <= 1) {  // (rows within one of the tile: the only ones the x-combination reads)
+                VT x[2];  // x order: cell 2 (gm + e) + parity
 #pragma unroll
-            for (int e = 0; e < N; ++e) {  // x order: cell 2 (gm + e) + parity
-                rxw[2 * e + pq] = rin ? rred[e] : (T)0;
-                rxw[2 * e + (pq ^ 1)] = rin ? rblk[e] : (T)0;
+                for (int e = 0; e < N; ++e) {
+                    x[(2 * e) / N].v[(2 * e) % N] = rin ? (pq ? rblk[e] : rred[e]) : (T)0;
+                    x[(2 * e + 1) / N].v[(2 * e + 1) % N] = rin ? (pq ? rred[e] : rblk[e]) : (T)0;
+                }
+                T* const rxw = lds + S::OFFRX + (p & 1) * S::RXSLOT + t * N;
+                vstore<T, N>(rxw, x[0]);
+                vstore<T, N>(rxw + RXH, x[1]);
             }
+            const T wfv = (T)3 - clc, w3 = (T)3;
             // the x-combination of plane p - 6 (written to RX one step ago) for the tile's coarse columns, rows within
             // one of the tile: fine cells 2I - 1 .. 2I + 2 of coarse I = gm + e
             const bool tile_x = gx >= S::HXG && gx < G - S::HXG;
             if (tile_x && ydist <= 1) {
-                const T* rxr = lds + S::OFFRX + ((p - 1) & 1) * S::RXSLOT + (ye * G + gx) * 2 * N;
-                T* const axw = lds + S::OFFAX + (p & 1) * S::AXSLOT + (ye * G + gx) * N;
-                const T wfv = (T)3 - clc, w3 = (T)3;
+                const T* rxr = lds + S::OFFRX + ((p - 1) & 1) * S::RXSLOT;
+                T x[2 * N + 2];
+                const VT lo = vload_lds_whole<T, N>(rxr + t * N), hi = vload_lds_whole<T, N>(rxr + RXH + t * N);
+                x[0] = vload_lds_whole<T, N>(rxr + RXH + (t - 1) * N).v[N - 1];
+                x[2 * N + 1] = vload_lds_whole<T, N>(rxr + (t + 1) * N).v[0];
+#pragma unroll
+                for (int e = 0; e < N; ++e) {
+                    x[1 + e] = lo.v[e];
+                    x[1 + N + e] = hi.v[e];
+                }
                 const int cxn = g.nx >> 1;
+                VT ax;
 #pragma unroll
                 for (int e = 0; e < N; ++e) {
                     const int I = col.gm + e;
-                    axw[e] = fw_axis(rxr[2 * e - 1], rxr[2 * e], rxr[2 * e + 1], rxr[2 * e + 2], I == 0 ? wfv : w3,
-                                     I == cxn - 1 ? wfv : w3);
+                    ax.v[e] = fw_axis(x[2 * e], x[2 * e + 1], x[2 * e + 2], x[2 * e + 3], I == 0 ? wfv : w3,
+                                      I == cxn - 1 ? wfv : w3);
                 }
+                vstore<T, N>(lds + S::OFFAX + (p & 1) * S::AXSLOT + t * N, ax);
             }
-            // the y-combination of plane p - 7 (its x-combinations were written one step ago) in the owner rows (even
-            // tile rows: coarse row J = gy / 2, fine rows 2J - 1 .. 2J + 2), then coarse plane K when p - 7 = 2K + 2
-            const int rl = ye - H;
-            if (tile_x && rl >= 0 && rl < TY && (rl & 1) == 0) {
-                const T* axr = lds + S::OFFAX + ((p - 1) & 1) * S::AXSLOT + gx * N;
-                const T wfv = (T)3 - clc, w3 = (T)3;
-                const int J = gy >> 1, cyn = g.ny >> 1;
-                const int q2 = p - 7;
-                T* const ayw = lds + S::OFFAY + (rl >> 1) * (TX / 2) + (gx - S::HXG) * N;
-#pragma unroll
-                for (int e = 0; e < N; ++e) {
-                    T ay = axr[(ye - 1) * G * N + e];
-                    ay = ay + (J == 0 ? wfv : w3) * axr[ye * G * N + e];
-                    ay = ay + (J == cyn - 1 ? wfv : w3) * axr[(ye + 1) * G * N + e];
-                    ay = ay + axr[(ye + 2) * G * N + e];
-                    ayw[(q2 & 3) * S::AYSLOT + e] = ay;
-                }
+            // the y-combination of plane p - 7 (its x-combinations were written one step ago) for every coarse cell
+            // group of the tile (coarse row J: fine rows 2J - 1 .. 2J + 2), then coarse plane K when p - 7 = 2K + 2.
+            // The TY / 2 x TX / (2 N) items run in wave FWY (ZsShape: the wave that shares no SIMD when the
+            // workgroup has 4 k + 3 waves), each item on the same lane every step (the AY ring is lane-private)
+            if (tid >= S::FWY * 64 && tid < S::FWY * 64 + 64) {
+                const T* axr = lds + S::OFFAX + ((p - 1) & 1) * S::AXSLOT;
+                const int cyn = g.ny >> 1, q2 = p - 7;
                 const int dq2 = q2 - 2 - (ST ? (Z0 & ~1) : Z0);  // 2K - z0 - Z0 for the coarse plane K ending at q2
-                if (dq2 >= 0 && dq2 < zc && (dq2 & 1) == 0) {
-                    const int K = (z0 + q2 - 2) >> 1;  // global coarse plane
-                    const T wk0 = K == 0 ? wfv : w3, wk1 = K == gc.gnz - 1 ? wfv : w3;
-                    T* rowc = R + (int64_t)(K - cz0) * gc.P + (int64_t)J * gc.hw;
+                const bool emit = dq2 >= 0 && dq2 < zc && (dq2 & 1) == 0;
+                const int K = (z0 + q2 - 2) >> 1;  // global coarse plane
+                const T wk0 = K == 0 ? wfv : w3, wk1 = K == gc.gnz - 1 ? wfv : w3;
+                constexpr int CG = TX / (2 * N);  // coarse groups per coarse row
 #pragma unroll
-                    for (int e = 0; e < N; ++e) {
-                        T az = ayw[((q2 - 3) & 3) * S::AYSLOT + e];
-                        az = az + wk0 * ayw[((q2 - 2) & 3) * S::AYSLOT + e];
-                        az = az + wk1 * ayw[((q2 - 1) & 3) * S::AYSLOT + e];
-                        az = az + ayw[(q2 & 3) * S::AYSLOT + e];
-                        const int I = col.gm + e;
-                        rowc[((I + J + K) & 1) * gc.H + (I >> 1)] = (T)(1.0 / 512.0) * az;
+                for (int k = 0; k < S::FWYI; ++k) {
+                    const int i = tid - S::FWY * 64 + 64 * k;
+                    const int jl = i / CG, cg = i % CG;
+                    const int J = (Y0 >> 1) + jl, ty = (H + 2 * jl) * G + S::HXG + cg;
+                    const VT a0 = vload_lds_whole<T, N>(axr + (ty - G) * N), a1 = vload_lds_whole<T, N>(axr + ty * N),
+                             a2 = vload_lds_whole<T, N>(axr + (ty + G) * N), a3 = vload_lds_whole<T, N>(axr + (ty + 2 * G) * N);
+                    const T wj0 = J == 0 ? wfv : w3, wj1 = J == cyn - 1 ? wfv : w3;
+                    VT ay;
+#pragma unroll
+                    for (int e = 0; e < N; ++e) ay.v[e] = ((a0.v[e] + wj0 * a1.v[e]) + wj1 * a2.v[e]) + a3.v[e];
+                    T* const ayb = lds + S::OFFAY + i * N;
+                    vstore<T, N>(ayb + (q2 & 3) * S::AYSLOT, ay);
+                    if (emit) {
+                        const VT b0 = vload_lds_whole<T, N>(ayb + ((q2 - 3) & 3) * S::AYSLOT),
+                                 b1 = vload_lds_whole<T, N>(ayb + ((q2 - 2) & 3) * S::AYSLOT),
+                                 b2 = vload_lds_whole<T, N>(ayb + ((q2 - 1) & 3) * S::AYSLOT);
+                        // coarse cells I = gm .. gm + N - 1 (gm even): the even ones at m = gm / 2 .. of one colour
+                        // half, the odd ones of the other
+                        const int gm = X0 / 2 + cg * N;
+                        T* rowc = R + (int64_t)(K - cz0) * gc.P + (int64_t)J * gc.hw + (gm >> 1);
+                        Vec<T, N / 2> ev, od;
+#pragma unroll
+                        for (int e = 0; e < N; ++e) {
+                            const T az = ((b0.v[e] + wk0 * b1.v[e]) + wk1 * b2.v[e]) + ay.v[e];
+                            if (e & 1)
+                                od.v[e >> 1] = (T)(1.0 / 512.0) * az;
+                            else
+                                ev.v[e >> 1] = (T)(1.0 / 512.0) * az;
+                        }
+                        const int ce = (gm + J + K) & 1;
+                        vstore<T, N / 2>(rowc + ce * gc.H, ev);
+                        vstore<T, N / 2>(rowc + (ce ^ 1) * gc.H, od);
                     }
                 }
             }
