@@ -210,6 +210,9 @@ __global__ __launch_bounds__(FwShape<DIM>::NT) void k_resfw(const T* __restrict_
     }
 }
 
+#ifndef FW_KMIN  // (build knob: the smallest z-chunk in coarse planes; 128^3 -> 64^3: 39 -> 18.6 us at 2 against 8)
+#define FW_KMIN 2
+#endif
 #ifndef FW_WGS  // (build knob: workgroups the z-chunking aims for; 512^3 FW cycle 1.600 ms at 1024, 1.620 at 2048, 1.639 at 4096)
 #define FW_WGS 1024
 #endif
@@ -227,7 +230,7 @@ hipError_t resfw_t(const void* u, const void* f, void* R, Geo g, Geo gc, double 
         // coarse planes per chunk: halve while there are fewer than 2048 workgroups (8 per CU) and a chunk keeps
         // >= 8 coarse planes (a chunk re-reads 2 of every 2 kc + 2 fine planes of its neighbours)
         kc = cz;
-        while (tiles * (cz / kc) < FW_WGS && kc >= 16) kc /= 2;
+        while (tiles * (cz / kc) < FW_WGS && kc >= 2 * FW_KMIN) kc /= 2;
         chunks = (cz + kc - 1) / kc;
     }
     const int64_t nb = tiles * chunks;
