@@ -1001,7 +1001,7 @@ int fused_pre(mgp_ctx* c, int l, double h)
     const bool fw = c->o.restriction == MGP_RESTRICT_FULL_WEIGHTING;
     // the full weighting fused into the phase (fp32 level 0 of one rank's whole box), else smoothing only (both
     // colours stored) and the full weighting after it
-    const bool fwf = fw && mgp::fused_fwf_supported(c->rb, c->o.dim, coarse_coef(c->o.coarse_bc, l) == 0.0, L.p.dist);
+    const bool fwf = fw && mgp::fused_fwf_supported(c->rb, c->o.dim, coarse_coef(c->o.coarse_bc, l) == 0.0, L.p.dist, c->tu);
     mgp::FusedArgs a{};
     a.tu = c->tu;
     a.pre = true;

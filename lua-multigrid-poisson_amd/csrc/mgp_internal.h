@@ -139,6 +139,7 @@ struct FusedTuning {
     // (MGP_ZS_PATCH=px,py sets both phases, MGP_ZS_PATCH_PRE / MGP_ZS_PATCH_POST one; "0" off; -1: POST's default,
     // 4 x 8 on planes of >= 4096 tiles)
     int patch_pre = 0, patch_post = -1;
+    bool fwf = true;     // MGP_ZS_FWF=0: the full weighting after the fused PRE instead of inside it
 };
 FusedTuning fused_tuning_from_env();
 
@@ -167,7 +168,7 @@ int fused_zc(int rb, const Geo& g, bool pre, bool clz, const FusedTuning& tu);
 int fused_blocks(int rb, const Geo& g, int zc, bool clz, const FusedTuning& tu);
 hipError_t launch_fused(int rb, const FusedArgs& a, hipStream_t s);
 // PRE with the full weighting fused (FusedArgs::linear = 2): fp32, cl = 0, a replicated level (MGP_ZS_FWF=0: off)
-bool fused_fwf_supported(int rb, int dim, bool clz, bool dist);
+bool fused_fwf_supported(int rb, int dim, bool clz, bool dist, const FusedTuning& tu);
 
 // Tiled smoothing phases of a small replicated red/black level (k_blk: one launch per phase, the 3D
 // or 2D tile and its halo in LDS):

@@ -1481,6 +1481,9 @@ __device__ __forceinline__ void lds_barrier()
 #ifndef ZS_YROLE
 #define ZS_YROLE 1
 #endif
+#ifndef ZS_XROLE  // (with ZS_YROLE: the tile rows' x-halo column groups in waves of their own)
+#define ZS_XROLE 1
+#endif
 #ifndef ZS_FHALO
 #define ZS_FHALO 1
 #endif
@@ -1601,12 +1604,17 @@ struct ZsShape {
     // d in 1..3 skips the residual (a third of the step's VALU for the halo waves; only where it costs no wave)
     static constexpr int YT0 = TY * G, YT1 = YT0 + 6 * G, YT2S = (YT1 + 63) / 64 * 64, YT2 = YT2S + 4 * G;
     static constexpr bool YROLE = ZS_YROLE && PRE && !PS && H == 5 && (YT2 + 63) / 64 * 64 <= NTL;
+    // ZS_XROLE: the tile rows' own columns (TC threads, whole waves) first, then their x-halo column groups (HXG per
+    // side; those need stages 1..4 but no residual, role 1), so that the waves that run everything are TC / 64 (4 of
+    // 7 at 64 x 32: one per SIMD, where 5 put two on one SIMD)
+    static constexpr int GC = G - 2 * HXG, TC = TY * GC;
+    static constexpr bool XROLE = YROLE && ZS_XROLE && TC % 64 == 0;
     // extended row (0 .. YE - 1) of thread t (-1: no row) and the role of wave w (0: tile rows, every stage and the
-    // residual; 1: rows d <= 3, stages 1..4; 2: rows d >= 4, stage 1)
+    // residual; 1: rows d <= 3 (XROLE: and the tile rows' x-halo groups), stages 1..4; 2: rows d >= 4, stage 1)
     static __device__ __forceinline__ int yrow(int t)
     {
         if (!YROLE) return t < NT ? t / G : -1;
-        if (t < YT0) return H + t / G;
+        if (t < YT0) return H + (XROLE ? (t < TC ? t / GC : (t - TC) / (2 * HXG)) : t / G);
         if (t < YT1) {  // d = 1, 2, 3: the row above, then below the tile
             const int r = (t - YT0) / G, d = 1 + (r >> 1);
             return (r & 1) ? H + TY - 1 + d : H - d;
@@ -1617,8 +1625,19 @@ struct ZsShape {
         }
         return -1;
     }
-    static __device__ __forceinline__ int ycol(int t) { return YROLE && t >= YT2S ? (t - YT2S) % G : t % G; }
-    static constexpr int wave_role(int w) { return !YROLE || 64 * w < YT0 ? 0 : (64 * w < YT1 ? 1 : 2); }
+    static __device__ __forceinline__ int ycol(int t)
+    {
+        if (XROLE && t < YT0) {
+            if (t < TC) return HXG + t % GC;
+            const int k = (t - TC) % (2 * HXG);
+            return k < HXG ? k : GC + k;
+        }
+        return YROLE && t >= YT2S ? (t - YT2S) % G : t % G;
+    }
+    static constexpr int wave_role(int w)
+    {
+        return !YROLE || 64 * w < (XROLE ? TC : YT0) ? 0 : (64 * w < YT1 ? 1 : 2);
+    }
     static constexpr int SLOT = YE * HWE;              // reals per LDS slot (one colour of a plane)
     // stage-3 slots: PRE's residual reads 2 back (3 needed; 4 while LDS allows: power-of-2 ring)
     static constexpr int NS3 = PRE ? (TY > 32 ? 3 : 4) : 2;
@@ -4518,6 +4537,7 @@ FusedTuning fused_tuning_from_env()
     // POST's default: 4 x 8 patches on planes of >= 4096 tiles (auto, -1; round 5: the configs[4] slab's POST
     // 32.7 -> 30.8 ms per F-cycle, while on the configs[3] slab's 2048 tiles per plane it lost 3.50 -> 3.80 ms)
     t.patch_post = parse_patch(std::getenv("MGP_ZS_PATCH_POST"), vb ? both : -1);
+    if (const char* v = std::getenv("MGP_ZS_FWF")) t.fwf = std::atoi(v) != 0;
     return t;
 }
 
@@ -4693,12 +4713,12 @@ int fused_blocks(int rb, const Geo& g, int zc, bool clz, const FusedTuning& tu) 
 
 int fused_halo(bool pre) { return pre ? 5 : 4; }
 
-bool fused_fwf_supported(int rb, int dim, bool clz, bool dist)
+bool fused_fwf_supported(int rb, int dim, bool clz, bool dist, const FusedTuning& tu)
 {
     // fp32 levels without a boundary-modified operator (level 0), one rank's whole level: the fused PRE's trapezoid
-    // is 6 deep with the full weighting, deeper than a slab's kZsHaloPre ghost planes; fp64 tiles would exceed the LDS
-    const char* v = std::getenv("MGP_ZS_FWF");
-    return rb == 4 && dim == 3 && clz && !dist && !(v && std::atoi(v) == 0);  // (3D: k_zs; k_ys has no variant)
+    // is 6 deep with the full weighting, deeper than a slab's kZsHaloPre ghost planes; fp64 tiles would exceed the LDS;
+    // 3D only (k_ys has no such variant)
+    return rb == 4 && dim == 3 && clz && !dist && tu.fwf;
 }
 
 template <typename T, bool CLZ>

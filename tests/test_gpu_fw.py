@@ -138,3 +138,26 @@ def test_fw_slab_decomposition_loopback(box, world, gather, cfg, fused, monkeypa
     o.step()
     o.step()
     assert np.array_equal(psi, o.get(0))
+
+
+@pytest.mark.parametrize("n,cycle", [((512, 512, 512), "V"), ((256, 128, 256), "F")], ids=["512-V", "256x128x256-F"])
+def test_fw_fused_pre_equals_restriction_after_phase(n, cycle, monkeypatch):
+    """The full weighting fused into k_zs PRE (LINEAR 2: level 0 of an fp32 box, the bench's 512^3 among them) ==
+    the same phase followed by k_resfw (MGP_ZS_FWF=0, read at creation), bit for bit, on a random field."""
+    kw = dict(dim=3, n=n, real="float", smoother="rbgs", nu1=2, nu2=2, prolong="linear", coarse_bc="consistent",
+              restriction="full_weighting", cycle=cycle)
+    if n[0] < 512:
+        monkeypatch.setenv("MGP_FUSED_MIN_CELLS", "65536")
+    rng = np.random.default_rng(7)
+    f = rng.uniform(-1, 1, (n[2], n[1], n[0])).astype(np.float32)
+    out = []
+    for fwf in ("1", "0"):
+        monkeypatch.setenv("MGP_ZS_FWF", fwf)
+        ctx = _ctx(**kw)
+        assert ctx.levels[0]["engine"] == "zs"
+        ctx.set_f(f, 0)
+        errs = [ctx.cycle() for _ in range(2)]
+        out.append((ctx.get_psi(), errs))
+        ctx.close()
+    assert np.array_equal(out[0][0], out[1][0])
+    assert out[0][1] == out[1][1]
