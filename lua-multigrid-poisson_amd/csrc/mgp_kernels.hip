@@ -2620,7 +2620,10 @@ __attribute__((amdgpu_waves_per_eu(1, PRE ? ZS_WPE_PRE : ZS_WPE_POST))) void k_z
     pe -= (pe - ps + 1) % UNR;             // and in the steady part
     // no steady part (the epilogue takes all) without a whole group or with odd z0 / Z0 (static parity)
     // POST with the BQ cache: (z0 + Z0) % 4 == 0 as well (static parity of the coarse plane)
-    if (pe < ps || ((z0 | Z0) & 1) || (!PRE && LINEAR == 1 && ZS_BQ && ((z0 + Z0) & 3))) ps = pe = zlo - 1;
+#ifndef ZS_ALL_GENERIC  // timing experiment: every step generic (the price of the box-face steps)
+#define ZS_ALL_GENERIC 0
+#endif
+    if (ZS_ALL_GENERIC || pe < ps || ((z0 | Z0) & 1) || (!PRE && LINEAR == 1 && ZS_BQ && ((z0 + Z0) & 3))) ps = pe = zlo - 1;
     int p = zlo;
     const std::integral_constant<int, -1> RPL;
     // UNR steps from p0 (p0 - zlo a multiple of UNR): ring slot k & 3, buffers k % NPF and (k + PFD) % NPF;
