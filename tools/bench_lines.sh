@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round 3 GPU check: selected new tests first, then the whole GPU suite, then bench lines (BENCHES, one per line).
+# Bench lines on the GPU box (BENCHES, one per line; optional FIRST tests and the whole GPU suite before them).
 # Every GPU step has its own time limit; the script stops at the first failure.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Copy the end-of-round evidence in gpurun_out/ (tools/r05_final.sh; earlier rounds: r03_final_tests.sh + r03_final.sh, r04_final.sh) into profiles/
+"""Copy the end-of-round evidence in gpurun_out/ (tools/r05_final.sh) into profiles/
 under a round prefix and print the bench lines.
 
 usage: tools/install_evidence.py [prefix]   (default r03)

@@ -48,7 +48,7 @@ python3 bench.py --real double --steps 30 $TR
 python3 bench.py --config0 --steps 20 $TR
 python3 bench.py --restriction full_weighting --steps 30 $TR
 python3 bench.py --box 2048,2048,256 --steps 10 --warmup 2 $TR
-python3 bench.py --box 4096,4096,512 --cycle F --steps 5 --warmup 1 $TR" bash tools/r03_check.sh || exit $?
+python3 bench.py --box 4096,4096,512 --cycle F --steps 5 --warmup 1 $TR" bash tools/bench_lines.sh || exit $?
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof2d -o run --output-format csv -- python3 bench.py --dim 2 --n 4096 --steps 50 --cpu-cycles 0 > gpurun_out/prof2d.log 2>&1
 rc=$?; tail -n 2 gpurun_out/prof2d.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/proffw -o run --output-format csv -- python3 bench.py --restriction full_weighting --steps 20 --cpu-cycles 0 --no-north-star > gpurun_out/proffw.log 2>&1
