@@ -140,6 +140,7 @@ struct FusedTuning {
     // 4 x 8 on planes of >= 4096 tiles)
     int patch_pre = 0, patch_post = -1;
     bool fwf = true;     // MGP_ZS_FWF=0: the full weighting after the fused PRE instead of inside it
+    int post_zc = 256;   // MGP_ZS_POST_ZC: POST's z-chunks hold at most this many planes (0: no limit)
 };
 FusedTuning fused_tuning_from_env();
 

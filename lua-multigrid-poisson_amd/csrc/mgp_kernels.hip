@@ -4541,6 +4541,7 @@ FusedTuning fused_tuning_from_env()
     // 32.7 -> 30.8 ms per F-cycle, while on the configs[3] slab's 2048 tiles per plane it lost 3.50 -> 3.80 ms)
     t.patch_post = parse_patch(std::getenv("MGP_ZS_PATCH_POST"), vb ? both : -1);
     if (const char* v = std::getenv("MGP_ZS_FWF")) t.fwf = std::atoi(v) != 0;
+    if (const char* v = std::getenv("MGP_ZS_POST_ZC")) t.post_zc = std::max(0, std::atoi(v));
     return t;
 }
 
@@ -4703,6 +4704,10 @@ int fused_zc(int rb, const Geo& g, bool pre, bool clz, const FusedTuning& tu)
     const int64_t tiles = (int64_t)(g.nx / TX) * (g.ny / TY);
     int64_t chunks = 1;
     while (tiles * chunks < target && g.nz / (chunks * 2) >= 16) chunks *= 2;
+    // POST: streams of at most tu.post_zc planes (planes of many tiles run as one chunk otherwise: the 4096^2 x 512
+    // slab's POST 30.5 -> 28.5 ms per F-cycle with 256-plane chunks; the workgroups drift apart over long streams and
+    // the y-neighbours' halo rows miss in L2)
+    while (!pre && tu.post_zc > 0 && g.nz / chunks > tu.post_zc && g.nz / (chunks * 2) >= 16) chunks *= 2;
     return (int)(g.nz / chunks);
 }
 
