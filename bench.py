@@ -538,9 +538,13 @@ def source_hash():
     """sha256 (16 hex) of the library's kernel and ABI sources: tags PMC traffic to the build it measured."""
     import hashlib
 
+    import glob
+
     h = hashlib.sha256()
-    for f in ("mgp_kernels.hip", "mgp_api.cpp", "mgp_internal.h"):
-        with open(os.path.join(ROOT, "lua-multigrid-poisson_amd", "csrc", f), "rb") as fh:
+    csrc = os.path.join(ROOT, "lua-multigrid-poisson_amd", "csrc")
+    for f in sorted(glob.glob(os.path.join(csrc, "*.hip")) + glob.glob(os.path.join(csrc, "*.cpp")) +
+                    glob.glob(os.path.join(csrc, "*.h"))):
+        with open(f, "rb") as fh:
             h.update(fh.read())
     return h.hexdigest()[:16]
 
