@@ -25,6 +25,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <map>
 #include <vector>
 
 #include <dlfcn.h>
@@ -259,6 +260,7 @@ struct mgp_ctx {
     size_t stage_bytes = 0;
     uint64_t* d_stats_h = nullptr;  // mgp_field_stats scratch: kSumBlocks + 1 hashes, then 3 kSumBlocks + 3 doubles
     double* d_part = nullptr;
+    std::map<char*, char*> pad_base;  // (MGP_PAD_BYTES) offset pointer -> its allocation
     int64_t part_cap = 0;
     double* d_errs = nullptr;
     int errs_cap = 0;
@@ -965,6 +967,43 @@ int materialize_zero(mgp_ctx* c, Level& L)
     return MGP_OK;
 }
 
+// A level's u, f, t (and the finest level's xbuf) start k * MGP_PAD_BYTES (default 4352 = 4 KiB + 256) into their
+// allocations (k = 1, 2, 3, 4).  The arrays are power-of-two sized, so without it equal offsets of u, f, t and xbuf
+// share their address bits below 4 KiB, and the phases' concurrent streams of the four arrays meet on the same
+// memory channels: 512^3 POST 430 -> 409 us (every offset that is not a multiple of 4 KiB measured alike, 256 B ..
+// 64 KiB + 256; multiples of 4 KiB did not help).  MGP_PAD_BYTES=0: no offsets.
+size_t pad_bytes()
+{
+    static const size_t v = [] {
+        const char* e = std::getenv("MGP_PAD_BYTES");
+        return e ? (size_t)std::atoll(e) & ~(size_t)255 : (size_t)4352;
+    }();
+    return v;
+}
+int pad_levels(size_t l)  // MGP_PAD_LEVELS (experiment): pad levels < this (default every level)
+{
+    static const int v = [] {
+        const char* e = std::getenv("MGP_PAD_LEVELS");
+        return e ? std::atoi(e) : 64;
+    }();
+    return (int)l < v ? 1 : 0;
+}
+hipError_t dev_alloc(mgp_ctx* c, char** p, size_t bytes, int k)
+{
+    const size_t off = (size_t)k * pad_bytes();
+    char* base = nullptr;
+    const hipError_t e = hipMalloc(&base, bytes + off);
+    if (e != hipSuccess) return e;
+    *p = base + off;
+    if (off) c->pad_base[*p] = base;
+    return hipSuccess;
+}
+void dev_free(mgp_ctx* c, char* p)
+{
+    auto it = c->pad_base.find(p);
+    (void)hipFree(it == c->pad_base.end() ? p : it->second);
+}
+
 double level_h(const mgp_ctx* c, int level) { return std::ldexp(1.0 / (double)c->lev[0].p.nx, level); }
 
 // The black u planes a temporally blocked POST on slab level l reads from its z-neighbours are final once
@@ -1065,6 +1104,7 @@ int fused_post(mgp_ctx* c, int l, double h, bool want_err)
     a.old = want_err ? c->ui(L, L.t) : nullptr;
     a.V = c->ui(C, C.u) + (size_t)(zc * C.g.P) * c->rb;
     a.partials = want_err ? c->d_part : nullptr;
+    if (std::getenv("MGP_STAMP_R")) a.R = c->ui(C, C.f);  // (ZS_STAMP timing builds: POST's stamps into level l+1's f)
     a.g = L.g;
     a.gc = gc;
     a.h = h;
@@ -1726,14 +1766,14 @@ static void destroy_impl(mgp_ctx* c)
     if (!c) return;
     if (c->s) (void)hipStreamSynchronize(c->s);
     for (auto& L : c->lev) {
-        if (L.u) (void)hipFree(L.u);
-        if (L.f) (void)hipFree(L.f);
-        if (L.t) (void)hipFree(L.t);
+        if (L.u) dev_free(c, L.u);
+        if (L.f) dev_free(c, L.f);
+        if (L.t) dev_free(c, L.t);
     }
     if (c->zbuf) (void)hipFree(c->zbuf);
     if (c->psi_old) (void)hipFree(c->psi_old);
     if (c->rscratch) (void)hipFree(c->rscratch);
-    if (c->xbuf) (void)hipFree(c->xbuf);
+    if (c->xbuf) dev_free(c, c->xbuf);
     if (c->stage) (void)hipFree(c->stage);
     if (c->d_stats_h) (void)hipFree(c->d_stats_h);
     if (c->d_part) (void)hipFree(c->d_part);
@@ -1914,8 +1954,9 @@ static int create_impl(mgp_ctx** out, const mgp_opts* o, mgp_loopback* lb, ncclC
         Level& L = c->lev[l];
         const size_t bytes = (size_t)L.alloc * rb;
         const bool need_t = c->o.smoother == MGP_JACOBI || (l == 0 && c->err_fuse) || L.fused || L.blk || L.zpost;
-        if (hipMalloc(&L.u, bytes) != hipSuccess || hipMalloc(&L.f, bytes) != hipSuccess ||
-            (need_t && hipMalloc(&L.t, bytes) != hipSuccess)) {
+        const int pk = pad_levels(l);
+        if (dev_alloc(c, &L.u, bytes, pk) != hipSuccess || dev_alloc(c, &L.f, bytes, 2 * pk) != hipSuccess ||
+            (need_t && dev_alloc(c, &L.t, bytes, 3 * pk) != hipSuccess)) {
             c->err = "hipMalloc failed for level " + std::to_string(l) + " (" + std::to_string(bytes) + " bytes)";
             return bail(MGP_ERR_OOM);
         }
@@ -1935,7 +1976,7 @@ static int create_impl(mgp_ctx** out, const mgp_opts* o, mgp_loopback* lb, ncclC
     {
         const char* v = std::getenv("MGP_KEEP_PSI_OLD");
         if (c->o.err_mode && c->err_fuse && L0.fused && !(v && std::atoi(v) == 0)) {
-            if (hipMalloc(&c->xbuf, (size_t)L0.alloc * rb) != hipSuccess ||
+            if (dev_alloc(c, &c->xbuf, (size_t)L0.alloc * rb, 4) != hipSuccess ||
                 hipMemsetAsync(c->xbuf, 0, (size_t)L0.alloc * rb, c->s) != hipSuccess) {
                 c->err = "hipMalloc failed for the psiOld-keeping output buffer";
                 return bail(MGP_ERR_OOM);

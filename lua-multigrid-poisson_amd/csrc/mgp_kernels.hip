@@ -2662,7 +2662,17 @@ __attribute__((amdgpu_waves_per_eu(1, PRE ? ZS_WPE_PRE : ZS_WPE_POST))) void k_z
                 bq_fill(rp, BQ[1], K - 1);
             }
         }
-        for (; p <= pe; p += UNR) group(STY, rp, ro, p, p + UNR);
+        for (; p <= pe; p += UNR) {
+#ifdef ZS_STAMP  // timing experiment (wrong results): POST's wall clock every 16 steps into R (level 1's f)
+            if (!PRE && tid == 0 && ((p - zlo) & 15) == 0 && (p - zlo) / 16 < 32) {
+                const unsigned long long w = wall_clock64();
+                float* out = reinterpret_cast<float*>(R) + 64 * (int)blockIdx.x + 2 * ((p - zlo) / 16);
+                out[0] = __uint_as_float((unsigned)(w & 0xffffffffu));
+                out[1] = __uint_as_float((unsigned)(w >> 32));
+            }
+#endif
+            group(STY, rp, ro, p, p + UNR);
+        }
     };
     if constexpr (S::PS) {  // wave-uniform: one copy of the steady loop per row parity
         if (((H + wcls) & 1) == 0)
