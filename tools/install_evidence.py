@@ -46,7 +46,8 @@ if os.path.exists(G + "pytest_gpu.log") and os.path.exists(G + "smoke.log"):
 if os.path.isdir(G + "sq"):  # SQ / TCC counter passes (tools/r04_final.sh)
     tool(["tools/pmc_summary.py", G + "sq", "k_zs|k_tail_c|k_fresh"], f"{pre}_sq_counters_summary.txt")
 tool(["tools/trace_summary.py", G + "prof/run_kernel_trace.csv"], f"{pre}_trace_summary.txt")
-tool(["tools/cycle_breakdown.py", G + "prof/run_kernel_trace.csv", "8"], f"{pre}_cycle_breakdown.txt")
+tool(["tools/cycle_breakdown.py", G + "prof/run_kernel_trace.csv", "3", "k_zs<float, true, 0, false, true, false>=114688"],
+     f"{pre}_cycle_breakdown.txt")
 if os.path.exists(G + "prof2d/run_kernel_stats.csv"):
     shutil.copy(G + "prof2d/run_kernel_stats.csv", P + f"{pre}_2d_kernel_stats.csv")
     tool(["tools/trace_summary.py", G + "prof2d/run_kernel_trace.csv"], f"{pre}_2d_trace_summary.txt")
