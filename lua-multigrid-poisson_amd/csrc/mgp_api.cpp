@@ -261,6 +261,7 @@ struct mgp_ctx {
     uint64_t* d_stats_h = nullptr;  // mgp_field_stats scratch: kSumBlocks + 1 hashes, then 3 kSumBlocks + 3 doubles
     double* d_part = nullptr;
     std::map<char*, char*> pad_base;  // (MGP_PAD_BYTES) offset pointer -> its allocation
+    size_t pad = 0;                   // MGP_PAD_BYTES at creation
     int64_t part_cap = 0;
     double* d_errs = nullptr;
     int errs_cap = 0;
@@ -972,25 +973,14 @@ int materialize_zero(mgp_ctx* c, Level& L)
 // share their address bits below 4 KiB, and the phases' concurrent streams of the four arrays meet on the same
 // memory channels: 512^3 POST 430 -> 409 us (every offset that is not a multiple of 4 KiB measured alike, 256 B ..
 // 64 KiB + 256; multiples of 4 KiB did not help).  MGP_PAD_BYTES=0: no offsets.
-size_t pad_bytes()
+size_t pad_bytes()  // (read when a context is created)
 {
-    static const size_t v = [] {
-        const char* e = std::getenv("MGP_PAD_BYTES");
-        return e ? (size_t)std::atoll(e) & ~(size_t)255 : (size_t)4352;
-    }();
-    return v;
-}
-int pad_levels(size_t l)  // MGP_PAD_LEVELS (experiment): pad levels < this (default every level)
-{
-    static const int v = [] {
-        const char* e = std::getenv("MGP_PAD_LEVELS");
-        return e ? std::atoi(e) : 64;
-    }();
-    return (int)l < v ? 1 : 0;
+    const char* e = std::getenv("MGP_PAD_BYTES");
+    return e ? (size_t)std::max(0LL, std::atoll(e)) & ~(size_t)255 : (size_t)4352;
 }
 hipError_t dev_alloc(mgp_ctx* c, char** p, size_t bytes, int k)
 {
-    const size_t off = (size_t)k * pad_bytes();
+    const size_t off = (size_t)k * c->pad;
     char* base = nullptr;
     const hipError_t e = hipMalloc(&base, bytes + off);
     if (e != hipSuccess) return e;
@@ -1950,13 +1940,13 @@ static int create_impl(mgp_ctx** out, const mgp_opts* o, mgp_loopback* lb, ncclC
         return bail(MGP_ERR_HIP);
     }
     const size_t rb = (size_t)c->rb;
+    c->pad = pad_bytes();
     for (size_t l = 0; l < c->lev.size(); ++l) {
         Level& L = c->lev[l];
         const size_t bytes = (size_t)L.alloc * rb;
         const bool need_t = c->o.smoother == MGP_JACOBI || (l == 0 && c->err_fuse) || L.fused || L.blk || L.zpost;
-        const int pk = pad_levels(l);
-        if (dev_alloc(c, &L.u, bytes, pk) != hipSuccess || dev_alloc(c, &L.f, bytes, 2 * pk) != hipSuccess ||
-            (need_t && dev_alloc(c, &L.t, bytes, 3 * pk) != hipSuccess)) {
+        if (dev_alloc(c, &L.u, bytes, 1) != hipSuccess || dev_alloc(c, &L.f, bytes, 2) != hipSuccess ||
+            (need_t && dev_alloc(c, &L.t, bytes, 3) != hipSuccess)) {
             c->err = "hipMalloc failed for level " + std::to_string(l) + " (" + std::to_string(bytes) + " bytes)";
             return bail(MGP_ERR_OOM);
         }
