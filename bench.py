@@ -241,6 +241,12 @@ def run_workload(a, cfg, box, strong, rank, world, local, dist, steps, warmup, p
         if world > 1:
             dist.barrier()
 
+    # the copy-bandwidth probe (the line's measured copy peak) runs before the warmup cycles: it is the run's first
+    # sustained GPU load, so the clocks have ramped when the warmup starts (MGP_BENCH_PROBE_LATE=1: after the timing)
+    copy_peak = None
+    probe_first = os.environ.get("MGP_BENCH_PROBE_LATE", "0") == "0"
+    if primary and a.copy_probe_mb > 0 and local == 0 and rank == 0 and probe_first:
+        copy_peak = mgpoisson.copy_bandwidth(local, a.copy_probe_mb << 20, 10)
     # warmup (untimed; also captures the hipGraphs of the cycle)
     if warmup:
         ctx.cycles(warmup)
@@ -261,8 +267,7 @@ def run_workload(a, cfg, box, strong, rank, world, local, dist, steps, warmup, p
         ctx.timing(False)
         barrier_sync()
 
-    copy_peak = None
-    if primary and a.copy_probe_mb > 0 and local == 0 and rank == 0:
+    if primary and a.copy_probe_mb > 0 and local == 0 and rank == 0 and not probe_first:
         copy_peak = mgpoisson.copy_bandwidth(local, a.copy_probe_mb << 20, 10)
     if world > 1:
         t = torch.tensor([dt], dtype=torch.float64)
