@@ -49,7 +49,7 @@ sys.path.insert(0, os.path.join(ROOT, "lua-multigrid-poisson_amd"))
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 
 
-def parse():
+def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=50)
@@ -85,8 +85,9 @@ def parse():
                                                  ("pmc_traffic_current.json", "pmc_traffic_slab4.json",
                                                   "pmc_traffic_slab3.json")),
                    help="comma list of JSONs with the PMC-measured HBM bytes per launch (tools/pmc_traffic.py); the "
-                        "first one measured on this build and this workload's cells per rank is used")
-    a = p.parse_args()
+                        "first one measured on this build, this workload (box, world, options) and the timed launch's "
+                        "kernel and grid is used (pick_traffic)")
+    a = p.parse_args(argv)
     if a.config0:
         a.dim, a.n, a.real, a.smoother, a.nu, a.prolong, a.coarse_bc, a.cycle = 2, 256, "double", "jacobi", 7, "pc", "zero", "V"
     return a
@@ -177,6 +178,21 @@ def workload_box(a, world):
             raise SystemExit("2D runs are single-GPU (the slab decomposition is 3D)")
         return (n, n, 1), False
     return (n, n, n * world), False
+
+
+def workload_key(a, box, world):
+    """What a PMC traffic file must have been measured on to describe this run's launches: the global box, the
+    ranks it is split over and every option that changes the kernels or their grids (pick_traffic)."""
+    return {"box": list(box), "world": world, "dim": a.dim if not a.box else 3, "real": a.real, "cycle": a.cycle,
+            "smoother": a.smoother, "nu": a.nu, "prolong": a.prolong, "coarse_bc": a.coarse_bc,
+            "restriction": a.restriction}
+
+
+def workload_key_from_argv(argv, world=1):
+    """workload_key of `bench.py <argv>` run with `world` ranks (tools/pmc_traffic.py tags its JSON with it)."""
+    a = parse(list(argv))
+    box, _ = workload_box(a, world)
+    return workload_key(a, box, world)
 
 
 def make_cfg(a, box, rank, world, local, comm_id):
@@ -355,6 +371,11 @@ def run_workload(a, cfg, box, strong, rank, world, local, dist, steps, warmup, p
     # SURVEY.md §8(d) per-sweep accounting (what one launch per half-sweep would move) of the fused phases
     per_sweep = {"half_sweep": 1.5, "fused_pre": 3.0 * a.nu + 2.0 + coarse, "fused_post": 3.0 * a.nu + 2.0 + coarse + 2.0}
     per_kind = {k: v for k, v in timed.items() if k in kernels and v[1] > 0}
+    # the fused kinds' kernels as the library launched them (symbol and grid: mgp_timing_kernel), not re-derived
+    launched = ctx.timing_kernels() if timed else {}
+    for k, (nm, _) in launched.items():
+        if k in kernels:
+            kernels[k] = nm
     cells = cells_rank
     if per_kind:
         # per kind: (ms, launches, algorithmic bytes as the library counts them: include/mgpoisson.h
@@ -388,23 +409,33 @@ def run_workload(a, cfg, box, strong, rank, world, local, dist, steps, warmup, p
             roof["copy_probe"] = (f"mgp_copy_bandwidth: 16-byte streaming copy of {a.copy_probe_mb} MiB, best of 10, "
                                   "read + write bytes (BASELINE.md: measured copy-kernel peak)")
         roof["traffic_measured_this_run"] = False
-        tpath = pick_traffic(a.traffic, cells_rank)
-        if tpath:
-            with open(tpath) as fh:
-                tr = json.load(fh)
-            # the launch's full template name carries the tile / segment variant the library picked (k_zs's WIDE,
-            # k_ys's segment width): match on the name this table knows plus any trailing template arguments
-            tk = tr.get("kernels", {})
-            full = [n for n in tk if n == kernels[dom] or n.startswith(kernels[dom][:-1] + ", ")]
-            ent = tk.get(full[0]) if len(full) == 1 else None
-            if len(full) == 1:
-                roof["kernel"] = full[0]
-            src_ok = tr.get("source_hash") == source_hash()
-            wl_ok = tr.get("cells_rank") in (None, cells_rank)
-            roof["traffic_source"] = os.path.relpath(tpath, ROOT)
-            roof["traffic_source_matches_build"] = bool(src_ok and wl_ok)
-            if ent and src_ok and wl_ok:
-                roof["traffic"] = ent.get("bytes_per_launch")
+        if dom in launched:
+            roof["grid"] = launched[dom][1]
+        wkey = workload_key(a, box, world)
+        want = {k: launched[k] for k in kinds if k in launched}
+        tpath, tr, why = pick_traffic(a.traffic, wkey, want)
+        roof["traffic_source"] = os.path.relpath(tpath, ROOT) if tpath else None
+        roof["traffic_source_matches_build"] = tpath is not None
+        if not tpath:
+            roof["traffic_rejected"] = why  # per candidate file: why it does not describe this run's launches
+        else:
+            tk = tr["kernels"]
+            ent = tk[launched[dom][0]] if dom in launched else None
+            if ent:
+                roof["traffic"] = ent["bytes_per_launch"]
+                roof["traffic_ratio"] = ent["bytes_per_launch"] / (by / cnt)
+            # the measured counterpart of BASELINE's "finest-smoother achieved HBM GB/s": the PMC bytes of the
+            # level-0 smoothing phases (PRE + POST) over their event-timed duration
+            fin = [(tk[launched[k][0]]["bytes_per_launch"], kinds[k]) for k in ("fused_pre", "fused_post")
+                   if k in kinds and k in launched]
+            if len(fin) == 2:
+                byt = sum(b * c for b, (_, c, _) in fin)
+                sec = sum(ms_ for _, (ms_, _, _) in fin) * 1e-3
+                line["finest_level_hbm_GBps"] = {
+                    "value": byt / sec / 1e9, "pmc_bytes": byt, "kernel_s": sec, "source": roof["traffic_source"],
+                    "definition": "PMC-measured HBM bytes (FETCH_SIZE x2 + WRITE_SIZE, tools/pmc_traffic.py) of the "
+                                  "finest level's PRE and POST launches over their HIP-event time: bytes actually "
+                                  "moved, bounded by 8 TB/s (finest_smoother_GBps is the per-sweep-equivalent figure)"}
         line["roofline"] = roof
         # finest-smoother GB/s = 3 sizeof(real) cells_per_rank sweeps / summed smoother kernel time
         # (the level-0 smoothing launches; a fused phase is counted with its nu sweeps)
@@ -427,18 +458,36 @@ def run_workload(a, cfg, box, strong, rank, world, local, dist, steps, warmup, p
     return line
 
 
-def pick_traffic(paths, cells_rank):
-    """The first existing traffic JSON of the comma list measured at this workload's cells per rank (else the first
-    existing one, whose mismatch the line then reports)."""
-    found = [p for p in (paths or "").split(",") if p and os.path.exists(p)]
-    for p in found:
+def pick_traffic(paths, wkey, launched, src_hash=None):
+    """(path, json, rejected) of the first traffic JSON of the comma list that describes this run's launches: measured
+    on this build (source hash), on this workload (workload_key: box, ranks and options — not merely the same cell
+    count, which 2048^3 and 4096^2 x 512 share) and holding every timed kernel `launched` = {kind: (symbol, grid)}
+    with the same grid.  Else (None, None, {path: reason}): the line then carries traffic null."""
+    src_hash = src_hash or source_hash()
+    rejected = {}
+    for p in (paths or "").split(","):
+        if not p or not os.path.exists(p):
+            continue
         try:
             with open(p) as fh:
-                if json.load(fh).get("cells_rank") in (None, cells_rank):
-                    return p
-        except (OSError, ValueError):
+                tr = json.load(fh)
+        except (OSError, ValueError) as e:
+            rejected[p] = f"unreadable: {e}"
             continue
-    return found[0] if found else None
+        tk = tr.get("kernels", {})
+        if tr.get("source_hash") != src_hash:
+            rejected[p] = f"measured on source {tr.get('source_hash')}, this build is {src_hash}"
+        elif tr.get("workload") != wkey:
+            rejected[p] = f"measured on workload {tr.get('workload')}"
+        elif not launched:
+            rejected[p] = "no timed launch to match"
+        else:
+            bad = [f"{nm} grid {g}" for nm, g in launched.values() if tk.get(nm, {}).get("grid") != g]
+            if bad:
+                rejected[p] = "no measured launch of " + ", ".join(bad)
+            else:
+                return p, tr, None
+    return None, None, rejected
 
 
 def cycle_compulsory_bytes(levels, cfg, a, rb):

@@ -110,7 +110,12 @@ void        mgp_opts_default(mgp_opts* o);
 /* RCCL unique id for a world > 1 context (call on rank 0, broadcast the bytes).  With the environment variable
  * MGP_TRANSPORT=rccl when it is created, a world-1 context (or a one-device group) takes the multi-GPU code
  * path on a one-rank RCCL communicator of its own (3D: its levels are "distributed" slabs without neighbours),
- * so that every RCCL call of a cycle executes on a one-GPU machine; results equal the plain world-1 run. */
+ * so that every RCCL call of a cycle executes on a one-GPU machine; results equal the plain world-1 run.
+ * A context on its own RCCL communicator (one process per GPU, or MGP_TRANSPORT=rccl) waits for its streams under
+ * a deadline, MGP_COMM_TIMEOUT_S seconds at creation (default 600, 0 = block): when it expires the call prints and
+ * returns MGP_ERR_RCCL naming the rank and the first exchange / collective that has not completed (its level and
+ * stream), after ncclCommAbort of the context's communicators; the context then refuses every exchange (destroy
+ * it).  MGP_TEST_STALL=k (tests): the context's k-th halo exchange first holds its stream like an absent peer. */
 int         mgp_comm_unique_id(void* out, int64_t nbytes);
 
 /* Replaces MultigridCPU:init{size,...} (cpu.lua:173-194) / MultigridCPURaw:init(size, real)
@@ -261,6 +266,12 @@ enum { MGP_TIMING_HALF_SWEEP = 0, MGP_TIMING_FUSED_PRE = 1, MGP_TIMING_FUSED_POS
        MGP_TIMING_COLLECTIVE = 4, MGP_TIMING_KINDS = 5 };
 int         mgp_timing(mgp_ctx* c, int enable);
 int         mgp_timing_read(mgp_ctx* c, int kind, double* ms_total, int64_t* launches, double* bytes);
+/* The kernel the last timed launch of a kind ran (MGP_TIMING_FUSED_PRE / _POST; level 0): its symbol with the
+ * template arguments as rocprofv3 prints it (NUL-terminated, truncated to cap bytes) and its grid in work-items
+ * (rocprofv3's Grid_Size), so that PMC counters measured separately can be matched to exactly this launch.
+ * MGP_ERR_STATE when no launch of that kind was timed since mgp_timing(c, 1).  No reference counterpart
+ * (measurement only). */
+int         mgp_timing_kernel(mgp_ctx* c, int kind, char* name, int cap, int64_t* grid);
 
 /* The exchanges and collectives this rank has issued since creation or the last reset (reset != 0 clears after
  * reading), in issue order: up to max_rows rows of 5 int64 {op, side, level, msgs, bytes}, op 0 = halo exchange

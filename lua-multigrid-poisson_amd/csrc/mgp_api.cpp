@@ -273,7 +273,33 @@ struct mgp_ctx {
     // set by the owning group when another rank failed: no new exchange / collective is issued, and the
     // communicator (aborted by the group) is not touched again
     const std::atomic<bool>* group_stop = nullptr;
-    bool stopped() const { return group_stop && group_stop->load(); }
+    // a per-process RCCL context whose deadline expired (comm_deadline): its communicators were aborted
+    bool comm_dead = false;
+    bool stopped() const { return comm_dead || (group_stop && group_stop->load()); }
+    const char* stop_msg() const
+    {
+        return comm_dead ? "communicators aborted after the communication deadline expired (MGP_COMM_TIMEOUT_S)"
+                         : "group aborted: another rank failed";
+    }
+    bool deadline_on() const { return comm_timeout_s > 0.0 && comm && !lb && !nb_comm && !dry; }
+    // Deadline of every wait for this rank's streams on a per-process RCCL context (one process per GPU, blocking
+    // communicators): MGP_COMM_TIMEOUT_S at creation, default 600 s, 0 = block as before.  An expired wait reports
+    // the first exchange / collective whose completion event has not fired, aborts the communicators and fails
+    // with MGP_ERR_RCCL (the driver's 8-GPU run must not hang without a record).
+    double comm_timeout_s = 0.0;
+    struct CommMark {
+        hipEvent_t ev = nullptr;
+        int op = 0, side = 0, level = 0;
+        int64_t seq = -1, bytes = 0;
+    };
+    std::vector<CommMark> marks;  // ring of completion events of the last calls (kCommMarks)
+    int64_t mark_seq = 0;
+    static constexpr int kCommMarks = 32;
+    // test hook (MGP_TEST_STALL=k, read at creation): the k-th exchange of this context first enqueues a kernel that
+    // holds its stream until `stall_flag` is set (or, bounded, 4 x the deadline + 10 s): a peer that never arrives
+    int64_t stall_at = 0, exch_seq = 0;
+    int* stall_flag = nullptr;    // host-pinned, mapped
+    int* stall_flag_d = nullptr;  // its device address
     bool first_done = false;
     bool err_done = false;
     // hipGraph replay of whole cycles (single GPU): one instantiated graph per pointer state of
@@ -302,6 +328,9 @@ struct mgp_ctx {
     // for non-finite cells on the device; d_dbg = the first failing check's index into dbg_names (0x7f7f7f7f: none)
     int debug = 0;
     int* d_dbg = nullptr;
+    // the last failure was raised after the call's final synchronisation (the debug NaN check): every collective of
+    // the call had completed on this rank, so a group's call sequences still match (group_run keeps the group)
+    bool fail_after_sync = false;
     std::vector<std::string> dbg_names;
     int dbg_cycle = 0;
     // finest-level kernel timing: event pairs around level-0 launches of each timed kind
@@ -318,6 +347,7 @@ struct mgp_ctx {
     double t_ms[MGP_TIMING_KINDS] = {};
     int64_t t_launch[MGP_TIMING_KINDS] = {};
     double t_bytes[MGP_TIMING_KINDS] = {};
+    mgp::LaunchInfo t_info[MGP_TIMING_KINDS] = {};  // the last timed launch of each kernel kind (mgp_timing_kernel)
 
     int fail(int code, const char* fmt, ...)
     {
@@ -504,11 +534,98 @@ int nccl_done(mgp_ctx* c, ncclComm_t comm, ncclResult_t r, const char* what)
     return MGP_OK;
 }
 
+// ---- communication deadline (per-process RCCL contexts) ----
+
+// A completion event after each exchange / collective, in a ring of the last kCommMarks calls: when a wait expires,
+// the first of them that has not fired names the call the rank is stuck in.
+void comm_mark(mgp_ctx* c, hipStream_t st, int op, int side, int level, int64_t bytes)
+{
+    if (!c->deadline_on()) return;
+    if (c->marks.empty()) {
+        c->marks.resize(mgp_ctx::kCommMarks);
+        for (auto& m : c->marks)
+            if (hipEventCreateWithFlags(&m.ev, hipEventDisableTiming) != hipSuccess) m.ev = nullptr;
+    }
+    auto& m = c->marks[(size_t)(c->mark_seq % mgp_ctx::kCommMarks)];
+    if (!m.ev || hipEventRecord(m.ev, st) != hipSuccess) return;
+    m.op = op;
+    m.side = side;
+    m.level = level;
+    m.bytes = bytes;
+    m.seq = c->mark_seq++;
+}
+
+// The deadline expired while this rank waited for its streams: name what it is stuck in (stderr, so that a bench
+// run's tail shows it, and the error text), abort both communicators (their kernels exit) and fail.  The context
+// refuses every later exchange / collective; destroy it.  No restart.
+int comm_deadline(mgp_ctx* c, double waited)
+{
+    static const char* ops[] = {"halo exchange", "all-gather", "all-reduce"};
+    std::string stuck = "no exchange or collective pending (a kernel of this rank's own stream)";
+    for (int64_t k = std::max<int64_t>(0, c->mark_seq - mgp_ctx::kCommMarks); k < c->mark_seq; ++k) {
+        const auto& m = c->marks[(size_t)(k % mgp_ctx::kCommMarks)];
+        if (m.seq != k || hipEventQuery(m.ev) != hipErrorNotReady) continue;
+        char b[200];
+        std::snprintf(b, sizeof b, "call #%lld, a %s of level %d on the %s stream (%lld bytes per neighbour)",
+                      (long long)k, ops[std::min(2, std::max(0, m.op))], m.level, m.side ? "side" : "compute",
+                      (long long)m.bytes);
+        stuck = b;
+        break;
+    }
+    std::string recent;
+    const size_t n = c->clog.size();
+    for (size_t i = n > 4 ? n - 4 : 0; i < n; ++i) {
+        const auto& r = c->clog[i];
+        char b[96];
+        std::snprintf(b, sizeof b, "%s{%s L%d side %d %lld B}", recent.empty() ? "" : ", ",
+                      ops[std::min(2, std::max(0, r.op))], r.level, r.side, (long long)r.bytes);
+        recent += b;
+    }
+    c->comm_dead = true;
+    if (c->xcomm) (void)ncclCommAbort(c->xcomm);
+    if (c->comm) (void)ncclCommAbort(c->comm);
+    c->xcomm = c->comm = nullptr;
+    if (c->stall_flag) __atomic_store_n(c->stall_flag, 1, __ATOMIC_RELEASE);  // (test hook) release the held stream
+    c->fail(MGP_ERR_RCCL,
+            "communication deadline: rank %d of %d waited %.1f s (MGP_COMM_TIMEOUT_S=%g) for its streams; stuck in %s; "
+            "last issued: %s; communicators aborted",
+            c->o.rank, c->o.world, waited, c->comm_timeout_s, stuck.c_str(), recent.c_str());
+    std::fprintf(stderr, "mgpoisson: %s\n", c->err.c_str());
+    return MGP_ERR_RCCL;
+}
+
+// Wait for stream st: hipStreamSynchronize, or, with a deadline, poll the stream and the communicators' async
+// errors until it drains or the deadline expires.
+int stream_wait(mgp_ctx* c, hipStream_t st)
+{
+    if (!c->deadline_on()) {
+        HIP_TRY(c, hipStreamSynchronize(st));
+        return MGP_OK;
+    }
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int spin = 0;; ++spin) {
+        const hipError_t q = hipStreamQuery(st);
+        if (q == hipSuccess) return MGP_OK;
+        if (q != hipErrorNotReady) HIP_TRY(c, q);
+        for (ncclComm_t comm : {c->comm, c->xcomm}) {
+            ncclResult_t ar = ncclSuccess;
+            if (comm && ncclCommGetAsyncError(comm, &ar) == ncclSuccess && ar != ncclSuccess && ar != ncclInProgress)
+                return c->fail(MGP_ERR_RCCL, "RCCL async error on rank %d: %s", c->o.rank, ncclGetErrorString(ar));
+        }
+        const double waited = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        if (waited > c->comm_timeout_s) return comm_deadline(c, waited);
+        if (spin < 4096)
+            std::this_thread::yield();
+        else
+            std::this_thread::sleep_for(std::chrono::microseconds(200));
+    }
+}
+
 #define NCCL_CALL(c, comm, expr, what)                                                                    \
     do {                                                                                                 \
         if ((c)->dry) break;                                                                             \
         NcclScope scope_(c);                                                                             \
-        if ((c)->stopped()) return (c)->fail(MGP_ERR_STATE, "group aborted: another rank failed");       \
+        if ((c)->stopped()) return (c)->fail(MGP_ERR_STATE, "%s", (c)->stop_msg());       \
         TRY(nccl_done((c), (comm), (expr), (what)));                                                     \
     } while (0)
 
@@ -535,7 +652,7 @@ int exchange_buf_impl(mgp_ctx* c, Level& L, char* buf, int depth, int colour, hi
     const size_t cnt = colour < 0 ? (size_t)(depth * L.g.P) : (size_t)L.g.H;
     ncclComm_t comm = c->xs && st == c->xs && c->xcomm ? c->xcomm : c->comm;
     NcclScope scope(c);
-    if (c->stopped()) return c->fail(MGP_ERR_STATE, "group aborted: another rank failed");
+    if (c->stopped()) return c->fail(MGP_ERR_STATE, "%s", c->stop_msg());
     ncclResult_t r = ncclGroupStart();
     for (int i = 0; i < msgs && r == ncclSuccess; ++i) {
         if (c->o.rank > 0) {
@@ -559,7 +676,7 @@ int exchange_buf(mgp_ctx* c, Level& L, char* buf, int depth = 1, int colour = -1
     if (!st) st = c->s;
     if (depth > c->G || depth > L.g.nz)
         return c->fail(MGP_ERR_STATE, "internal: exchange depth %d (ghost %d, slab %d)", depth, c->G, (int)L.g.nz);
-    if (c->stopped()) return c->fail(MGP_ERR_STATE, "group aborted: another rank failed");
+    if (c->stopped()) return c->fail(MGP_ERR_STATE, "%s", c->stop_msg());
     ++L.exchanges;
     // bytes this rank sends per neighbour: depth planes, or the colour half of each
     const int64_t per_nb = (int64_t)depth * (colour < 0 ? L.g.P : L.g.H) * c->rb;
@@ -569,10 +686,13 @@ int exchange_buf(mgp_ctx* c, Level& L, char* buf, int depth = 1, int colour = -1
     if (c->dry) return MGP_OK;
     hipEvent_t e;
     TRY(timed_begin_on(c, st, &e));
+    if (c->stall_at && ++c->exch_seq == c->stall_at && c->stall_flag_d)  // test hook: a peer that never arrives
+        HIP_TRY(c, mgp::launch_stall(c->stall_flag_d, 4.0 * c->comm_timeout_s + 10.0, st));
     {
         WaitScope w(c);  // the loopback barrier waits for the peers too
         TRY(exchange_buf_impl(c, L, buf, depth, colour, st));
     }
+    comm_mark(c, st, 0, c->xs != nullptr && st == c->xs, (int)(&L - c->lev.data()), per_nb);
     return timed_end_on(c, st, e, MGP_TIMING_EXCHANGE, (double)(per_nb * nbs));
 }
 
@@ -605,8 +725,8 @@ int timed_begin_on(mgp_ctx* c, hipStream_t st, hipEvent_t* e1)
     *e1 = nullptr;
     if (!c->timing) return MGP_OK;
     if (c->ev_used + 2 > c->ev.size()) {
-        HIP_TRY(c, hipStreamSynchronize(c->s));
-        if (c->xs) HIP_TRY(c, hipStreamSynchronize(c->xs));
+        TRY(stream_wait(c, c->s));
+        if (c->xs) TRY(stream_wait(c, c->xs));
         timing_collect(c);
     }
     *e1 = c->ev[c->ev_used];
@@ -788,6 +908,7 @@ int gather_coarse_rhs(mgp_ctx* c, Level& L, Level& C, char* R)
         TRY(lb_allgather(c, c->ui(C, C.f), count));
     else
         NCCL_CALL(c, c->comm, ncclAllGather(R, c->ui(C, C.f), count, c->nccl_real(), c->comm, c->s), "all-gather");
+    comm_mark(c, c->s, 1, 0, (int)(&C - c->lev.data()), (int64_t)(count * c->rb));
     return timed_end_on(c, c->s, e, MGP_TIMING_COLLECTIVE, (double)(count * c->rb * (c->o.world - 1)));
 }
 
@@ -1046,6 +1167,7 @@ int fused_pre(mgp_ctx* c, int l, double h)
     a.cl = coarse_coef(c->o.coarse_bc, l);
     a.zc = L.zc_pre;
     a.ghost = c->G;
+    if (l == 0 && c->timing) a.info = &c->t_info[MGP_TIMING_FUSED_PRE];
     hipEvent_t e;
     TRY(timed_begin(c, l, &e));
     HIP_TRY(c, mgp::launch_fused(c->rb, a, c->s));
@@ -1094,7 +1216,7 @@ int fused_post(mgp_ctx* c, int l, double h, bool want_err)
     a.old = want_err ? c->ui(L, L.t) : nullptr;
     a.V = c->ui(C, C.u) + (size_t)(zc * C.g.P) * c->rb;
     a.partials = want_err ? c->d_part : nullptr;
-    if (std::getenv("MGP_STAMP_R")) a.R = c->ui(C, C.f);  // (ZS_STAMP timing builds: POST's stamps into level l+1's f)
+    if (c->tu.stamp_r) a.R = c->ui(C, C.f);  // (ZS_STAMP timing builds: POST's stamps into level l+1's f)
     a.g = L.g;
     a.gc = gc;
     a.h = h;
@@ -1102,6 +1224,7 @@ int fused_post(mgp_ctx* c, int l, double h, bool want_err)
     a.clc = coarse_coef(c->o.coarse_bc, l + 1);
     a.zc = L.zc;
     a.ghost = c->G;
+    if (l == 0 && c->timing) a.info = &c->t_info[MGP_TIMING_FUSED_POST];
     hipEvent_t e;
     TRY(timed_begin(c, l, &e));
     HIP_TRY(c, mgp::launch_fused(c->rb, a, c->s));
@@ -1449,6 +1572,7 @@ int one_cycle(mgp_ctx* c, double* dst)
             TRY(lb_allreduce(c, dst));
         else
             NCCL_CALL(c, c->comm, ncclAllReduce(dst, dst, 1, ncclDouble, ncclSum, c->comm, c->s), "err all-reduce");
+        comm_mark(c, c->s, 2, 0, 0, (int64_t)sizeof(double));
         TRY(timed_end_on(c, c->s, e, MGP_TIMING_COLLECTIVE, (double)sizeof(double)));
     }
     update_metrics_old(c);
@@ -1571,14 +1695,14 @@ int sync_and_check(mgp_ctx* c)
             }
         } w{c, c->multi()};
         if (w.on) c->waiting.fetch_add(1);
-        HIP_TRY(c, hipStreamSynchronize(c->s));
-        if (c->xs) HIP_TRY(c, hipStreamSynchronize(c->xs));
+        TRY(stream_wait(c, c->s));
+        if (c->xs) TRY(stream_wait(c, c->xs));
     }
-    if (c->stopped()) return c->fail(MGP_ERR_STATE, "group aborted: another rank failed");
+    if (c->stopped()) return c->fail(MGP_ERR_STATE, "%s", c->stop_msg());
     for (ncclComm_t comm : {c->comm, c->xcomm}) {
         if (!comm) continue;
         NcclScope scope(c);
-        if (c->stopped()) return c->fail(MGP_ERR_STATE, "group aborted: another rank failed");
+        if (c->stopped()) return c->fail(MGP_ERR_STATE, "%s", c->stop_msg());
         ncclResult_t ar = ncclSuccess;
         NCCL_TRY(c, ncclCommGetAsyncError(comm, &ar));
         if (ar != ncclSuccess && ar != ncclInProgress)
@@ -1651,6 +1775,12 @@ static void host_setup(mgp_ctx* c, const mgp_opts& o, const std::vector<LevelPla
     c->rb = o.real_bytes;
     c->rk = real_kind(o);
     c->rccl1 = env_rccl1(o);
+    {
+        const char* v = std::getenv("MGP_COMM_TIMEOUT_S");  // (used by per-process RCCL contexts only: deadline_on)
+        c->comm_timeout_s = v ? std::max(0.0, std::atof(v)) : 600.0;
+        const char* vs = std::getenv("MGP_TEST_STALL");  // test hook: the k-th exchange holds its stream
+        c->stall_at = vs ? std::max(0LL, std::atoll(vs)) : 0;
+    }
     c->tu = mgp::fused_tuning_from_env();
     c->G = o.dim == 3 ? mgp::kGhost3D : 0;  // widened below when a distributed level is fused
     {
@@ -1754,6 +1884,7 @@ int mgp_plan_comm(const mgp_opts* o, int32_t cycles, int64_t* rows, int max_rows
 static void destroy_impl(mgp_ctx* c)
 {
     if (!c) return;
+    if (c->stall_flag) __atomic_store_n(c->stall_flag, 1, __ATOMIC_RELEASE);
     if (c->s) (void)hipStreamSynchronize(c->s);
     for (auto& L : c->lev) {
         if (L.u) dev_free(c, L.u);
@@ -1789,6 +1920,9 @@ static void destroy_impl(mgp_ctx* c)
     if (c->d_metrics) (void)hipFree(c->d_metrics);
     if (c->d_rn) (void)hipFree(c->d_rn);
     if (c->d_dbg) (void)hipFree(c->d_dbg);
+    for (auto& m : c->marks)
+        if (m.ev) (void)hipEventDestroy(m.ev);
+    if (c->stall_flag) (void)hipHostFree(c->stall_flag);
     if (c->s) (void)hipStreamDestroy(c->s);
     delete c;
 }
@@ -2076,6 +2210,14 @@ static int create_impl(mgp_ctx** out, const mgp_opts* o, mgp_loopback* lb, ncclC
             return bail(MGP_ERR_RCCL);
         }
     }
+    if (c->stall_at && c->deadline_on()) {  // (test hook MGP_TEST_STALL) the flag that releases the held stream
+        if (hipHostMalloc((void**)&c->stall_flag, sizeof(int), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+            hipHostGetDevicePointer((void**)&c->stall_flag_d, c->stall_flag, 0) != hipSuccess) {
+            c->err = "MGP_TEST_STALL: no pinned flag";
+            return bail(MGP_ERR_HIP);
+        }
+        *c->stall_flag = 0;
+    }
     if (hipStreamSynchronize(c->s) != hipSuccess) {
         c->err = "stream synchronisation after allocation failed";
         return bail(MGP_ERR_HIP);
@@ -2227,7 +2369,7 @@ static int planes_io(mgp_ctx* c, int level, int which, int64_t z_begin, int64_t 
             HIP_TRY(c, mgp::launch_unpack(c->rb, packed, lex, gs, c->s));
             if (mem != MGP_MEM_DEVICE) {
                 HIP_TRY(c, hipMemcpyAsync(hb, c->stage, bytes, hipMemcpyDeviceToHost, c->s));
-                HIP_TRY(c, hipStreamSynchronize(c->s));  // the next chunk reuses the staging buffer
+                TRY(stream_wait(c, c->s));  // the next chunk reuses the staging buffer
             }
         }
     }
@@ -2323,9 +2465,11 @@ int mgp_cycles(mgp_ctx* c, int32_t k, double* errs)
     if (c->debug) {
         int first = 0;
         HIP_TRY(c, hipMemcpy(&first, c->d_dbg, sizeof(int), hipMemcpyDeviceToHost));
-        if (first >= 0 && first < (int)c->dbg_names.size())
+        if (first >= 0 && first < (int)c->dbg_names.size()) {
+            c->fail_after_sync = true;
             return c->fail(MGP_ERR_STATE, "found a nan (cpu-raw.lua:135-139, gpu.lua:279-283): %s",
                            c->dbg_names[(size_t)first].c_str());
+        }
     }
     if (errs) {
         if (!c->o.err_mode) {
@@ -2372,7 +2516,18 @@ int mgp_two_grid(mgp_ctx* c, double h, void* u, const void* f, int64_t L, int me
         step(hipMemcpyAsync(sf, Lv.f, bytes, hipMemcpyDeviceToDevice, c->s) == hipSuccess ? MGP_OK : MGP_ERR_HIP);
         step(mgp_set_field(c, l, MGP_FIELD_U, u, n, mem));
         step(mgp_set_field(c, l, MGP_FIELD_F, f, n, mem));
+        if (rc == MGP_OK && c->debug) {  // the reference checks inside twoGrid (cpu-raw.lua:126-140): a fresh record
+            c->dbg_names.clear();
+            step(hipMemsetAsync(c->d_dbg, 0x7f, sizeof(int), c->s) == hipSuccess ? MGP_OK : MGP_ERR_HIP);
+        }
         if (rc == MGP_OK) step(cycle_rec(c, l, h, c->o.cycle == MGP_CYCLE_F));
+        int dbg_first = -1;
+        if (rc == MGP_OK && c->debug)
+            step(hipMemcpy(&dbg_first, c->d_dbg, sizeof(int), hipMemcpyDeviceToHost) == hipSuccess ? MGP_OK : MGP_ERR_HIP);
+        if (rc == MGP_OK && dbg_first >= 0 && dbg_first < (int)c->dbg_names.size())
+            rc = c->fail(MGP_ERR_STATE, "found a nan (cpu-raw.lua:135-139, gpu.lua:279-283): %s",
+                         c->dbg_names[(size_t)dbg_first].c_str());
+        if (c->debug) c->dbg_names.clear();
         step(mgp_get_field(c, l, MGP_FIELD_U, u, n, mem));
         TRY(materialize_zero(c, Lv));
         const bool r1 = hipMemcpyAsync(Lv.u, su, bytes, hipMemcpyDeviceToDevice, c->s) == hipSuccess;
@@ -2614,8 +2769,18 @@ int mgp_timing(mgp_ctx* c, int enable)
         c->t_ms[k] = 0.0;
         c->t_launch[k] = 0;
         c->t_bytes[k] = 0.0;
+        c->t_info[k] = {};
     }
     return MGP_OK;
+}
+
+int mgp_timing_kernel(mgp_ctx* c, int kind, char* name, int cap, int64_t* grid)
+{
+    if (!c || kind < 0 || kind >= MGP_TIMING_KINDS || cap < 1 || !name) return MGP_ERR_ARG;
+    const mgp::LaunchInfo& i = c->t_info[kind];
+    std::snprintf(name, (size_t)cap, "%s", i.name);
+    if (grid) *grid = i.grid;
+    return i.name[0] ? MGP_OK : MGP_ERR_STATE;
 }
 
 int mgp_comm_log(mgp_ctx* c, int64_t* rows, int max_rows, int reset)
@@ -2763,6 +2928,7 @@ static int group_run(mgp_group* g, const std::function<int(mgp_ctx*, int)>& fn)
     for (int r = 0; r < n; ++r)
         th.emplace_back([&, r] {
             int v;
+            g->ranks[(size_t)r]->fail_after_sync = false;
             if (hipSetDevice(g->dev[(size_t)r]) != hipSuccess)
                 v = MGP_ERR_HIP;
             else if (r == fail_rank)
@@ -2803,12 +2969,16 @@ static int group_run(mgp_group* g, const std::function<int(mgp_ctx*, int)>& fn)
     for (auto& t : th) t.join();
     // A rank failed and the others returned: their call sequences on the communicators no longer match (the
     // failed rank skipped what the others issued), so the group is unusable and its communicators are aborted
-    // now (one rank included: ncclCommAbort then runs on the world-1 RCCL group).  Only argument errors of every
-    // rank alike, found before any peer call, leave the group usable.
+    // now (one rank included: ncclCommAbort then runs on the world-1 RCCL group).  Argument errors of every rank
+    // alike, found before any peer call, leave the group usable, and so do failures raised only after a rank's
+    // final synchronisation (the debug NaN check): every rank completed the call's collectives.
     if (first >= 0 && !aborted) {
-        bool all_arg = true;
-        for (int r = 0; r < n; ++r) all_arg = all_arg && rc[(size_t)r] == MGP_ERR_ARG;
-        if (!all_arg) group_abort(g);
+        bool all_arg = true, late = true;
+        for (int r = 0; r < n; ++r) {
+            all_arg = all_arg && rc[(size_t)r] == MGP_ERR_ARG;
+            late = late && (rc[(size_t)r] == MGP_OK || g->ranks[(size_t)r]->fail_after_sync);
+        }
+        if (!all_arg && !late) group_abort(g);
     }
     if (g->stop.load() && !g->lb)
         for (auto* c : g->ranks) c->comm = c->xcomm = nullptr;  // freed by ncclCommAbort

@@ -141,11 +141,21 @@ struct FusedTuning {
     int patch_pre = 0, patch_post = -1;
     bool fwf = true;     // MGP_ZS_FWF=0: the full weighting after the fused PRE instead of inside it
     int post_zc = 256;   // MGP_ZS_POST_ZC: POST's z-chunks hold at most this many planes (0: no limit)
+    bool stamp_r = false;  // MGP_STAMP_R=1 (ZS_STAMP timing builds only): POST's wall-clock stamps go to level l+1's f
 };
 FusedTuning fused_tuning_from_env();
 
+// What a launcher actually launched: the kernel's symbol as rocprofv3 prints it (template arguments included)
+// and its grid in work-items (rocprofv3's Grid_Size), so measured PMC traffic can be matched to this launch
+// (bench.py) instead of being re-derived from the options.
+struct LaunchInfo {
+    char name[96];
+    int64_t grid;
+};
+
 struct FusedArgs {
     FusedTuning tu;
+    LaunchInfo* info;  // optional out: the launched kernel
     bool pre;
     int linear;  // POST: linear prolongation; PRE: 1 = no restriction (both colours stored, full weighting after),
                  // 2 = the full-weighting restriction fused (fused_fwf_supported)
@@ -236,6 +246,10 @@ hipError_t launch_cg(int rb, int dim, CgArgs& a, hipStream_t s);
 // grid-stride / one pass / one pass non-temporal; kinds 3 and 4 (calibration only): 8- and 4-byte lanes
 constexpr int kCopyKinds = 3, kCopyCalibKinds = 5;
 hipError_t launch_copy16(int kind, const void* src, void* dst, int64_t bytes, hipStream_t s);
+
+// Test hook of the communication deadline (MGP_TEST_STALL): one wave that holds stream s until *flag (host-pinned,
+// mapped) is non-zero, and in any case at most max_s seconds of wall clock (every wave reaches that exit).
+hipError_t launch_stall(const int* flag, double max_s, hipStream_t s);
 
 constexpr int kSumBlocks = 1024;
 

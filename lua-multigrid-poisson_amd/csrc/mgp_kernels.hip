@@ -4569,6 +4569,7 @@ FusedTuning fused_tuning_from_env()
     t.patch_post = parse_patch(std::getenv("MGP_ZS_PATCH_POST"), vb ? both : -1);
     if (const char* v = std::getenv("MGP_ZS_FWF")) t.fwf = std::atoi(v) != 0;
     if (const char* v = std::getenv("MGP_ZS_POST_ZC")) t.post_zc = std::max(0, std::atoi(v));
+    if (const char* v = std::getenv("MGP_STAMP_R")) t.stamp_r = std::atoi(v) != 0;
     return t;
 }
 
@@ -4583,12 +4584,19 @@ static int zs_patch(int patch, int tiles_x, int tiles_y, unsigned nb)
     return patch;
 }
 
+static const char* tf(bool v) { return v ? "true" : "false"; }
+
 template <typename T, bool PRE, int LINEAR, bool ERR, bool CLZ, bool WIDE = false>
 static hipError_t zs_launch(const FusedArgs& a, hipStream_t s)
 {
     using S = ZsShape<T, PRE, CLZ, WIDE, PRE && LINEAR == 2>;
     const Op<T, 3> op = make_op<T, 3>(a.h, a.cl);
     const unsigned nb = (unsigned)((a.g.nx / S::TX) * (a.g.ny / S::TY) * (a.g.nz / a.zc));
+    if (a.info) {  // rocprofv3's spelling of the instantiation
+        std::snprintf(a.info->name, sizeof a.info->name, "k_zs<%s, %s, %d, %s, %s, %s>", sizeof(T) == 4 ? "float" : "double",
+                      tf(PRE), LINEAR, tf(ERR), tf(CLZ), tf(WIDE));
+        a.info->grid = (int64_t)nb * S::NTL;
+    }
     k_zs<T, PRE, LINEAR, ERR, CLZ, WIDE><<<nb, S::NTL, S::lds_bytes, s>>>((const T*)a.src, (const T*)a.f, (T*)a.dst,
                                                                            (const T*)(a.old ? a.old : a.dst), (T*)a.R,
                                                                            (const T*)a.V, a.partials, a.g, a.gc,
@@ -4617,6 +4625,11 @@ static hipError_t ys_launch_tx(const FusedArgs& a, hipStream_t s)
     using S = YsShape<T, PRE, TXV>;
     const Op<T, 2> op = make_op<T, 2>(a.h, a.cl);
     const unsigned nb = (unsigned)((a.g.nx / S::TX) * (a.g.ny / a.zc));
+    if (a.info) {
+        std::snprintf(a.info->name, sizeof a.info->name, "k_ys<%s, %s, %d, %s, %s, %d>", sizeof(T) == 4 ? "float" : "double",
+                      tf(PRE), LINEAR, tf(ERR), tf(CLZ), TXV);
+        a.info->grid = (int64_t)nb * S::NTL;
+    }
     k_ys<T, PRE, LINEAR, ERR, CLZ, TXV><<<nb, S::NTL, 0, s>>>((const T*)a.src, (const T*)a.f, (T*)a.dst,
                                                          (const T*)(a.old ? a.old : a.dst), (T*)a.R, (const T*)a.V,
                                                          a.partials, a.g, a.gc, op, (T)a.clc, a.zc);
@@ -5061,6 +5074,30 @@ hipError_t launch_metrics(int rb, const void* psi, const void* old, int64_t n, d
 // The reference's debugging check (cpu-raw.lua:135-139, gpu.lua:279-283: error "found a nan" when a dumped grid
 // holds a non-finite cell): any cell of p[0, n) with an all-ones exponent lowers *first to `id`, the check's
 // position in the cycle, so the host names the first phase that produced one.  16-byte loads, grid-stride.
+// ---- test hook of the communication deadline (mgp_api.cpp stream_wait; MGP_TEST_STALL) ----
+
+// One wave polls a host-pinned flag with system-scope vector loads (never the scalar cache) and leaves when it is
+// set or after max_ticks of the 100 MHz wall clock: a stream held like an exchange whose peer never arrives.
+__global__ __launch_bounds__(64) void k_stall(const int* flag, uint64_t max_ticks)
+{
+    const uint64_t t0 = wall_clock64();
+    const int* p = flag + (threadIdx.x >> 6);  // a per-lane (VGPR) address
+    while (__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == 0 && wall_clock64() - t0 < max_ticks)
+        __builtin_amdgcn_s_sleep(127);
+}
+
+hipError_t launch_stall(const int* flag, double max_s, hipStream_t s)
+{
+    int khz = 0;  // wall clock rate in kHz (100 MHz on CDNA)
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess ||
+        khz <= 0)
+        khz = 100000;
+    const uint64_t ticks = (uint64_t)(std::min(max_s, 120.0) * 1e3 * khz);
+    k_stall<<<1, 64, 0, s>>>(flag, ticks);
+    return hipGetLastError();
+}
+
 template <typename T>
 __global__ __launch_bounds__(kBlock) void k_nonfinite(const T* __restrict__ p, int64_t n, int id, int* first, bool vec)
 {

@@ -121,6 +121,7 @@ SIGNATURES = {
     "mgp_timing": (ctypes.c_int, [_vp, ctypes.c_int]),
     "mgp_set_debug": (ctypes.c_int, [_vp, ctypes.c_int]),
     "mgp_timing_read": (ctypes.c_int, [_vp, ctypes.c_int, _P(_dbl), _P(_i64), _P(_dbl)]),
+    "mgp_timing_kernel": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_char_p, ctypes.c_int, _P(_i64)]),
     "mgp_comm_log": (ctypes.c_int, [_vp, _P(_i64), ctypes.c_int, ctypes.c_int]),
     "mgp_plan_comm": (ctypes.c_int, [_P(MGPOpts), _i32, _P(_i64), ctypes.c_int]),
     "mgp_copy_bandwidth": (ctypes.c_int, [ctypes.c_int, _i64, _i32, _P(_dbl)]),

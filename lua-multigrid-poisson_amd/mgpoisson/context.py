@@ -294,6 +294,16 @@ class Context:
             out[name] = (ms.value, n.value, by.value)
         return out
 
+    def timing_kernels(self):
+        """{kind name: (kernel symbol as rocprofv3 prints it, grid in work-items)} of the last timed level-0 fused
+        launch of each kind (mgp_timing_kernel); kinds without a timed launch are absent."""
+        out = {}
+        for kind, name in L.TIMING_KINDS.items():
+            buf, grid = ctypes.create_string_buffer(128), ctypes.c_int64()
+            if L.lib.mgp_timing_kernel(self._h, kind, buf, len(buf), ctypes.byref(grid)) == 0:
+                out[name] = (buf.value.decode(), grid.value)
+        return out
+
 
 class Group:
     """One host process driving `ngpu` GPUs (mgp_group_create): one z-slab context per rank, RCCL

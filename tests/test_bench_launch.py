@@ -116,3 +116,44 @@ def test_plan_comm_without_side_stream(monkeypatch):
     off = mg.plan_comm(mg.make_opts(**kw), 1)
     assert any(r[1] == 1 for r in on) and not any(r[1] == 1 for r in off)
     assert len(off) == len(on)
+
+
+def _traffic_file(tmp_path, name, bench_args, kernels, src):
+    sys.path.insert(0, ROOT)
+    import shlex
+
+    import bench
+
+    p = tmp_path / name
+    p.write_text(json.dumps({"kernels": kernels, "source_hash": src,
+                             "workload": bench.workload_key_from_argv(shlex.split(bench_args)), "bench_args": bench_args}))
+    return str(p)
+
+
+def test_pick_traffic_keys_on_workload_and_grid(tmp_path):
+    """2048^3 and 4096^2 x 512 have the same cells (8,589,934,592), so the configs[4] slab's PMC
+    file must not be taken for the 2048^3 box; a file of the right workload whose launch grid differs is refused too;
+    the right file is taken only when every timed launch's symbol and grid are in it."""
+    sys.path.insert(0, ROOT)
+    import bench
+
+    post = "k_zs<float, false, 1, true, true, true>"
+    pre = "k_zs<float, true, 0, false, true, false>"
+    ent = lambda g: {"grid": g, "launches": 2, "read_bytes": 1.0, "write_bytes": 1.0, "bytes_per_launch": 2.0}  # noqa: E731
+    slab4 = _traffic_file(tmp_path, "slab4.json", "--box 4096,4096,512 --cycle F", {post: ent(100), pre: ent(50)}, "h")
+    box_badgrid = _traffic_file(tmp_path, "box_g.json", "--box 2048,2048,2048", {post: ent(101), pre: ent(50)}, "h")
+    box_oldsrc = _traffic_file(tmp_path, "box_s.json", "--box 2048,2048,2048", {post: ent(100), pre: ent(50)}, "old")
+    box = _traffic_file(tmp_path, "box.json", "--box 2048,2048,2048", {post: ent(100), pre: ent(50)}, "h")
+    a = bench.parse(["--box", "2048,2048,2048"])
+    wkey = bench.workload_key(a, (2048, 2048, 2048), 1)
+    launched = {"fused_post": (post, 100), "fused_pre": (pre, 50)}
+    p, tr, why = bench.pick_traffic(",".join([slab4, box_badgrid, box_oldsrc]), wkey, launched, src_hash="h")
+    assert p is None and tr is None
+    assert "workload" in why[slab4] and "grid 100" in why[box_badgrid] and "source" in why[box_oldsrc]
+    p, tr, why = bench.pick_traffic(",".join([slab4, box_badgrid, box]), wkey, launched, src_hash="h")
+    assert p == box and why is None
+    # the slab itself is matched by its own file, and the weak-scaling key differs by world
+    a4 = bench.parse(["--box", "4096,4096,512", "--cycle", "F"])
+    assert bench.pick_traffic(slab4, bench.workload_key(a4, (4096, 4096, 512), 1), launched, src_hash="h")[0] == slab4
+    d = bench.parse([])
+    assert bench.workload_key(d, (512, 512, 1024), 2) != bench.workload_key(d, (512, 512, 512), 1)

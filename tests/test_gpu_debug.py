@@ -79,3 +79,33 @@ def test_positional_protocol_debugging_field():
     clean.quiet = True
     clean.debugging = True
     assert len(clean.run()) == 2
+
+
+@pytest.mark.parametrize("dim", [2, 3])
+def test_two_grid_debug_check(dim):
+    """the positional twoGrid(h, u, f, L) runs the reference's check as well (cpu-raw.lua:126-140 sits
+    inside twoGrid): a NaN in the caller's f is reported, a clean call raises nothing and equals the unchecked one,
+    and the record does not grow across calls."""
+    mg = _mg()
+    n = 32
+    kw = dict(dim=dim, n=(n, n, n if dim == 3 else 1), real="double", **NS)
+    shape = (n, n, n) if dim == 3 else (n, n)
+    rng = np.random.default_rng(7)
+    f = rng.standard_normal(shape)
+    u0 = rng.standard_normal(shape)
+    ref = mg.Context(mg.make_opts(**kw))
+    u_ref = u0.copy()
+    ref.two_grid(1.0 / n, u_ref, f, n)
+    ctx = mg.Context(mg.make_opts(**kw))
+    ctx.set_debug(1)
+    for _ in range(2):
+        u = u0.copy()
+        ctx.two_grid(1.0 / n, u, f, n)
+        assert np.array_equal(u, u_ref)
+    bad = f.copy()
+    bad.flat[bad.size // 2] = np.nan
+    with pytest.raises(mg.MGPError, match=r"found a nan .*level 0"):
+        ctx.two_grid(1.0 / n, u0.copy(), bad, n)
+    u = u0.copy()
+    ctx.two_grid(1.0 / n, u, f, n)  # usable afterwards, the level's own fields restored
+    assert np.array_equal(u, u_ref)

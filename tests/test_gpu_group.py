@@ -82,3 +82,27 @@ def test_group_rank_failure_aborts_instead_of_hanging(world, monkeypatch):
         g.cycle()
     assert torch.cuda.current_device() == 0
     g.close()
+
+
+def test_group_debug_nan_keeps_group_usable():
+    """the debugging check's "found a nan" is raised after a rank's final synchronisation, when every
+    collective of the call has completed on every rank, so the group's call sequences still match: it is reported,
+    and the group is not aborted (a clean call afterwards runs and equals the single domain)."""
+    mg = _mg()
+    cfg = dict(real="double", smoother="rbgs", nu1=2, nu2=2, prolong="linear", coarse_bc="consistent")
+    box = (32, 32, 64)
+    g = mg.Group(mg.make_opts(dim=3, n=box, **cfg), 2, devices=[0, 0])
+    for r in g.ranks:
+        r.set_debug(1)
+    g.init_point_charge()
+    f = g.get_field(mg.FIELD_F)
+    f[box[2] - 3, 5, 7] = np.nan  # in rank 1's slab
+    g.set_field(mg.FIELD_F, f)
+    with pytest.raises(mg.MGPError, match="found a nan"):
+        g.cycles(1)
+    g.init_point_charge()
+    ref = mg.Context(mg.make_opts(dim=3, n=box, **cfg))
+    ref.init_point_charge()
+    np.testing.assert_allclose(g.cycles(2), ref.cycles(2), rtol=1e-12, atol=0)
+    assert np.array_equal(g.get_psi(), ref.get_psi())
+    g.close()

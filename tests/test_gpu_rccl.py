@@ -8,8 +8,9 @@ takes that same slab path on a real one-rank RCCL communicator (include/mgpoisso
   - a cycle: the grouped ncclSend/ncclRecv halo exchanges (peerless at world 1: empty groups, on both
     communicators), the agglomeration ncclAllGather (in place), the err ncclAllReduce; residual norm and metrics
     all-reduces;
-  - mgp_group_create on one device: the non-blocking ncclCommInitRankConfig + grouped ncclCommSplit + polling,
-    and after an injected rank failure group_abort's ncclCommAbort.
+  - mgp_group_create on one device: the non-blocking ncclCommInitRankConfig (a second grouped non-blocking init
+    makes the side-stream communicators: a grouped ncclCommSplit of non-blocking communicators fails in RCCL 7.2)
+    + polling, and after an injected rank failure group_abort's ncclCommAbort.
 
 Bar: psi bit-identical to the plain world-1 context, err / norms to 1e-12, the executed call log equal to the
 host-only plan, every logged call timed on its stream (so it ran on the RCCL transport: a world-1 context has
@@ -93,7 +94,7 @@ def test_rccl_world1_group_nonblocking_init_and_abort(monkeypatch):
     ref.close()
 
     monkeypatch.setenv("MGP_TRANSPORT", "rccl")
-    g = mg.Group(opts, 1, devices=[0])  # non-blocking ncclCommInitRankConfig + grouped split, polled
+    g = mg.Group(opts, 1, devices=[0])  # two grouped non-blocking ncclCommInitRankConfig, polled
     assert g.ranks[0].levels[0]["distributed"]
     g.init_point_charge()
     np.testing.assert_allclose(g.cycles(2), e_ref, rtol=1e-12, atol=0)
@@ -161,3 +162,46 @@ def test_group_on_two_devices_real_rccl(monkeypatch):
     with pytest.raises(mg.MGPError, match="aborted"):
         g.cycle()
     g.close()
+
+
+def test_comm_deadline_reports_the_stalled_exchange_and_aborts(monkeypatch):
+    """a per-process RCCL context waits for its streams under a deadline (MGP_COMM_TIMEOUT_S,
+    default 600 s).  An exchange held on the GPU (MGP_TEST_STALL=2: the context's second exchange first enqueues a
+    kernel that holds the stream, as a peer that never arrives would) makes cycles() return within the deadline with
+    MGP_ERR_RCCL naming the rank, the stalled call and its level, the communicators aborted (ncclCommAbort); the
+    context then refuses further exchanges instead of hanging, and closes."""
+    import time
+
+    mg = _mg()
+    monkeypatch.setenv("MGP_TRANSPORT", "rccl")
+    monkeypatch.setenv("MGP_COMM_TIMEOUT_S", "3")
+    monkeypatch.setenv("MGP_TEST_STALL", "2")
+    ctx = mg.Context(mg.make_opts(dim=3, n=(64, 64, 64), gather_cells=4096, **NS))
+    assert ctx.levels[0]["distributed"]
+    ctx.init_point_charge()
+    t0 = time.perf_counter()
+    with pytest.raises(mg.MGPError, match=r"communication deadline: rank 0 of 1 waited .* stuck in call #1, a halo "
+                                          r"exchange of level \d+ .*communicators aborted") as ei:
+        ctx.cycles(2)
+    dt = time.perf_counter() - t0
+    assert 2.9 < dt < 30, dt
+    assert ei.value.code == -3  # MGP_ERR_RCCL
+    with pytest.raises(mg.MGPError, match="deadline"):
+        ctx.cycle()
+    ctx.close()
+
+
+def test_comm_deadline_is_silent_on_a_healthy_run(monkeypatch):
+    """The deadline's polling wait changes nothing on a healthy run: psi bit-identical to the blocking wait."""
+    mg = _mg()
+    opts = mg.make_opts(dim=3, n=(64, 64, 64), gather_cells=4096, **NS)
+    monkeypatch.setenv("MGP_TRANSPORT", "rccl")
+    out = []
+    for t in ("0", "5"):
+        monkeypatch.setenv("MGP_COMM_TIMEOUT_S", t)
+        ctx = mg.Context(opts)
+        ctx.init_point_charge()
+        out.append((ctx.cycles(2), ctx.get_psi()))
+        ctx.close()
+    np.testing.assert_array_equal(out[0][0], out[1][0])
+    assert np.array_equal(out[0][1], out[1][1])

@@ -8,9 +8,10 @@ bytes per launch; with an output path, a JSON file bench.py --traffic reads:
 {"kernels": {name: {grid, launches, read_bytes, write_bytes, bytes_per_launch}}, "method": ...}
 holding, per kernel name, the launch grid with the most bytes (the finest level's launches).
 
-usage: tools/pmc_traffic.py gpurun_out/pmc [out.json [cells_rank]]
-The JSON carries the source hash of the library it measured (bench.py source_hash()) and the
-workload's level-0 cells per rank; bench.py uses the traffic only when both match its own run.
+usage: tools/pmc_traffic.py gpurun_out/pmc [out.json ["bench args of the measured run"]]
+The JSON carries the source hash of the library it measured (bench.py source_hash()) and the workload key of
+the bench arguments the passes ran (bench.workload_key: box, ranks, options); bench.py uses the traffic only
+when both match its own run and every timed launch's kernel and grid is in the file (bench.pick_traffic).
 """
 import collections
 import csv
@@ -18,13 +19,14 @@ import glob
 import json
 import os
 import re
+import shlex
 import sys
 
 root = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc"
 out = sys.argv[2] if len(sys.argv) > 2 else None
-cells_rank = int(sys.argv[3]) if len(sys.argv) > 3 else 512 ** 3
+bench_args = sys.argv[3] if len(sys.argv) > 3 else ""
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
-from bench import source_hash  # noqa: E402
+from bench import source_hash, workload_key_from_argv  # noqa: E402
 
 vals = collections.defaultdict(lambda: collections.defaultdict(list))
 for path in glob.glob(os.path.join(root, "p*", "*counter_collection.csv")):
@@ -50,7 +52,8 @@ if out:
         if name not in kernels:
             kernels[name] = {"grid": grid, "launches": n, "read_bytes": fetch, "write_bytes": write,
                              "bytes_per_launch": fetch + write}
-    json.dump({"kernels": kernels, "source_hash": source_hash(), "cells_rank": cells_rank,
+    json.dump({"kernels": kernels, "source_hash": source_hash(),
+               "workload": workload_key_from_argv(shlex.split(bench_args)), "bench_args": bench_args,
                "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate passes over bench.py, KiB -> B, "
                          "FETCH_SIZE x2 (gfx950 wide-load correction, MI355X_MICROARCH.md); per kernel the "
                          "launch grid with the most bytes"}, open(out, "w"), indent=1)
