@@ -275,11 +275,12 @@ def run_workload(a, cfg, box, strong, rank, world, local, dist, steps, warmup, p
     # roofline window: the same K cycles again, launched eagerly with a HIP event pair around
     # every timed level-0 launch and every exchange / collective on the stream it runs on (graph replay cannot
     # bracket single launches); the kernels are identical, only the host launch path differs
-    timed = {}
+    timed, launched = {}, {}
     if not a.no_timing:
         ctx.timing(True)
         ctx.cycles(steps)
         timed = ctx.timing_read()
+        launched = ctx.timing_kernels()  # (before mgp_timing(c, 0), which resets the record)
         ctx.timing(False)
         barrier_sync()
 
@@ -372,7 +373,6 @@ def run_workload(a, cfg, box, strong, rank, world, local, dist, steps, warmup, p
     per_sweep = {"half_sweep": 1.5, "fused_pre": 3.0 * a.nu + 2.0 + coarse, "fused_post": 3.0 * a.nu + 2.0 + coarse + 2.0}
     per_kind = {k: v for k, v in timed.items() if k in kernels and v[1] > 0}
     # the fused kinds' kernels as the library launched them (symbol and grid: mgp_timing_kernel), not re-derived
-    launched = ctx.timing_kernels() if timed else {}
     for k, (nm, _) in launched.items():
         if k in kernels:
             kernels[k] = nm
@@ -472,19 +472,20 @@ def pick_traffic(paths, wkey, launched, src_hash=None):
             with open(p) as fh:
                 tr = json.load(fh)
         except (OSError, ValueError) as e:
-            rejected[p] = f"unreadable: {e}"
+            rejected[os.path.relpath(p, ROOT)] = f"unreadable: {e}"
             continue
         tk = tr.get("kernels", {})
+        key = os.path.relpath(p, ROOT)
         if tr.get("source_hash") != src_hash:
-            rejected[p] = f"measured on source {tr.get('source_hash')}, this build is {src_hash}"
+            rejected[key] = f"measured on source {tr.get('source_hash')}, this build is {src_hash}"
         elif tr.get("workload") != wkey:
-            rejected[p] = f"measured on workload {tr.get('workload')}"
+            rejected[key] = f"measured on workload {tr.get('workload')}"
         elif not launched:
-            rejected[p] = "no timed launch to match"
+            rejected[key] = "no timed launch to match"
         else:
             bad = [f"{nm} grid {g}" for nm, g in launched.values() if tk.get(nm, {}).get("grid") != g]
             if bad:
-                rejected[p] = "no measured launch of " + ", ".join(bad)
+                rejected[key] = "no measured launch of " + ", ".join(bad)
             else:
                 return p, tr, None
     return None, None, rejected

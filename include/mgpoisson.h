@@ -38,7 +38,10 @@ typedef enum mgp_status {
     MGP_ERR_STATE = -5  /* call not valid in the context's current state */
 } mgp_status;
 
-enum { MGP_JACOBI = 0, MGP_RBGS = 1 };                 /* cpu.lua:56-57 inPlaceIterativeSolver */
+/* cpu.lua:56-57 inPlaceIterativeSolver: Jacobi (cpu.lua:40-54), red/black GS (build-defined, the temporally blocked
+ * engines), lexicographic in-place GS (cpu.lua:24-37 GaussSeidel, bit-identical hyperplane-ordered sweeps; one
+ * rank's whole box, MGP_ARITH_REAL) */
+enum { MGP_JACOBI = 0, MGP_RBGS = 1, MGP_GS_LEX = 2 };
 enum { MGP_CYCLE_V = 0, MGP_CYCLE_F = 1 };             /* twoGrid recursion (gamma 1) / F-cycle */
 enum { MGP_PROLONG_PC = 0, MGP_PROLONG_LINEAR = 1 };   /* cpu.lua:142-150 injection / (tri)linear */
 enum { MGP_COARSE_FRESH = 0, MGP_COARSE_WARM = 1 };    /* cpu.lua:138 zeros / cpu-raw.lua:221 Vs */
@@ -78,7 +81,7 @@ typedef struct mgp_opts {
     int64_t n[3];          /* GLOBAL cells per axis, powers of two (n[2] = 1 in 2D) */
     int32_t real_bytes;    /* 4 = float, 8 = double (gpu.lua:32 "real") */
     int32_t nu1, nu2;      /* pre/post sweeps (cpu.lua:20 smooth = 7) */
-    int32_t smoother;      /* MGP_JACOBI | MGP_RBGS */
+    int32_t smoother;      /* MGP_JACOBI | MGP_RBGS | MGP_GS_LEX */
     int32_t cycle;         /* MGP_CYCLE_V | MGP_CYCLE_F */
     int32_t prolong;       /* MGP_PROLONG_PC | MGP_PROLONG_LINEAR */
     int32_t coarse_init;   /* MGP_COARSE_FRESH | MGP_COARSE_WARM */

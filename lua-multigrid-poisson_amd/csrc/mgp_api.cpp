@@ -96,7 +96,20 @@ int plan_levels(const mgp_opts& o, std::vector<LevelPlan>& out, std::string& err
     if (!is_pow2(nx) || !is_pow2(ny) || !is_pow2(nz)) { err = "n[] must be powers of two"; return MGP_ERR_ARG; }
     if (nx * ny >= (int64_t(1) << 31)) { err = "nx*ny must be < 2^31"; return MGP_ERR_ARG; }
     if (o.real_bytes != 4 && o.real_bytes != 8) { err = "real_bytes must be 4 or 8"; return MGP_ERR_ARG; }
-    if (o.smoother != MGP_JACOBI && o.smoother != MGP_RBGS) { err = "unknown smoother"; return MGP_ERR_ARG; }
+    if (o.smoother != MGP_JACOBI && o.smoother != MGP_RBGS && o.smoother != MGP_GS_LEX) {
+        err = "unknown smoother";
+        return MGP_ERR_ARG;
+    }
+    // cpu.lua's lexicographic sweep is sequential along every axis, so it runs on one rank's whole box only; and
+    // cpu-raw.lua (the double-arithmetic float path) has no Gauss-Seidel
+    if (o.smoother == MGP_GS_LEX && (o.world > 1 || env_rccl1(o))) {
+        err = "smoother MGP_GS_LEX (lexicographic, cpu.lua:24-37) is sequential across slabs: world 1 only";
+        return MGP_ERR_ARG;
+    }
+    if (o.smoother == MGP_GS_LEX && o.arith != MGP_ARITH_REAL) {
+        err = "smoother MGP_GS_LEX: arith MGP_ARITH_REAL only (cpu-raw.lua has no Gauss-Seidel)";
+        return MGP_ERR_ARG;
+    }
     if (o.cycle != MGP_CYCLE_V && o.cycle != MGP_CYCLE_F) { err = "unknown cycle"; return MGP_ERR_ARG; }
     if (o.prolong != MGP_PROLONG_PC && o.prolong != MGP_PROLONG_LINEAR) { err = "unknown prolong"; return MGP_ERR_ARG; }
     if (o.coarse_init != MGP_COARSE_FRESH && o.coarse_init != MGP_COARSE_WARM) { err = "unknown coarse_init"; return MGP_ERR_ARG; }
@@ -837,6 +850,12 @@ int smooth(mgp_ctx* c, int l, int sweeps, double h, bool want_err = false, bool 
     if (L.zero_pending && (c->o.smoother != MGP_RBGS || !c->zbuf || L.alloc > c->zbuf_reals))
         TRY(materialize_zero(c, L));
     for (int sw = 0; sw < sweeps; ++sw) {
+        if (c->o.smoother == MGP_GS_LEX) {  // cpu.lua:24-37 in place (a replicated level: validated at creation)
+            HIP_TRY(c, mgp::launch_gslex_sweep(c->rb, c->o.dim, c->ui(L, L.u), c->ui(L, L.f), L.g, h, cl, c->s));
+            L.ghost_ok = !L.p.dist;
+            L.ghost_zero = false;
+            continue;
+        }
         if (c->o.smoother == MGP_JACOBI) {
             // both colours from the old iterate into t, then swap (no copy back, cf. gpu.lua:292)
             TRY(exchange(c, L));
@@ -1334,6 +1353,7 @@ bool try_tail(mgp_ctx* c, int T)
     const int last = (int)c->lev.size() - 1;
     if (T < 1 || T > last || c->lev[T].p.dist) return false;
     if (c->rk == mgp::kRealF32D) return false;  // the tail evaluates in the real type
+    if (c->o.smoother == MGP_GS_LEX) return false;  // the tail runs Jacobi and red/black sweeps only
     const int nlev = last - T + 1;
     if (nlev > mgp::kTailMaxLevels) return false;
     std::vector<Geo> g;

@@ -247,6 +247,10 @@ hipError_t launch_cg(int rb, int dim, CgArgs& a, hipStream_t s);
 constexpr int kCopyKinds = 3, kCopyCalibKinds = 5;
 hipError_t launch_copy16(int kind, const void* src, void* dst, int64_t bytes, hipStream_t s);
 
+// One in-place lexicographic Gauss-Seidel sweep (cpu.lua:24-37) of a whole replicated level, bit-identical to the
+// sequential ascending-order sweep: tiles in tile-hyperplane order, one launch per tile-hyperplane (k_gslex).
+hipError_t launch_gslex_sweep(int rb, int dim, void* u, const void* f, Geo g, double h, double cl, hipStream_t s);
+
 // Test hook of the communication deadline (MGP_TEST_STALL): one wave that holds stream s until *flag (host-pinned,
 // mapped) is non-zero, and in any case at most max_s seconds of wall clock (every wave reaches that exit).
 hipError_t launch_stall(const int* flag, double max_s, hipStream_t s);

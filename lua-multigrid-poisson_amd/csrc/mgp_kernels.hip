@@ -5074,6 +5074,110 @@ hipError_t launch_metrics(int rb, const void* psi, const void* old, int64_t n, d
 // The reference's debugging check (cpu-raw.lua:135-139, gpu.lua:279-283: error "found a nan" when a dumped grid
 // holds a non-finite cell): any cell of p[0, n) with an all-ones exponent lowers *first to `id`, the check's
 // position in the cycle, so the host names the first phase that produced one.  16-byte loads, grid-stride.
+// ---- lexicographic Gauss-Seidel (cpu.lua:24-37, the reference's inPlaceIterativeSolver = GaussSeidel) ----
+//
+// cpu.lua's sweep updates u in place in ascending lexicographic order, so a cell reads the NEW values of its lower
+// neighbours (i-1, j-1, k-1) and the OLD values of its upper ones.  The cells of one hyperplane i + j + k = s
+// therefore depend only on hyperplane s - 1 (already new) and s + 1 (still old), and updating the hyperplanes in
+// order s = 0, 1, ... reproduces the sequential sweep bit for bit (same operands, same expression).  Every cell
+// of a hyperplane has the colour of s's parity, so the packed red/black layout is read as it is.
+//
+// Tiled wavefront: tiles of TX x TY x TZ cells run in tile-hyperplanes I + J + K = S, one launch per S (face-
+// adjacent tiles differ by one in S, so no tile of a launch reads a face halo another tile of the launch writes).
+// A workgroup holds its tile with a one-cell face halo in LDS (lower faces: final values of earlier launches;
+// upper faces: old values; outside the box: 0, the reference's ghost), walks the tile's TX + TY + TZ - 2 cell
+// hyperplanes with one barrier each, and writes the tile back.
+template <int DIM>
+constexpr int gsl_edge() { return DIM == 3 ? 8 : 32; }
+template <int DIM>
+constexpr int gsl_threads() { return DIM == 3 ? 512 : 1024; }
+
+template <typename T, int DIM>
+__global__ __launch_bounds__(gsl_threads<DIM>()) void k_gslex(T* __restrict__ u, const T* __restrict__ f, Geo g,
+                                                             Op<T, DIM> op, int S, int TX, int TY, int TZ)
+{
+    constexpr int E = gsl_edge<DIM>() + 2;
+    __shared__ T s[DIM == 3 ? E * E * E : E * E];
+    const int ntx = g.nx / TX;
+    int I, J, K;  // this workgroup's tile on tile-hyperplane S (workgroup-uniform exit before any barrier)
+    if (DIM == 3) {
+        I = (int)blockIdx.x % ntx;
+        J = (int)blockIdx.x / ntx;
+        K = S - I - J;
+        if (K < 0 || K >= (int)g.nz / TZ) return;
+    } else {
+        I = (int)blockIdx.x;
+        J = S - I;
+        K = 0;
+        if (J < 0 || J >= g.ny / TY) return;
+    }
+    const int x0 = I * TX, y0 = J * TY, z0 = K * TZ;
+    const int EZ = DIM == 3 ? TZ + 2 : 1;
+    const int ncells = (TX + 2) * (TY + 2) * EZ;
+    // tile + face halo (edges and corners are never read by the 5 / 7-point stencil: skipped)
+    for (int q = (int)threadIdx.x; q < ncells; q += (int)blockDim.x) {
+        const int lx = q % (TX + 2) - 1, ly = (q / (TX + 2)) % (TY + 2) - 1;
+        const int lz = DIM == 3 ? q / ((TX + 2) * (TY + 2)) - 1 : 0;
+        const int outs = (lx < 0 || lx >= TX) + (ly < 0 || ly >= TY) + (lz < 0 || lz >= TZ);
+        if (outs > 1) continue;
+        const int gi = x0 + lx, gj = y0 + ly, gk = z0 + lz;
+        const bool in = gi >= 0 && gi < g.nx && gj >= 0 && gj < g.ny && gk >= 0 && gk < (int)g.nz;
+        s[(lx + 1) + E * ((ly + 1) + E * (DIM == 3 ? lz + 1 : 0))] = in ? u[pidx(g, gi, gj, gk)] : (T)0;
+    }
+    const int t = (int)threadIdx.x;
+    const bool mine = t < TX * TY * TZ;
+    const int lx = t % TX, ly = (t / TX) % TY, lz = DIM == 3 ? t / (TX * TY) : 0;
+    const int gi = x0 + lx, gj = y0 + ly, gk = z0 + lz;
+    const int c = (lx + 1) + E * ((ly + 1) + E * (DIM == 3 ? lz + 1 : 0));
+    T fc = (T)0;
+    int nb = 0;
+    if (mine) {
+        fc = f[pidx(g, gi, gj, gk)];
+        nb = (gi == 0) + (gi == g.nx - 1) + (gj == 0) + (gj == g.ny - 1);
+        if (DIM == 3) nb += (gk == 0) + (gk == (int)g.nz - 1);
+    }
+    __syncthreads();
+    const int last = (TX - 1) + (TY - 1) + (DIM == 3 ? TZ - 1 : 0);
+    const int mys = lx + ly + lz;
+    for (int st = 0; st <= last; ++st) {
+        if (mine && mys == st) {
+            T sum = s[c - 1] + s[c + 1];  // ((((xl + xr) + yl) + yr) + zl) + zr, cpu.lua:28-33
+            sum = sum + s[c - E];
+            sum = sum + s[c + E];
+            if (DIM == 3) {
+                sum = sum + s[c - E * E];
+                sum = sum + s[c + E * E];
+            }
+            s[c] = op.relax(sum, fc, nb);
+        }
+        __syncthreads();
+    }
+    if (mine) u[pidx(g, gi, gj, gk)] = s[c];
+}
+
+template <typename T, int D>
+static hipError_t gslex_t(void* u, const void* f, Geo g, double h, double cl, hipStream_t st)
+{
+    constexpr int B = gsl_edge<D>();
+    const int TX = std::min(B, g.nx), TY = std::min(B, g.ny), TZ = D == 3 ? (int)std::min<int64_t>(B, g.nz) : 1;
+    const int ntx = g.nx / TX, nty = g.ny / TY, ntz = D == 3 ? (int)(g.nz / TZ) : 1;
+    const Op<T, D> op = make_op<T, D>(h, cl);
+    const unsigned nb = (unsigned)(D == 3 ? ntx * nty : ntx);
+    for (int S = 0; S < ntx + nty + ntz - 2; ++S) {
+        k_gslex<T, D><<<nb, gsl_threads<D>(), 0, st>>>((T*)u, (const T*)f, g, op, S, TX, TY, TZ);
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+
+hipError_t launch_gslex_sweep(int rb, int dim, void* u, const void* f, Geo g, double h, double cl, hipStream_t s)
+{
+    if (rb != 4 && rb != 8) return hipErrorInvalidValue;  // real arithmetic only (cpu-raw.lua has no GS)
+    if (dim == 3) return rb == 8 ? gslex_t<double, 3>(u, f, g, h, cl, s) : gslex_t<float, 3>(u, f, g, h, cl, s);
+    return rb == 8 ? gslex_t<double, 2>(u, f, g, h, cl, s) : gslex_t<float, 2>(u, f, g, h, cl, s);
+}
+
 // ---- test hook of the communication deadline (mgp_api.cpp stream_wait; MGP_TEST_STALL) ----
 
 // One wave polls a host-pinned flag with system-scope vector loads (never the scalar cache) and leaves when it is

@@ -31,7 +31,7 @@ It accepts the constructor protocols of the reference:
     (mgp_group_*); fields are the global box.
 mg:metrics() returns relErr, count, frobErr of the last outer iteration (gpu.lua:173-200);
 mg:residualNorm() returns ||f - A psi||, ||f|| (device reduction).
-Extra table fields select the build's configurations: dim (2|3), real, smoother ('jacobi'|'rbgs'),
+Extra table fields select the build's configurations: dim (2|3), real, smoother ('jacobi'|'rbgs'|'gs_lex'),
 cycle ('V'|'F'), prolong ('pc'|'linear'), coarse_init ('fresh'|'warm'), coarse_bc
 ('zero'|'consistent'), restriction ('average'|'full_weighting'), arith ('real'|'double'), device.
 Defaults reproduce cpu.lua
@@ -104,7 +104,7 @@ int         mgp_group_residual_norm(mgp_group* g, int level, double* rnorm, doub
 local lib = ffi.load(os.getenv('MGP_LIBRARY') or 'mgpoisson')
 
 local CODES = {
-	smoother = {jacobi = 0, rbgs = 1},
+	smoother = {jacobi = 0, rbgs = 1, gs_lex = 2},
 	cycle = {V = 0, F = 1},
 	prolong = {pc = 0, linear = 1},
 	coarse_init = {fresh = 0, warm = 1},
@@ -128,7 +128,8 @@ end
 local MultigridHIP = {}
 -- cpu.lua:56-57 inPlaceIterativeSolver values (functions there, markers here)
 MultigridHIP.Jacobi = 'jacobi'
-MultigridHIP.GaussSeidel = 'rbgs'  -- the deterministic red/black form of cpu.lua:24-37 / gpu.lua:61-81
+MultigridHIP.GaussSeidel = 'gs_lex'  -- cpu.lua:24-37's lexicographic in-place sweep, bit-identical (hyperplane order)
+MultigridHIP.RedBlackGaussSeidel = 'rbgs'  -- the build's red/black form (the temporally blocked engines)
 
 local LEVEL_FIELDS = {rs = true, Rs = true, vs = true, Vs = true}
 local IMAGE_FIELDS = {psiOld = true, errorBuf = true, tmpU = true}
@@ -157,8 +158,10 @@ MultigridHIP.__newindex = function(self, k, v)
 	if k == 'smooth' then
 		rawset(self, 'pendingSmooth', v)
 	elseif k == 'inPlaceIterativeSolver' then
-		local name = (v == MultigridHIP.GaussSeidel or v == 'GaussSeidel') and 'rbgs' or
-			((v == MultigridHIP.Jacobi or v == 'Jacobi') and 'jacobi' or error('inPlaceIterativeSolver: Jacobi | GaussSeidel'))
+		local name = (v == MultigridHIP.GaussSeidel or v == 'GaussSeidel') and 'gs_lex' or
+			((v == MultigridHIP.RedBlackGaussSeidel or v == 'RedBlackGaussSeidel') and 'rbgs' or
+			((v == MultigridHIP.Jacobi or v == 'Jacobi') and 'jacobi' or
+			error('inPlaceIterativeSolver: Jacobi | GaussSeidel | RedBlackGaussSeidel')))
 		rawset(self, 'pendingSmoother', name)
 	else
 		rawset(self, k, v)
@@ -266,7 +269,9 @@ function MultigridHIP:init(a, real, cpuDepth, engine)
 	rawset(self, 'devices', args.devices)
 	local smoother = args.smoother
 	if args.inPlaceIterativeSolver then
-		smoother = (args.inPlaceIterativeSolver == MultigridHIP.GaussSeidel) and 'rbgs' or 'jacobi'
+		local v = args.inPlaceIterativeSolver
+		smoother = (v == MultigridHIP.GaussSeidel) and 'gs_lex' or
+			((v == MultigridHIP.RedBlackGaussSeidel) and 'rbgs' or 'jacobi')
 	end
 	rawset(self, 'build', {real = rawget(self, 'real'), smooth = args.smooth or MultigridHIP.smooth,
 		smoother = smoother or 'jacobi', cycle = args.cycle, prolong = args.prolong,

@@ -33,7 +33,7 @@ lib = ctypes.CDLL(LIB_PATH)
 
 MGP_OK = 0
 STATUS = {-1: "MGP_ERR_ARG", -2: "MGP_ERR_HIP", -3: "MGP_ERR_RCCL", -4: "MGP_ERR_OOM", -5: "MGP_ERR_STATE"}
-JACOBI, RBGS = 0, 1
+JACOBI, RBGS, GS_LEX = 0, 1, 2
 CYCLE_V, CYCLE_F = 0, 1
 PROLONG_PC, PROLONG_LINEAR = 0, 1
 COARSE_FRESH, COARSE_WARM = 0, 1

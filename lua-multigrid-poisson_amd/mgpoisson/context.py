@@ -12,7 +12,7 @@ import numpy as np
 
 from . import _lib as L
 
-SMOOTHERS = {"jacobi": L.JACOBI, "rbgs": L.RBGS}
+SMOOTHERS = {"jacobi": L.JACOBI, "rbgs": L.RBGS, "gs_lex": L.GS_LEX}
 CYCLES = {"V": L.CYCLE_V, "F": L.CYCLE_F}
 PROLONGS = {"pc": L.PROLONG_PC, "linear": L.PROLONG_LINEAR}
 COARSE_INITS = {"fresh": L.COARSE_FRESH, "warm": L.COARSE_WARM}

@@ -29,8 +29,10 @@ log = logging.getLogger(__name__)
 
 class _Smoother(str):
     """The values of ``inPlaceIterativeSolver`` (cpu.lua:56-57): ``MultigridHIP.Jacobi`` (the
-    reference's active choice) or ``MultigridHIP.GaussSeidel`` (in the reference a lexicographic
-    in-place sweep that is racy on a GPU, gpu.lua:61-62; here its deterministic red/black form)."""
+    reference's active choice), ``MultigridHIP.GaussSeidel`` (cpu.lua:24-37's lexicographic in-place
+    sweep, bit for bit: hyperplane-ordered on the GPU, one rank's box) or
+    ``MultigridHIP.RedBlackGaussSeidel`` (the build's red/black form, which the temporally blocked
+    engines run; gpu.lua:61-81's racy GPU variant is not offered)."""
 
 
 class LevelFields:
@@ -111,7 +113,8 @@ class MultigridHIP(_RawFields):
     epsilon = 1e-10  # cpu.lua:21
     maxiter = 1000  # cpu.lua:22
     Jacobi = _Smoother("jacobi")  # cpu.lua:40-54
-    GaussSeidel = _Smoother("rbgs")  # cpu.lua:24-37, red/black on the GPU
+    GaussSeidel = _Smoother("gs_lex")  # cpu.lua:24-37, lexicographic, bit-identical
+    RedBlackGaussSeidel = _Smoother("rbgs")  # build-defined red/black (the north-star smoother)
 
     def __init__(self, args=None, **kw):
         a = dict(args or {})
@@ -143,8 +146,8 @@ class MultigridHIP(_RawFields):
     # sweep counts are baked into the device context, so a change rebuilds it, keeping psi/f.
     @property
     def inPlaceIterativeSolver(self):
-        """cpu.lua:56-57's knob: MultigridHIP.Jacobi or MultigridHIP.GaussSeidel (writable)."""
-        return self.Jacobi if self._build["smoother"] == "jacobi" else self.GaussSeidel
+        """cpu.lua:56-57's knob: MultigridHIP.Jacobi, .GaussSeidel or .RedBlackGaussSeidel (writable)."""
+        return {"jacobi": self.Jacobi, "gs_lex": self.GaussSeidel}.get(self._build["smoother"], self.RedBlackGaussSeidel)
 
     @inPlaceIterativeSolver.setter
     def inPlaceIterativeSolver(self, value):
@@ -226,12 +229,13 @@ class MultigridHIP(_RawFields):
 
 
 def _smoother_name(v):
-    if callable(v) and getattr(v, "__name__", "") in ("Jacobi", "GaussSeidel"):
+    if callable(v) and getattr(v, "__name__", "") in ("Jacobi", "GaussSeidel", "RedBlackGaussSeidel"):
         v = v.__name__
     v = str(v)
-    names = {"jacobi": "jacobi", "Jacobi": "jacobi", "rbgs": "rbgs", "GaussSeidel": "rbgs", "gaussseidel": "rbgs"}
+    names = {"jacobi": "jacobi", "Jacobi": "jacobi", "gs_lex": "gs_lex", "GaussSeidel": "gs_lex",
+             "gaussseidel": "gs_lex", "rbgs": "rbgs", "RedBlackGaussSeidel": "rbgs"}
     if v not in names:
-        raise ValueError(f"inPlaceIterativeSolver: {v!r} (Jacobi | GaussSeidel)")
+        raise ValueError(f"inPlaceIterativeSolver: {v!r} (Jacobi | GaussSeidel | RedBlackGaussSeidel)")
     return names[v]
 
 

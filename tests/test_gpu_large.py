@@ -284,7 +284,7 @@ def test_cpu_lua_knobs_and_matrix_two_grid():
     s.inPlaceIterativeSolver = mg.MultigridHIP.GaussSeidel
     assert s.inPlaceIterativeSolver == mg.MultigridHIP.GaussSeidel
     assert np.array_equal(s.psi, psi)
-    o = Oracle(dim=2, n=(16, 16, 1), smoother="rbgs")
+    o = Oracle(dim=2, n=(16, 16, 1), smoother="gs_lex")  # GaussSeidel = cpu.lua:24-37's lexicographic sweep
     o.set(0, psi)
     o.set(1, s.f)
     s.step()
