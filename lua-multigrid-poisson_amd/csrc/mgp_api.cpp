@@ -236,6 +236,7 @@ struct mgp_ctx {
     bool nb_comm = false;  // non-blocking communicators (mgp_group_create): every call is polled to completion
     mgp::FusedTuning tu;   // tile settings of the temporally blocked phases (env, snapshot at creation)
     bool resfw = true;     // the full weighting's residual + restriction as one pass (MGP_RESFW=0: two passes)
+    bool bres = true;      // the last pre black half-sweep fused with residual + restriction (MGP_BRES=0: apart)
     bool rccl1 = false;    // world 1 on a one-rank RCCL communicator (MGP_TRANSPORT=rccl, env_rccl1)
     // the multi-rank code path: a communicator (or the loopback transport), collectives, the side stream
     bool multi() const { return o.world > 1 || rccl1; }
@@ -841,7 +842,10 @@ int smooth_deep(mgp_ctx* c, int l, int sweeps, double h)
 }
 
 // red_done: the first sweep's red half-sweep already ran (k_post1), start at its black half
-int smooth(mgp_ctx* c, int l, int sweeps, double h, bool want_err = false, bool red_done = false)
+// black_later: the last sweep's black half-sweep is left to k_bres (black_residual_restrict), which runs it fused
+// with the residual and the restriction
+int smooth(mgp_ctx* c, int l, int sweeps, double h, bool want_err = false, bool red_done = false,
+           bool black_later = false)
 {
     Level& L = c->lev[l];
     const double cl = coarse_coef(c->o.coarse_bc, l);
@@ -887,6 +891,7 @@ int smooth(mgp_ctx* c, int l, int sweeps, double h, bool want_err = false, bool 
             TRY(half(c, l, 0, L.zero_pending ? c->zbuf : L.u, dst, old, h, cl, 0));  // red from black
         }
         L.zero_pending = false;
+        if (black_later && sw == sweeps - 1 && !oop && !last_err) break;  // (the caller's k_bres runs it)
         if (L.p.dist) {  // black reads the new red planes of dst
             TRY(exchange_buf(c, L, dst));
         }
@@ -992,6 +997,30 @@ int residual_restrict_fw(mgp_ctx* c, int l, double h)
                                        coarse_coef(c->o.coarse_bc, l + 1), c->s));
     C.fghost_ok = !C.p.dist;
     if (L.p.dist && !C.p.dist) TRY(gather_coarse_rhs(c, L, C, R));
+    return MGP_OK;
+}
+
+// Pre-smoothing whose last black half-sweep runs fused with the residual and the restriction (k_bres): a replicated
+// red/black per-piece level with the average restriction and at least two sweeps (the last one is then a plain red +
+// black pair, never the fresh-guess pass).  MGP_BRES=0: the separate half-sweep and k_resrestrict.
+bool bres_ok(const mgp_ctx* c, const Level& L)
+{
+    return c->bres && c->o.smoother == MGP_RBGS && c->o.nu1 >= 2 && c->o.restriction == MGP_RESTRICT_AVERAGE &&
+           !L.p.dist && (c->rk == 4 || c->rk == 8) && mgp::bres_supported(c->rk, L.g) && (c->o.dim == 2 || L.g.nz >= 2);
+}
+
+int black_residual_restrict(mgp_ctx* c, int l, double h)
+{
+    Level& L = c->lev[l];
+    Level& C = c->lev[l + 1];
+    int64_t zc = 0;
+    const Geo gc = coarse_view(L, C, &zc);
+    char* R = c->ui(C, C.f) + (size_t)(zc * C.g.P) * c->rb;
+    HIP_TRY(c, mgp::launch_black_residual_restrict(c->rk, c->o.dim, c->ui(L, L.u), c->ui(L, L.f), R, L.g, gc, h,
+                                                   coarse_coef(c->o.coarse_bc, l), c->s));
+    L.ghost_ok = true;
+    L.ghost_zero = false;
+    C.fghost_ok = !C.p.dist;
     return MGP_OK;
 }
 
@@ -1516,6 +1545,9 @@ int cycle_rec(mgp_ctx* c, int l, double h, bool fcycle)
         TRY(early_exchange_post(c, l));
     } else if (blk) {
         TRY(block_pre(c, l, h));
+    } else if (bres_ok(c, c->lev[l])) {
+        TRY(smooth(c, l, c->o.nu1, h, false, false, true));
+        TRY(black_residual_restrict(c, l, h));
     } else {
         TRY(smooth(c, l, c->o.nu1, h));
         TRY(residual_restrict(c, l, h));
@@ -1816,6 +1848,8 @@ static void host_setup(mgp_ctx* c, const mgp_opts& o, const std::vector<LevelPla
         c->early_x = !(ve && std::atoi(ve) == 0);
         const char* vr = std::getenv("MGP_RESFW");
         c->resfw = !(vr && std::atoi(vr) == 0);
+        const char* vbr = std::getenv("MGP_BRES");
+        c->bres = !(vbr && std::atoi(vbr) == 0);
     }
     // distributed 3D levels sweep with deep halos (smooth_deep): kGhostZs ghost planes per side
     if (c->deep_halo && o.dim == 3 && c->multi()) c->G = mgp::kGhostZs;

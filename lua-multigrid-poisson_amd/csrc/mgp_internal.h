@@ -84,6 +84,13 @@ hipError_t launch_post_first(int rb, int dim, int linear, void* u, const void* V
 // coarse plane of this rank's fine plane 0; its Geo is gc) from u, f of the fine level.
 hipError_t launch_residual_restrict(int rb, int dim, const void* u, const void* f, void* R, Geo g, Geo gc, double h,
                                     double cl, hipStream_t s);
+// The last black half-sweep of a red/black pre-smoothing + residual + restriction in one pass (k_bres): u's black
+// cells relaxed in place from its (final) red cells and f, R as launch_residual_restrict would compute it from the
+// swept u.  Bit-identical to launch_half_sweep(colour 1, in place) + launch_residual_restrict.  Real arithmetic
+// (rb 4 / 8), a replicated level (planes -1 and nz are not read) with nx, ny (and nz) >= 2.
+bool bres_supported(int rb, const Geo& g);
+hipError_t launch_black_residual_restrict(int rb, int dim, void* u, const void* f, void* R, Geo g, Geo gc, double h,
+                                          double cl, hipStream_t s);
 // Full-weighting restriction (mgp_opts.restriction, build-defined): r = f - A u of the level's own planes
 // into the scratch r (same packed layout and ghost planes as the level), then R (coarse packed, Geo gc)
 // from r, which must have current planes -1 and g.nz (zero at the physical boundary, the neighbours'

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round 5: interleaved A/B of bench lines.  $AB = lines "label|ENV=.. ENV2=..|bench args"; $REPS rounds.
+# Interleaved A/B of bench lines.  $AB = lines "label|ENV=.. ENV2=..|bench args"; $REPS rounds.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out/ab
