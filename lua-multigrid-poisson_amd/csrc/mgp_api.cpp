@@ -237,6 +237,7 @@ struct mgp_ctx {
     mgp::FusedTuning tu;   // tile settings of the temporally blocked phases (env, snapshot at creation)
     bool resfw = true;     // the full weighting's residual + restriction as one pass (MGP_RESFW=0: two passes)
     bool bres = true;      // the last pre black half-sweep fused with residual + restriction (MGP_BRES=0: apart)
+    bool rbsweep = true;   // whole red/black sweeps of levels below the finest in one pass (MGP_RBSWEEP=0: halves)
     bool rccl1 = false;    // world 1 on a one-rank RCCL communicator (MGP_TRANSPORT=rccl, env_rccl1)
     // the multi-rank code path: a communicator (or the loopback transport), collectives, the side stream
     bool multi() const { return o.world > 1 || rccl1; }
@@ -841,6 +842,8 @@ int smooth_deep(mgp_ctx* c, int l, int sweeps, double h)
     return MGP_OK;
 }
 
+bool rbsweep_level(const mgp_ctx* c, const Level& L, int l);
+
 // red_done: the first sweep's red half-sweep already ran (k_post1), start at its black half
 // black_later: the last sweep's black half-sweep is left to k_bres (black_residual_restrict), which runs it fused
 // with the residual and the restriction
@@ -880,6 +883,16 @@ int smooth(mgp_ctx* c, int l, int sweeps, double h, bool want_err = false, bool 
                                                sweeps < 2));
             L.zero_pending = false;
             L.ghost_ok = true;
+            L.ghost_zero = false;
+            continue;
+        }
+        if (L.t && rbsweep_level(c, L, l) && !L.zero_pending && !oop && !last_err && !(red_done && sw == 0) &&
+            !(black_later && sw == sweeps - 1)) {
+            // the whole sweep in one pass into t; its red cells are needed only if no red half-sweep follows
+            HIP_TRY(c, mgp::launch_rb_sweep(c->rk, c->o.dim, c->ui(L, L.u), c->ui(L, L.f), c->ui(L, L.t), L.g, h, cl,
+                                            sw == sweeps - 1, c->s));
+            std::swap(L.u, L.t);
+            L.ghost_ok = !L.p.dist;
             L.ghost_zero = false;
             continue;
         }
@@ -1007,6 +1020,14 @@ bool bres_ok(const mgp_ctx* c, const Level& L)
 {
     return c->bres && c->o.smoother == MGP_RBGS && c->o.nu1 >= 2 && c->o.restriction == MGP_RESTRICT_AVERAGE &&
            !L.p.dist && (c->rk == 4 || c->rk == 8) && mgp::bres_supported(c->rk, L.g) && (c->o.dim == 2 || L.g.nz >= 2);
+}
+
+// Whole red/black sweeps as one out-of-place pass each (k_rbsweep, u -> t, swapped) on a replicated red/black level
+// below the finest (level 0's t is psiOld under the fused err).  MGP_RBSWEEP=0: the k_half pair per sweep.
+bool rbsweep_level(const mgp_ctx* c, const Level& L, int l)
+{
+    return c->rbsweep && c->o.smoother == MGP_RBGS && l > 0 && !L.p.dist && (c->rk == 4 || c->rk == 8) &&
+           mgp::bres_supported(c->rk, L.g) && (c->o.dim == 2 || L.g.nz >= 2);
 }
 
 int black_residual_restrict(mgp_ctx* c, int l, double h)
@@ -1850,6 +1871,8 @@ static void host_setup(mgp_ctx* c, const mgp_opts& o, const std::vector<LevelPla
         c->resfw = !(vr && std::atoi(vr) == 0);
         const char* vbr = std::getenv("MGP_BRES");
         c->bres = !(vbr && std::atoi(vbr) == 0);
+        const char* vrs = std::getenv("MGP_RBSWEEP");
+        c->rbsweep = !(vrs && std::atoi(vrs) == 0);
     }
     // distributed 3D levels sweep with deep halos (smooth_deep): kGhostZs ghost planes per side
     if (c->deep_halo && o.dim == 3 && c->multi()) c->G = mgp::kGhostZs;
@@ -2132,7 +2155,8 @@ static int create_impl(mgp_ctx** out, const mgp_opts* o, mgp_loopback* lb, ncclC
     for (size_t l = 0; l < c->lev.size(); ++l) {
         Level& L = c->lev[l];
         const size_t bytes = (size_t)L.alloc * rb;
-        const bool need_t = c->o.smoother == MGP_JACOBI || (l == 0 && c->err_fuse) || L.fused || L.blk || L.zpost;
+        const bool need_t = c->o.smoother == MGP_JACOBI || (l == 0 && c->err_fuse) || L.fused || L.blk || L.zpost ||
+                            rbsweep_level(c, L, (int)l);
         if (dev_alloc(c, &L.u, bytes, 1) != hipSuccess || dev_alloc(c, &L.f, bytes, 2) != hipSuccess ||
             (need_t && dev_alloc(c, &L.t, bytes, 3) != hipSuccess)) {
             c->err = "hipMalloc failed for level " + std::to_string(l) + " (" + std::to_string(bytes) + " bytes)";

@@ -91,6 +91,11 @@ hipError_t launch_residual_restrict(int rb, int dim, const void* u, const void* 
 bool bres_supported(int rb, const Geo& g);
 hipError_t launch_black_residual_restrict(int rb, int dim, void* u, const void* f, void* R, Geo g, Geo gc, double h,
                                           double cl, hipStream_t s);
+// One whole red/black sweep in one pass (k_rbsweep): dst's black cells (and with store_red its red ones) = the sweep
+// of src, read from src's black cells and f only (src != dst; same shapes as launch_black_residual_restrict).
+// Bit-identical to the red and black launch_half_sweep pair.
+hipError_t launch_rb_sweep(int rb, int dim, const void* src, const void* f, void* dst, Geo g, double h, double cl,
+                           bool store_red, hipStream_t s);
 // Full-weighting restriction (mgp_opts.restriction, build-defined): r = f - A u of the level's own planes
 // into the scratch r (same packed layout and ghost planes as the level), then R (coarse packed, Geo gc)
 // from r, which must have current planes -1 and g.nz (zero at the physical boundary, the neighbours'

@@ -1,10 +1,13 @@
-"""GPU: the pre-smoothing's last black half-sweep fused with calcResidual + reduceResidual (k_bres).
+"""GPU: fused passes of the per-piece red/black levels below the finest (round 6).
 
-A red/black sweep's black half reads only red cells, so one pass can relax the black cells, form the residual
-of both colours and restrict it (cpu.lua:40-54 update, cpu.lua:108-135); it replaces k_half (black) +
-k_resrestrict_s on every replicated per-piece level of a red/black cycle with >= 2 pre-sweeps and the average
-restriction.  Bar: psi bit-identical to the oracle and to the unfused pieces (MGP_BRES=0) after whole cycles, on
-cubic / square / non-cubic boxes, fp32 / fp64, both coarse boundaries, V and F, fresh and warm coarse guesses."""
+- k_bres: the pre-smoothing's last black half-sweep + calcResidual + reduceResidual in one pass.  A red/black
+  sweep's black half reads only red cells, so one pass can relax the black cells, form the residual of both
+  colours and restrict it (cpu.lua:40-54 update, cpu.lua:108-135).
+- k_rbsweep: a whole red/black sweep in one out-of-place pass (u -> t, swapped), the red cells the black half
+  reads recomputed at the block edge; only the last sweep of a run stores its red cells.
+Bar: psi bit-identical to the oracle and to the separate pieces (MGP_BRES=0 MGP_RBSWEEP=0) after whole cycles, on
+cubic / square / non-cubic boxes, fp32 / fp64, both coarse boundaries, V and F, fresh and warm coarse guesses, odd
+and even sweep counts; and single smoothing calls on levels 1 and 2 against the oracle's sweeps."""
 import numpy as np
 import pytest
 
@@ -21,10 +24,14 @@ CASES = [
     dict(dim=3, n=(32, 32, 32), real="float", prolong="linear", coarse_bc="consistent", coarse_init="warm", **RB),
     dict(dim=2, n=(256, 256, 1), real="float", prolong="linear", coarse_bc="consistent", **RB),
     dict(dim=2, n=(128, 64, 1), real="double", prolong="pc", coarse_bc="zero", smoother="rbgs", nu1=3, nu2=1),
+    dict(dim=3, n=(32, 32, 32), real="float", prolong="linear", coarse_bc="consistent", smoother="rbgs", nu1=4, nu2=3),
+    dict(dim=2, n=(64, 64, 1), real="float", prolong="linear", coarse_bc="consistent", smoother="rbgs", nu1=1, nu2=1,
+         cycle="F"),
 ]
 
 
-@pytest.mark.parametrize("cfg", CASES, ids=["3d64-f32", "3d64-f64-F", "3d-noncubic", "3d32-warm", "2d256", "2d-3+1"])
+@pytest.mark.parametrize("cfg", CASES, ids=["3d64-f32", "3d64-f64-F", "3d-noncubic", "3d32-warm", "2d256", "2d-3+1",
+                                            "3d-4+3", "2d-1+1-F"])
 def test_bres_cycles_match_oracle_and_pieces(cfg, monkeypatch):
     monkeypatch.setenv("MGP_TAIL", "0")  # every level below the finest runs its own pieces
     monkeypatch.setenv("MGP_BLK", "0")
@@ -32,6 +39,7 @@ def test_bres_cycles_match_oracle_and_pieces(cfg, monkeypatch):
     ctx = _ctx(**cfg)
     ctx.init_point_charge()
     monkeypatch.setenv("MGP_BRES", "0")
+    monkeypatch.setenv("MGP_RBSWEEP", "0")
     ref = _ctx(**cfg)
     ref.init_point_charge()
     o = Oracle(**cfg)
@@ -56,3 +64,26 @@ def test_bres_default_engines_512_box_levels():
     ctx.cycle()
     o.step()
     assert np.array_equal(ctx.get_psi(), o.get(0))
+
+
+@pytest.mark.parametrize("dim,n", [(3, (32, 32, 32)), (3, (16, 32, 64)), (2, (128, 128, 1)), (2, (64, 16, 1))])
+@pytest.mark.parametrize("real", ["float", "double"])
+@pytest.mark.parametrize("level", [1, 2])
+def test_rbsweep_smoothing_calls_match_oracle(dim, n, real, level):
+    """mgp_smooth on a level below the finest runs k_rbsweep for every sweep (the last one stores both colours):
+    1, 2 and 3 sweeps of random fields equal the oracle's red/black sweeps with the consistent boundary."""
+    from oracle_lib import coarse_coef, smooth_arr
+    from test_gpu_parity import REAL, _rand
+
+    ctx = _ctx(dim=dim, n=n, real=real, smoother="rbgs", nu1=2, nu2=2, coarse_bc="consistent")
+    shp = ctx.shape(level)
+    u = _rand(shp, REAL[real], 21)
+    f = _rand(shp, REAL[real], 22)
+    ctx.set_psi(u, level)
+    ctx.set_f(f, level)
+    ref = u
+    h = (2.0 ** level) / n[0]
+    for sweeps in (1, 2, 3):
+        ctx.smooth(level, sweeps)
+        ref = smooth_arr(dim, ref, f, "rbgs", sweeps, h, coarse_coef("consistent", level))
+        assert np.array_equal(ctx.get_psi(level), ref)
