@@ -898,192 +898,6 @@ __global__ __launch_bounds__(kBlock) void k_resrestrict(const T* __restrict__ u,
     }
 }
 
-// ---- the last black half-sweep of a pre-smoothing + calcResidual + reduceResidual in one pass (k_bres) ----
-//
-// A red/black sweep's black half-sweep reads only red cells, and nothing reads the black cells of u before it
-// replaces them, so one pass can relax the black cells, form the residual of both colours and restrict it: a
-// thread owns one coarse cell, relaxes its 4 black children (stored, in place: no thread loads a black cell) and
-// the 12 black cells just outside its 2^3 block that neighbour its red children (recomputed by the neighbouring
-// threads that own them, with the same expression), then sums the 8 children's residuals in the reference order
-// (k_resrestrict_s).  Replaces k_half (black) + k_resrestrict_s on a replicated per-piece level: one pass over
-// red u and f instead of two (cpu.lua:40-54 update, cpu.lua:108-135), bit-identical.
-template <typename T, int DIM>
-__global__ __launch_bounds__(kBlock) void k_bres(T* __restrict__ u, const T* __restrict__ f, T* __restrict__ R,
-                                                 Geo g, Geo gc, Op<T, DIM> op)
-{
-    const int64_t it = (int64_t)xcd_remap(blockIdx.x, gridDim.x) * kBlock + threadIdx.x;
-    if (it >= resrestrict_items<T, DIM>(g)) return;
-    const int lcx = g.lx - 1, lcy = g.ly - 1;
-    const int I = (int)(it & ((g.nx >> 1) - 1));
-    const int J = (int)((it >> lcx) & ((g.ny >> 1) - 1));
-    const int64_t K = DIM == 3 ? it >> (lcx + lcy) : 0;
-    const int i0 = 2 * I, j0 = 2 * J;
-    const int64_t k0 = DIM == 3 ? 2 * K : 0;
-    const int64_t gz = g.z0;
-    auto inside = [&](int i, int j, int64_t k) {
-        return i >= 0 && i < g.nx && j >= 0 && j < g.ny && (DIM == 2 || (k >= 0 && k < g.nz));
-    };
-    auto red = [&](int i, int j, int64_t k) { return inside(i, j, k) ? u[pidx(g, i, j, k)] : (T)0; };
-    auto nfaces = [&](int i, int j, int64_t k) {
-        int nb = (i == 0) + (i == g.nx - 1) + (j == 0) + (j == g.ny - 1);
-        if (DIM == 3) nb += (gz + k == 0) + (gz + k == g.gnz - 1);
-        return nb;
-    };
-    // the black half-sweep's value of black cell (i, j, k) inside the box: its neighbours are all red (final)
-    auto black = [&](int i, int j, int64_t k) {
-        T s = red(i - 1, j, k) + red(i + 1, j, k);
-        s = s + red(i, j - 1, k);
-        s = s + red(i, j + 1, k);
-        if (DIM == 3) {
-            s = s + red(i, j, k - 1);
-            s = s + red(i, j, k + 1);
-        }
-        return op.relax(s, f[pidx(g, i, j, k)], nfaces(i, j, k));
-    };
-    auto is_black = [&](int i, int j, int64_t k) { return ((i + j + gz + k) & 1) != 0; };
-    // the block's black children, relaxed once: bv[dz][dy][dx] (red entries unused)
-    T bv[DIM == 3 ? 2 : 1][2][2];
-#pragma unroll
-    for (int dz = 0; dz < (DIM == 3 ? 2 : 1); ++dz)
-#pragma unroll
-        for (int dy = 0; dy < 2; ++dy)
-#pragma unroll
-            for (int dx = 0; dx < 2; ++dx) {
-                const int i = i0 + dx, j = j0 + dy;
-                const int64_t k = k0 + dz;
-                bv[dz][dy][dx] = is_black(i, j, k) ? black(i, j, k) : (T)0;
-            }
-    // a neighbour's value after the half-sweep: inside the block from bv / u, outside recomputed or loaded
-    auto val = [&](int i, int j, int64_t k) {
-        if (!inside(i, j, k)) return (T)0;
-        const int dx = i - i0, dy = j - j0;
-        const int64_t dz = k - k0;
-        const bool in_blk = dx >= 0 && dx < 2 && dy >= 0 && dy < 2 && dz >= 0 && dz < (DIM == 3 ? 2 : 1);
-        if (!is_black(i, j, k)) return u[pidx(g, i, j, k)];
-        return in_blk ? bv[dz][dy][dx] : black(i, j, k);
-    };
-    auto res = [&](int dx, int dy, int dz) {
-        const int i = i0 + dx, j = j0 + dy;
-        const int64_t k = k0 + dz;
-        T s = val(i - 1, j, k) + val(i + 1, j, k);
-        s = s + val(i, j - 1, k);
-        s = s + val(i, j + 1, k);
-        if (DIM == 3) {
-            s = s + val(i, j, k - 1);
-            s = s + val(i, j, k + 1);
-        }
-        const T uc = is_black(i, j, k) ? bv[dz][dy][dx] : u[pidx(g, i, j, k)];
-        return op.residual(s, f[pidx(g, i, j, k)], uc, nfaces(i, j, k));
-    };
-    T acc = res(0, 0, 0) + res(1, 0, 0);
-    acc = acc + res(0, 1, 0);
-    acc = acc + res(1, 1, 0);
-    if (DIM == 3) {
-        acc = acc + res(0, 0, 1);
-        acc = acc + res(1, 0, 1);
-        acc = acc + res(0, 1, 1);
-        acc = acc + res(1, 1, 1);
-    }
-    R[pidx(gc, I, J, K)] = (DIM == 3 ? (T)0.125 : (T)0.25) * acc;
-#pragma unroll
-    for (int dz = 0; dz < (DIM == 3 ? 2 : 1); ++dz)
-#pragma unroll
-        for (int dy = 0; dy < 2; ++dy)
-#pragma unroll
-            for (int dx = 0; dx < 2; ++dx)
-                if (is_black(i0 + dx, j0 + dy, k0 + dz)) u[pidx(g, i0 + dx, j0 + dy, k0 + dz)] = bv[dz][dy][dx];
-}
-
-// ---- one whole red/black sweep per pass, out of place (k_rbsweep) ----
-//
-// A sweep's red half reads only black cells and its black half only red ones.  A thread owns a 2^DIM block: it
-// relaxes the block's red cells from src's black cells, then the block's black cells from those and from the red
-// cells just outside the block (each recomputed from src's black cells with the same expression, as the owning
-// thread does), and stores the black cells (and with STORE_RED the red ones) into dst != src, so that no thread
-// reads what another writes.  Consecutive sweeps alternate src / dst; only the last of them needs its red cells
-// (a red half-sweep replaces red cells unread), so the others store black only.  Bit-identical to the red then
-// black k_half pair of each sweep (cpu.lua:40-54 update), one pass of 2 (2.5) reals per cell instead of 3.
-template <typename T, int DIM, bool STORE_RED>
-__global__ __launch_bounds__(kBlock) void k_rbsweep(const T* __restrict__ src, const T* __restrict__ f,
-                                                    T* __restrict__ dst, Geo g, Op<T, DIM> op)
-{
-    const int64_t it = (int64_t)xcd_remap(blockIdx.x, gridDim.x) * kBlock + threadIdx.x;
-    if (it >= resrestrict_items<T, DIM>(g)) return;
-    const int lcx = g.lx - 1, lcy = g.ly - 1;
-    const int I = (int)(it & ((g.nx >> 1) - 1));
-    const int J = (int)((it >> lcx) & ((g.ny >> 1) - 1));
-    const int64_t K = DIM == 3 ? it >> (lcx + lcy) : 0;
-    const int i0 = 2 * I, j0 = 2 * J;
-    const int64_t k0 = DIM == 3 ? 2 * K : 0;
-    const int64_t gz = g.z0;
-    auto inside = [&](int i, int j, int64_t k) {
-        return i >= 0 && i < g.nx && j >= 0 && j < g.ny && (DIM == 2 || (k >= 0 && k < g.nz));
-    };
-    auto nfaces = [&](int i, int j, int64_t k) {
-        int nb = (i == 0) + (i == g.nx - 1) + (j == 0) + (j == g.ny - 1);
-        if (DIM == 3) nb += (gz + k == 0) + (gz + k == g.gnz - 1);
-        return nb;
-    };
-    auto is_black = [&](int i, int j, int64_t k) { return ((i + j + gz + k) & 1) != 0; };
-    auto old_black = [&](int i, int j, int64_t k) { return inside(i, j, k) ? src[pidx(g, i, j, k)] : (T)0; };
-    // the red half-sweep's value of red cell (i, j, k) (inside the box)
-    auto red = [&](int i, int j, int64_t k) {
-        T s = old_black(i - 1, j, k) + old_black(i + 1, j, k);
-        s = s + old_black(i, j - 1, k);
-        s = s + old_black(i, j + 1, k);
-        if (DIM == 3) {
-            s = s + old_black(i, j, k - 1);
-            s = s + old_black(i, j, k + 1);
-        }
-        return op.relax(s, f[pidx(g, i, j, k)], nfaces(i, j, k));
-    };
-    constexpr int NZ = DIM == 3 ? 2 : 1;
-    T rv[NZ][2][2];  // the block's red cells after the red half (black entries unused)
-#pragma unroll
-    for (int dz = 0; dz < NZ; ++dz)
-#pragma unroll
-        for (int dy = 0; dy < 2; ++dy)
-#pragma unroll
-            for (int dx = 0; dx < 2; ++dx)
-                rv[dz][dy][dx] = is_black(i0 + dx, j0 + dy, k0 + dz) ? (T)0 : red(i0 + dx, j0 + dy, k0 + dz);
-    auto new_red = [&](int i, int j, int64_t k) {
-        if (!inside(i, j, k)) return (T)0;
-        const int dx = i - i0, dy = j - j0;
-        const int64_t dz = k - k0;
-        if (dx >= 0 && dx < 2 && dy >= 0 && dy < 2 && dz >= 0 && dz < NZ) return rv[dz][dy][dx];
-        return red(i, j, k);
-    };
-#pragma unroll
-    for (int dz = 0; dz < NZ; ++dz)
-#pragma unroll
-        for (int dy = 0; dy < 2; ++dy)
-#pragma unroll
-            for (int dx = 0; dx < 2; ++dx) {
-                const int i = i0 + dx, j = j0 + dy;
-                const int64_t k = k0 + dz;
-                const int64_t p = pidx(g, i, j, k);
-                if (!is_black(i, j, k)) {
-                    if (STORE_RED) dst[p] = rv[dz][dy][dx];
-                    continue;
-                }
-                T s = new_red(i - 1, j, k) + new_red(i + 1, j, k);
-                s = s + new_red(i, j - 1, k);
-                s = s + new_red(i, j + 1, k);
-                if (DIM == 3) {
-                    s = s + new_red(i, j, k - 1);
-                    s = s + new_red(i, j, k + 1);
-                }
-                dst[p] = op.relax(s, f[p], nfaces(i, j, k));
-            }
-}
-
-template <typename T, int D>
-static void bres_t(void* u, const void* f, void* R, Geo g, Geo gc, double h, double cl, hipStream_t s)
-{
-    const int64_t items = (int64_t)(g.nx / 2) * (g.ny / 2) * (D == 3 ? g.nz / 2 : 1);
-    k_bres<T, D><<<nblk(items), kBlock, 0, s>>>((T*)u, (const T*)f, (T*)R, g, gc, make_op<T, D>(h, cl));
-}
-
 // ---- full-weighting restriction (build-defined option, north_star) ------------------------------
 //
 // The cell-centred adjoint of the linear prolongation (oracle: restrict_fw in mgp_oracle_impl.h): per
@@ -4611,46 +4425,6 @@ hipError_t launch_residual_restrict(int rb, int dim, const void* u, const void* 
     } else {
         if (dim == 3) rr_t<float, 3>(u, f, R, g, gc, h, cl, s);
         else rr_t<float, 2>(u, f, R, g, gc, h, cl, s);
-    }
-    return hipGetLastError();
-}
-
-bool bres_supported(int rb, const Geo& g) { return (rb == 4 || rb == 8) && g.nx >= 2 && g.ny >= 2; }
-
-template <typename T, int D>
-static void rbsweep_t(const void* src, const void* f, void* dst, Geo g, double h, double cl, bool store_red,
-                      hipStream_t s)
-{
-    const int64_t items = (int64_t)(g.nx / 2) * (g.ny / 2) * (D == 3 ? g.nz / 2 : 1);
-    const Op<T, D> op = make_op<T, D>(h, cl);
-    if (store_red) k_rbsweep<T, D, true><<<nblk(items), kBlock, 0, s>>>((const T*)src, (const T*)f, (T*)dst, g, op);
-    else k_rbsweep<T, D, false><<<nblk(items), kBlock, 0, s>>>((const T*)src, (const T*)f, (T*)dst, g, op);
-}
-
-hipError_t launch_rb_sweep(int rb, int dim, const void* src, const void* f, void* dst, Geo g, double h, double cl,
-                           bool store_red, hipStream_t s)
-{
-    if (!bres_supported(rb, g) || (dim == 3 && g.nz < 2) || src == dst) return hipErrorInvalidValue;
-    if (rb == 8) {
-        if (dim == 3) rbsweep_t<double, 3>(src, f, dst, g, h, cl, store_red, s);
-        else rbsweep_t<double, 2>(src, f, dst, g, h, cl, store_red, s);
-    } else {
-        if (dim == 3) rbsweep_t<float, 3>(src, f, dst, g, h, cl, store_red, s);
-        else rbsweep_t<float, 2>(src, f, dst, g, h, cl, store_red, s);
-    }
-    return hipGetLastError();
-}
-
-hipError_t launch_black_residual_restrict(int rb, int dim, void* u, const void* f, void* R, Geo g, Geo gc, double h,
-                                          double cl, hipStream_t s)
-{
-    if (!bres_supported(rb, g) || (dim == 3 && g.nz < 2)) return hipErrorInvalidValue;
-    if (rb == 8) {
-        if (dim == 3) bres_t<double, 3>(u, f, R, g, gc, h, cl, s);
-        else bres_t<double, 2>(u, f, R, g, gc, h, cl, s);
-    } else {
-        if (dim == 3) bres_t<float, 3>(u, f, R, g, gc, h, cl, s);
-        else bres_t<float, 2>(u, f, R, g, gc, h, cl, s);
     }
     return hipGetLastError();
 }
