@@ -19,6 +19,8 @@
 // order are k_half's / residual_at's / k_resrestrict's, so the results are bit-identical to the separate pieces.
 #include "mgp_device.h"
 
+#include <cstdlib>
+
 namespace mgp {
 namespace {
 
@@ -259,6 +261,304 @@ __global__ __launch_bounds__(kBlock) void k_rbsweep(const T* __restrict__ src, c
     }
 }
 
+// ---- vector forms: a thread owns N coarse cells along x (N packed cells of each fine row and colour) ----
+//
+// The fine rows of a thread's coarse cells I0 .. I0+N-1 (coarse row J, plane K) are rows j0 + dy, planes k0 + dz
+// (j0 = 2J, k0 = 2K) at packed m0 .. m0+N-1 (m0 = I0) of either colour half: one 16-byte vector each.  The colour's
+// x parity in a row is c ^ ((dy + dz) & 1) (block origins and z0 even), a compile-time constant once the loops over
+// dy / dz are unrolled, so every vector, its neighbours and the one x-edge cell outside the segment are static.  Row
+// vectors of rows / planes outside the box are zero (the reference's ghost 0).  Per 4 coarse cells k_bres_v loads
+// 24 red row vectors and 16 f vectors where the scalar form issued ~150 loads per coarse cell.
+template <typename T, int N, int DIM>
+struct VB {
+    const Geo& g;
+    const Op<T, DIM>& op;
+    int m0, j0;
+    int64_t k0;
+    __device__ __forceinline__ bool valid(int dz, int dy) const
+    {
+        const int j = j0 + dy;
+        if (j < 0 || j >= g.ny) return false;
+        if (DIM == 3) {
+            const int64_t k = k0 + dz;
+            return k >= 0 && k < g.nz;
+        }
+        return true;
+    }
+    __device__ __forceinline__ int64_t off(int dz, int dy, int c) const
+    {
+        return (k0 + dz) * g.P + c * g.H + (int64_t)(j0 + dy) * g.hw + m0;
+    }
+    __device__ __forceinline__ Vec<T, N> ld(const T* p, int dz, int dy, int c) const
+    {
+        return valid(dz, dy) ? vload<T, N>(p + off(dz, dy, c)) : vzero<T, N>();
+    }
+    // colour c's cell at packed m of row (dz, dy), 0 outside the box
+    __device__ __forceinline__ T lds(const T* p, int dz, int dy, int c, int m) const
+    {
+        return valid(dz, dy) && m >= 0 && m < g.hw ? p[off(dz, dy, c) - m0 + m] : (T)0;
+    }
+    __device__ __forceinline__ int nbyz(int dz, int dy) const
+    {
+        const int j = j0 + dy;
+        int n = (j == 0) + (j == g.ny - 1);
+        if (DIM == 3) {
+            const int64_t k = g.z0 + k0 + dz;
+            n += (k == 0) + (k == g.gnz - 1);
+        }
+        return n;
+    }
+    // relax the N cells (x parity o) of a row from the other colour: the row's own vector cen with the x-edge value
+    // outside it, rows y -+ 1 and planes z -+ 1 (k_half's half_store expression and order)
+    __device__ __forceinline__ Vec<T, N> relax_row(int o, const Vec<T, N>& cen, T edge, const Vec<T, N>& yl,
+                                                   const Vec<T, N>& yr, const Vec<T, N>& zl, const Vec<T, N>& zr,
+                                                   const Vec<T, N>& fv, int nbyz_) const
+    {
+        T d0, y0, d1, y1;
+        row_diag_fast(op, nbyz_, d0, y0, d1, y1);
+        Vec<T, N> out;
+#pragma unroll
+        for (int e = 0; e < N; ++e) {
+            const int i = 2 * (m0 + e) + o;
+            const T xl = o == 0 ? (e == 0 ? edge : cen.v[e - 1]) : cen.v[e];
+            const T xr = o == 0 ? cen.v[e] : (e == N - 1 ? edge : cen.v[e + 1]);
+            T s = xl + xr;
+            s = s + yl.v[e];
+            s = s + yr.v[e];
+            if (DIM == 3) {
+                s = s + zl.v[e];
+                s = s + zr.v[e];
+            }
+            const bool xf = i == 0 || i == g.nx - 1;
+            out.v[e] = div_rn(fv.v[e] - s * op.inv_hSq, xf ? d1 : d0, xf ? y1 : y0);
+        }
+        return out;
+    }
+    // the residuals f - (sum / h^2 + diag u) of the N cells (x parity o) of a row (k_resrestrict's expression)
+    __device__ __forceinline__ void residual_row(int o, const Vec<T, N>& cen, T edge, const Vec<T, N>& yl,
+                                                 const Vec<T, N>& yr, const Vec<T, N>& zl, const Vec<T, N>& zr,
+                                                 const Vec<T, N>& fv, const Vec<T, N>& uc, int nbyz_, T (&r)[N]) const
+    {
+        T d0, y0, d1, y1;
+        row_diag_fast(op, nbyz_, d0, y0, d1, y1);
+#pragma unroll
+        for (int e = 0; e < N; ++e) {
+            const int i = 2 * (m0 + e) + o;
+            const T xl = o == 0 ? (e == 0 ? edge : cen.v[e - 1]) : cen.v[e];
+            const T xr = o == 0 ? cen.v[e] : (e == N - 1 ? edge : cen.v[e + 1]);
+            T s = xl + xr;
+            s = s + yl.v[e];
+            s = s + yr.v[e];
+            if (DIM == 3) {
+                s = s + zl.v[e];
+                s = s + zr.v[e];
+            }
+            const bool xf = i == 0 || i == g.nx - 1;
+            const T askew = s * op.inv_hSq;
+            const T a_u = askew + (xf ? d1 : d0) * uc.v[e];
+            r[e] = fv.v[e] - a_u;
+        }
+    }
+    // the cell of colour x (x parity ox in row (dz, dy)) at packed me, relaxed from colour 1 - x read from p: the
+    // x-edge value just outside a row vector (0 outside the box)
+    __device__ __forceinline__ T edge_relax(const T* p, const T* f, int dz, int dy, int cx, int ox, int me) const
+    {
+        if (!valid(dz, dy) || me < 0 || me >= g.hw) return (T)0;
+        const int cy = cx ^ 1;
+        const int i = 2 * me + ox;
+        T s = lds(p, dz, dy, cy, ox == 0 ? me - 1 : me) + lds(p, dz, dy, cy, ox == 0 ? me : me + 1);
+        s = s + lds(p, dz, dy - 1, cy, me);
+        s = s + lds(p, dz, dy + 1, cy, me);
+        if (DIM == 3) {
+            s = s + lds(p, dz - 1, dy, cy, me);
+            s = s + lds(p, dz + 1, dy, cy, me);
+        }
+        return op.relax(s, f[off(dz, dy, cx) - m0 + me], nbyz(dz, dy) + (i == 0) + (i == g.nx - 1));
+    }
+};
+
+// rows (dz, dy) a thread reads of the colour its rows are relaxed from, and the rows it relaxes: the block rows
+// (dz, dy in 0..1) and the rows just outside the block in y and z whose cells neighbour the block's cells
+template <int DIM>
+__device__ constexpr bool vb_need_src(int dz, int dy)
+{
+    if (DIM == 2) return dz == 0 && dy >= -2 && dy <= 3;
+    return ((dz == 0 || dz == 1) && dy >= -2 && dy <= 3) || ((dz == -1 || dz == 2) && dy >= -1 && dy <= 2) ||
+           ((dz == -2 || dz == 3) && (dy == 0 || dy == 1));
+}
+template <int DIM>
+__device__ constexpr bool vb_need_mid(int dz, int dy)
+{
+    if (DIM == 2) return dz == 0 && dy >= -1 && dy <= 2;
+    return ((dz == 0 || dz == 1) && dy >= -1 && dy <= 2) || ((dz == -1 || dz == 2) && (dy == 0 || dy == 1));
+}
+
+template <typename T, int N, int DIM>
+__device__ __forceinline__ bool vb_coords(const Geo& g, int& m0, int& J, int64_t& K)
+{
+    constexpr int LN = N == 4 ? 2 : (N == 2 ? 1 : 0);
+    const int64_t it = (int64_t)xcd_remap(blockIdx.x, gridDim.x) * kBlock + threadIdx.x;
+    const int lgpr = (g.lx - 1) - LN;
+    const int cy = g.ny >> 1;
+    const int grp = (int)(it & ((1 << lgpr) - 1));
+    J = (int)((it >> lgpr) & (cy - 1));
+    K = DIM == 3 ? it >> (lgpr + g.ly - 1) : 0;
+    m0 = grp * N;
+    return DIM == 2 ? (it >> (lgpr + g.ly - 1)) == 0 : K < (g.nz >> 1);
+}
+
+#define VB_ZLO (DIM == 3 ? -2 : 0)
+#define VB_ZHI (DIM == 3 ? 3 : 0)
+#define VB_IDX(dz, dy) [(dz) - VB_ZLO][(dy) + 2]
+
+template <typename T, int N, int DIM>
+__global__ __launch_bounds__(kBlock) void k_bres_v(T* __restrict__ u, const T* __restrict__ f, T* __restrict__ R,
+                                                   Geo g, Geo gc, Op<T, DIM> op)
+{
+    int m0, J;
+    int64_t K;
+    if (!vb_coords<T, N, DIM>(g, m0, J, K)) return;
+    const VB<T, N, DIM> b{g, op, m0, 2 * J, DIM == 3 ? 2 * K : 0};
+    constexpr int NZ = DIM == 3 ? 2 : 1;
+    constexpr int ZS = VB_ZHI - VB_ZLO + 1;
+    Vec<T, N> rv[ZS][6], bv[ZS][6], fb[ZS][6];
+    T re[ZS][6];
+    // the red rows (final after the red half-sweep) and, for the rows relaxed below, their x-edge red cell
+#pragma unroll
+    for (int dz = VB_ZLO; dz <= VB_ZHI; ++dz)
+#pragma unroll
+        for (int dy = -2; dy <= 3; ++dy) {
+            if (!vb_need_src<DIM>(dz, dy)) continue;
+            rv VB_IDX(dz, dy) = b.ld(u, dz, dy, 0);
+            if (vb_need_mid<DIM>(dz, dy)) {
+                const int ob = 1 ^ ((dy + dz) & 1);  // x parity of the black cells
+                re VB_IDX(dz, dy) = b.lds(u, dz, dy, 0, ob == 0 ? m0 - 1 : m0 + N);
+                fb VB_IDX(dz, dy) = b.ld(f, dz, dy, 1);
+            }
+        }
+    // the black half-sweep on the block rows and the rows around the block
+#pragma unroll
+    for (int dz = VB_ZLO; dz <= VB_ZHI; ++dz)
+#pragma unroll
+        for (int dy = -2; dy <= 3; ++dy) {
+            if (!vb_need_mid<DIM>(dz, dy)) continue;
+            const int ob = 1 ^ ((dy + dz) & 1);
+            const Vec<T, N> z0v = vzero<T, N>();
+            bv VB_IDX(dz, dy) =
+                b.valid(dz, dy)
+                    ? b.relax_row(ob, rv VB_IDX(dz, dy), re VB_IDX(dz, dy), rv VB_IDX(dz, dy - 1), rv VB_IDX(dz, dy + 1),
+                                  DIM == 3 ? rv VB_IDX(dz - (DIM == 3), dy) : z0v,
+                                  DIM == 3 ? rv VB_IDX(dz + (DIM == 3), dy) : z0v, fb VB_IDX(dz, dy), b.nbyz(dz, dy))
+                    : z0v;
+        }
+    // residuals of the block rows, both colours, restricted in k_resrestrict's order
+    T acc[N];
+#pragma unroll
+    for (int dz = 0; dz < NZ; ++dz)
+#pragma unroll
+        for (int dy = 0; dy < 2; ++dy) {
+            const int ob = 1 ^ ((dy + dz) & 1), orr = ob ^ 1;
+            const int nb = b.nbyz(dz, dy);
+            const Vec<T, N> z0v = vzero<T, N>();
+            T rr[2][N], rb[N], rd[N];
+            // black cells: red neighbours (loaded), own value the new black
+            b.residual_row(ob, rv VB_IDX(dz, dy), re VB_IDX(dz, dy), rv VB_IDX(dz, dy - 1), rv VB_IDX(dz, dy + 1),
+                           DIM == 3 ? rv VB_IDX(dz - (DIM == 3), dy) : z0v, DIM == 3 ? rv VB_IDX(dz + (DIM == 3), dy) : z0v,
+                           fb VB_IDX(dz, dy), bv VB_IDX(dz, dy), nb, rb);
+            // red cells: black neighbours (new; the x-edge one recomputed), own value loaded
+            const T eb = b.edge_relax(u, f, dz, dy, 1, ob, orr == 0 ? m0 - 1 : m0 + N);
+            b.residual_row(orr, bv VB_IDX(dz, dy), eb, bv VB_IDX(dz, dy - 1), bv VB_IDX(dz, dy + 1),
+                           DIM == 3 ? bv VB_IDX(dz - (DIM == 3), dy) : z0v, DIM == 3 ? bv VB_IDX(dz + (DIM == 3), dy) : z0v,
+                           b.ld(f, dz, dy, 0), rv VB_IDX(dz, dy), nb, rd);
+#pragma unroll
+            for (int e = 0; e < N; ++e) {
+                rr[ob][e] = rb[e];
+                rr[orr][e] = rd[e];
+            }
+#pragma unroll
+            for (int e = 0; e < N; ++e) {
+                if (dz == 0 && dy == 0) {
+                    acc[e] = rr[0][e] + rr[1][e];
+                } else {
+                    acc[e] = acc[e] + rr[0][e];
+                    acc[e] = acc[e] + rr[1][e];
+                }
+            }
+        }
+    const int64_t gK = gc.z0 + K;
+    const int pc = (int)((J + gK) & 1);
+    const int64_t rowc = K * gc.P + (int64_t)J * gc.hw;
+#pragma unroll
+    for (int e = 0; e < N; ++e) {
+        const int I = m0 + e;
+        R[rowc + ((I + pc) & 1) * gc.H + (I >> 1)] = (DIM == 3 ? (T)0.125 : (T)0.25) * acc[e];
+    }
+#pragma unroll
+    for (int dz = 0; dz < NZ; ++dz)
+#pragma unroll
+        for (int dy = 0; dy < 2; ++dy) vstore<T, N>(u + b.off(dz, dy, 1), bv VB_IDX(dz, dy));
+}
+
+template <typename T, int N, int DIM, bool STORE_RED>
+__global__ __launch_bounds__(kBlock) void k_rbsweep_v(const T* __restrict__ src, const T* __restrict__ f,
+                                                      T* __restrict__ dst, Geo g, Op<T, DIM> op)
+{
+    int m0, J;
+    int64_t K;
+    if (!vb_coords<T, N, DIM>(g, m0, J, K)) return;
+    const VB<T, N, DIM> b{g, op, m0, 2 * J, DIM == 3 ? 2 * K : 0};
+    constexpr int NZ = DIM == 3 ? 2 : 1;
+    constexpr int ZS = VB_ZHI - VB_ZLO + 1;
+    Vec<T, N> bo[ZS][6], rn[ZS][6];
+    T be[ZS][6];
+    // the black rows (the sweep's input) and, for the rows whose red half is relaxed, their x-edge black cell
+#pragma unroll
+    for (int dz = VB_ZLO; dz <= VB_ZHI; ++dz)
+#pragma unroll
+        for (int dy = -2; dy <= 3; ++dy) {
+            if (!vb_need_src<DIM>(dz, dy)) continue;
+            bo VB_IDX(dz, dy) = b.ld(src, dz, dy, 1);
+            if (vb_need_mid<DIM>(dz, dy)) {
+                const int orr = (dy + dz) & 1;  // x parity of the red cells
+                be VB_IDX(dz, dy) = b.lds(src, dz, dy, 1, orr == 0 ? m0 - 1 : m0 + N);
+            }
+        }
+    // the red half-sweep on the block rows and the rows around the block
+#pragma unroll
+    for (int dz = VB_ZLO; dz <= VB_ZHI; ++dz)
+#pragma unroll
+        for (int dy = -2; dy <= 3; ++dy) {
+            if (!vb_need_mid<DIM>(dz, dy)) continue;
+            const int orr = (dy + dz) & 1;
+            const Vec<T, N> z0v = vzero<T, N>();
+            rn VB_IDX(dz, dy) =
+                b.valid(dz, dy)
+                    ? b.relax_row(orr, bo VB_IDX(dz, dy), be VB_IDX(dz, dy), bo VB_IDX(dz, dy - 1), bo VB_IDX(dz, dy + 1),
+                                  DIM == 3 ? bo VB_IDX(dz - (DIM == 3), dy) : z0v,
+                                  DIM == 3 ? bo VB_IDX(dz + (DIM == 3), dy) : z0v, b.ld(f, dz, dy, 0), b.nbyz(dz, dy))
+                    : z0v;
+        }
+    // the black half-sweep on the block rows
+#pragma unroll
+    for (int dz = 0; dz < NZ; ++dz)
+#pragma unroll
+        for (int dy = 0; dy < 2; ++dy) {
+            const int ob = 1 ^ ((dy + dz) & 1), orr = ob ^ 1;
+            const Vec<T, N> z0v = vzero<T, N>();
+            const T er = b.edge_relax(src, f, dz, dy, 0, orr, ob == 0 ? m0 - 1 : m0 + N);
+            const Vec<T, N> nb_ = b.relax_row(ob, rn VB_IDX(dz, dy), er, rn VB_IDX(dz, dy - 1), rn VB_IDX(dz, dy + 1),
+                                              DIM == 3 ? rn VB_IDX(dz - (DIM == 3), dy) : z0v,
+                                              DIM == 3 ? rn VB_IDX(dz + (DIM == 3), dy) : z0v, b.ld(f, dz, dy, 1),
+                                              b.nbyz(dz, dy));
+            vstore<T, N>(dst + b.off(dz, dy, 1), nb_);
+            if (STORE_RED) vstore<T, N>(dst + b.off(dz, dy, 0), rn VB_IDX(dz, dy));
+        }
+}
+
+#undef VB_IDX
+#undef VB_ZHI
+#undef VB_ZLO
+
 template <typename T, int D>
 unsigned blocks_of(const Geo& g)
 {
@@ -272,26 +572,58 @@ bool bres_supported(int rb, const Geo& g)
     return (rb == 4 || rb == 8) && g.nx >= 2 && g.ny >= 2 && (g.z0 & 1) == 0;
 }
 
+// cells per thread of the vector forms (MGP_BRES_VN, read once: 0 = the scalar forms, 1 / 2 / 4; default one 16-byte
+// vector) on levels whose half rows hold a whole number of them
+static int bres_vn(int rb, const Geo& g)
+{
+    static const int env = [] {
+        const char* v = std::getenv("MGP_BRES_VN");
+        return v ? std::atoi(v) : -1;
+    }();
+    int n = env < 0 ? 16 / (rb == 8 ? 8 : 4) : env;
+    if (n != 0 && n != 1 && n != 2 && n != 4) n = 16 / (rb == 8 ? 8 : 4);
+    while (n > 1 && g.hw % n) n >>= 1;
+    return n;
+}
+
+template <typename T, int D, int N>
+static void bres_v_t(void* u, const void* f, void* R, const Geo& g, const Geo& gc, double h, double cl, hipStream_t s)
+{
+    const int64_t items = (int64_t)(g.nx / 2 / N) * (g.ny / 2) * (D == 3 ? g.nz / 2 : 1);
+    k_bres_v<T, N, D><<<nblk(items), kBlock, 0, s>>>((T*)u, (const T*)f, (T*)R, g, gc, make_op<T, D>(h, cl));
+}
+
+template <typename T, int D>
+static void bres_t(void* u, const void* f, void* R, const Geo& g, const Geo& gc, double h, double cl, hipStream_t s)
+{
+    const int n = bres_vn(sizeof(T), g);
+    if (n == 4 && sizeof(T) == 4) bres_v_t<T, D, 4>(u, f, R, g, gc, h, cl, s);
+    else if (n >= 2) bres_v_t<T, D, 2>(u, f, R, g, gc, h, cl, s);
+    else if (n == 1) bres_v_t<T, D, 1>(u, f, R, g, gc, h, cl, s);
+    else k_bres<T, D><<<blocks_of<T, D>(g), kBlock, 0, s>>>((T*)u, (const T*)f, (T*)R, g, gc, make_op<T, D>(h, cl));
+}
+
 hipError_t launch_black_residual_restrict(int rb, int dim, void* u, const void* f, void* R, Geo g, Geo gc, double h,
                                           double cl, hipStream_t s)
 {
     if (!bres_supported(rb, g) || (dim == 3 && g.nz < 2)) return hipErrorInvalidValue;
     if (rb == 8) {
-        if (dim == 3)
-            k_bres<double, 3><<<blocks_of<double, 3>(g), kBlock, 0, s>>>((double*)u, (const double*)f, (double*)R, g, gc,
-                                                                          make_op<double, 3>(h, cl));
-        else
-            k_bres<double, 2><<<blocks_of<double, 2>(g), kBlock, 0, s>>>((double*)u, (const double*)f, (double*)R, g, gc,
-                                                                          make_op<double, 2>(h, cl));
+        if (dim == 3) bres_t<double, 3>(u, f, R, g, gc, h, cl, s);
+        else bres_t<double, 2>(u, f, R, g, gc, h, cl, s);
     } else {
-        if (dim == 3)
-            k_bres<float, 3><<<blocks_of<float, 3>(g), kBlock, 0, s>>>((float*)u, (const float*)f, (float*)R, g, gc,
-                                                                        make_op<float, 3>(h, cl));
-        else
-            k_bres<float, 2><<<blocks_of<float, 2>(g), kBlock, 0, s>>>((float*)u, (const float*)f, (float*)R, g, gc,
-                                                                        make_op<float, 2>(h, cl));
+        if (dim == 3) bres_t<float, 3>(u, f, R, g, gc, h, cl, s);
+        else bres_t<float, 2>(u, f, R, g, gc, h, cl, s);
     }
     return hipGetLastError();
+}
+
+template <typename T, int D, int N>
+static void rbsweep_v_t(const void* src, const void* f, void* dst, const Geo& g, const Op<T, D>& op, bool store_red,
+                        hipStream_t s)
+{
+    const int64_t items = (int64_t)(g.nx / 2 / N) * (g.ny / 2) * (D == 3 ? g.nz / 2 : 1);
+    if (store_red) k_rbsweep_v<T, N, D, true><<<nblk(items), kBlock, 0, s>>>((const T*)src, (const T*)f, (T*)dst, g, op);
+    else k_rbsweep_v<T, N, D, false><<<nblk(items), kBlock, 0, s>>>((const T*)src, (const T*)f, (T*)dst, g, op);
 }
 
 template <typename T, int D>
@@ -299,7 +631,11 @@ static void rbsweep_t(const void* src, const void* f, void* dst, Geo g, double h
                       hipStream_t s)
 {
     const Op<T, D> op = make_op<T, D>(h, cl);
-    if (store_red)
+    const int n = bres_vn(sizeof(T), g);
+    if (n == 4 && sizeof(T) == 4) rbsweep_v_t<T, D, 4>(src, f, dst, g, op, store_red, s);
+    else if (n >= 2) rbsweep_v_t<T, D, 2>(src, f, dst, g, op, store_red, s);
+    else if (n == 1) rbsweep_v_t<T, D, 1>(src, f, dst, g, op, store_red, s);
+    else if (store_red)
         k_rbsweep<T, D, true><<<blocks_of<T, D>(g), kBlock, 0, s>>>((const T*)src, (const T*)f, (T*)dst, g, op);
     else
         k_rbsweep<T, D, false><<<blocks_of<T, D>(g), kBlock, 0, s>>>((const T*)src, (const T*)f, (T*)dst, g, op);
