@@ -237,7 +237,10 @@ struct mgp_ctx {
     mgp::FusedTuning tu;   // tile settings of the temporally blocked phases (env, snapshot at creation)
     bool resfw = true;     // the full weighting's residual + restriction as one pass (MGP_RESFW=0: two passes)
     bool bres = true;      // the last pre black half-sweep fused with residual + restriction (MGP_BRES=0: apart)
-    bool rbsweep = true;   // whole red/black sweeps of levels below the finest in one pass (MGP_RBSWEEP=0: halves)
+    // whole red/black sweeps of levels below the finest in one pass (MGP_RBSWEEP=1; off by default: at 128^3 11.5 us
+    // per sweep against 10.4 for the k_half pair, round 6 — the recomputed edge cells double the VALU of a pass that
+    // is latency-bound at that size)
+    bool rbsweep = false;
     bool rccl1 = false;    // world 1 on a one-rank RCCL communicator (MGP_TRANSPORT=rccl, env_rccl1)
     // the multi-rank code path: a communicator (or the loopback transport), collectives, the side stream
     bool multi() const { return o.world > 1 || rccl1; }
@@ -1871,8 +1874,8 @@ static void host_setup(mgp_ctx* c, const mgp_opts& o, const std::vector<LevelPla
         c->resfw = !(vr && std::atoi(vr) == 0);
         const char* vbr = std::getenv("MGP_BRES");
         c->bres = !(vbr && std::atoi(vbr) == 0);
-        const char* vrs = std::getenv("MGP_RBSWEEP");
-        c->rbsweep = !(vrs && std::atoi(vrs) == 0);
+        const char* vrs = std::getenv("MGP_RBSWEEP");  // (measured slower, round 6: opt-in)
+        c->rbsweep = vrs && std::atoi(vrs) != 0;
     }
     // distributed 3D levels sweep with deep halos (smooth_deep): kGhostZs ghost planes per side
     if (c->deep_halo && o.dim == 3 && c->multi()) c->G = mgp::kGhostZs;

@@ -3,8 +3,9 @@
 - k_bres: the pre-smoothing's last black half-sweep + calcResidual + reduceResidual in one pass.  A red/black
   sweep's black half reads only red cells, so one pass can relax the black cells, form the residual of both
   colours and restrict it (cpu.lua:40-54 update, cpu.lua:108-135).
-- k_rbsweep: a whole red/black sweep in one out-of-place pass (u -> t, swapped), the red cells the black half
-  reads recomputed at the block edge; only the last sweep of a run stores its red cells.
+- k_rbsweep (opt-in, MGP_RBSWEEP=1: measured slower than the k_half pair): a whole red/black sweep in one
+  out-of-place pass (u -> t, swapped), the red cells the black half reads recomputed at the block edge; only the
+  last sweep of a run stores its red cells.
 Bar: psi bit-identical to the oracle and to the separate pieces (MGP_BRES=0 MGP_RBSWEEP=0) after whole cycles, on
 cubic / square / non-cubic boxes, fp32 / fp64, both coarse boundaries, V and F, fresh and warm coarse guesses, odd
 and even sweep counts; and single smoothing calls on levels 1 and 2 against the oracle's sweeps."""
@@ -36,6 +37,7 @@ def test_bres_cycles_match_oracle_and_pieces(cfg, monkeypatch):
     monkeypatch.setenv("MGP_TAIL", "0")  # every level below the finest runs its own pieces
     monkeypatch.setenv("MGP_BLK", "0")
     monkeypatch.setenv("MGP_FUSED", "0")
+    monkeypatch.setenv("MGP_RBSWEEP", "1")  # (opt-in: measured slower than the k_half pair)
     ctx = _ctx(**cfg)
     ctx.init_point_charge()
     monkeypatch.setenv("MGP_BRES", "0")
@@ -69,12 +71,13 @@ def test_bres_default_engines_512_box_levels():
 @pytest.mark.parametrize("dim,n", [(3, (32, 32, 32)), (3, (16, 32, 64)), (2, (128, 128, 1)), (2, (64, 16, 1))])
 @pytest.mark.parametrize("real", ["float", "double"])
 @pytest.mark.parametrize("level", [1, 2])
-def test_rbsweep_smoothing_calls_match_oracle(dim, n, real, level):
+def test_rbsweep_smoothing_calls_match_oracle(dim, n, real, level, monkeypatch):
     """mgp_smooth on a level below the finest runs k_rbsweep for every sweep (the last one stores both colours):
     1, 2 and 3 sweeps of random fields equal the oracle's red/black sweeps with the consistent boundary."""
     from oracle_lib import coarse_coef, smooth_arr
     from test_gpu_parity import REAL, _rand
 
+    monkeypatch.setenv("MGP_RBSWEEP", "1")
     ctx = _ctx(dim=dim, n=n, real=real, smoother="rbgs", nu1=2, nu2=2, coarse_bc="consistent")
     shp = ctx.shape(level)
     u = _rand(shp, REAL[real], 21)
