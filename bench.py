@@ -81,9 +81,8 @@ def parse(argv=None):
     p.add_argument("--cpu-cycles", type=int, default=4, help="oracle cycles timed for cpu_baseline (0 = skip)")
     p.add_argument("--cpu-threads", type=int, default=0,
                    help="threads of the OpenMP cpu_baseline (0 = OMP_NUM_THREADS or all host cores)")
-    p.add_argument("--traffic", default=",".join(os.path.join(ROOT, "profiles", f) for f in
-                                                 ("pmc_traffic_current.json", "pmc_traffic_slab4.json",
-                                                  "pmc_traffic_slab3.json")),
+    p.add_argument("--traffic", default=",".join(os.path.join(ROOT, "profiles", f"pmc_traffic_{w}.json") for w in
+                                                 ("current", "slab3", "slab4", "box2048", "fw", "2d", "2d64", "f64")),
                    help="comma list of JSONs with the PMC-measured HBM bytes per launch (tools/pmc_traffic.py); the "
                         "first one measured on this build, this workload (box, world, options) and the timed launch's "
                         "kernel and grid is used (pick_traffic)")

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Copy the end-of-round evidence in gpurun_out/ (tools/r05_final.sh) into profiles/
+"""Copy the end-of-round evidence in gpurun_out/ (tools/r06_final.sh) into profiles/
 under a round prefix and print the bench lines.
 
 usage: tools/install_evidence.py [prefix]   (default r03)
@@ -33,10 +33,12 @@ shutil.copy(G + "pmc_traffic.json", P + f"{pre}_pmc_traffic.json")
 shutil.copy(G + "pmc_traffic.json", P + "pmc_traffic_current.json")
 shutil.copy(G + "pmc_traffic.txt", P + f"{pre}_pmc_traffic_summary.txt")
 shutil.copy(G + "prof/run_kernel_stats.csv", P + f"{pre}_kernel_stats.csv")
-for slab in ("slab4", "slab3"):  # PMC traffic of the rank slabs (tools/r05_final.sh), read by bench.py's --traffic default
-    if os.path.exists(G + f"pmc_traffic_{slab}.json"):
-        shutil.copy(G + f"pmc_traffic_{slab}.json", P + f"pmc_traffic_{slab}.json")
-        shutil.copy(G + f"pmc_traffic_{slab}.txt", P + f"{pre}_pmc_traffic_{slab}_summary.txt")
+# PMC traffic of the other workloads (tools/r06_final.sh), each tagged with its workload key; read by bench.py's
+# --traffic default
+for w in ("slab4", "slab3", "box2048", "fw", "2d", "2d64", "f64"):
+    if os.path.exists(G + f"pmc_traffic_{w}.json"):
+        shutil.copy(G + f"pmc_traffic_{w}.json", P + f"pmc_traffic_{w}.json")
+        shutil.copy(G + f"pmc_traffic_{w}.txt", P + f"{pre}_pmc_traffic_{w}_summary.txt")
 if os.path.exists(G + "fetch_calib.json"):
     shutil.copy(G + "fetch_calib.json", P + f"{pre}_fetch_calib.json")
 if os.path.exists(G + "pytest_gpu.log") and os.path.exists(G + "smoke.log"):
@@ -53,9 +55,10 @@ if os.path.exists(G + "prof2d/run_kernel_stats.csv"):
     tool(["tools/trace_summary.py", G + "prof2d/run_kernel_trace.csv"], f"{pre}_2d_trace_summary.txt")
     tool(["tools/cycle_breakdown.py", G + "prof2d/run_kernel_trace.csv", "8"], f"{pre}_2d_cycle_breakdown.txt")
 
-if os.path.exists(G + "proffw/run_kernel_stats.csv"):  # the full-weighting 512^3 line (tools/r05_final.sh)
-    shutil.copy(G + "proffw/run_kernel_stats.csv", P + f"{pre}_fw_kernel_stats.csv")
-    tool(["tools/cycle_breakdown.py", G + "proffw/run_kernel_trace.csv", "8"], f"{pre}_fw_cycle_breakdown.txt")
+for w in ("fw", "f64"):  # one workload per trace: the full-weighting and fp64 512^3 lines
+    if os.path.exists(G + f"prof{w}/run_kernel_stats.csv"):
+        shutil.copy(G + f"prof{w}/run_kernel_stats.csv", P + f"{pre}_{w}_kernel_stats.csv")
+        tool(["tools/cycle_breakdown.py", G + f"prof{w}/run_kernel_trace.csv", "8"], f"{pre}_{w}_cycle_breakdown.txt")
 
 open(P + f"{pre}_bench.json", "w").write(last(G + "bench.log"))
 files = [f"{pre}_bench.json"]
