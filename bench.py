@@ -431,7 +431,8 @@ def run_workload(a, cfg, box, strong, rank, world, local, dist, steps, warmup, p
                 byt = sum(b * c for b, (_, c, _) in fin)
                 sec = sum(ms_ for _, (ms_, _, _) in fin) * 1e-3
                 line["finest_level_hbm_GBps"] = {
-                    "value": byt / sec / 1e9, "pmc_bytes": byt, "kernel_s": sec, "source": roof["traffic_source"],
+                    "value": byt / sec / 1e9, "pmc_bytes_per_cycle": byt / steps, "kernel_us_per_cycle": 1e6 * sec / steps,
+                    "source": roof["traffic_source"],
                     "definition": "PMC-measured HBM bytes (FETCH_SIZE x2 + WRITE_SIZE, tools/pmc_traffic.py) of the "
                                   "finest level's PRE and POST launches over their HIP-event time: bytes actually "
                                   "moved, bounded by 8 TB/s (finest_smoother_GBps is the per-sweep-equivalent figure)"}

@@ -1879,10 +1879,16 @@ static void host_setup(mgp_ctx* c, const mgp_opts& o, const std::vector<LevelPla
     }
     // distributed 3D levels sweep with deep halos (smooth_deep): kGhostZs ghost planes per side
     if (c->deep_halo && o.dim == 3 && c->multi()) c->G = mgp::kGhostZs;
+    // MGP_PLANE_PAD (bytes, a multiple of 16; experiment): the plane stride of 3D levels with planes of >= 2^16 slots
+    // is 2 H + pad instead of 2 H, so that equal cells of consecutive planes (which a z-streamed phase reads in the same
+    // step) no longer share their address bits below the plane size
+    const char* vpp = std::getenv("MGP_PLANE_PAD");
+    const int64_t plane_pad = vpp ? (std::max(0LL, std::atoll(vpp)) & ~15LL) / c->rb : 0;
     for (auto& p : plan) {
         Level L;
         L.p = p;
         L.g = make_geo(p, c->o.dim);
+        if (plane_pad && c->o.dim == 3 && L.g.P >= 65536) L.g.P += plane_pad;
         c->lev.push_back(L);
     }
     select_engines(c);

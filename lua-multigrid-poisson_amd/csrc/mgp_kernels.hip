@@ -36,16 +36,25 @@ namespace {
 
 // ---- init / pack / unpack -------------------------------------------------------------------
 
-// thread per packed slot: slot -> (k, c, j, m) -> i = 2m + (c ^ parity); i >= nx only when nx = 1
+// thread per packed slot: slot -> (k, c, j, m) -> i = 2m + (c ^ parity); i >= nx only when nx = 1.  A plane stride
+// beyond 2 H (MGP_PLANE_PAD) leaves pad slots after each plane's two halves: no cell (they stay 0)
 __device__ __forceinline__ bool slot_cell(int64_t s, const Geo& g, int& i, int& j, int64_t& k)
 {
-    const int m = (int)(s & (g.hw - 1));
-    j = (int)((s >> g.lhw) & (g.ny - 1));
-    const int c = (int)((s >> (g.lhw + g.ly)) & 1);
-    k = s >> (g.lhw + g.ly + 1);
+    int64_t r = s;
+    bool pad = false;
+    if (g.P == 2 * g.H) {
+        k = s >> (g.lhw + g.ly + 1);
+    } else {
+        k = s / g.P;
+        r = s - k * g.P;
+        pad = r >= 2 * g.H;
+    }
+    const int m = (int)(r & (g.hw - 1));
+    j = (int)((r >> g.lhw) & (g.ny - 1));
+    const int c = (int)((r >> (g.lhw + g.ly)) & 1);
     const int p = (int)((j + g.z0 + k) & 1);
     i = 2 * m + (c ^ p);
-    return i < g.nx;
+    return i < g.nx && !pad;
 }
 
 // Element-wise kernels over every packed slot of a level run grid-stride over at most kMaxBlocks
