@@ -121,7 +121,8 @@ def main():
         sub = run_workload(fa, make_cfg(fa, box, rank, world, local, None), box, strong, rank, world, local, dist,
                            a.ns_steps * 4, a.ns_warmup)
         line["fp64_line"] = {k: sub.get(k) for k in ("value", "unit", "ms_per_step", "steps", "warmup", "dtype", "config",
-                                                     "final_err", "relative_residual", "roofline", "finest_smoother_GBps")}
+                                                     "final_err", "relative_residual", "roofline", "finest_smoother_GBps",
+                                                     "finest_level_hbm_GBps")}
     if want_north_star(a, world):
         extra = {}
         for name, nbox, cyc, _ in NORTH_STAR:
@@ -139,7 +140,8 @@ def main():
             if rank == 0:
                 extra[name] = {k: sub.get(k) for k in ("value", "unit", "ms_per_step", "steps", "warmup", "config",
                                                        "final_err", "relative_residual", "hbm_used_GB_rank0",
-                                                       "roofline", "comm_per_rank", "finest_smoother_GBps")}
+                                                       "roofline", "comm_per_rank", "finest_smoother_GBps",
+                                                       "finest_level_hbm_GBps")}
                 if fit:
                     extra[name]["env"] = fit
         if rank == 0:
