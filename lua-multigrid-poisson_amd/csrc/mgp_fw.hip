@@ -37,18 +37,12 @@ struct FwShape {
 };
 
 // A thread's share of the staging of one u plane (both colours, cells X0-2 .. X0+TX+1, Y0-2 .. Y0+TY+1, zero outside
-// the box) and of f on the residual region (cells X0-1 .. X0+TX, Y0-1 .. Y0+TY), each as whole 16-byte vectors of one
-// colour's packed row (N cells; the vectors start at packed X0/2 - N, so every one is aligned and lies wholly inside or
-// outside the box), unpacked into LDS; and of the residual ring: fixed items, so the in-plane addressing is computed
-// once and each plane's loads are issued a step ahead of their use.  (Round 6: 4-byte gathers of u and of f per
-// residual cell before, 61.6 us at 256^3.)
-template <typename T, int DIM>
+// the box; runs of one colour's packed row per wave, coalesced) and of the residual ring: fixed items, so the
+// in-plane addressing is computed once and each plane's loads are issued a step ahead of their use.
+template <int DIM>
 struct FwItems {
     using S = FwShape<DIM>;
-    static constexpr int N = VN<T>::n;
-    static constexpr int MV = S::TX / (2 * N) + 2;                                  // vectors per colour row
-    static constexpr int NUV = 2 * S::UH * MV, IU = (NUV + S::NT - 1) / S::NT;     // u vectors per thread
-    static constexpr int NFV = 2 * S::RH * MV, IF = (NFV + S::NT - 1) / S::NT;     // f vectors per thread
+    static constexpr int NUI = 2 * S::UH * S::MW, IU = (NUI + S::NT - 1) / S::NT;  // u items per thread
     static constexpr int IR = (S::RSLOT + S::NT - 1) / S::NT;                      // r cells per thread
 };
 
@@ -58,12 +52,9 @@ __global__ __launch_bounds__(FwShape<DIM>::NT) void k_resfw(const T* __restrict_
                                                             int kc, int gz)
 {
     using S = FwShape<DIM>;
-    using I = FwItems<T, DIM>;
-    constexpr int N = I::N;
-    using VT = Vec<T, N>;
+    using I = FwItems<DIM>;
     __shared__ T us[S::NU][S::USLOT];
     __shared__ T rs[S::RSLOT];
-    __shared__ T fs[S::RSLOT];  // f of the plane being evaluated, on the residual region (0 outside the box)
     const int tid = threadIdx.x;
     const int tiles_x = g.nx / S::TX, tiles_y = g.ny / S::TY;
     const int b = xcd_remap(blockIdx.x, gridDim.x);
@@ -78,69 +69,57 @@ __global__ __launch_bounds__(FwShape<DIM>::NT) void k_resfw(const T* __restrict_
     const T wbx = Ic == 0 ? wf : w3, wcx = Ic == cx - 1 ? wf : w3;
     const T wby = Jc == 0 ? wf : w3, wcy = Jc == cy - 1 ? wf : w3;
 
-    // vector items of one colour's packed row (a staged row of u, or a residual row of f): in-plane packed offset
-    // (-1: outside the box, the row stays 0), the unpacked x of the vector's first cell minus its x parity, relative
-    // to the staged window, and that parity at even local planes (it flips with the plane)
-    auto vitem = [&](int q, int nv, int rows, int ylo, int xlo, int& off, int& xb, int& par0, int& row) {
-        const int mv = q % I::MV, c = (q / I::MV) & 1, jl = q / (2 * I::MV);
-        const int j = ylo + jl, m0 = X0 / 2 - N + N * mv;
-        par0 = (int)((c + j + g.z0) & 1);
-        const bool ok = q < nv && jl < rows && j >= 0 && j < g.ny && m0 >= 0 && m0 + N <= g.hw;
-        off = ok ? (int)(c * g.H + (int64_t)j * g.hw + m0) : -1;
-        xb = 2 * m0 - xlo;
-        row = q < nv ? jl : -1;
-    };
-    int uoff[I::IU], uxb[I::IU], upar[I::IU], urow[I::IU];
+    // u items: in-plane packed offset (colour c's row j at m) and the LDS cell of each of the two plane parities
+    // (the x parity of colour c's cells in row j flips with the plane); -1 = outside the box (stays 0)
+    int uoff[I::IU], ul0[I::IU], ul1[I::IU];
 #pragma unroll
-    for (int e = 0; e < I::IU; ++e) vitem(tid + e * S::NT, I::NUV, S::UH, Y0 - 2, X0 - 2, uoff[e], uxb[e], upar[e], urow[e]);
-    int foff[I::IF], fxb[I::IF], fpar[I::IF], frow[I::IF];
-#pragma unroll
-    for (int e = 0; e < I::IF; ++e) vitem(tid + e * S::NT, I::NFV, S::RH, Y0 - 1, X0 - 1, foff[e], fxb[e], fpar[e], frow[e]);
-    // r cells: box face count, inside the box
-    int fnb[I::IR];
-    bool rin[I::IR];
+    for (int e = 0; e < I::IU; ++e) {
+        const int q = tid + e * S::NT;
+        const int mm = q % S::MW, c = (q / S::MW) & 1, jl = q / (2 * S::MW);
+        const int j = Y0 - 2 + jl, m = X0 / 2 - 1 + mm;
+        const int par0 = (int)((c + j + g.z0) & 1);  // x parity of colour c's cells in row j at even local planes
+        const bool ok = q < I::NUI && j >= 0 && j < g.ny && m >= 0 && m < g.hw;
+        uoff[e] = ok ? (int)(c * g.H + (int64_t)j * g.hw + m) : -1;
+        const int i0 = 2 * m + par0, i1 = 2 * m + (par0 ^ 1);
+        ul0[e] = q < I::NUI && i0 - (X0 - 2) >= 0 && i0 - (X0 - 2) < S::UW ? jl * S::UW + i0 - (X0 - 2) : -1;
+        ul1[e] = q < I::NUI && i1 - (X0 - 2) >= 0 && i1 - (X0 - 2) < S::UW ? jl * S::UW + i1 - (X0 - 2) : -1;
+    }
+    // r cells: in-plane packed offset of f (colour parity of even local planes), box face count, inside the box
+    int foff[I::IR], fpar[I::IR], fnb[I::IR];
 #pragma unroll
     for (int e = 0; e < I::IR; ++e) {
         const int q = tid + e * S::NT;
         const int il = q % S::RW, jl = q / S::RW;
         const int i = X0 - 1 + il, j = Y0 - 1 + jl;
-        rin[e] = q < S::RSLOT && i >= 0 && i < g.nx && j >= 0 && j < g.ny;
+        const bool in = q < S::RSLOT && i >= 0 && i < g.nx && j >= 0 && j < g.ny;
+        foff[e] = in ? (int)((int64_t)j * g.hw + (i >> 1)) : -1;
+        fpar[e] = (int)((i + j + g.z0) & 1);
         fnb[e] = (i == 0) + (i == g.nx - 1) + (j == 0) + (j == g.ny - 1);
     }
-    auto uload = [&](VT (&v)[I::IU], int64_t k) {
+    auto uload = [&](T (&v)[I::IU], int64_t k) {
         const bool readable = DIM == 2 || (k >= -gz && k < g.nz + gz);
         const T* up = u + k * g.P;
 #pragma unroll
-        for (int e = 0; e < I::IU; ++e) v[e] = readable && uoff[e] >= 0 ? vload<T, N>(up + uoff[e]) : vzero<T, N>();
+        for (int e = 0; e < I::IU; ++e) v[e] = readable && uoff[e] >= 0 ? up[uoff[e]] : (T)0;
     };
-    // one staged vector into an unpacked LDS window of width w: cell n at x = xb + 2 n + parity (inside the window)
-    auto vstore_un = [&](T* dst, int w, const VT& v, int xb, int par, int row) {
-        if (row < 0) return;
+    auto ustore = [&](T* dst, const T (&v)[I::IU], int64_t k) {
+        const bool odd = ((k & 1) != 0);
 #pragma unroll
-        for (int n = 0; n < N; ++n) {
-            const int x = xb + 2 * n + par;
-            if (x >= 0 && x < w) dst[row * w + x] = v.v[n];
+        for (int e = 0; e < I::IU; ++e) {
+            const int x = odd ? ul1[e] : ul0[e];
+            if (x >= 0) dst[x] = v[e];
         }
     };
-    auto ustore = [&](T* dst, const VT (&v)[I::IU], int64_t k) {
-        const int kp = (int)(k & 1);
-#pragma unroll
-        for (int e = 0; e < I::IU; ++e) vstore_un(dst, S::UW, v[e], uxb[e], upar[e] ^ kp, urow[e]);
-    };
-    auto fload = [&](VT (&v)[I::IF], int64_t k) {
+    auto fload = [&](T (&v)[I::IR], int64_t k) {
         const int64_t gk = g.z0 + k;
         const bool kin = DIM == 2 || (gk >= 0 && gk < g.gnz);
         const T* fp = f + k * g.P;
-#pragma unroll
-        for (int e = 0; e < I::IF; ++e) v[e] = kin && foff[e] >= 0 ? vload<T, N>(fp + foff[e]) : vzero<T, N>();
-    };
-    auto fstore = [&](const VT (&v)[I::IF], int64_t k) {
         const int kp = (int)(k & 1);
 #pragma unroll
-        for (int e = 0; e < I::IF; ++e) vstore_un(fs, S::RW, v[e], fxb[e], fpar[e] ^ kp, frow[e]);
+        for (int e = 0; e < I::IR; ++e) v[e] = kin && foff[e] >= 0 ? fp[((fpar[e] ^ kp) * g.H) + foff[e]] : (T)0;
     };
     // r of local plane k on the tile and its one-cell ring into rs (0 outside the box), then my cell's `ay`
-    auto plane_ay = [&](int64_t k, const T* um, const T* uc, const T* up) -> T {
+    auto plane_ay = [&](int64_t k, const T* um, const T* uc, const T* up, const T (&fv)[I::IR]) -> T {
         const int64_t gk = g.z0 + k;
         const bool kin = DIM == 2 || (gk >= 0 && gk < g.gnz);
         const int nbz = DIM == 3 ? (gk == 0) + (gk == g.gnz - 1) : 0;
@@ -149,7 +128,7 @@ __global__ __launch_bounds__(FwShape<DIM>::NT) void k_resfw(const T* __restrict_
             const int q = tid + e * S::NT;
             if (q < S::RSLOT) {
                 T r = (T)0;
-                if (kin && rin[e]) {
+                if (kin && foff[e] >= 0) {
                     const int il = q % S::RW, jl = q / S::RW;
                     const int x = (jl + 1) * S::UW + (il + 1);  // in the staged planes
                     T sm = uc[x - 1] + uc[x + 1];
@@ -159,7 +138,7 @@ __global__ __launch_bounds__(FwShape<DIM>::NT) void k_resfw(const T* __restrict_
                         sm = sm + um[x];
                         sm = sm + up[x];
                     }
-                    r = op.residual(sm, fs[q], uc[x], fnb[e] + nbz);
+                    r = op.residual(sm, fv[e], uc[x], fnb[e] + nbz);
                 }
                 rs[q] = r;
             }
@@ -179,13 +158,12 @@ __global__ __launch_bounds__(FwShape<DIM>::NT) void k_resfw(const T* __restrict_
     };
     const T scale = DIM == 3 ? (T)(1.0 / 512.0) : (T)(1.0 / 64.0);
     if constexpr (DIM == 2) {
-        VT uv[I::IU], fv[I::IF];
+        T uv[I::IU], fv[I::IR];
         uload(uv, 0);
         fload(fv, 0);
         ustore(us[0], uv, 0);
-        fstore(fv, 0);
         __syncthreads();
-        const T ay = plane_ay(0, us[0], us[0], us[0]);
+        const T ay = plane_ay(0, us[0], us[0], us[0], fv);
         R[((Ic + Jc) & 1) * gc.H + (int64_t)Jc * gc.hw + (Ic >> 1)] = scale * ay;
         return;
     } else {
@@ -197,7 +175,7 @@ __global__ __launch_bounds__(FwShape<DIM>::NT) void k_resfw(const T* __restrict_
         // plane k + 1's u (loaded during step k - 1) goes into its slot at the top of step k, f of plane k was loaded
         // during step k - 1 as well (a prefetch distance of 2 with double buffers measured slower: 134 VGPRs, 3
         // workgroups per CU, 609 against 470 us at 512^3)
-        VT uv[I::IU], fv[I::IF];
+        T uv[I::IU], fv[I::IR], fn[I::IR];
         uload(uv, k0 - 1);
         ustore(slot(k0 - 1), uv, k0 - 1);
         uload(uv, k0);
@@ -208,15 +186,16 @@ __global__ __launch_bounds__(FwShape<DIM>::NT) void k_resfw(const T* __restrict_
         int K = K0;
         for (int64_t k = k0; k <= klast; ++k) {
             ustore(slot(k + 1), uv, k + 1);
-            fstore(fv, k);
             if (k + 2 <= klast + 1) uload(uv, k + 2);
-            if (k + 1 <= klast) fload(fv, k + 1);
+            if (k + 1 <= klast) fload(fn, k + 1);
             __syncthreads();
-            const T ay = plane_ay(k, slot(k - 1), slot(k), slot(k + 1));
+            const T ay = plane_ay(k, slot(k - 1), slot(k), slot(k + 1), fv);
             a0 = a1;
             a1 = a2;
             a2 = a3;
             a3 = ay;
+#pragma unroll
+            for (int e = 0; e < I::IR; ++e) fv[e] = fn[e];
             if (k == 2 * (int64_t)K + 2) {  // coarse plane K complete (fine planes 2K-1 .. 2K+2)
                 const int64_t gK = gc.z0 + K;
                 T az = a0;
