@@ -40,7 +40,7 @@ typedef enum mgp_status {
 
 /* cpu.lua:56-57 inPlaceIterativeSolver: Jacobi (cpu.lua:40-54), red/black GS (build-defined, the temporally blocked
  * engines), lexicographic in-place GS (cpu.lua:24-37 GaussSeidel, bit-identical hyperplane-ordered sweeps; one
- * rank's whole box, MGP_ARITH_REAL) */
+ * rank's whole box; with MGP_ARITH_DOUBLE cpu-raw.lua:22-32's GaussSeidel over float images) */
 enum { MGP_JACOBI = 0, MGP_RBGS = 1, MGP_GS_LEX = 2 };
 enum { MGP_CYCLE_V = 0, MGP_CYCLE_F = 1 };             /* twoGrid recursion (gamma 1) / F-cycle */
 enum { MGP_PROLONG_PC = 0, MGP_PROLONG_LINEAR = 1 };   /* cpu.lua:142-150 injection / (tri)linear */

@@ -100,16 +100,12 @@ int plan_levels(const mgp_opts& o, std::vector<LevelPlan>& out, std::string& err
         err = "unknown smoother";
         return MGP_ERR_ARG;
     }
-    // cpu.lua's lexicographic sweep is sequential along every axis, so it runs on one rank's whole box only; and
-    // cpu-raw.lua (the double-arithmetic float path) has no Gauss-Seidel
+    // cpu.lua's lexicographic sweep is sequential along every axis, so it runs on one rank's whole box only
     if (o.smoother == MGP_GS_LEX && (o.world > 1 || env_rccl1(o))) {
         err = "smoother MGP_GS_LEX (lexicographic, cpu.lua:24-37) is sequential across slabs: world 1 only";
         return MGP_ERR_ARG;
     }
-    if (o.smoother == MGP_GS_LEX && o.arith != MGP_ARITH_REAL) {
-        err = "smoother MGP_GS_LEX: arith MGP_ARITH_REAL only (cpu-raw.lua has no Gauss-Seidel)";
-        return MGP_ERR_ARG;
-    }
+
     if (o.cycle != MGP_CYCLE_V && o.cycle != MGP_CYCLE_F) { err = "unknown cycle"; return MGP_ERR_ARG; }
     if (o.prolong != MGP_PROLONG_PC && o.prolong != MGP_PROLONG_LINEAR) { err = "unknown prolong"; return MGP_ERR_ARG; }
     if (o.coarse_init != MGP_COARSE_FRESH && o.coarse_init != MGP_COARSE_WARM) { err = "unknown coarse_init"; return MGP_ERR_ARG; }
@@ -861,7 +857,7 @@ int smooth(mgp_ctx* c, int l, int sweeps, double h, bool want_err = false, bool 
         TRY(materialize_zero(c, L));
     for (int sw = 0; sw < sweeps; ++sw) {
         if (c->o.smoother == MGP_GS_LEX) {  // cpu.lua:24-37 in place (a replicated level: validated at creation)
-            HIP_TRY(c, mgp::launch_gslex_sweep(c->rb, c->o.dim, c->ui(L, L.u), c->ui(L, L.f), L.g, h, cl, c->s));
+            HIP_TRY(c, mgp::launch_gslex_sweep(c->rk, c->o.dim, c->ui(L, L.u), c->ui(L, L.f), L.g, h, cl, c->s));
             L.ghost_ok = !L.p.dist;
             L.ghost_zero = false;
             continue;

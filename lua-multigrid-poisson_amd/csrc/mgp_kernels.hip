@@ -5101,9 +5101,11 @@ constexpr int gsl_edge() { return DIM == 3 ? 8 : 32; }
 template <int DIM>
 constexpr int gsl_threads() { return DIM == 3 ? 512 : 1024; }
 
-template <typename T, int DIM>
+// C: the type the update is evaluated in (C = double with T = float: cpu-raw.lua's GaussSeidel under real = 'float',
+// cpu-raw.lua:22-32: LuaJIT doubles over the float image, rounded once at the store)
+template <typename T, int DIM, typename C = T>
 __global__ __launch_bounds__(gsl_threads<DIM>()) void k_gslex(T* __restrict__ u, const T* __restrict__ f, Geo g,
-                                                             Op<T, DIM> op, int S, int TX, int TY, int TZ)
+                                                             Op<C, DIM> op, int S, int TX, int TY, int TZ)
 {
     constexpr int E = gsl_edge<DIM>() + 2;
     __shared__ T s[DIM == 3 ? E * E * E : E * E];
@@ -5150,30 +5152,30 @@ __global__ __launch_bounds__(gsl_threads<DIM>()) void k_gslex(T* __restrict__ u,
     const int mys = lx + ly + lz;
     for (int st = 0; st <= last; ++st) {
         if (mine && mys == st) {
-            T sum = s[c - 1] + s[c + 1];  // ((((xl + xr) + yl) + yr) + zl) + zr, cpu.lua:28-33
-            sum = sum + s[c - E];
-            sum = sum + s[c + E];
+            C sum = (C)s[c - 1] + (C)s[c + 1];  // ((((xl + xr) + yl) + yr) + zl) + zr, cpu.lua:28-33
+            sum = sum + (C)s[c - E];
+            sum = sum + (C)s[c + E];
             if (DIM == 3) {
-                sum = sum + s[c - E * E];
-                sum = sum + s[c + E * E];
+                sum = sum + (C)s[c - E * E];
+                sum = sum + (C)s[c + E * E];
             }
-            s[c] = op.relax(sum, fc, nb);
+            s[c] = (T)op.relax(sum, (C)fc, nb);
         }
         __syncthreads();
     }
     if (mine) u[pidx(g, gi, gj, gk)] = s[c];
 }
 
-template <typename T, int D>
+template <typename T, int D, typename C = T>
 static hipError_t gslex_t(void* u, const void* f, Geo g, double h, double cl, hipStream_t st)
 {
     constexpr int B = gsl_edge<D>();
     const int TX = std::min(B, g.nx), TY = std::min(B, g.ny), TZ = D == 3 ? (int)std::min<int64_t>(B, g.nz) : 1;
     const int ntx = g.nx / TX, nty = g.ny / TY, ntz = D == 3 ? (int)(g.nz / TZ) : 1;
-    const Op<T, D> op = make_op<T, D>(h, cl);
+    const Op<C, D> op = make_op<C, D>(h, cl);
     const unsigned nb = (unsigned)(D == 3 ? ntx * nty : ntx);
     for (int S = 0; S < ntx + nty + ntz - 2; ++S) {
-        k_gslex<T, D><<<nb, gsl_threads<D>(), 0, st>>>((T*)u, (const T*)f, g, op, S, TX, TY, TZ);
+        k_gslex<T, D, C><<<nb, gsl_threads<D>(), 0, st>>>((T*)u, (const T*)f, g, op, S, TX, TY, TZ);
         const hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
@@ -5182,7 +5184,9 @@ static hipError_t gslex_t(void* u, const void* f, Geo g, double h, double cl, hi
 
 hipError_t launch_gslex_sweep(int rb, int dim, void* u, const void* f, Geo g, double h, double cl, hipStream_t s)
 {
-    if (rb != 4 && rb != 8) return hipErrorInvalidValue;  // real arithmetic only (cpu-raw.lua has no GS)
+    if (rb == kRealF32D)  // float image, double arithmetic (cpu-raw.lua:22-32 under real = 'float')
+        return dim == 3 ? gslex_t<float, 3, double>(u, f, g, h, cl, s) : gslex_t<float, 2, double>(u, f, g, h, cl, s);
+    if (rb != 4 && rb != 8) return hipErrorInvalidValue;
     if (dim == 3) return rb == 8 ? gslex_t<double, 3>(u, f, g, h, cl, s) : gslex_t<float, 3>(u, f, g, h, cl, s);
     return rb == 8 ? gslex_t<double, 2>(u, f, g, h, cl, s) : gslex_t<float, 2>(u, f, g, h, cl, s);
 }

@@ -166,13 +166,13 @@ def test_create_without_gpu_fails_loudly():
 
 
 def test_gs_lex_option_rules():
-    """The lexicographic GS (MGP_GS_LEX) plans on one rank's box (every level one launch per piece) and is refused
-    for a slab decomposition (it is sequential along z) and for cpu-raw.lua's double arithmetic (no GS there)."""
+    """The lexicographic GS (MGP_GS_LEX) plans on one rank's box (every level one launch per piece), also under
+    cpu-raw.lua's double arithmetic, and is refused for a slab decomposition (it is sequential along z)."""
     import mgpoisson as mg
 
     rows = mg.plan(mg.make_opts(dim=3, n=(32, 32, 32), smoother="gs_lex", nu1=2, nu2=2))
     assert all(r["engine"] == "piece" for r in rows)
     with pytest.raises(mg.MGPError, match="world 1 only"):
         mg.plan(mg.make_opts(dim=3, n=(32, 32, 64), smoother="gs_lex", rank=0, world=2, comm_id=b"\0" * 128))
-    with pytest.raises(mg.MGPError, match="ARITH_REAL"):
-        mg.plan(mg.make_opts(dim=2, n=(32, 32, 1), real="float", smoother="gs_lex", arith="double"))
+    # cpu-raw.lua's GaussSeidel (cpu-raw.lua:22-32) under real = 'float': float images, double arithmetic
+    assert len(mg.plan(mg.make_opts(dim=2, n=(32, 32, 1), real="float", smoother="gs_lex", arith="double"))) == 6

@@ -95,3 +95,28 @@ def test_cpu_lua_protocol_gauss_seidel():
     s.step()
     o2.step()
     assert np.array_equal(s.psi, o2.get(0))
+
+
+@pytest.mark.parametrize("dim,n", [(2, (64, 64, 1)), (2, (32, 16, 1)), (3, (16, 16, 16))])
+def test_gslex_cpu_raw_float_arithmetic(dim, n):
+    """cpu-raw.lua's own GaussSeidel (cpu-raw.lua:22-32) under real = 'float': float images, every update evaluated
+    in LuaJIT doubles and rounded once at the store (mgp_opts.arith = MGP_ARITH_DOUBLE): sweeps and whole cycles
+    bit-identical to the oracle's arith="double" mode, and different from gpu.lua's all-float arithmetic."""
+    kw = dict(dim=dim, n=n, real="float", smoother="gs_lex", nu1=7, nu2=7, coarse_init="warm")
+    ctx = _ctx(arith="double", **kw)
+    u = _rand(ctx.shape(0), np.float32, 31)
+    f = _rand(ctx.shape(0), np.float32, 32)
+    ctx.set_psi(u, 0)
+    ctx.set_f(f, 0)
+    ctx.smooth(0, 2)
+    ref = smooth_arr(dim, u.copy(), f, "gs_lex", 2, 1.0 / n[0], 0.0, arith="double")
+    assert np.array_equal(ctx.get_psi(0), ref)
+    assert not np.array_equal(ref, smooth_arr(dim, u.copy(), f, "gs_lex", 2, 1.0 / n[0], 0.0))
+    c2 = _ctx(arith="double", **kw)
+    c2.init_point_charge()
+    o = Oracle(arith="double", **kw)
+    o.init_point_charge()
+    for _ in range(2):
+        c2.cycle()
+        o.step()
+        assert np.array_equal(c2.get_psi(), o.get(0))
