@@ -3077,6 +3077,9 @@ template <typename T, int DIM>
 struct TailArgs {
     int nlev, nops, jacobi, zero0;  // zero0: level 0's u is a fresh zero guess (not read)
     int fw;                          // full-weighting restriction (TAIL_RR)
+    // bit l: the program reads level l's u / f before it writes them (copied in; the others start as 0), and writes
+    // level l's f (copied out; u is always copied out)  (tail_io_masks)
+    uint32_t in_u, in_f, out_f;
     int64_t off[kTailMaxLevels];     // element offset of the level's LDS region
     int64_t region[kTailMaxLevels];  // elements of one LDS array of the level (ghost planes included)
     T* u[kTailMaxLevels];            // global interior plane 0 of u / f
@@ -3104,8 +3107,8 @@ __global__ __launch_bounds__(tail_threads<T>()) void k_tail(const TailArgs<T, DI
         for (int64_t e = tid; e < a.region[l]; e += kTailThreads) {
             const int64_t ie = e - lo;
             const bool in = ie >= 0 && ie < n;
-            U[e] = in && !(l == 0 && a.zero0) ? a.u[l][ie] : (T)0;
-            F[e] = in ? a.f[l][ie] : (T)0;
+            U[e] = in && ((a.in_u >> l) & 1) ? a.u[l][ie] : (T)0;
+            F[e] = in && ((a.in_f >> l) & 1) ? a.f[l][ie] : (T)0;
             if (a.jacobi) U[e + 2 * a.region[l]] = (T)0;
         }
     }
@@ -3197,9 +3200,10 @@ __global__ __launch_bounds__(tail_threads<T>()) void k_tail(const TailArgs<T, DI
         const T* U = cur(l);
         const T* F = rhs(l);
         const int64_t n = a.g[l].nz * a.g[l].P;
+        const bool st_f = (a.out_f >> l) & 1;
         for (int64_t e = tid; e < n; e += kTailThreads) {
             a.u[l][e] = U[e];
-            a.f[l][e] = F[e];
+            if (st_f) a.f[l][e] = F[e];
         }
     }
 }
@@ -3271,15 +3275,42 @@ constexpr int tc_threads() { return sizeof(T) == 4 ? (DIM == 2 ? TC_THREADS_2D_F
 #ifndef TC_MAXL  // timing experiment: skip the ops of levels >= TC_MAXL (wrong results)
 #define TC_MAXL 16
 #endif
+// Levels of at most this many cells run on wave 0 alone, without workgroup barriers (build knob, 0: every level on the
+// workgroup).  Measured slower (round 6, interleaved A/B): 3D 512 / 64 cells +6 / +3 us per 512^3 cycle, 2D 1024 cells
+// +8 us, 256 cells neutral; a 16-wave barrier costs less than one wave walking a small level's cells alone.
+#ifndef TC_WAVE_CELLS_3D
+#define TC_WAVE_CELLS_3D 0
+#endif
+#ifndef TC_WAVE_CELLS_2D
+#define TC_WAVE_CELLS_2D 0
+#endif
+template <int DIM, int NX, int NY, int NZ>
+constexpr bool tc_wave_level()
+{
+    return TcLev<DIM, NX, NY, NZ>::CELLS <= (DIM == 3 ? TC_WAVE_CELLS_3D : TC_WAVE_CELLS_2D);
+}
+// The tail's phase boundary: a workgroup barrier, or on a level run by wave 0 alone its own ordering (the LDS accesses
+// of one wave are performed in issue order; the wavefront-scope fences keep the compiler from moving them across)
+template <bool WV>
+__device__ __forceinline__ void tc_sync()
+{
+    if constexpr (WV) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    } else {
+        __syncthreads();
+    }
+}
 
-template <typename T, int DIM, int NX, int NY, int NZ>
+template <typename T, int DIM, int NX, int NY, int NZ, int NTH = tc_threads<T, DIM>()>
 __device__ __forceinline__ void tc_half(T* U, const T* F, const Op<T, DIM>& op, int c, int tid)
 {
     using L = TcLev<DIM, NX, NY, NZ>;
     if constexpr (NX >= 2) {
         constexpr int HN = NX / 2, CNT = L::CELLS / 2;
 #pragma unroll
-        for (int q0 = 0; q0 < CNT; q0 += tc_threads<T, DIM>()) {
+        for (int q0 = 0; q0 < CNT; q0 += NTH) {
             const int q = q0 + tid;
             if (q < CNT) {
                 const int i2 = q % HN, j = (q / HN) % NY, k = DIM == 3 ? q / (HN * NY) : 0;
@@ -3297,7 +3328,7 @@ __device__ __forceinline__ void tc_half(T* U, const T* F, const Op<T, DIM>& op, 
         }
     } else {  // one cell per row: cell (0, j, k) has colour (j + k) & 1 (half_item's empty slot is skipped)
         constexpr int CNT = L::CELLS;
-        for (int q = tid; q < CNT; q += tc_threads<T, DIM>()) {
+        for (int q = tid; q < CNT; q += NTH) {
             const int j = q % NY, k = DIM == 3 ? q / NY : 0;
             if (((j + k) & 1) != c) continue;
             const int x = L::idx(0, j, k);
@@ -3328,14 +3359,14 @@ __device__ __forceinline__ T tc_res(const T* U, const T* F, const Op<T, DIM>& op
     return op.residual_idx(sm, F[x], U[x], L::nb(i, j, k));
 }
 
-template <typename T, int DIM, int NX, int NY, int NZ>
+template <typename T, int DIM, int NX, int NY, int NZ, int NTH = tc_threads<T, DIM>()>
 __device__ __forceinline__ void tc_rr(const T* U, const T* F, T* Fc, const Op<T, DIM>& op, int tid)
 {
     constexpr int MX = NX / 2, MY = NY / 2, MZ = DIM == 3 ? NZ / 2 : 1;
     using C = TcLev<DIM, MX, MY, MZ>;
     constexpr int CNT = C::CELLS;
     auto res = [&](int i, int j, int k) { return tc_res<T, DIM, NX, NY, NZ>(U, F, op, i, j, k); };
-    for (int q = tid; q < CNT; q += tc_threads<T, DIM>()) {
+    for (int q = tid; q < CNT; q += NTH) {
         const int I = q % MX, J = (q / MX) % MY, K = DIM == 3 ? q / (MX * MY) : 0;
         const int i = 2 * I, j = 2 * J, k = 2 * K;
         T sm = res(i, j, k) + res(i + 1, j, k);
@@ -3352,7 +3383,7 @@ __device__ __forceinline__ void tc_rr(const T* U, const T* F, T* Fc, const Op<T,
 }
 
 // tc_rr with the full-weighting restriction (fw_eval over the residuals of the 4^DIM fine cells)
-template <typename T, int DIM, int NX, int NY, int NZ>
+template <typename T, int DIM, int NX, int NY, int NZ, int NTH = tc_threads<T, DIM>()>
 __device__ __forceinline__ void tc_rr_fw(const T* U, const T* F, T* Fc, const Op<T, DIM>& op, T wf, int tid)
 {
     constexpr int MX = NX / 2, MY = NY / 2, MZ = DIM == 3 ? NZ / 2 : 1;
@@ -3366,7 +3397,7 @@ __device__ __forceinline__ void tc_rr_fw(const T* U, const T* F, T* Fc, const Op
     gc.ny = MY;
     gc.gnz = MZ;
     auto res = [&](int i, int j, int64_t k64) { return tc_res<T, DIM, NX, NY, NZ>(U, F, op, i, j, (int)k64); };
-    for (int q = tid; q < CNT; q += tc_threads<T, DIM>()) {
+    for (int q = tid; q < CNT; q += NTH) {
         const int I = q % MX, J = (q / MX) % MY, K = DIM == 3 ? q / (MX * MY) : 0;
         Fc[C::idx(I, J, K)] = fw_eval<T, DIM>(res, g, gc, wf, I, J, (int64_t)K);
     }
@@ -3375,17 +3406,17 @@ __device__ __forceinline__ void tc_rr_fw(const T* U, const T* F, T* Fc, const Op
 // tc_rr_fw through a residual scratch: r of every cell of the level into RS (the level's unpacked layout) once, then
 // the full weighting of each coarse cell from RS (tc_rr_fw evaluates each fine residual for all 8 coarse cells that
 // weight it: 64 residuals per coarse cell, the FW tail's extra 27 us per 512^3 cycle)
-template <typename T, int DIM, int NX, int NY, int NZ>
+template <typename T, int DIM, int NX, int NY, int NZ, int NTH = tc_threads<T, DIM>()>
 __device__ __forceinline__ void tc_rr_fw_s(const T* U, const T* F, T* Fc, const Op<T, DIM>& op, T wf, int tid, T* RS)
 {
     using L = TcLev<DIM, NX, NY, NZ>;
     constexpr int MX = NX / 2, MY = NY / 2, MZ = DIM == 3 ? NZ / 2 : 1;
     using C = TcLev<DIM, MX, MY, MZ>;
-    for (int q = tid; q < L::CELLS; q += tc_threads<T, DIM>()) {
+    for (int q = tid; q < L::CELLS; q += NTH) {
         const int i = q % NX, j = (q / NX) % NY, k = DIM == 3 ? q / (NX * NY) : 0;
         RS[L::idx(i, j, k)] = tc_res<T, DIM, NX, NY, NZ>(U, F, op, i, j, k);
     }
-    __syncthreads();
+    tc_sync<(NTH < tc_threads<T, DIM>())>();
     Geo g{}, gc{};
     g.nx = NX;
     g.ny = NY;
@@ -3394,13 +3425,13 @@ __device__ __forceinline__ void tc_rr_fw_s(const T* U, const T* F, T* Fc, const 
     gc.ny = MY;
     gc.gnz = MZ;
     auto get = [&](int i, int j, int64_t k) { return RS[L::idx(i, j, (int)k)]; };
-    for (int q = tid; q < C::CELLS; q += tc_threads<T, DIM>()) {
+    for (int q = tid; q < C::CELLS; q += NTH) {
         const int I = q % MX, J = (q / MX) % MY, K = DIM == 3 ? q / (MX * MY) : 0;
         Fc[C::idx(I, J, K)] = fw_eval<T, DIM>(get, g, gc, wf, I, J, (int64_t)K);
     }
 }
 
-template <typename T, int DIM, int NX, int NY, int NZ, int LINEAR>
+template <typename T, int DIM, int NX, int NY, int NZ, int LINEAR, int NTH = tc_threads<T, DIM>()>
 __device__ __forceinline__ void tc_prolong(T* U, const T* V, T cl, int tid)
 {
     using L = TcLev<DIM, NX, NY, NZ>;
@@ -3408,7 +3439,7 @@ __device__ __forceinline__ void tc_prolong(T* U, const T* V, T cl, int tid)
     using C = TcLev<DIM, MX, MY, MZ>;
     constexpr int CNT = L::CELLS;
 #pragma unroll 1
-    for (int q0 = 0; q0 < CNT; q0 += tc_threads<T, DIM>()) {
+    for (int q0 = 0; q0 < CNT; q0 += NTH) {
         const int q = q0 + tid;
         if (q < CNT) {
             const int i = q % NX, j = (q / NX) % NY, k = DIM == 3 ? q / (NX * NY) : 0;
@@ -3463,10 +3494,11 @@ __device__ __forceinline__ int64_t tc_global(int q)
     return inside ? (int64_t)k * P + ((i + j + k) & 1) * H + (int64_t)j * HW + (i >> 1) : -1;
 }
 
-// level l of the tail: copy in (zero halo; zero_u: a fresh guess) or out, packed global layout; a
-// thread's loads are all issued before its LDS stores (compile-time trip count)
+// level l of the tail: copy in (zero halo; a field the program writes before it reads it is not loaded: ld_u / ld_f
+// false, zero) or out (f only where the program wrote it: st_f), packed global layout; a thread's loads are all issued
+// before its LDS stores (compile-time trip count)
 template <typename T, int DIM, int NX, int NY, int NZ>
-__device__ __forceinline__ void tc_copy(T* U, T* F, T* gu, T* gf, bool in, bool zero_u, int tid)
+__device__ __forceinline__ void tc_copy(T* U, T* F, T* gu, T* gf, bool in, bool ld_u, bool ld_f, bool st_f, int tid)
 {
     using L = TcLev<DIM, NX, NY, NZ>;
     constexpr int IT = (L::P + tc_threads<T, DIM>() - 1) / tc_threads<T, DIM>();
@@ -3476,11 +3508,11 @@ __device__ __forceinline__ void tc_copy(T* U, T* F, T* gu, T* gf, bool in, bool 
         const int q = tid + r * tc_threads<T, DIM>();
         const int64_t gi = tc_global<DIM, NX, NY, NZ>(q);
         if (in) {
-            uv[r] = gi >= 0 && !zero_u ? gu[gi] : (T)0;
-            fv[r] = gi >= 0 ? gf[gi] : (T)0;
+            uv[r] = gi >= 0 && ld_u ? gu[gi] : (T)0;
+            fv[r] = gi >= 0 && ld_f ? gf[gi] : (T)0;
         } else if (gi >= 0) {
             gu[gi] = U[q];
-            gf[gi] = F[q];
+            if (st_f) gf[gi] = F[q];
         }
     }
     if (in) {
@@ -3503,13 +3535,14 @@ struct TcRegs {
     T u[IT], f[IT];
 };
 template <typename T, int DIM, int NX, int NY, int NZ>
-__device__ __forceinline__ void tc_load(TcRegs<T, DIM, NX, NY, NZ>& rg, const T* gu, const T* gf, bool zero_u, int tid)
+__device__ __forceinline__ void tc_load(TcRegs<T, DIM, NX, NY, NZ>& rg, const T* gu, const T* gf, bool ld_u, bool ld_f,
+                                        int tid)
 {
 #pragma unroll
     for (int r = 0; r < TcRegs<T, DIM, NX, NY, NZ>::IT; ++r) {
         const int64_t gi = tc_global<DIM, NX, NY, NZ>(tid + r * tc_threads<T, DIM>());
-        rg.u[r] = gi >= 0 && !zero_u ? gu[gi] : (T)0;
-        rg.f[r] = gi >= 0 ? gf[gi] : (T)0;
+        rg.u[r] = gi >= 0 && ld_u ? gu[gi] : (T)0;
+        rg.f[r] = gi >= 0 && ld_f ? gf[gi] : (T)0;
     }
 }
 template <typename T, int DIM, int NX, int NY, int NZ>
@@ -3544,12 +3577,13 @@ __global__ __launch_bounds__((tc_threads<T, DIM>())) void k_tail_c(const TailArg
 #define TC_SH(l) TC_NX(l), TC_NY(l), TC_NZ(l)
 #define TC_U(l) (lds + tc_off<DIM, TX, TY, TZ>(l))
 #define TC_F(l) (lds + tc_off<DIM, TX, TY, TZ>(l) + TcLev<DIM, TC_SH(l)>::P)
-#define TC_COPY(l, IN)                                                                                        \
-    if constexpr ((l) < NL) tc_copy<T, DIM, TC_SH(l)>(TC_U(l), TC_F(l), a.u[l], a.f[l], IN, IN && (l) == 0 && a.zero0, \
+#define TC_COPY(l, IN)                                                                                      \
+    if constexpr ((l) < NL) tc_copy<T, DIM, TC_SH(l)>(TC_U(l), TC_F(l), a.u[l], a.f[l], IN, (a.in_u >> (l)) & 1,     \
+                                                      (a.in_f >> (l)) & 1, (a.out_f >> (l)) & 1, threadIdx.x);
+#define TC_LOAD(l)                                                                                          \
+    TcRegs<T, DIM, TC_SH(l)> rg##l;                                                                         \
+    if constexpr ((l) < NL) tc_load<T, DIM, TC_SH(l)>(rg##l, a.u[l], a.f[l], (a.in_u >> (l)) & 1, (a.in_f >> (l)) & 1, \
                                                       threadIdx.x);
-#define TC_LOAD(l)                         \
-    TcRegs<T, DIM, TC_SH(l)> rg##l;        \
-    if constexpr ((l) < NL) tc_load<T, DIM, TC_SH(l)>(rg##l, a.u[l], a.f[l], (l) == 0 && a.zero0, threadIdx.x);
 #define TC_STORE(l) \
     if constexpr ((l) < NL) tc_store<T, DIM, TC_SH(l)>(TC_U(l), TC_F(l), rg##l, threadIdx.x);
     if constexpr (DIM == 2) {  // (3D: the held values push the kernel past 64 VGPRs into spills; level by level)
@@ -3566,6 +3600,7 @@ __global__ __launch_bounds__((tc_threads<T, DIM>())) void k_tail_c(const TailArg
     __shared__ long long tcp[130];
     if (threadIdx.x == 0) tcp[0] = wall_clock64();
 #endif
+    bool wave_prev = false;  // the last op ran on wave 0 alone (the same on every wave)
     for (int pc = 0; pc < a.nops; ++pc) {
         const uint32_t w = a.ops[pc];
         const int op = (int)(w & 15), l = (int)((w >> 4) & 15), arg = (int)(w >> 8);
@@ -3577,32 +3612,42 @@ __global__ __launch_bounds__((tc_threads<T, DIM>())) void k_tail_c(const TailArg
     case L:                                                                                            \
         if constexpr ((L) < NL && (L) < TC_MAXL) {                                                     \
             using LV = TcLev<DIM, TC_SH(L)>;                                                           \
+            /* a small level runs on wave 0 alone (the other waves skip to the next workgroup-wide op) */ \
+            constexpr bool WV = tc_wave_level<DIM, TC_SH(L)>() && tc_threads<T, DIM>() > 64;          \
+            constexpr int NTH = WV ? 64 : tc_threads<T, DIM>();                                        \
+            if constexpr (WV) {                                                                        \
+                wave_prev = true;                                                                      \
+                if (tid >= 64) break;                                                                  \
+            } else {                                                                                   \
+                if (wave_prev) __syncthreads();                                                        \
+                wave_prev = false;                                                                     \
+            }                                                                                          \
             if (op == TAIL_SMOOTH) {                                                                   \
                 for (int sw = 0; sw < arg; ++sw) {                                                     \
-                    tc_half<T, DIM, TC_SH(L)>(TC_U(L), TC_F(L), sop[L], 0, tid);                       \
-                    __syncthreads();                                                                   \
+                    tc_half<T, DIM, TC_SH(L), NTH>(TC_U(L), TC_F(L), sop[L], 0, tid);                  \
+                    tc_sync<WV>();                                                                     \
                     if (LV::CELLS >= 2) {                                                              \
-                        tc_half<T, DIM, TC_SH(L)>(TC_U(L), TC_F(L), sop[L], 1, tid);                   \
-                        __syncthreads();                                                               \
+                        tc_half<T, DIM, TC_SH(L), NTH>(TC_U(L), TC_F(L), sop[L], 1, tid);              \
+                        tc_sync<WV>();                                                                 \
                     }                                                                                  \
                 }                                                                                      \
             } else if (op == TAIL_ZERO) {                                                              \
                 T* u = TC_U(L);                                                                        \
                 constexpr int NXL = TC_NX(L), NYL = TC_NY(L);                                          \
-                for (int q = tid; q < LV::CELLS; q += tc_threads<T, DIM>())                                      \
+                for (int q = tid; q < LV::CELLS; q += NTH)                                             \
                     u[LV::idx(q % NXL, (q / NXL) % NYL, DIM == 3 ? q / (NXL * NYL) : 0)] = (T)0;       \
-                __syncthreads();                                                                       \
+                tc_sync<WV>();                                                                         \
             } else if constexpr ((L) + 1 < NL) {                                                       \
                 if (op == TAIL_RR) {                                                                   \
                     if (a.fw) {                                                                        \
                         if constexpr (FWR)                                                             \
-                            tc_rr_fw_s<T, DIM, TC_SH(L)>(TC_U(L), TC_F(L), TC_F((L) + 1), sop[L],          \
-                                                         (T)3 - sop[(L) + 1].cl, tid, lds + FWR_OFF);      \
+                            tc_rr_fw_s<T, DIM, TC_SH(L), NTH>(TC_U(L), TC_F(L), TC_F((L) + 1), sop[L],     \
+                                                              (T)3 - sop[(L) + 1].cl, tid, lds + FWR_OFF); \
                         else                                                                           \
-                            tc_rr_fw<T, DIM, TC_SH(L)>(TC_U(L), TC_F(L), TC_F((L) + 1), sop[L],            \
-                                                       (T)3 - sop[(L) + 1].cl, tid);                      \
+                            tc_rr_fw<T, DIM, TC_SH(L), NTH>(TC_U(L), TC_F(L), TC_F((L) + 1), sop[L],       \
+                                                            (T)3 - sop[(L) + 1].cl, tid);                 \
                     } else                                                                             \
-                        tc_rr<T, DIM, TC_SH(L)>(TC_U(L), TC_F(L), TC_F((L) + 1), sop[L], tid);         \
+                        tc_rr<T, DIM, TC_SH(L), NTH>(TC_U(L), TC_F(L), TC_F((L) + 1), sop[L], tid);    \
                     /* a fresh guess of the next level (its ZERO op follows) in the same phase: RR writes */ \
                     /* that level's f, ZERO its u                                                        */ \
                     const uint32_t wn = pc + 1 < a.nops ? a.ops[pc + 1] : 0u;                          \
@@ -3610,14 +3655,14 @@ __global__ __launch_bounds__((tc_threads<T, DIM>())) void k_tail_c(const TailArg
                         using CV = TcLev<DIM, TC_SH((L) + 1)>;                                         \
                         constexpr int MX = TC_NX((L) + 1), MY = TC_NY((L) + 1);                        \
                         T* uc = TC_U((L) + 1);                                                         \
-                        for (int q = tid; q < CV::CELLS; q += tc_threads<T, DIM>())                              \
+                        for (int q = tid; q < CV::CELLS; q += NTH)                                     \
                             uc[CV::idx(q % MX, (q / MX) % MY, DIM == 3 ? q / (MX * MY) : 0)] = (T)0;   \
                         ++pc;                                                                          \
                     }                                                                                  \
-                    __syncthreads();                                                                   \
+                    tc_sync<WV>();                                                                     \
                 } else if (op == TAIL_PROLONG) {                                                       \
-                    tc_prolong<T, DIM, TC_SH(L), LINEAR>(TC_U(L), TC_U((L) + 1), sop[(L) + 1].cl, tid); \
-                    __syncthreads();                                                                   \
+                    tc_prolong<T, DIM, TC_SH(L), LINEAR, NTH>(TC_U(L), TC_U((L) + 1), sop[(L) + 1].cl, tid); \
+                    tc_sync<WV>();                                                                     \
                 }                                                                                      \
             }                                                                                          \
         }                                                                                              \
@@ -3656,6 +3701,7 @@ __global__ __launch_bounds__((tc_threads<T, DIM>())) void k_tail_c(const TailArg
     }
     __syncthreads();
 #endif
+    if (wave_prev) __syncthreads();
     TC_COPY(0, false) TC_COPY(1, false) TC_COPY(2, false) TC_COPY(3, false) TC_COPY(4, false) TC_COPY(5, false)
     TC_COPY(6, false)
 #undef TC_COPY
@@ -4902,6 +4948,36 @@ static int tail_shape(const TailSpec& t, int dim)
     return found;
 }
 
+// Which fields a tail program reads before writing them (in_u / in_f, bit l = level l: only those are loaded into
+// LDS) and which f it writes (out_f: only those are stored back; u is always stored).  A V- or F-cycle tail reads
+// level 0's f (and its u unless it is a fresh guess); every level below gets its f from the restriction and, with
+// fresh coarse guesses, its u from the zeroing before anything reads them.
+static void tail_io_masks(const TailSpec& t, uint32_t& in_u, uint32_t& in_f, uint32_t& out_f)
+{
+    uint32_t wu = t.zero_first ? 1u : 0u, wf = 0;
+    in_u = in_f = 0;
+    auto rd = [&](int l) {
+        if (!((wu >> l) & 1)) in_u |= 1u << l;
+        if (!((wf >> l) & 1)) in_f |= 1u << l;
+    };
+    for (int i = 0; i < t.nops; ++i) {
+        const uint32_t w = t.ops[i];
+        const int op = (int)(w & 15), l = (int)((w >> 4) & 15);
+        if (op == TAIL_SMOOTH) {
+            rd(l);
+        } else if (op == TAIL_RR) {
+            rd(l);
+            wf |= 1u << (l + 1);
+        } else if (op == TAIL_ZERO) {
+            wu |= 1u << l;
+        } else if (op == TAIL_PROLONG) {
+            if (!((wu >> (l + 1)) & 1)) in_u |= 1u << (l + 1);
+            if (!((wu >> l) & 1)) in_u |= 1u << l;
+        }
+    }
+    out_f = wf;
+}
+
 template <typename T, int D>
 static hipError_t tail_t(const TailSpec& t, hipStream_t s)
 {
@@ -4911,6 +4987,7 @@ static hipError_t tail_t(const TailSpec& t, hipStream_t s)
     a.jacobi = t.jacobi;
     a.zero0 = t.zero_first;
     a.fw = t.fw;
+    tail_io_masks(t, a.in_u, a.in_f, a.out_f);
     const int G = D == 3 ? kGhost3D : 0;
     int64_t off = 0;
     for (int l = 0; l < t.nlev; ++l) {
