@@ -237,6 +237,8 @@ struct mgp_ctx {
     // per sweep against 10.4 for the k_half pair, round 6 — the recomputed edge cells double the VALU of a pass that
     // is latency-bound at that size)
     bool rbsweep = false;
+    // PRE of two consecutive small 2D levels in one launch (k_blk2_pre; MGP_BLK2=0: one k_blk launch per level)
+    bool blk2 = true;
     bool rccl1 = false;    // world 1 on a one-rank RCCL communicator (MGP_TRANSPORT=rccl, env_rccl1)
     // the multi-rank code path: a communicator (or the loopback transport), collectives, the side stream
     bool multi() const { return o.world > 1 || rccl1; }
@@ -1343,6 +1345,100 @@ int block_pre(mgp_ctx* c, int l, double h)
     return MGP_OK;
 }
 
+// block_pre(l), the fresh guess of l + 1 and block_pre(l + 1) as one launch (k_blk2_pre): two consecutive k_blk 2D
+// levels of a V-cycle (average restriction, fp32; the tile divides level l + 1).  The state afterwards is the same as
+// after the three steps: u of both levels smoothed (black cells), f of l + 1 and l + 2 restricted.
+// block_post(l + 1) and block_post(l) likewise (k_blk2_post).  Both pair level l with l + 1 in the V-cycle part of a
+// cycle (cycle_rec with fcycle false).
+bool pair2_ok(const mgp_ctx* c, int l, double h, bool fcycle, int ns)
+{
+    const int last = (int)c->lev.size() - 1;
+    if (!c->blk2 || fcycle || l + 2 > last || c->rk != 4 || c->o.dim != 2 || c->o.smoother != MGP_RBGS) return false;
+    if (l + 1 == c->tail_level || l + 1 == c->handoff_level || h != level_h(c, l)) return false;
+    const Level &L = c->lev[l], &C = c->lev[l + 1], &D = c->lev[l + 2];
+    if (!L.blk || !C.blk || L.fused || C.fused || L.p.dist || C.p.dist || D.p.dist) return false;
+    return mgp::block2_supported(c->rb, c->o.dim, ns, L.g, C.g, D.g);
+}
+bool pre2_ok(const mgp_ctx* c, int l, double h, bool fcycle)
+{
+    return c->o.restriction != MGP_RESTRICT_FULL_WEIGHTING && pair2_ok(c, l, h, fcycle, c->o.nu1);
+}
+bool post2_ok(const mgp_ctx* c, int l, double h, bool fcycle) { return pair2_ok(c, l, h, fcycle, c->o.nu2); }
+
+int block_pre2(mgp_ctx* c, int l, double h)
+{
+    Level& L = c->lev[l];
+    Level& C = c->lev[l + 1];
+    Level& D = c->lev[l + 2];
+    int64_t zc = 0, zc2 = 0;
+    mgp::Block2Args a{};
+    a.pre = true;
+    a.ns = c->o.nu1;
+    a.src = L.zero_pending ? nullptr : c->ui(L, L.u);
+    a.f = c->ui(L, L.f);
+    a.dst = c->ui(L, L.t);
+    a.g = L.g;
+    a.g1 = coarse_view(L, C, &zc);
+    a.f1 = c->ui(C, C.f) + (size_t)(zc * C.g.P) * c->rb;
+    // level l + 1's guess: cycle_rec's fresh zero (cpu.lua:138), or the warm one unless a zero is pending
+    const bool fresh1 = c->o.coarse_init == MGP_COARSE_FRESH || C.zero_pending;
+    a.src1 = fresh1 ? nullptr : c->ui(C, C.u);
+    a.dst1 = c->ui(C, C.t);
+    a.g2 = coarse_view(C, D, &zc2);
+    a.R = c->ui(D, D.f) + (size_t)(zc2 * D.g.P) * c->rb;
+    a.h = h;
+    a.cl = coarse_coef(c->o.coarse_bc, l);
+    a.cl1 = coarse_coef(c->o.coarse_bc, l + 1);
+    HIP_TRY(c, mgp::launch_block2(c->rb, c->o.dim, a, c->s));
+    L.zero_pending = false;
+    std::swap(L.u, L.t);
+    L.ghost_ok = true;
+    L.ghost_zero = false;
+    C.fghost_ok = true;
+    C.zero_pending = false;
+    std::swap(C.u, C.t);
+    C.ghost_ok = true;
+    C.ghost_zero = false;
+    D.fghost_ok = true;
+    return MGP_OK;
+}
+
+int block_post2(mgp_ctx* c, int l, double h)
+{
+    Level& L = c->lev[l];
+    Level& C = c->lev[l + 1];
+    Level& D = c->lev[l + 2];
+    TRY(materialize_zero(c, L));
+    TRY(materialize_zero(c, C));
+    TRY(materialize_zero(c, D));
+    mgp::Block2Args a{};
+    a.pre = false;
+    a.linear = c->o.prolong == MGP_PROLONG_LINEAR;
+    a.ns = c->o.nu2;
+    a.src = c->ui(L, L.u);
+    a.f = c->ui(L, L.f);
+    a.dst = c->ui(L, L.t);
+    a.src1 = c->ui(C, C.u);
+    a.f1 = c->ui(C, C.f);
+    a.dst1 = c->ui(C, C.t);
+    a.V2 = c->ui(D, D.u);
+    a.g = L.g;
+    a.g1 = C.g;
+    a.g2 = D.g;
+    a.h = h;
+    a.cl = coarse_coef(c->o.coarse_bc, l);
+    a.cl1 = coarse_coef(c->o.coarse_bc, l + 1);
+    a.cl2 = coarse_coef(c->o.coarse_bc, l + 2);
+    HIP_TRY(c, mgp::launch_block2(c->rb, c->o.dim, a, c->s));
+    std::swap(C.u, C.t);
+    C.ghost_ok = true;
+    C.ghost_zero = false;
+    std::swap(L.u, L.t);
+    L.ghost_ok = true;
+    L.ghost_zero = false;
+    return MGP_OK;
+}
+
 // prolong_correct(l) + smooth(l, nu2) of a small replicated level as one 3D-tiled launch: u + P V -> t
 int block_post(mgp_ctx* c, int l, double h)
 {
@@ -1539,7 +1635,9 @@ int debug_check(mgp_ctx* c, int l, const char* what, bool f_field = false)
     return MGP_OK;
 }
 
-int cycle_rec(mgp_ctx* c, int l, double h, bool fcycle)
+// pre_done: the level above ran this level's pre-smoothing and restriction in its launch (block_pre2); post_skip: the
+// level above runs this level's prolongation and post-smoothing in its launch (block_post2)
+int cycle_rec(mgp_ctx* c, int l, double h, bool fcycle, bool pre_done = false, bool post_skip = false)
 {
     const int last = (int)c->lev.size() - 1;
     if (l == c->handoff_level && c->handoff_fn) {
@@ -1560,9 +1658,13 @@ int cycle_rec(mgp_ctx* c, int l, double h, bool fcycle)
     const bool blk = !fused && c->lev[l].blk && h == level_h(c, l);
     const bool zpost = c->lev[l].zpost && h == level_h(c, l);
     std::optional<Range> pre_range(std::in_place, "L%d pre-smooth + restrict", l);
-    if (fused) {
+    const bool pre2 = !pre_done && blk && pre2_ok(c, l, h, fcycle);
+    if (pre_done) {
+    } else if (fused) {
         TRY(fused_pre(c, l, h));
         TRY(early_exchange_post(c, l));
+    } else if (pre2) {
+        TRY(block_pre2(c, l, h));
     } else if (blk) {
         TRY(block_pre(c, l, h));
     } else if (bres_ok(c, c->lev[l])) {
@@ -1573,15 +1675,22 @@ int cycle_rec(mgp_ctx* c, int l, double h, bool fcycle)
         TRY(residual_restrict(c, l, h));
     }
     TRY(debug_check(c, l, "pre-smoothing (u)"));
-    TRY(debug_check(c, l + 1, "the restriction (R = f of the coarse level)", true));
-    if (c->o.coarse_init == MGP_COARSE_FRESH) TRY(zero_level(c, c->lev[l + 1]));
+    TRY(debug_check(c, l + 1, pre2 ? "the restriction and its pre-smoothing (block_pre2)"
+                                   : "the restriction (R = f of the coarse level)", true));
+    // (block_pre2 already smoothed level l + 1 from its fresh guess)
+    if (c->o.coarse_init == MGP_COARSE_FRESH && !pre2) TRY(zero_level(c, c->lev[l + 1]));
     pre_range.reset();
-    if (fcycle) TRY(cycle_rec(c, l + 1, 2 * h, true));
-    TRY(cycle_rec(c, l + 1, 2 * h, false));
     const bool want_err = l == 0 && c->in_cycle && c->err_fuse;
+    const bool post2 = !post_skip && blk && !want_err && post2_ok(c, l, h, fcycle);  // (pairs like pre2)
+    if (fcycle) TRY(cycle_rec(c, l + 1, 2 * h, true));
+    TRY(cycle_rec(c, l + 1, 2 * h, false, pre2, post2));
+    if (post_skip) return MGP_OK;  // (block_post2 of the level above)
     Range post_range("L%d prolong + post-smooth", l);
     if (fused || zpost) {
         TRY(fused_post(c, l, h, want_err));
+    } else if (post2) {
+        TRY(block_post2(c, l, h));
+        TRY(debug_check(c, l + 1, "the prolongation + correction and post-smoothing (u, block_post2)"));
     } else if (blk && !want_err) {
         TRY(block_post(c, l, h));
     } else if (post1_ok(c, l, want_err)) {
@@ -1872,6 +1981,8 @@ static void host_setup(mgp_ctx* c, const mgp_opts& o, const std::vector<LevelPla
         c->bres = !(vbr && std::atoi(vbr) == 0);
         const char* vrs = std::getenv("MGP_RBSWEEP");  // (measured slower, round 6: opt-in)
         c->rbsweep = vrs && std::atoi(vrs) != 0;
+        const char* vb2 = std::getenv("MGP_BLK2");
+        c->blk2 = !(vb2 && std::atoi(vb2) == 0);
     }
     // distributed 3D levels sweep with deep halos (smooth_deep): kGhostZs ghost planes per side
     if (c->deep_halo && o.dim == 3 && c->multi()) c->G = mgp::kGhostZs;

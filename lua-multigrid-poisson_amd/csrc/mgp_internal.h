@@ -216,6 +216,28 @@ struct BlockArgs {
 bool block_supported(int rb, int dim, int ns, const Geo& g);
 hipError_t launch_block(int rb, int dim, const BlockArgs& a, hipStream_t s);
 
+// PRE (POST) of two consecutive small 2D levels in one launch (mgp_blk2.hip): level l (g) smoothed and restricted, then
+// level l + 1 (g1) smoothed from its guess and restricted onto level l + 2 (g2); POST: level l + 1 corrected from
+// level l + 2 and smoothed, then level l corrected from it and smoothed
+struct Block2Args {
+    bool pre;          // false: POST of level l + 1 then of level l (k_blk2_post)
+    int ns;
+    int linear;        // POST: linear prolongation
+    const void* src;   // level l's u (PRE: nullptr = a fresh zero guess)
+    const void* f;
+    void* dst;         // level l's smoothed u (PRE: black cells; POST: both colours)
+    void* f1;          // level l + 1's f (PRE: written, both colours; POST: read)
+    const void* src1;  // level l + 1's u (PRE: the warm guess, nullptr = a fresh zero guess)
+    void* dst1;        // level l + 1's smoothed u
+    void* R;           // level l + 2's f
+    const void* V2;    // POST: level l + 2's u (the correction prolongated into level l + 1)
+    Geo g, g1, g2;
+    double h, cl, cl1, cl2;  // h of level l (level l + 1: 2 h); the coarse-boundary coefficients of levels l .. l + 2
+};
+bool block2_supported(int rb, int dim, int ns, const Geo& g, const Geo& g1, const Geo& g2);
+hipError_t launch_block2(int rb, int dim, const Block2Args& a, hipStream_t s);
+hipError_t blk2_attr();
+
 // Coarse-level tail: the sub-cycle below one level as a single one-workgroup launch with every
 // level in LDS.  ops[] = (op | level << 4 | arg << 8), levels relative to the tail's first level.
 constexpr int kTailMaxLevels = 8;

@@ -1083,56 +1083,6 @@ __global__ __launch_bounds__(kBlock) void k_fw_v(const T* __restrict__ r, T* __r
 
 // ---- prolongation + correction --------------------------------------------------------------
 
-// The oracle's cval() factor: -cl per out-of-box axis, in x, y, z order, applied to coarse value v
-template <typename T>
-__device__ __forceinline__ T cfac(T v, bool ox, bool oy, bool oz, T cl)
-{
-    T s = (T)1;
-    if (ox) s = -cl * s;
-    if (oy) s = -cl * s;
-    if (oz) s = -cl * s;
-    return s == (T)1 ? v : s * v;
-}
-
-// (P V) at fine cell (i, j, local plane k): the oracle's per-cell prolongation value, with the coarse
-// values read through get(I, J, K) (K relative to the V pointer; always inside the box).
-template <typename T, int DIM, int LINEAR, typename Get>
-__device__ __forceinline__ T prolong_eval(const Get& get, const Geo& gc, T cl, int i, int j, int64_t k)
-{
-    const int I = i >> 1, J = j >> 1;
-    const int64_t K = DIM == 3 ? (k >> 1) : 0;
-    T v;
-    if (!LINEAR) {
-        v = get(I, J, K);
-    } else {
-        const T w0 = (T)0.75, w1 = (T)0.25;
-        int In = (i & 1) ? I + 1 : I - 1;
-        int Jn = (j & 1) ? J + 1 : J - 1;
-        const bool ox = In < 0 || In >= gc.nx;
-        const bool oy = Jn < 0 || Jn >= gc.ny;
-        if (ox) In = I;
-        if (oy) Jn = J;
-        if (DIM == 2) {
-            const T a0 = w0 * cfac(get(I, J, 0), false, false, false, cl) + w1 * cfac(get(In, J, 0), ox, false, false, cl);
-            const T a1 = w0 * cfac(get(I, Jn, 0), false, oy, false, cl) + w1 * cfac(get(In, Jn, 0), ox, oy, false, cl);
-            v = w0 * a0 + w1 * a1;
-        } else {
-            int64_t Kn = (k & 1) ? K + 1 : K - 1;
-            const int64_t Kng = gc.z0 + Kn;
-            const bool oz = Kng < 0 || Kng >= gc.gnz;
-            if (oz) Kn = K;
-            const T a00 = w0 * cfac(get(I, J, K), false, false, false, cl) + w1 * cfac(get(In, J, K), ox, false, false, cl);
-            const T a10 = w0 * cfac(get(I, Jn, K), false, oy, false, cl) + w1 * cfac(get(In, Jn, K), ox, oy, false, cl);
-            const T a01 = w0 * cfac(get(I, J, Kn), false, false, oz, cl) + w1 * cfac(get(In, J, Kn), ox, false, oz, cl);
-            const T a11 = w0 * cfac(get(I, Jn, Kn), false, oy, oz, cl) + w1 * cfac(get(In, Jn, Kn), ox, oy, oz, cl);
-            const T b0 = w0 * a00 + w1 * a10;
-            const T b1 = w0 * a01 + w1 * a11;
-            v = w0 * b0 + w1 * b1;
-        }
-    }
-    return v;
-}
-
 // (P V) at fine cell (i, j, local plane k) from the packed coarse level V
 template <typename T, int DIM, int LINEAR>
 __device__ __forceinline__ T prolong_value(const T* V, const Geo& g, const Geo& gc, T cl, int i, int j, int64_t k)
@@ -4894,6 +4844,7 @@ hipError_t prepare_kernels(int rb)
         MGP_CHAIN((tail_attr<float, 3>()));
         MGP_CHAIN((tail_c_attr<float>()));
         MGP_CHAIN((blk_attr<float>()));
+        MGP_CHAIN((blk2_attr()));
     } else {
         MGP_CHAIN((fused_attr<double, true>()));
         MGP_CHAIN((fused_attr<double, false>()));
