@@ -1353,7 +1353,8 @@ int block_pre(mgp_ctx* c, int l, double h)
 bool pair2_ok(const mgp_ctx* c, int l, double h, bool fcycle, int ns)
 {
     const int last = (int)c->lev.size() - 1;
-    if (!c->blk2 || fcycle || l + 2 > last || c->rk != 4 || c->o.dim != 2 || c->o.smoother != MGP_RBGS) return false;
+    if (!c->blk2 || fcycle || l + 2 > last || (c->rk != 4 && c->rk != 8) || c->o.dim != 2 || c->o.smoother != MGP_RBGS)
+        return false;
     if (l + 1 == c->tail_level || l + 1 == c->handoff_level || h != level_h(c, l)) return false;
     const Level &L = c->lev[l], &C = c->lev[l + 1], &D = c->lev[l + 2];
     if (!L.blk || !C.blk || L.fused || C.fused || L.p.dist || C.p.dist || D.p.dist) return false;

@@ -24,7 +24,10 @@ namespace mgp {
 namespace {
 
 constexpr int kB2Threads = 1024;
-constexpr int kB2Tile = 32;  // owned tile edge of level l + 1
+// owned tile edge of level l + 1: 32, or 16 where 32 would give fewer than B2_T16_BELOW workgroups (build knob)
+#ifndef B2_T16_BELOW
+#define B2_T16_BELOW 64
+#endif
 
 // An LDS box of a 2D level: EX x EY cells from a global origin (xs even, ys), k_blk's layout: the slots of row ly and
 // colour c at (2 ly + c) EH, EH = EX / 2, so LDS cell (lx, ly) of colour c sits at slot lx >> 1 of that row.
@@ -34,9 +37,9 @@ struct B2Box {
     static __device__ __forceinline__ int lidx(int ly, int c, int mm) { return (2 * ly + c) * EH + mm; }
 };
 
-template <int NS>
+template <int NS, int BT>
 struct B2Shape {
-    static constexpr int B = kB2Tile;
+    static constexpr int B = BT;
     static constexpr int EC = 2 * NS + 1, HXC = (EC + 1) & ~1;  // level l + 1: k_blk's PRE halo
     using C = B2Box<B + 2 * HXC, B + 2 * EC>;
     static constexpr int EF = 2 * NS + 1, HXF = (EF + 1) & ~1;  // level l: the same halo around the coarse box's children
@@ -112,14 +115,14 @@ __device__ __forceinline__ T b2_restrict(const T* U, const T* F, const Op<T, 2>&
     return (T)0.25 * sm;
 }
 
-template <typename T, int NS>
+template <typename T, int NS, int BT>
 __global__ __launch_bounds__(kB2Threads) void k_blk2_pre(const T* __restrict__ src, const T* __restrict__ f,
                                                          T* __restrict__ dst, T* __restrict__ f1,
                                                          const T* __restrict__ src1, T* __restrict__ dst1,
                                                          T* __restrict__ R, Geo g, Geo g1, Geo g2, Op<T, 2> op,
                                                          Op<T, 2> op1)
 {
-    using S = B2Shape<NS>;
+    using S = B2Shape<NS, BT>;
     using FB = typename S::F;
     using CB = typename S::C;
     constexpr int NT = kB2Threads, B = S::B, EC = S::EC, HXC = S::HXC, EF = S::EF, HXF = S::HXF;
@@ -235,9 +238,9 @@ __global__ __launch_bounds__(kB2Threads) void k_blk2_pre(const T* __restrict__ s
     }
 }
 
-template <int NS>
+template <int NS, int BT>
 struct B2PostShape {
-    static constexpr int B = kB2Tile;                      // owned tile of level l + 1 (level l: 2B x 2B)
+    static constexpr int B = BT;                           // owned tile of level l + 1 (level l: 2B x 2B)
     static constexpr int EF = 2 * NS, HXF = (EF + 1) & ~1;  // level l: k_blk's POST halo
     using F = B2Box<2 * B + 2 * HXF, 2 * B + 2 * EF>;
     // level l + 1's final values that level l's prolongation reads: the tile and G cells around it (even)
@@ -249,14 +252,14 @@ struct B2PostShape {
     static constexpr size_t lds_reals = 2 * (size_t)F::cells + 2 * (size_t)C::cells + (size_t)c2cells;
 };
 
-template <typename T, int NS, int LINEAR>
+template <typename T, int NS, int LINEAR, int BT>
 __global__ __launch_bounds__(kB2Threads) void k_blk2_post(const T* __restrict__ src, const T* __restrict__ f,
                                                           T* __restrict__ dst, const T* __restrict__ src1,
                                                           const T* __restrict__ f1, T* __restrict__ dst1,
                                                           const T* __restrict__ V2, Geo g, Geo g1, Geo g2, Op<T, 2> op,
                                                           Op<T, 2> op1, T cl1, T cl2)
 {
-    using S = B2PostShape<NS>;
+    using S = B2PostShape<NS, BT>;
     using FB = typename S::F;
     using CB = typename S::C;
     constexpr int NT = kB2Threads, B = S::B, EC = S::EC, HXC = S::HXC, EF = S::EF, HXF = S::HXF, G = S::G;
@@ -385,54 +388,59 @@ __global__ __launch_bounds__(kB2Threads) void k_blk2_post(const T* __restrict__ 
     }
 }
 
-template <int NS>
+template <typename T, int NS, int BT>
 constexpr size_t b2_pre_lds()
 {
-    return B2Shape<NS>::lds_reals * sizeof(float);
+    return B2Shape<NS, BT>::lds_reals * sizeof(T);
 }
-template <int NS>
+template <typename T, int NS, int BT>
 constexpr size_t b2_post_lds()
 {
-    return B2PostShape<NS>::lds_reals * sizeof(float);
+    return B2PostShape<NS, BT>::lds_reals * sizeof(T);
 }
 
-}  // namespace
-
-// level l (g) and l + 1 (g1) of a 2D fp32 box, level l + 2 (g2) below: the tile divides level l + 1
-bool block2_supported(int rb, int dim, int ns, const Geo& g, const Geo& g1, const Geo& g2)
+// the tile edge for level l + 1 (g1): 32 unless that leaves fewer than B2_T16_BELOW workgroups and 16 divides it;
+// fp64 always 16 (its 32-tile PRE needs 180 KB of LDS)
+int b2_tile(int rb, const Geo& g1)
 {
-    if (rb != 4 || dim != 2 || (ns != 1 && ns != 2)) return false;
-    if (g.z0 != 0 || g1.z0 != 0 || g.nz != 1 || g1.nz != 1 || g2.nz != 1) return false;
-    if (g1.nx < kB2Tile || g1.ny < kB2Tile || g1.nx % kB2Tile || g1.ny % kB2Tile) return false;
-    if (g.nx != 2 * g1.nx || g.ny != 2 * g1.ny || g2.nx != g1.nx / 2 || g2.ny != g1.ny / 2) return false;
-    return b2_pre_lds<2>() <= 160 * 1024 && b2_post_lds<2>() <= 160 * 1024;
+    const bool t32 = g1.nx % 32 == 0 && g1.ny % 32 == 0, t16 = g1.nx % 16 == 0 && g1.ny % 16 == 0;
+    if (rb == 8) return t16 ? 16 : 0;
+    if (t32 && (g1.nx / 32) * (g1.ny / 32) >= B2_T16_BELOW) return 32;
+    return t16 ? 16 : t32 ? 32 : 0;
 }
 
-hipError_t blk2_attr()
+template <typename T, typename F>
+hipError_t b2_each(F&& f)  // every instantiation of real type T: f(kernel, lds bytes)
 {
-    const auto A = hipFuncAttributeMaxDynamicSharedMemorySize;
-    hipError_t e = hipFuncSetAttribute((const void*)k_blk2_pre<float, 1>, A, (int)b2_pre_lds<1>());
-    if (e == hipSuccess) e = hipFuncSetAttribute((const void*)k_blk2_pre<float, 2>, A, (int)b2_pre_lds<2>());
-    if (e == hipSuccess) e = hipFuncSetAttribute((const void*)k_blk2_post<float, 1, 0>, A, (int)b2_post_lds<1>());
-    if (e == hipSuccess) e = hipFuncSetAttribute((const void*)k_blk2_post<float, 1, 1>, A, (int)b2_post_lds<1>());
-    if (e == hipSuccess) e = hipFuncSetAttribute((const void*)k_blk2_post<float, 2, 0>, A, (int)b2_post_lds<2>());
-    if (e == hipSuccess) e = hipFuncSetAttribute((const void*)k_blk2_post<float, 2, 1>, A, (int)b2_post_lds<2>());
+    hipError_t e = hipSuccess;
+#define B2_EACH(BT)                                                                                         \
+    if (e == hipSuccess) e = f((const void*)k_blk2_pre<T, 1, BT>, b2_pre_lds<T, 1, BT>());                  \
+    if (e == hipSuccess) e = f((const void*)k_blk2_pre<T, 2, BT>, b2_pre_lds<T, 2, BT>());                  \
+    if (e == hipSuccess) e = f((const void*)k_blk2_post<T, 1, 0, BT>, b2_post_lds<T, 1, BT>());             \
+    if (e == hipSuccess) e = f((const void*)k_blk2_post<T, 1, 1, BT>, b2_post_lds<T, 1, BT>());             \
+    if (e == hipSuccess) e = f((const void*)k_blk2_post<T, 2, 0, BT>, b2_post_lds<T, 2, BT>());             \
+    if (e == hipSuccess) e = f((const void*)k_blk2_post<T, 2, 1, BT>, b2_post_lds<T, 2, BT>());
+    B2_EACH(16)
+    if constexpr (sizeof(T) == 4) {
+        B2_EACH(32)
+    }
+#undef B2_EACH
     return e;
 }
 
-hipError_t launch_block2(int rb, int dim, const Block2Args& a, hipStream_t s)
+template <typename T, int BT>
+hipError_t b2_launch(const Block2Args& a, hipStream_t s)
 {
-    if (!block2_supported(rb, dim, a.ns, a.g, a.g1, a.g2)) return hipErrorInvalidValue;
-    const unsigned nb = (unsigned)((a.g1.nx / kB2Tile) * (a.g1.ny / kB2Tile));
-    const Op<float, 2> op = make_op<float, 2>(a.h, a.cl), op1 = make_op<float, 2>(2 * a.h, a.cl1);
+    const unsigned nb = (unsigned)((a.g1.nx / BT) * (a.g1.ny / BT));
+    const Op<T, 2> op = make_op<T, 2>(a.h, a.cl), op1 = make_op<T, 2>(2 * a.h, a.cl1);
     if (!a.pre) {
-        const float *src = (const float*)a.src, *f = (const float*)a.f, *src1 = (const float*)a.src1,
-                    *f1 = (const float*)a.f1, *V2 = (const float*)a.V2;
-        float *dst = (float*)a.dst, *dst1 = (float*)a.dst1;
-        const float cl1 = (float)a.cl1, cl2 = (float)a.cl2;
-#define B2POST(NS, LIN)                                                                                         \
-    k_blk2_post<float, NS, LIN><<<nb, kB2Threads, b2_post_lds<NS>(), s>>>(src, f, dst, src1, f1, dst1, V2, a.g, a.g1, \
-                                                                       a.g2, op, op1, cl1, cl2)
+        const T *src = (const T*)a.src, *f = (const T*)a.f, *src1 = (const T*)a.src1, *f1 = (const T*)a.f1,
+                *V2 = (const T*)a.V2;
+        T *dst = (T*)a.dst, *dst1 = (T*)a.dst1;
+        const T cl1 = (T)a.cl1, cl2 = (T)a.cl2;
+#define B2POST(NS, LIN)                                                                                             \
+    k_blk2_post<T, NS, LIN, BT><<<nb, kB2Threads, b2_post_lds<T, NS, BT>(), s>>>(src, f, dst, src1, f1, dst1, V2, a.g, \
+                                                                              a.g1, a.g2, op, op1, cl1, cl2)
         if (a.ns == 1) {
             if (a.linear) B2POST(1, 1); else B2POST(1, 0);
         } else {
@@ -442,14 +450,44 @@ hipError_t launch_block2(int rb, int dim, const Block2Args& a, hipStream_t s)
         return hipGetLastError();
     }
     if (a.ns == 1)
-        k_blk2_pre<float, 1><<<nb, kB2Threads, b2_pre_lds<1>(), s>>>(
-            (const float*)a.src, (const float*)a.f, (float*)a.dst, (float*)a.f1, (const float*)a.src1, (float*)a.dst1,
-            (float*)a.R, a.g, a.g1, a.g2, op, op1);
+        k_blk2_pre<T, 1, BT><<<nb, kB2Threads, b2_pre_lds<T, 1, BT>(), s>>>(
+            (const T*)a.src, (const T*)a.f, (T*)a.dst, (T*)a.f1, (const T*)a.src1, (T*)a.dst1, (T*)a.R, a.g, a.g1, a.g2,
+            op, op1);
     else
-        k_blk2_pre<float, 2><<<nb, kB2Threads, b2_pre_lds<2>(), s>>>(
-            (const float*)a.src, (const float*)a.f, (float*)a.dst, (float*)a.f1, (const float*)a.src1, (float*)a.dst1,
-            (float*)a.R, a.g, a.g1, a.g2, op, op1);
+        k_blk2_pre<T, 2, BT><<<nb, kB2Threads, b2_pre_lds<T, 2, BT>(), s>>>(
+            (const T*)a.src, (const T*)a.f, (T*)a.dst, (T*)a.f1, (const T*)a.src1, (T*)a.dst1, (T*)a.R, a.g, a.g1, a.g2,
+            op, op1);
     return hipGetLastError();
+}
+
+}  // namespace
+
+static_assert(b2_pre_lds<float, 2, 32>() <= 160 * 1024 && b2_post_lds<float, 2, 32>() <= 160 * 1024 &&
+                  b2_pre_lds<double, 2, 16>() <= 160 * 1024 && b2_post_lds<double, 2, 16>() <= 160 * 1024,
+              "k_blk2 LDS");
+
+// level l (g) and l + 1 (g1) of a 2D box (fp32 or fp64), level l + 2 (g2) below: a tile edge divides level l + 1
+bool block2_supported(int rb, int dim, int ns, const Geo& g, const Geo& g1, const Geo& g2)
+{
+    if ((rb != 4 && rb != 8) || dim != 2 || (ns != 1 && ns != 2)) return false;
+    if (g.z0 != 0 || g1.z0 != 0 || g.nz != 1 || g1.nz != 1 || g2.nz != 1) return false;
+    if (b2_tile(rb, g1) == 0) return false;
+    return g.nx == 2 * g1.nx && g.ny == 2 * g1.ny && g2.nx == g1.nx / 2 && g2.ny == g1.ny / 2;
+}
+
+hipError_t blk2_attr(int rb)
+{
+    auto set = [](const void* k, size_t lds) {
+        return hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    };
+    return rb == 8 ? b2_each<double>(set) : b2_each<float>(set);
+}
+
+hipError_t launch_block2(int rb, int dim, const Block2Args& a, hipStream_t s)
+{
+    if (!block2_supported(rb, dim, a.ns, a.g, a.g1, a.g2)) return hipErrorInvalidValue;
+    if (rb == 8) return b2_launch<double, 16>(a, s);
+    return b2_tile(rb, a.g1) == 16 ? b2_launch<float, 16>(a, s) : b2_launch<float, 32>(a, s);
 }
 
 }  // namespace mgp

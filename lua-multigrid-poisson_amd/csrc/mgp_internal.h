@@ -236,7 +236,7 @@ struct Block2Args {
 };
 bool block2_supported(int rb, int dim, int ns, const Geo& g, const Geo& g1, const Geo& g2);
 hipError_t launch_block2(int rb, int dim, const Block2Args& a, hipStream_t s);
-hipError_t blk2_attr();
+hipError_t blk2_attr(int rb);
 
 // Coarse-level tail: the sub-cycle below one level as a single one-workgroup launch with every
 // level in LDS.  ops[] = (op | level << 4 | arg << 8), levels relative to the tail's first level.

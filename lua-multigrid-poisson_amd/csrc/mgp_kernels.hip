@@ -4844,7 +4844,7 @@ hipError_t prepare_kernels(int rb)
         MGP_CHAIN((tail_attr<float, 3>()));
         MGP_CHAIN((tail_c_attr<float>()));
         MGP_CHAIN((blk_attr<float>()));
-        MGP_CHAIN((blk2_attr()));
+        MGP_CHAIN((blk2_attr(4)));
     } else {
         MGP_CHAIN((fused_attr<double, true>()));
         MGP_CHAIN((fused_attr<double, false>()));
@@ -4852,6 +4852,7 @@ hipError_t prepare_kernels(int rb)
         MGP_CHAIN((tail_attr<double, 3>()));
         MGP_CHAIN((tail_c_attr<double>()));
         MGP_CHAIN((blk_attr<double>()));
+        MGP_CHAIN((blk2_attr(8)));
     }
 #undef MGP_CHAIN
     return e;
