@@ -172,30 +172,31 @@ __global__ __launch_bounds__(FwShape<DIM>::NT) void k_resfw(const T* __restrict_
         const int64_t k0 = 2 * (int64_t)K0 - 1;  // the chunk's first fine plane
         const int kend = K0 + kc < (int)(g.nz >> 1) ? K0 + kc : (int)(g.nz >> 1);
         const int64_t klast = 2 * (int64_t)kend;  // the last fine plane (2 K + 2 of the last coarse plane)
-        // plane k + 1's u (loaded during step k - 1) goes into its slot at the top of step k, f of plane k was loaded
-        // during step k - 1 as well (a prefetch distance of 2 with double buffers measured slower: 134 VGPRs, 3
-        // workgroups per CU, 609 against 470 us at 512^3)
-        T uv[I::IU], fv[I::IR], fn[I::IR];
+        // plane k + 1's u (loaded during step k - 1) goes into its slot at the top of step k; f of plane k was loaded
+        // during step k - 1 into the other of two buffers (a prefetch distance of 2 with double buffers measured slower:
+        // 134 VGPRs, 3 workgroups per CU, 609 against 470 us at 512^3).  The step is unrolled by two so that the buffers
+        // swap roles without a copy: copying the prefetched f at the end of a step made it wait for those loads there.
+        T uv[I::IU], fa[I::IR], fb[I::IR];
         uload(uv, k0 - 1);
         ustore(slot(k0 - 1), uv, k0 - 1);
         uload(uv, k0);
         ustore(slot(k0), uv, k0);
         uload(uv, k0 + 1);  // in flight into the first step
-        fload(fv, k0);
+        fload(fa, k0);
         T a0 = (T)0, a1 = (T)0, a2 = (T)0, a3 = (T)0;
         int K = K0;
-        for (int64_t k = k0; k <= klast; ++k) {
+        auto step = [&](int64_t k, const T (&fc)[I::IR], T (&fnx)[I::IR]) {
             ustore(slot(k + 1), uv, k + 1);
             if (k + 2 <= klast + 1) uload(uv, k + 2);
-            if (k + 1 <= klast) fload(fn, k + 1);
+            if (k + 1 <= klast) fload(fnx, k + 1);
             __syncthreads();
-            const T ay = plane_ay(k, slot(k - 1), slot(k), slot(k + 1), fv);
+            // (plane_ay's barrier also frees slot k - 1, restaged next step, and every read of rs precedes the next
+            // step's first barrier: no barrier at the end of a step)
+            const T ay = plane_ay(k, slot(k - 1), slot(k), slot(k + 1), fc);
             a0 = a1;
             a1 = a2;
             a2 = a3;
             a3 = ay;
-#pragma unroll
-            for (int e = 0; e < I::IR; ++e) fv[e] = fn[e];
             if (k == 2 * (int64_t)K + 2) {  // coarse plane K complete (fine planes 2K-1 .. 2K+2)
                 const int64_t gK = gc.z0 + K;
                 T az = a0;
@@ -205,7 +206,10 @@ __global__ __launch_bounds__(FwShape<DIM>::NT) void k_resfw(const T* __restrict_
                 R[(int64_t)K * gc.P + ((Ic + Jc + gK) & 1) * gc.H + (int64_t)Jc * gc.hw + (Ic >> 1)] = scale * az;
                 ++K;
             }
-            __syncthreads();  // rs and the slot restaged next are free again
+        };
+        for (int64_t k = k0; k <= klast; k += 2) {
+            step(k, fa, fb);
+            if (k + 1 <= klast) step(k + 1, fb, fa);
         }
     }
 }
